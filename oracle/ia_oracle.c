@@ -1,0 +1,182 @@
+/* CPU ORACLE for the B' synthesis hot path — TEST INFRASTRUCTURE ONLY.
+ *
+ * C restatement of the reference's per-level synthesis loop
+ * (image_analogies.py:130-220) with the exact brute-force matcher in place of FLANN
+ * (algorithms.py:73-75; see oracle/ia_oracle.py for why), used by tests/ as the fast
+ * checker for the HIP path and by bench.py's cpu_baseline leg.  Never linked into or
+ * called by the product library.
+ *
+ * It follows oracle/ia_oracle.py operation for operation (and is checked against it
+ * bit for bit in tests/test_oracle.py):
+ *   features      algorithms.py:11-47, 78-89   symmetric-padded 3x3 coarse + 5x5 fine
+ *   brute force   algorithms.py:73-75 (exact) d = pairwise8( (a-q)*(a-q) ), first min
+ *   coherence     algorithms.py:92-130         argmin sqrt(pairwise8(x*x)), first min
+ *   kappa test    algorithms.py:133-135 + image_analogies.py:200-211
+ *                 d = s*s, s = sqrt(pairwise8(((a-q)*w)^2)); coh iff d_coh <= d_app*f
+ *   update        image_analogies.py:214-220
+ * pairwise8 is numpy's pairwise_sum (8 accumulators for n <= 128, recursive halves
+ * above).  Build: see oracle/Makefile (-O2 -ffp-contract=off: no FMA contraction).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NSM 3
+#define NLG 5
+#define NHALF 12
+
+static double pairwise8(const double *a, long n) {
+    if (n < 8) {
+        double res = 0.;
+        for (long i = 0; i < n; i++) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        long i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    } else {
+        long n2 = n / 2;
+        n2 -= n2 % 8;
+        return pairwise8(a, n2) + pairwise8(a + n2, n - n2);
+    }
+}
+
+static inline long symi(long i, long n) {   /* np.pad 'symmetric' index map */
+    long p = 2 * n;
+    i %= p;
+    if (i < 0) i += p;
+    return i >= n ? p - 1 - i : i;
+}
+
+/* 1-channel feature of pixel (r, c): [3x3 of sm at (r/2, c/2) | 5x5 (or first 12) of lg] */
+static int pixel_feature(const double *sm, long hs, long ws, const double *lg, long h, long w,
+                         long r, long c, int full, double *out) {
+    int k = 0;
+    for (int dr = -1; dr <= 1; dr++)
+        for (int dc = -1; dc <= 1; dc++)
+            out[k++] = sm[symi(r / 2 + dr, hs) * ws + symi(c / 2 + dc, ws)];
+    int nfine = full ? NLG * NLG : NHALF;
+    for (int t = 0; t < nfine; t++) {
+        int dr = t / NLG - 2, dc = t % NLG - 2;
+        out[k++] = lg[symi(r + dr, h) * w + symi(c + dc, w)];
+    }
+    return k;
+}
+
+typedef struct {
+    const double *A_sm, *A_lg;   /* A level l-1 (A_hs x A_ws), level l (Ah x Aw)        */
+    const double *Ap_sm, *Ap_lg; /* nAp A' images stacked, same shapes as A             */
+    int A_hs, A_ws, Ah, Aw, nAp;
+    const double *B_sm, *B_lg;   /* B level l-1 (B_hs x B_ws), level l (H x W)          */
+    int B_hs, B_ws, H, W;
+    const double *Bp_sm;         /* B' level l-1 (already synthesized / init)           */
+    double *Bp_lg;               /* B' level l, in: init values, out: synthesized       */
+    const double *weights;       /* 55 Gaussian weights (config.py:68-79)               */
+    double kappa_factor;         /* 1 + 2**(level-max_levels)*k                          */
+    int32_t *s;                  /* out: H*W*2 source pixel (row, col) in A'            */
+    int32_t *im;                 /* out: H*W source image number                        */
+    long max_pixels;             /* <0: whole level; else stop after this many pixels   */
+} IaOracleLevel;
+
+#define D 55
+
+/* database row ix -> 55 features (algorithms.py:63-67: [A full | A'_img half]) */
+static void db_row(const IaOracleLevel *L, long ix, double *f) {
+    long hw = (long)L->Ah * L->Aw;
+    long img = ix / hw, rem = ix - img * hw;
+    long r = rem / L->Aw, c = rem % L->Aw;
+    int k = pixel_feature(L->A_sm, L->A_hs, L->A_ws, L->A_lg, L->Ah, L->Aw, r, c, 1, f);
+    pixel_feature(L->Ap_sm + img * (long)L->A_hs * L->A_ws, L->A_hs, L->A_ws,
+                  L->Ap_lg + img * hw, L->Ah, L->Aw, r, c, 0, f + k);
+}
+
+double *ia_oracle_build_db(const IaOracleLevel *L) {
+    long N = (long)L->nAp * L->Ah * L->Aw;
+    double *db = (double *)malloc(sizeof(double) * N * D);
+    if (!db) return NULL;
+    for (long ix = 0; ix < N; ix++) db_row(L, ix, db + ix * D);
+    return db;
+}
+
+void ia_oracle_free(void *p) { free(p); }
+
+/* exact 1-NN over db (N x 55): first minimum of pairwise8((a-q)^2) */
+long ia_oracle_nn(const double *db, long N, const double *q, double *dmin_out) {
+    double t[D], best = INFINITY;
+    long bi = -1;
+    for (long i = 0; i < N; i++) {
+        const double *a = db + i * D;
+        for (int j = 0; j < D; j++) { double x = a[j] - q[j]; t[j] = x * x; }
+        double d = pairwise8(t, D);
+        if (d < best) { best = d; bi = i; }
+    }
+    if (dmin_out) *dmin_out = best;
+    return bi;
+}
+
+static double wdist(const double *a, const double *q, const double *w) {
+    double t[D];
+    for (int j = 0; j < D; j++) { double v = (a[j] - q[j]) * w[j]; t[j] = v * v; }
+    double s = sqrt(pairwise8(t, D));
+    return s * s;
+}
+
+/* image_analogies.py:161-220 for one level (db may be NULL: rows built on the fly).
+ * Returns the number of pixels processed. */
+long ia_oracle_synth_level(const IaOracleLevel *L, const double *db) {
+    const long H = L->H, W = L->W, Ah = L->Ah, Aw = L->Aw;
+    const long N = (long)L->nAp * Ah * Aw;
+    double *own = NULL;
+    if (!db) { own = ia_oracle_build_db(L); db = own; if (!db) return -1; }
+    long npx = H * W;
+    if (L->max_pixels >= 0 && L->max_pixels < npx) npx = L->max_pixels;
+    double q[D], x[D], t[D];
+    for (long qi = 0; qi < npx; qi++) {
+        long row = qi / W, col = qi % W;
+        /* BBp_feat = [B_features[level][ix] | extract_pixel_feature(Bp pads, half)] */
+        int k = pixel_feature(L->B_sm, L->B_hs, L->B_ws, L->B_lg, H, W, row, col, 1, q);
+        pixel_feature(L->Bp_sm, L->B_hs, L->B_ws, L->Bp_lg, H, W, row, col, 0, q + k);
+        long p_app_ix = ia_oracle_nn(db, N, q, NULL);
+        long hw = Ah * Aw;
+        long i_app = p_app_ix / hw, rem = p_app_ix - i_app * hw;
+        long pr_app = rem / Aw, pc_app = rem % Aw;
+        long pr = pr_app, pc = pc_app, pi = i_app;
+        if (qi > 0) {
+            /* best_coherence_match (algorithms.py:92-130) */
+            double bestd = INFINITY;
+            long bsr = -1, bsc = -1, bim = 0, bix = -1;
+            for (long rr = row - 2 < 0 ? 0 : row - 2; rr <= row; rr++) {
+                long cend = col + 3 < W ? col + 3 : W;
+                for (long cc = col - 2 < 0 ? 0 : col - 2; cc < cend; cc++) {
+                    long rix = rr * W + cc;
+                    if (rix >= qi) continue;
+                    long sr = L->s[2 * rix] + row - rr, sc = L->s[2 * rix + 1] + col - cc;
+                    if (!(sr >= 0 && sr < Ah && sc >= 0 && sc < Aw)) continue;
+                    long img = L->im[rix];
+                    long ix = (Ah * img + sr) * Aw + sc;
+                    const double *a = db + ix * D;
+                    for (int j = 0; j < D; j++) { x[j] = a[j] - q[j]; t[j] = x[j] * x[j]; }
+                    double d = sqrt(pairwise8(t, D));
+                    if (d < bestd) { bestd = d; bsr = sr; bsc = sc; bim = img; bix = ix; }
+                }
+            }
+            if (bix >= 0) {
+                double d_app = wdist(db + p_app_ix * D, q, L->weights);
+                double d_coh = wdist(db + bix * D, q, L->weights);
+                if (d_coh <= d_app * L->kappa_factor) { pr = bsr; pc = bsc; pi = bim; }
+            }
+        }
+        L->Bp_lg[row * W + col] = L->Ap_lg[pi * hw + pr * Aw + pc];
+        L->s[2 * qi] = (int32_t)pr;
+        L->s[2 * qi + 1] = (int32_t)pc;
+        L->im[qi] = (int32_t)pi;
+    }
+    free(own);
+    return npx;
+}

@@ -1,0 +1,486 @@
+"""CPU ORACLE for the B' synthesis hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the numpy restatement of the reference's algorithm and exists only to
+check the HIP product path.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import it; the product package
+(``image-analogies-python_amd/``) never does, and fails loudly without its HIP library.
+
+Parity pinning (see DESIGN.md "Oracle"):
+  * ``compute_weights`` / ``matlab_style_gauss2D``  -> golden from the reference's own
+    ``config.py`` (importable here) + the KAT in ``config_test.py:5-62``.
+  * YIQ / RGB                                       -> golden from the reference's
+    ``img_preprocess.py`` under /opt/conda python3.9 (tests/golden/make_golden.py).
+  * Gaussian pyramid                                -> golden from skimage 0.18.3
+    ``pyramid_gaussian`` (the library the reference calls at img_preprocess.py:56),
+    bit-exact.
+  * feature layout                                  -> KATs transcribed from
+    ``algorithms_test.py:10-115``.
+  * matcher: the reference calls FLANN's randomized kd-tree (``algorithms.py:69,74``),
+    an approximate, randomized search whose library (pyflann/libflann) is absent from
+    this image and which no reference test pins.  The oracle uses the exact brute-force
+    1-NN (FLANN ``linear`` semantics; ``output/shore-crop-filt-brute.jpg`` shows the
+    reference once ran that variant): fp64 ``np.add.reduce((As - q)**2, axis=1)``,
+    first minimum.  That choice is "parity unpinned" against FLANN itself.
+
+Every function cites the reference file:line it restates.  All arithmetic is IEEE
+fp64 in a fixed, documented operation order so that the C restatement
+(``oracle/ia_oracle.c``) and the HIP kernels can reproduce it bit for bit:
+  * sums over a feature vector use numpy's pairwise-8 order (``pairwise_sum`` for
+    n <= 128; verified identical to ``np.add.reduce(axis=1)`` here and under numpy
+    1.26.4),
+  * ``compute_distance`` (reference: ``norm(v, 2)**2`` = ``sqrt(ddot(v,v))**2``) is
+    restated as ``s = sqrt(add.reduce(v*v)); s*s`` — BLAS ``ddot``'s summation order is
+    CPU/BLAS-build dependent and therefore not reproducible; the difference is at most
+    a few ulp and only matters for exact kappa-test near-ties (documented, unpinned).
+"""
+import math
+
+import numpy as np
+
+# ----------------------------------------------------------------------------------
+# constants
+# ----------------------------------------------------------------------------------
+
+# scipy.ndimage gaussian taps for sigma = 2*2/6 (skimage pyramid_reduce default,
+# pyramids.py in skimage 0.18.3), truncate 4 -> radius 3, as computed by
+# scipy 1.7.1 ``_gaussian_kernel1d`` under numpy 1.26.4 (the skimage environment the
+# goldens come from).  numpy 2.2.6 differs by 1 ulp at +-2, hence fixed constants.
+# Index j = distance from the centre (w0, w1, w2, w3).
+PYR_TAPS = (
+    float.fromhex('0x1.324af5ad1bf73p-1'),
+    float.fromhex('0x1.8dc13f0096171p-3'),
+    float.fromhex('0x1.b38896102b1bcp-8'),
+    float.fromhex('0x1.921e9614385a4p-16'),
+)
+
+YIQ_M = np.array([[0.299, 0.587, 0.114],
+                  [0.596, -0.275, -0.321],
+                  [0.212, -0.523, 0.311]])   # img_preprocess.py:10-12
+RGB_M = np.array([[1., 0.956, 0.621],
+                  [1., -0.272, -0.647],
+                  [1., -1.105, 1.702]])      # img_preprocess.py:19-21
+
+N_SM, N_LG, N_HALF = 3, 5, 12                # config.py:15-18 (n_half as int)
+PAD_SM, PAD_LG = 1, 2                        # config.py:19-20
+
+
+# ----------------------------------------------------------------------------------
+# config.py
+# ----------------------------------------------------------------------------------
+
+def matlab_style_gauss2D(shape=(3, 3), sigma=0.5):
+    """config.py:52-65."""
+    m, n = [(ss - 1.) / 2. for ss in shape]
+    y, x = np.ogrid[-m:m + 1, -n:n + 1]
+    h = np.exp(-(x * x + y * y) / (2. * sigma * sigma))
+    h[h < np.finfo(h.dtype).eps * h.max()] = 0
+    sumh = h.sum()
+    if sumh != 0:
+        h /= sumh
+    return h
+
+
+def compute_weights(n_sm, n_lg, n_half, num_ch):
+    """config.py:68-79 (int n_half)."""
+    gauss_sm = matlab_style_gauss2D((n_sm, n_sm), 0.5)
+    gauss_lg = matlab_style_gauss2D((n_lg, n_lg), 1)
+    gauss_sm_stack = np.dstack([gauss_sm] * num_ch).flatten()
+    gauss_lg_stack = np.dstack([gauss_lg] * num_ch).flatten()
+    w_sm = (1. / (n_sm * n_sm)) * gauss_sm_stack
+    w_lg = (1. / (n_lg * n_lg)) * gauss_lg_stack
+    w_half = (1. / n_half) * gauss_lg_stack[:int(n_half) * num_ch]
+    return np.hstack([w_sm, w_lg, w_sm, w_half])
+
+
+# ----------------------------------------------------------------------------------
+# img_preprocess.py
+# ----------------------------------------------------------------------------------
+
+def convert_to_YIQ(img):
+    """img_preprocess.py:6-13 — einsum; on this numpy the per-channel order is
+    (m0*x0 + m2*x2) + m1*x1 (checked in tests against np.einsum)."""
+    assert 0 <= np.max(img) <= 1
+    return np.einsum('ij,klj->kli', YIQ_M, img)
+
+
+def convert_to_RGB(img):
+    """img_preprocess.py:16-22."""
+    return np.einsum('ij,klj->kli', RGB_M, img)
+
+
+def remap_luminance(A, Ap_list, B):
+    """img_preprocess.py:25-40."""
+    assert len(A.shape) == len(Ap_list[0].shape) == len(B.shape) == 2
+    m_A, m_B, s_A, s_B = np.mean(A), np.mean(B), np.std(A), np.std(B)
+    A_remap = (s_B / s_A) * (A - m_A) + m_B
+    return A_remap, [(s_B / s_A) * (Ap - m_A) + m_B for Ap in Ap_list]
+
+
+def compress_values(A, B, ratio):
+    """img_preprocess.py:43-44."""
+    return ratio * A, ratio * B
+
+
+def sym_index(i, n):
+    """np.pad 'symmetric' / ndimage 'reflect' index map (period 2n)."""
+    i = np.asarray(i) % (2 * n)
+    return np.where(i >= n, 2 * n - 1 - i, i)
+
+
+def mirror_index(i, n):
+    """skimage _warp_fast mode 'R' (reflect about the edge pixel, period 2(n-1))."""
+    i = np.asarray(i, dtype=np.int64)
+    cmax = n - 1
+    if cmax == 0:
+        return np.zeros_like(i)
+    out = i.copy()
+    neg = i < 0
+    a = -i[neg]
+    out[neg] = np.where((a // cmax) % 2 != 0, cmax - (a % cmax), a % cmax)
+    pos = i > cmax
+    b = i[pos]
+    out[pos] = np.where((b // cmax) % 2 != 0, cmax - (b % cmax), b % cmax)
+    return out
+
+
+def pyramid_num_layers(h, w, min_size, cap=None):
+    """img_preprocess.py:48-54 (+ optional ``levels`` cap used by configs 4/5)."""
+    curr_size = min(h, w)
+    levels = 0
+    while curr_size > min_size:
+        curr_size = math.floor(curr_size / 2.)
+        levels += 1
+    if cap is not None:
+        levels = min(levels, int(cap))
+    return levels
+
+
+def affine_coeffs(in_shape, out_shape):
+    """skimage 0.18.3 resize(): AffineTransform.estimate on 3 corner pairs
+    (transform/_warps.py:150-174 of that version), restated in numpy.  Returns the
+    (sx, tx, sy, ty) of ``src = s * dst + t`` after resize() zeroes the shear terms."""
+    rows, cols = out_shape
+    in_rows, in_cols = in_shape
+    if rows == 1 and cols == 1:
+        return 1.0, in_cols / 2.0 - 0.5, 1.0, in_rows / 2.0 - 0.5
+    factors = np.asarray(in_shape, dtype=float) / np.asarray(out_shape, dtype=float)
+    src = np.array([[1, 1], [1, rows], [cols, rows]]) - 1
+    dst = np.zeros(src.shape, dtype=np.double)
+    dst[:, 0] = factors[1] * (src[:, 0] + 0.5) - 0.5
+    dst[:, 1] = factors[0] * (src[:, 1] + 0.5) - 0.5
+
+    def center_norm(points):
+        centroid = np.mean(points, axis=0)
+        centered = points - centroid
+        rms = np.sqrt(np.sum(centered ** 2) / points.shape[0])
+        norm_factor = np.sqrt(2) / rms
+        matrix = np.array([[norm_factor, 0, -norm_factor * centroid[0]],
+                           [0, norm_factor, -norm_factor * centroid[1]],
+                           [0, 0, 1]])
+        pointsh = np.vstack([points.T, np.ones((points.shape[0]),)])
+        new_pointsh = (matrix @ pointsh).T
+        new_points = new_pointsh[:, :2]
+        new_points[:, 0] /= new_pointsh[:, 2]
+        new_points[:, 1] /= new_pointsh[:, 2]
+        return matrix, new_points
+
+    sm, s = center_norm(src)
+    dm, d = center_norm(dst)
+    xs, ys, xd, yd = s[:, 0], s[:, 1], d[:, 0], d[:, 1]
+    A = np.zeros((6, 9))
+    A[:3, 0] = xs; A[:3, 1] = ys; A[:3, 2] = 1
+    A[:3, 6] = -xd * xs; A[:3, 7] = -xd * ys
+    A[3:, 3] = xs; A[3:, 4] = ys; A[3:, 5] = 1
+    A[3:, 6] = -yd * xs; A[3:, 7] = -yd * ys
+    A[:3, 8] = xd; A[3:, 8] = yd
+    A = A[:, [0, 1, 2, 3, 4, 5, 8]]
+    _, _, V = np.linalg.svd(A)
+    H = np.zeros((3, 3))
+    H.flat[[0, 1, 2, 3, 4, 5, 8]] = -V[-1, :-1] / V[-1, -1]
+    H[2, 2] = 1
+    H = np.linalg.inv(dm) @ H @ sm
+    return float(H[0, 0]), float(H[0, 2]), float(H[1, 1]), float(H[1, 2])
+
+
+def gaussian_blur(img):
+    """scipy.ndimage.gaussian_filter(sigma=2/3, mode='reflect') as called by skimage
+    pyramid_reduce: 1-D correlate along axis 0, then axis 1.  Per output sample
+    (scipy NI_Correlate1D, symmetric-weights branch):
+        acc = x[0]*w0;  acc += (x[-3]+x[3])*w3;  acc += (x[-2]+x[2])*w2;
+        acc += (x[-1]+x[1])*w1."""
+    w0, w1, w2, w3 = PYR_TAPS
+    out = np.asarray(img, dtype=np.float64)
+    for axis in (0, 1):
+        n = out.shape[axis]
+        idx = np.arange(n)
+
+        def tap(off):
+            return np.take(out, sym_index(idx + off, n), axis=axis)
+        acc = out * w0
+        acc = acc + (tap(-3) + tap(3)) * w3
+        acc = acc + (tap(-2) + tap(2)) * w2
+        acc = acc + (tap(-1) + tap(1)) * w1
+        out = acc
+    return out
+
+
+def bilinear_resize(img, out_shape, coeffs):
+    """skimage _warp_fast bilinear (order=1, mode 'reflect' = mirror) + warp's clip to
+    [min, max] of the input.  src col c = sx*x + tx, row r = sy*y + ty;
+    top = (1-dc)*tl + dc*tr; bot = (1-dc)*bl + dc*br; out = (1-dr)*top + dr*bot."""
+    sx, tx, sy, ty = coeffs
+    h, w = out_shape
+    H, W = img.shape
+    c = np.arange(w, dtype=np.float64) * sx + tx
+    r = np.arange(h, dtype=np.float64) * sy + ty
+    minr = np.floor(r).astype(np.int64); maxr = np.ceil(r).astype(np.int64)
+    minc = np.floor(c).astype(np.int64); maxc = np.ceil(c).astype(np.int64)
+    dr = (r - minr)[:, None]
+    dc = (c - minc)[None, :]
+    r0 = mirror_index(minr, H)[:, None]; r1 = mirror_index(maxr, H)[:, None]
+    c0 = mirror_index(minc, W)[None, :]; c1 = mirror_index(maxc, W)[None, :]
+    tl, tr, bl, br = img[r0, c0], img[r0, c1], img[r1, c0], img[r1, c1]
+    top = (1 - dc) * tl + dc * tr
+    bot = (1 - dc) * bl + dc * br
+    out = (1 - dr) * top + dr * bot
+    return np.clip(out, img.min(), img.max())
+
+
+def pyramid_reduce(img):
+    """skimage pyramid_reduce(downscale=2) for a 2-D float64 image."""
+    h, w = img.shape
+    out_shape = (math.ceil(h / 2.0), math.ceil(w / 2.0))
+    sm = gaussian_blur(img)
+    return bilinear_resize(sm, out_shape, affine_coeffs((h, w), out_shape))
+
+
+def compute_gaussian_pyramid(img, min_size, cap=None):
+    """img_preprocess.py:47-63 -> skimage pyramid_gaussian(img, max_layer=levels),
+    reversed to smallest-first.  2-D images; a 3-D image is reduced per channel
+    (skimage ``multichannel=True`` semantics)."""
+    img = np.asarray(img, dtype=np.float64)
+    h, w = img.shape[:2]
+    levels = pyramid_num_layers(h, w, min_size, cap)
+    if img.ndim == 3:
+        chans = [compute_gaussian_pyramid(img[..., k], min_size, cap)
+                 for k in range(img.shape[2])]
+        return [np.dstack([ch[l] for ch in chans]) for l in range(len(chans[0]))]
+    pyr = [img]
+    cur = img
+    for _ in range(levels):
+        nxt = pyramid_reduce(cur)
+        if nxt.shape == cur.shape:
+            break
+        pyr.append(nxt)
+        cur = nxt
+    pyr.reverse()
+    assert np.min(pyr[1].shape[:2]) > min_size
+    assert np.min(pyr[1].shape[:2]) <= np.min(pyr[-1].shape[:2])
+    return pyr
+
+
+def initialize_Bp(B_pyr, init_rand=True, seed=0):
+    """img_preprocess.py:66-78, with a seeded RandomState in the same draw order."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for lvl in B_pyr:
+        if init_rand:
+            out.append(rs.rand(int(np.prod(lvl.shape))).reshape(lvl.shape))
+        else:
+            out.append(lvl.copy())
+    return out
+
+
+def pad_img_pair(img_sm, img_lg):
+    """img_preprocess.py:81-83 (1-channel padding)."""
+    return [np.pad(img_sm, PAD_SM, mode='symmetric'),
+            np.pad(img_lg, PAD_LG, mode='symmetric')]
+
+
+def px2ix(pxs, w):
+    """img_preprocess.py:85-87."""
+    return int(pxs[0]) * w + int(pxs[1])
+
+
+def Ap_ix2px(ix, h, w):
+    """img_preprocess.py:96-101 (scalar form)."""
+    rows, cols = ix // w, ix % w
+    img_num = rows // h
+    img_ix = ix - img_num * h * w
+    return (img_ix // w, img_ix % w), img_num
+
+
+def Ap_px2ix(px, img_num, h, w):
+    """img_preprocess.py:104-106."""
+    return ((h * img_num) + int(px[0])) * w + int(px[1])
+
+
+# ----------------------------------------------------------------------------------
+# algorithms.py
+# ----------------------------------------------------------------------------------
+
+def _window(img, rows, cols, pad, k):
+    """k x k window (row-major) around (rows, cols) with symmetric padding.
+    rows/cols: 1-D int arrays of centres.  Returns (len, k*k)."""
+    H, W = img.shape
+    offs = np.arange(-pad, pad + 1)
+    rr = sym_index(rows[:, None] + offs[None, :], H)          # (n, k)
+    cc = sym_index(cols[:, None] + offs[None, :], W)          # (n, k)
+    return img[rr[:, :, None], cc[:, None, :]].reshape(len(rows), k * k)
+
+
+def level_features(img_sm, img_lg, full_feat):
+    """One level of compute_feature_array (algorithms.py:11-47), 1 channel:
+    row (r, c) = [3x3 of coarse at (r//2, c//2) | 5x5 of fine at (r, c)] with
+    symmetric padding; half features keep the first n_half fine samples."""
+    H, W = img_lg.shape
+    rows = np.repeat(np.arange(H), W)
+    cols = np.tile(np.arange(W), H)
+    sm = _window(img_sm, rows // 2, cols // 2, PAD_SM, N_SM)
+    lg = _window(img_lg, rows, cols, PAD_LG, N_LG)
+    if not full_feat:
+        lg = lg[:, :N_HALF]
+    return np.hstack([sm, lg])
+
+
+def compute_feature_array(im_pyr, full_feat):
+    """algorithms.py:11-47 (level 0 is an empty placeholder)."""
+    feats = [[]]
+    for level in range(1, len(im_pyr)):
+        feats.append(level_features(im_pyr[level - 1], im_pyr[level], full_feat))
+    return feats
+
+
+def create_index(A_pyr, Ap_pyr_list, max_levels):
+    """algorithms.py:50-70 without the kd-tree: As[level] = vstack_i [A_full | Ap_i half]."""
+    A_feat = compute_feature_array(A_pyr, True)
+    Ap_feats = [compute_feature_array(p, False) for p in Ap_pyr_list]
+    As = [[]]
+    for level in range(1, max_levels):
+        As.append(np.vstack([np.hstack([A_feat[level], f[level]]) for f in Ap_feats]))
+    return As
+
+
+def best_approximate_match(As_level, BBp_feat):
+    """algorithms.py:73-75 restated as the exact brute-force 1-NN (see module doc)."""
+    d = np.add.reduce((As_level - BBp_feat) ** 2, axis=1)
+    return int(np.argmin(d))
+
+
+def extract_pixel_feature(img_sm, img_lg, px, full_feat):
+    """algorithms.py:78-89 via the symmetric index map (same values as padding)."""
+    r, c = np.array([px[0]]), np.array([px[1]])
+    sm = _window(img_sm, r // 2, c // 2, PAD_SM, N_SM)[0]
+    lg = _window(img_lg, r, c, PAD_LG, N_LG)[0]
+    f = np.hstack([sm, lg])
+    return f if full_feat else f[:N_SM * N_SM + N_HALF]
+
+
+def best_coherence_match(As_level, A_shape, BBp_feat, s, im, px, Bp_w):
+    """algorithms.py:92-130 (int pad_lg)."""
+    assert len(s) >= 1
+    row, col = px
+    A_h, A_w = A_shape
+    rs, ims, prs = [], [], []
+    for rr in range(max(0, row - PAD_LG), row + 1):
+        for cc in range(max(0, col - PAD_LG), min(Bp_w, col + PAD_LG + 1)):
+            rix = rr * Bp_w + cc
+            if rix < row * Bp_w + col:
+                pr = (s[rix][0] + row - rr, s[rix][1] + col - cc)
+                if 0 <= pr[0] < A_h and 0 <= pr[1] < A_w:
+                    rs.append((rr, cc))
+                    ims.append(im[rix])
+                    prs.append(Ap_px2ix(pr, im[rix], A_h, A_w))
+    if not rs:
+        return (-1, -1), 0, (0, 0)
+    x = As_level[np.array(prs)] - BBp_feat
+    rix = int(np.argmin(np.sqrt(np.add.reduce(x * x, axis=1))))
+    r_star = rs[rix]
+    sr = s[r_star[0] * Bp_w + r_star[1]]
+    return (sr[0] + row - r_star[0], sr[1] + col - r_star[1]), ims[rix], r_star
+
+
+def compute_distance(AAp_p, BBp_q, weights):
+    """algorithms.py:133-135: norm((a - q) * w, 2)**2, restated with the pairwise
+    reduce (module doc)."""
+    assert AAp_p.shape == BBp_q.shape == weights.shape
+    v = (AAp_p - BBp_q) * weights
+    s = np.sqrt(np.add.reduce(v * v))
+    return s * s
+
+
+def kappa_factor(level, max_levels, k):
+    """image_analogies.py:206: 1 + 2**(level - max_levels) * k."""
+    return 1 + (2.0 ** (level - max_levels)) * k
+
+
+# ----------------------------------------------------------------------------------
+# image_analogies.py
+# ----------------------------------------------------------------------------------
+
+def synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, As_level,
+                     weights, k):
+    """image_analogies.py:130-220 for ONE level, scanline order, luminance only.
+    Updates Bp_pyr[level] in place; returns (s, im) as int arrays (H*W, 2), (H*W,)."""
+    imh, imw = Bp_pyr[level].shape[:2]
+    A_h, A_w = Ap_pyr_list[0][level].shape[:2]
+    Bfeat = level_features(B_pyr[level - 1], B_pyr[level], True)
+    factor = kappa_factor(level, max_levels, k)
+    s, im = [], []
+    for row in range(imh):
+        for col in range(imw):
+            q = np.hstack([Bfeat[row * imw + col],
+                           extract_pixel_feature(Bp_pyr[level - 1], Bp_pyr[level],
+                                                 (row, col), False)])
+            p_app_ix = best_approximate_match(As_level, q)
+            p_app, i_app = Ap_ix2px(p_app_ix, A_h, A_w)
+            if len(s) < 1:
+                p, i = p_app, i_app
+            else:
+                p_coh, i_coh, _ = best_coherence_match(As_level, (A_h, A_w), q, s, im,
+                                                       (row, col), imw)
+                if p_coh == (-1, -1):
+                    p, i = p_app, i_app
+                else:
+                    d_app = compute_distance(As_level[p_app_ix], q, weights)
+                    d_coh = compute_distance(As_level[Ap_px2ix(p_coh, i_coh, A_h, A_w)],
+                                             q, weights)
+                    if d_coh <= d_app * factor:
+                        p, i = p_coh, i_coh
+                    else:
+                        p, i = p_app, i_app
+            Bp_pyr[level][row, col] = Ap_pyr_list[i][level][p[0], p[1]]
+            s.append((int(p[0]), int(p[1])))
+            im.append(int(i))
+    return np.array(s, dtype=np.int32).reshape(-1, 2), np.array(im, dtype=np.int32)
+
+
+def setup_luminance(A, Ap_list, B, AB_weight=1, remap_lum=False, min_size=N_SM,
+                    cap=None, init_rand=True, seed=0):
+    """image_analogies.py:58-92 from already-scaled luminance images."""
+    if remap_lum:
+        A, Ap_list = remap_luminance(A, Ap_list, B)
+    if not init_rand:
+        B_orig_pyr = compute_gaussian_pyramid(B, min_size, cap)
+    A, B = compress_values(A, B, AB_weight)
+    A_pyr = compute_gaussian_pyramid(A, min_size, cap)
+    B_pyr = compute_gaussian_pyramid(B, min_size, cap)
+    Ap_pyr_list = [compute_gaussian_pyramid(Ap, min_size, cap) for Ap in Ap_list]
+    max_levels = min(len(A_pyr), len(B_pyr))
+    Bp_pyr = initialize_Bp(B_pyr if init_rand else B_orig_pyr, init_rand, seed)
+    return A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels
+
+
+def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, levels=None):
+    """image_analogies.py:119-220: all levels (or the given subset), scanline order.
+    Returns {level: (Bp_level, s, im)}; Bp_pyr is updated in place."""
+    weights = compute_weights(N_SM, N_LG, N_HALF, 1)
+    As = create_index(A_pyr, Ap_pyr_list, max_levels)
+    out = {}
+    for level in range(1, max_levels):
+        if levels is not None and level not in levels:
+            continue
+        s, im = synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr,
+                                 As[level], weights, k)
+        out[level] = (Bp_pyr[level].copy(), s, im)
+    return out

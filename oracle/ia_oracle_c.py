@@ -1,0 +1,116 @@
+"""ctypes binding of the C oracle (oracle/ia_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (as the fast checker) and by bench.py's cpu_baseline leg.  Builds
+``oracle/_build/libia_oracle.so`` with ``make -C oracle`` on first use if missing.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, '_build', 'libia_oracle.so')
+_lib = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+class IaOracleLevel(ctypes.Structure):
+    _fields_ = [
+        ('A_sm', _dp), ('A_lg', _dp), ('Ap_sm', _dp), ('Ap_lg', _dp),
+        ('A_hs', ctypes.c_int), ('A_ws', ctypes.c_int), ('Ah', ctypes.c_int),
+        ('Aw', ctypes.c_int), ('nAp', ctypes.c_int),
+        ('B_sm', _dp), ('B_lg', _dp),
+        ('B_hs', ctypes.c_int), ('B_ws', ctypes.c_int), ('H', ctypes.c_int),
+        ('W', ctypes.c_int),
+        ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
+        ('kappa_factor', ctypes.c_double),
+        ('s', _ip), ('im', _ip), ('max_pixels', ctypes.c_long),
+    ]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            subprocess.check_call(['make', '-s', '-C', _HERE])
+        _lib = ctypes.CDLL(_LIB)
+        _lib.ia_oracle_synth_level.restype = ctypes.c_long
+        _lib.ia_oracle_synth_level.argtypes = [ctypes.POINTER(IaOracleLevel), _dp]
+        _lib.ia_oracle_build_db.restype = _dp
+        _lib.ia_oracle_build_db.argtypes = [ctypes.POINTER(IaOracleLevel)]
+        _lib.ia_oracle_free.argtypes = [ctypes.c_void_p]
+        _lib.ia_oracle_nn.restype = ctypes.c_long
+        _lib.ia_oracle_nn.argtypes = [_dp, ctypes.c_long, _dp, _dp]
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+class LevelJob:
+    """Holds contiguous copies of one level's inputs and the ctypes descriptor."""
+
+    def __init__(self, level, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, weights, kappa_factor,
+                 max_pixels=-1):
+        c = np.ascontiguousarray
+        self.A_sm, self.A_lg = c(A_pyr[level - 1], np.float64), c(A_pyr[level], np.float64)
+        self.Ap_sm = c(np.stack([p[level - 1] for p in Ap_pyr_list]), np.float64)
+        self.Ap_lg = c(np.stack([p[level] for p in Ap_pyr_list]), np.float64)
+        self.B_sm, self.B_lg = c(B_pyr[level - 1], np.float64), c(B_pyr[level], np.float64)
+        self.Bp_sm = c(Bp_pyr[level - 1], np.float64)
+        self.Bp_lg = np.array(Bp_pyr[level], dtype=np.float64, order='C')
+        self.w = c(weights, np.float64)
+        H, W = self.B_lg.shape
+        self.s = np.zeros((H * W, 2), np.int32)
+        self.im = np.zeros(H * W, np.int32)
+        L = IaOracleLevel()
+        L.A_sm, L.A_lg, L.Ap_sm, L.Ap_lg = _d(self.A_sm), _d(self.A_lg), _d(self.Ap_sm), _d(self.Ap_lg)
+        L.A_hs, L.A_ws = self.A_sm.shape
+        L.Ah, L.Aw = self.A_lg.shape
+        L.nAp = len(Ap_pyr_list)
+        L.B_sm, L.B_lg = _d(self.B_sm), _d(self.B_lg)
+        L.B_hs, L.B_ws = self.B_sm.shape
+        L.H, L.W = H, W
+        L.Bp_sm, L.Bp_lg, L.weights = _d(self.Bp_sm), _d(self.Bp_lg), _d(self.w)
+        L.kappa_factor = kappa_factor
+        L.s = self.s.ctypes.data_as(_ip)
+        L.im = self.im.ctypes.data_as(_ip)
+        L.max_pixels = max_pixels
+        self.L = L
+        self.db = None
+
+    def build_db(self):
+        if self.db is None:
+            self.db = lib().ia_oracle_build_db(ctypes.byref(self.L))
+        return self.db
+
+    def run(self, use_db=True):
+        db = self.build_db() if use_db else None
+        n = lib().ia_oracle_synth_level(ctypes.byref(self.L), db)
+        if n < 0:
+            raise MemoryError('oracle db allocation failed')
+        return n
+
+    def __del__(self):
+        if self.db is not None and _lib is not None:
+            _lib.ia_oracle_free(self.db)
+            self.db = None
+
+
+def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels=None):
+    """All levels (scanline order) with the C oracle; updates Bp_pyr in place.
+    Returns {level: (Bp_level, s, im)} like ia_oracle.synthesize."""
+    out = {}
+    for level in range(1, max_levels):
+        if levels is not None and level not in levels:
+            continue
+        f = 1 + (2.0 ** (level - max_levels)) * k
+        job = LevelJob(level, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, weights, f)
+        job.run()
+        Bp_pyr[level] = job.Bp_lg.reshape(Bp_pyr[level].shape)
+        out[level] = (Bp_pyr[level].copy(), job.s.copy(), job.im.copy())
+    return out
