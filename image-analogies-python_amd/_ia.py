@@ -1,0 +1,162 @@
+"""ctypes binding of libia.so (include/ia.h) and device-memory plumbing.
+
+PyTorch is used only as plumbing: device allocations (``torch.empty(..., device='cuda')``),
+the current HIP stream and ``torch.distributed`` for rendezvous.  ``torch`` is imported
+BEFORE libia.so is loaded so that the library's ``libamdhip64.so.7`` / ``librccl.so.1``
+dependencies resolve (by SONAME) to the copies torch already loaded: one HIP runtime per
+process, and torch's stream handles are valid inside libia.
+
+There is no CPU fallback anywhere in the product: every entry point raises if the
+library or a HIP device is missing.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import torch  # noqa: F401  (must precede libia.so, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libia.so')
+HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'ia.h')
+
+IA_D = 55
+IA_DP = 56
+
+_dp = ctypes.c_void_p
+
+
+class IaSrcLevel(ctypes.Structure):
+    _fields_ = [('A_sm', _dp), ('A_lg', _dp), ('Ap_sm', _dp), ('Ap_lg', _dp),
+                ('A_hs', ctypes.c_int), ('A_ws', ctypes.c_int), ('Ah', ctypes.c_int),
+                ('Aw', ctypes.c_int), ('nAp', ctypes.c_int)]
+
+
+class IaMatchArgs(ctypes.Structure):
+    _fields_ = [('src', IaSrcLevel), ('db', _dp), ('row0', ctypes.c_long),
+                ('nrows', ctypes.c_long), ('center', _dp), ('amax', _dp), ('q64', _dp),
+                ('M', ctypes.c_int), ('idx', _dp), ('dist', _dp), ('workspace', _dp)]
+
+
+class IaSynthArgs(ctypes.Structure):
+    _fields_ = [('src', IaSrcLevel), ('db', _dp), ('row0', ctypes.c_long),
+                ('nrows', ctypes.c_long), ('N_total', ctypes.c_long), ('center', _dp),
+                ('amax', _dp), ('B_sm', _dp), ('B_lg', _dp), ('B_hs', ctypes.c_int),
+                ('B_ws', ctypes.c_int), ('H', ctypes.c_int), ('W', ctypes.c_int),
+                ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
+                ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
+                ('workspace', _dp), ('comm', _dp), ('prof', ctypes.POINTER(ctypes.c_double))]
+
+
+_SIGS = {
+    'ia_last_error': (ctypes.c_char_p, []),
+    'ia_version': (ctypes.c_int, []),
+    'ia_rgb_to_yiq': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_long, ctypes.c_double, _dp, _dp, _dp]),
+    'ia_yiq_to_rgb': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp]),
+    'ia_scale_to_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_long, ctypes.c_double, _dp, _dp]),
+    'ia_axpb_f64': (ctypes.c_int, [_dp, ctypes.c_long, ctypes.c_int, ctypes.c_double,
+                                   ctypes.c_double, ctypes.c_double, _dp, _dp]),
+    'ia_pyr_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    'ia_pyr_reduce_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double), _dp, _dp]),
+    'ia_mean_workspace_bytes': (ctypes.c_size_t, [ctypes.c_long]),
+    'ia_mean_f64': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp, _dp]),
+    'ia_level_features_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, _dp, _dp]),
+    'ia_db_rows_padded': (ctypes.c_long, [ctypes.c_long]),
+    'ia_db_chunk_rows': (ctypes.c_int, [ctypes.c_long]),
+    'ia_db_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
+                                   _dp, _dp, _dp, _dp]),
+    'ia_center_fill': (ctypes.c_int, [_dp, ctypes.c_double, ctypes.c_double, _dp]),
+    'ia_match_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_long]),
+    'ia_match_batch': (ctypes.c_int, [ctypes.POINTER(IaMatchArgs), _dp]),
+    'ia_coherence_pick': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp]),
+    'ia_wdist_batch': (ctypes.c_int, [_dp, _dp, _dp, ctypes.c_int, _dp, _dp]),
+    'ia_synth_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                                                   ctypes.c_int]),
+    'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
+    'ia_comm_init': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_void_p)]),
+    'ia_comm_destroy': (ctypes.c_int, [_dp]),
+    'ia_comm_nranks': (ctypes.c_int, [_dp]),
+}
+
+_lib = None
+
+
+def declared_symbols():
+    """Function names declared in include/ia.h (the C-ABI contract)."""
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(ia_[a-z0-9_]+)\s*\(', src)))
+
+
+def lib():
+    """Load libia.so (no fallback: raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                'libia.so not found at %s — build it with `make -C %s/csrc` '
+                '(the MI355X core has no CPU fallback)' % (LIB_PATH, _HERE))
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError('%s failed (%d): %s' % (what, rc, lib().ia_last_error().decode()))
+
+
+def require_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError('a HIP (MI355X) device is required: this image-analogies core has '
+                           'no CPU path')
+    lib()
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def to_dev(a, dtype=torch.float64):
+    """numpy -> contiguous device tensor."""
+    dev = require_device()
+    return torch.as_tensor(np.ascontiguousarray(a)).to(device=dev, dtype=dtype)
+
+
+def workspace(nbytes):
+    dev = require_device()
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+
+
+def src_level(A_sm, A_lg, Ap_sm, Ap_lg):
+    """IaSrcLevel over device tensors (Ap_*: stacked (nAp, h, w))."""
+    s = IaSrcLevel()
+    s.A_sm, s.A_lg, s.Ap_sm, s.Ap_lg = (ptr(A_sm).value, ptr(A_lg).value, ptr(Ap_sm).value,
+                                        ptr(Ap_lg).value)
+    s.A_hs, s.A_ws = A_sm.shape[-2:]
+    s.Ah, s.Aw = A_lg.shape[-2:]
+    s.nAp = Ap_lg.shape[0]
+    return s
+
+
+def mean_dev(t):
+    """Deterministic device mean of a fp64 tensor (ia_mean_f64) -> python float."""
+    t = t.contiguous()
+    out = torch.empty(1, dtype=torch.float64, device=t.device)
+    ws = workspace(lib().ia_mean_workspace_bytes(t.numel()))
+    check(lib().ia_mean_f64(ptr(t), t.numel(), ptr(out), ptr(ws), stream()), 'ia_mean_f64')
+    return float(out.item())

@@ -1,0 +1,219 @@
+"""Feature construction and matching — drop-in for the reference's ``algorithms`` module
+(reference algorithms.py:1-135), computed by libia.so.
+
+    compute_feature_array   ia_level_features_f64 (a9)
+    create_index            per level: resident fp64 source pyramids + the fp32 MFMA
+                            screening database (ia_db_build, a10); returns
+                            (index handles, params, As, As_size) like the reference
+    best_approximate_match  ia_match_batch on one query (a11) — EXACT 1-NN, where the
+                            reference asks FLANN's randomized kd-tree
+    best_coherence_match    candidate bookkeeping as the reference + ia_coherence_pick (a13)
+    compute_distance        ia_wdist_batch (a14)
+
+The synthesis path (image_analogies.py) does not call the per-pixel functions: it runs
+whole levels on device through ``ia_synth_level``.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+import _ia
+
+
+# ---- features -----------------------------------------------------------------------------
+
+def level_features_dev(sm, lg, full_feat):
+    """One level of compute_feature_array on device: (h*w, 34 or 21) fp64."""
+    hs, ws = sm.shape
+    h, w = lg.shape
+    out = torch.empty((h * w, 34 if full_feat else 21), dtype=torch.float64, device=lg.device)
+    _ia.check(_ia.lib().ia_level_features_f64(_ia.ptr(sm), hs, ws, _ia.ptr(lg), h, w,
+                                              1 if full_feat else 0, _ia.ptr(out),
+                                              _ia.stream()), 'ia_level_features_f64')
+    return out
+
+
+def compute_feature_array(im_pyr, c, full_feat):
+    """Per-level [3x3 coarse | 5x5 (or half) fine] neighbourhood rows
+    (algorithms.py:11-47); entry 0 is an empty placeholder as in the reference."""
+    if np.asarray(im_pyr[0]).ndim != 2:
+        raise NotImplementedError('multi-channel features are not supported by this build '
+                                  '(luminance / YIQ matching only)')
+    dev = [_ia.to_dev(p) for p in im_pyr]
+    feats = [[]]
+    for level in range(1, len(im_pyr)):
+        feats.append(level_features_dev(dev[level - 1], dev[level], full_feat).cpu().numpy())
+    return feats
+
+
+# ---- the level database (index) ---------------------------------------------------------------
+
+class LevelIndex:
+    """Device-resident As[level] for rows [row0, row0 + nrows) (a shard when sharded).
+
+    Holds the fp64 A / A' pyramid levels (the exact rescore gathers features straight
+    from them) and the fp32 screening database built by ia_db_build.  Centre = the means
+    of A (34 A dims) and of the A' images (21 A' dims): any centre is exact for the
+    distances; centring only tightens the fp32 screen's error bound.
+    """
+
+    def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg, row0=0, nrows=None):
+        self.A_sm, self.A_lg = A_sm.contiguous(), A_lg.contiguous()
+        self.Ap_sm, self.Ap_lg = Ap_sm.contiguous(), Ap_lg.contiguous()
+        self.src = _ia.src_level(self.A_sm, self.A_lg, self.Ap_sm, self.Ap_lg)
+        self.N = int(Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2])
+        self.row0 = int(row0)
+        self.nrows = self.N - self.row0 if nrows is None else int(nrows)
+        self.shape = (self.N, 55)
+        dev = A_lg.device
+        lib = _ia.lib()
+        st = _ia.stream()
+        mA = _ia.mean_dev(self.A_lg)
+        mAp = _ia.mean_dev(self.Ap_lg)
+        self.center = torch.empty(55, dtype=torch.float64, device=dev)
+        _ia.check(lib.ia_center_fill(_ia.ptr(self.center), mA, mAp, st), 'ia_center_fill')
+        npad = lib.ia_db_rows_padded(self.nrows)
+        self.db = torch.empty((npad, _ia.IA_DP), dtype=torch.float32, device=dev)
+        self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
+        _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
+                                  _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),
+                                  st), 'ia_db_build')
+
+    def match(self, Q):
+        """Exact 1-NN rows (global index, fp64 distance) of queries Q (M x 55)."""
+        dev = self.A_lg.device
+        Q = torch.as_tensor(Q, dtype=torch.float64)
+        if Q.dim() == 1:
+            Q = Q[None]
+        M = Q.shape[0]
+        q = torch.zeros((M, _ia.IA_DP), dtype=torch.float64, device=dev)
+        q[:, :55] = Q.to(dev)
+        idx = torch.empty(M, dtype=torch.int64, device=dev)
+        dist = torch.empty(M, dtype=torch.float64, device=dev)
+        ws = _ia.workspace(_ia.lib().ia_match_workspace_bytes(M, self.nrows))
+        a = _ia.IaMatchArgs()
+        a.src = self.src
+        a.db, a.row0, a.nrows = _ia.ptr(self.db).value, self.row0, self.nrows
+        a.center, a.amax, a.q64, a.M = (_ia.ptr(self.center).value, _ia.ptr(self.amax).value,
+                                        _ia.ptr(q).value, M)
+        a.idx, a.dist, a.workspace = _ia.ptr(idx).value, _ia.ptr(dist).value, _ia.ptr(ws).value
+        _ia.check(_ia.lib().ia_match_batch(ctypes.byref(a), _ia.stream()), 'ia_match_batch')
+        return idx, dist
+
+    def features(self):
+        """The full fp64 As[level] matrix (N x 55), materialised on demand."""
+        A = level_features_dev(self.A_sm, self.A_lg, True)
+        rows = [torch.cat([A, level_features_dev(self.Ap_sm[i], self.Ap_lg[i], False)], 1)
+                for i in range(self.Ap_lg.shape[0])]
+        return torch.cat(rows, 0)
+
+
+class _LazyAs(list):
+    """``As`` of the reference: As[level] is the (N, 55) fp64 feature matrix.  Levels are
+    materialised from the device index only when a caller indexes them."""
+
+    def __init__(self, index):
+        super().__init__([[] for _ in index])
+        self._index = index
+
+    def __getitem__(self, level):
+        cur = super().__getitem__(level)
+        if isinstance(cur, list) and self._index[level] is not None:
+            cur = self._index[level].features().cpu().numpy()
+            super().__setitem__(level, cur)
+        return cur
+
+
+def level_index(A_pyr, Ap_pyr_list, level, row_range=None):
+    """Device index of one level from device pyramids.  row_range(level, N) ->
+    (row0, nrows) selects this rank's shard of the rows."""
+    Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list])
+    Ap_lg = torch.stack([p[level] for p in Ap_pyr_list])
+    N = Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2]
+    r0, nr = (0, N) if row_range is None else row_range(level, N)
+    return LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr)
+
+
+def create_index_dev(A_pyr, Ap_pyr_list, max_levels, row_range=None):
+    """Device index per level 1..max_levels-1 (entry 0 unused)."""
+    return [None] + [level_index(A_pyr, Ap_pyr_list, l, row_range) for l in range(1, max_levels)]
+
+
+def create_index(A_pyr, Ap_pyr_list, c):
+    """Per-level database of [A full | A'_i half] rows (algorithms.py:50-70).  Returns
+    (index, params, As, As_size) in the reference's shape: ``index[level]`` replaces the
+    FLANN object, ``params[level]`` describes it, ``As`` materialises lazily."""
+    dev = _ia.require_device()
+    A_dev = [_ia.to_dev(p) for p in A_pyr]
+    Ap_dev = [[_ia.to_dev(p) for p in pyr] for pyr in Ap_pyr_list]
+    index = create_index_dev(A_dev, Ap_dev, c.max_levels)
+    params = [[]] + [{'algorithm': 'brute', 'exact': True, 'device': str(dev)}
+                     for _ in range(1, c.max_levels)]
+    As_size = [[]] + [index[l].shape for l in range(1, c.max_levels)]
+    return index, params, _LazyAs(index), As_size
+
+
+def best_approximate_match(flann, params, BBp_feat):
+    """Nearest database row of one query (algorithms.py:73-75) — exact."""
+    idx, _ = flann.match(np.asarray(BBp_feat, dtype=np.float64)[None])
+    return int(idx[0].item())
+
+
+def best_approximate_match_batch(flann, Q):
+    """Batched form: nearest rows of M queries (M x 55) -> int64 numpy array."""
+    idx, _ = flann.match(np.asarray(Q, dtype=np.float64))
+    return idx.cpu().numpy()
+
+
+# ---- per-pixel helpers ---------------------------------------------------------------------------
+
+def extract_pixel_feature(padded_pair, px, c, full_feat):
+    """Feature of one pixel from a padded (coarse, fine) pair (algorithms.py:78-89)."""
+    im_sm_padded, im_lg_padded = padded_pair
+    row, col = int(px[0]), int(px[1])
+    rs, cs = row // 2, col // 2
+    f = np.concatenate([
+        im_sm_padded[rs:rs + 2 * c.pad_sm + 1, cs:cs + 2 * c.pad_sm + 1].ravel(),
+        im_lg_padded[row:row + 2 * c.pad_lg + 1, col:col + 2 * c.pad_lg + 1].ravel()])
+    return f if full_feat else f[:c.num_ch * (c.n_sm * c.n_sm + c.n_half)]
+
+
+def best_coherence_match(As, A_shape, BBp_feat, s, im, px, Bp_w, c):
+    """Coherence candidate p = s(r*) + (q - r*) over the causal 5x5 half window
+    (algorithms.py:92-130); the distance argmin runs on device."""
+    assert len(s) >= 1
+    A_h, A_w = A_shape
+    row, col = int(px[0]), int(px[1])
+    q_ix = row * Bp_w + col
+    cands, rows = [], []
+    for rr in range(max(0, row - c.pad_lg), row + 1):
+        for cc in range(max(0, col - c.pad_lg), min(Bp_w, col + c.pad_lg + 1)):
+            r_ix = rr * Bp_w + cc
+            if r_ix >= q_ix:
+                continue
+            pr = (int(s[r_ix][0]) + row - rr, int(s[r_ix][1]) + col - cc)
+            if 0 <= pr[0] < A_h and 0 <= pr[1] < A_w:
+                img = int(im[r_ix])
+                cands.append(((rr, cc), img))
+                rows.append(((A_h * img) + pr[0]) * A_w + pr[1])
+    if not cands:
+        return (-1, -1), 0, (0, 0)
+    feats = _ia.to_dev(np.asarray(As[np.array(rows)], dtype=np.float64))
+    q = _ia.to_dev(np.asarray(BBp_feat, dtype=np.float64))
+    out = torch.empty(1, dtype=torch.int32, device=q.device)
+    _ia.check(_ia.lib().ia_coherence_pick(_ia.ptr(feats), len(rows), _ia.ptr(q), _ia.ptr(out),
+                                          _ia.stream()), 'ia_coherence_pick')
+    (rr, cc), img = cands[int(out.item())]
+    sr = s[rr * Bp_w + cc]
+    return np.array([int(sr[0]) + row - rr, int(sr[1]) + col - cc]), img, np.array([rr, cc])
+
+
+def compute_distance(AAp_p, BBp_q, weights):
+    """Weighted squared distance |(a - q) * w|^2 (algorithms.py:133-135)."""
+    assert AAp_p.shape == BBp_q.shape == weights.shape
+    a, q, w = (_ia.to_dev(np.asarray(x, dtype=np.float64)) for x in (AAp_p, BBp_q, weights))
+    out = torch.empty(1, dtype=torch.float64, device=a.device)
+    _ia.check(_ia.lib().ia_wdist_batch(_ia.ptr(a), _ia.ptr(q), _ia.ptr(w), 1, _ia.ptr(out),
+                                       _ia.stream()), 'ia_wdist_batch')
+    return float(out.item())

@@ -1,0 +1,186 @@
+// ia_features.hip — neighbourhood feature construction.
+//   * compute_feature_array (algorithms.py:11-47) for the API,
+//   * the fp32 screening database (algorithms.py:50-70 As[level], centred, MFMA
+//     operand order, squared norm folded in as element 55),
+//   * per-wave query rows (image_analogies.py:166-168: B full | B' half) in fp64 for the
+//     exact rescore and in fp32 MFMA order for the screen.
+// Feature values are pure gathers (exact); centring and fp32 rounding only feed the
+// screen, whose error bound is accounted for in ia_match.hip.
+#include "ia_common.h"
+#include "ia_internal.h"
+
+namespace ia {
+
+__global__ void k_level_features(ImgPair p, int full, double *out) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)p.h * p.w) return;
+    const int r = (int)(i / p.w), c = (int)(i - (long)r * p.w);
+    if (full) {
+        double *o = out + i * 34;
+        emit_pixel<true>(p, r, c, 0, [&](int k, double v) { o[k] = v; });
+    } else {
+        double *o = out + i * 21;
+        emit_pixel<false>(p, r, c, 0, [&](int k, double v) { o[k] = v; });
+    }
+}
+
+// MFMA operand order of element k = 2s + h: position h*28 + s (see ia_match.hip).
+__device__ __forceinline__ int perm56(int k) { return (k & 1) * 28 + (k >> 1); }
+
+// One thread per database row: 55 gathers, centre, fp32, permute; 224 B per row written
+// through LDS so that the block's stores are contiguous 16-B vectors.
+__global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nrows, long npad,
+                                                  const double *__restrict__ center,
+                                                  float *__restrict__ db, float *amax) {
+    __shared__ float tile[256 * IA_DP];
+    __shared__ float redmax[4];
+    const long lr = (long)blockIdx.x * 256 + threadIdx.x;  // local row
+    float *my = tile + threadIdx.x * IA_DP;
+    float nrm = 0.f;
+    if (lr < nrows) {
+        ImgPair ap; int r, c;
+        src.locate(row0 + lr, ap, r, c);
+        double n2 = 0.0;
+        emit_feature(src.A, ap, r, c, [&](int k, double v) {
+            const double d = v - center[k];
+            n2 += d * d;
+            my[perm56(k)] = (float)d;
+        });
+        my[perm56(55)] = (float)n2;
+        nrm = (float)sqrt(n2);
+    } else if (lr < npad) {
+        for (int k = 0; k < 55; ++k) my[perm56(k)] = 0.f;
+        my[perm56(55)] = 1e30f;  // sentinel row: screen value 1e30, never a candidate
+    }
+    for (int o = 32; o > 0; o >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, o));
+    if ((threadIdx.x & 63) == 0) redmax[threadIdx.x >> 6] = nrm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = fmaxf(fmaxf(redmax[0], redmax[1]), fmaxf(redmax[2], redmax[3]));
+        atomicMax(reinterpret_cast<unsigned int *>(amax), __float_as_uint(m));
+    }
+    // coalesced copy-out: rows [blockIdx*256, +256) are contiguous in db
+    const long base = (long)blockIdx.x * 256;
+    const long rows_here = npad - base < 256 ? npad - base : 256;
+    const long nvec = rows_here * IA_DP / 4;
+    float4 *dst = reinterpret_cast<float4 *>(db + base * IA_DP);
+    const float4 *srcv = reinterpret_cast<const float4 *>(tile);
+    for (long i = threadIdx.x; i < nvec; i += 256) dst[i] = srcv[i];
+}
+
+__global__ void k_center_fill(double *c, double mA, double mAp) {
+    const int k = threadIdx.x;
+    if (k < IA_D) c[k] = k < 34 ? mA : mAp;
+}
+
+// Query rows for the pixels of wave t (y = y_lo + m, x = t - 3y):
+// q64[m][k] (fp64 feature), qp[m][perm56(k)] = fp32(-2 (q_k - c_k)), qp[..55] = 1,
+// nq[m] = |q - c|^2.  One 64-lane wave per query, lane = feature index.
+__global__ __launch_bounds__(64) void k_query_wave(ImgPair B, ImgPair Bp, int t, int y_lo,
+                                                   const double *__restrict__ center,
+                                                   double *__restrict__ q64,
+                                                   float *__restrict__ qp,
+                                                   double *__restrict__ nq) {
+    const int m = blockIdx.x;
+    const int y = y_lo + m, x = t - 3 * y;
+    const int lane = threadIdx.x;
+    double v = 0.0;
+    // lane-parallel gather: each lane picks its own element of the 55
+    if (lane < 34) {
+        const bool coarse = lane < 9;
+        const int tt = coarse ? lane : lane - 9;
+        v = coarse ? B.sm[(long)symi((y >> 1) + tt / 3 - 1, B.hs) * B.ws + symi((x >> 1) + tt % 3 - 1, B.ws)]
+                   : B.lg[(long)symi(y + tt / 5 - 2, B.h) * B.w + symi(x + tt % 5 - 2, B.w)];
+    } else if (lane < 55) {
+        const bool coarse = lane < 43;
+        const int tt = coarse ? lane - 34 : lane - 43;
+        v = coarse ? Bp.sm[(long)symi((y >> 1) + tt / 3 - 1, Bp.hs) * Bp.ws + symi((x >> 1) + tt % 3 - 1, Bp.ws)]
+                   : Bp.lg[(long)symi(y + tt / 5 - 2, Bp.h) * Bp.w + symi(x + tt % 5 - 2, Bp.w)];
+    }
+    double d = 0.0;
+    if (lane < 55) {
+        q64[(long)m * IA_DP + lane] = v;
+        d = v - center[lane];
+        qp[(long)m * IA_DP + perm56(lane)] = -2.0f * (float)d;
+    } else if (lane == 55) {
+        q64[(long)m * IA_DP + 55] = 0.0;
+        qp[(long)m * IA_DP + perm56(55)] = 1.0f;
+    }
+    double d2 = d * d;
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+    if (lane == 0) nq[m] = d2;
+}
+
+// Query rows from caller-provided fp64 features (ia_match_batch).
+__global__ __launch_bounds__(64) void k_query_rows(const double *__restrict__ qin, int M,
+                                                   const double *__restrict__ center,
+                                                   float *__restrict__ qp,
+                                                   double *__restrict__ nq) {
+    const int m = blockIdx.x;
+    const int lane = threadIdx.x;
+    double d = 0.0;
+    if (lane < 55) {
+        d = qin[(long)m * IA_DP + lane] - center[lane];
+        qp[(long)m * IA_DP + perm56(lane)] = -2.0f * (float)d;
+    } else if (lane == 55) {
+        qp[(long)m * IA_DP + perm56(55)] = 1.0f;
+    }
+    double d2 = d * d;
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+    if (lane == 0) nq[m] = d2;
+}
+
+int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
+                      const double *center, double *q64, float *qp, double *nq,
+                      hipStream_t st) {
+    k_query_wave<<<M, 64, 0, st>>>(B, Bp, t, y_lo, center, q64, qp, nq);
+    IA_LAUNCH_CHECK("k_query_wave");
+    return IA_OK;
+}
+
+int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
+                      hipStream_t st) {
+    k_query_rows<<<M, 64, 0, st>>>(qin, M, center, qp, nq);
+    IA_LAUNCH_CHECK("k_query_rows");
+    return IA_OK;
+}
+
+}  // namespace ia
+
+using namespace ia;
+
+extern "C" {
+
+int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, int h, int w,
+                          int full, double *out, void *stream) {
+    IA_ARG(sm && lg && out && hs > 0 && ws > 0 && h > 0 && w > 0, "ia_level_features_f64: bad args");
+    ImgPair p{sm, lg, hs, ws, h, w};
+    long n = (long)h * w;
+    k_level_features<<<(unsigned)((n + 255) / 256), 256, 0, S(stream)>>>(p, full, out);
+    IA_LAUNCH_CHECK("k_level_features");
+    return IA_OK;
+}
+
+int ia_db_chunk_rows(long nrows) { return db_chunk_rows(nrows); }
+long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
+
+int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                float *db, float *amax, void *stream) {
+    IA_ARG(src && center && db && amax && nrows > 0 && row0 >= 0, "ia_db_build: bad args");
+    IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build: rows out of range");
+    const long npad = db_rows_padded(nrows);
+    DbSrc d = make_dbsrc(*src);
+    k_db_build<<<(unsigned)((npad + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, npad,
+                                                                     center, db, amax);
+    IA_LAUNCH_CHECK("k_db_build");
+    return IA_OK;
+}
+
+int ia_center_fill(double *center, double mA, double mAp, void *stream) {
+    IA_ARG(center, "ia_center_fill: bad args");
+    k_center_fill<<<1, 64, 0, S(stream)>>>(center, mA, mAp);
+    IA_LAUNCH_CHECK("k_center_fill");
+    return IA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// ia_internal.h — declarations shared between libia.so translation units.
+#pragma once
+#include "ia_common.h"
+
+namespace ia {
+
+// ---- database chunking (shared by ia_db_build and the screen) -------------------
+// A screen workgroup owns one chunk of CH rows: 4 waves x (CH/4) rows, 32-row tiles.
+// CH is chosen so a DB produces ~1024 chunks (>= 4 workgroups per CU per query group).
+constexpr int SCREEN_K = 4;            // candidates kept per (query, chunk)
+constexpr int TARGET_CHUNKS = 1024;
+
+static inline int db_chunk_rows(long nrows) {
+    long tpw = (nrows + (long)TARGET_CHUNKS * 128 - 1) / ((long)TARGET_CHUNKS * 128);
+    if (tpw < 1) tpw = 1;
+    if (tpw > 64) tpw = 64;
+    return (int)(128 * tpw);
+}
+static inline long db_nchunks(long nrows) {
+    const long ch = db_chunk_rows(nrows);
+    return (nrows + ch - 1) / ch;
+}
+static inline long db_rows_padded(long nrows) { return db_nchunks(nrows) * db_chunk_rows(nrows); }
+
+struct Cand {            // one screen candidate: fp32 screen value + local row
+    float e;
+    int idx;
+};
+struct Best {            // exact winner of a (query, shard): fp64 distance + global row
+    double d;
+    long long idx;
+};
+
+// query-group split of M queries (32-query tiles, NQ tiles per group)
+struct QSplit {
+    int nq, groups, rows_pad;
+};
+static inline QSplit qsplit(int M) {
+    const int T = (M + 31) / 32;
+    QSplit s;
+    if (T <= 3) {
+        s.nq = T; s.groups = 1;
+    } else {
+        int bestnq = 3, bestpad = 1 << 30;
+        for (int nq = 3; nq >= 2; --nq) {
+            int pad = (T + nq - 1) / nq * nq;
+            if (pad < bestpad) { bestpad = pad; bestnq = nq; }
+        }
+        s.nq = bestnq; s.groups = (T + bestnq - 1) / bestnq;
+    }
+    s.rows_pad = s.nq * s.groups * 32;
+    return s;
+}
+static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + 4) * 32; }
+
+// ---- launchers ------------------------------------------------------------------
+int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
+                      const double *center, double *q64, float *qp, double *nq,
+                      hipStream_t st);
+int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
+                      hipStream_t st);
+// screen of M queries (qp) against nrows DB rows -> cand[M][nchunks][SCREEN_K]
+int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
+                  hipStream_t st);
+// exact rescore of the screen's candidates -> best[M]; stats[0..2] += (#cand, #overflow
+// chunks, #full scans) when stats != nullptr
+int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int M,
+                 const double *q64, const double *nq, const float *amax, Best *best,
+                 unsigned long long *stats, hipStream_t st);
+
+}  // namespace ia

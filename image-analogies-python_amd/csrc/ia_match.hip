@@ -1,0 +1,416 @@
+// ia_match.hip — the brute-force matcher (the hot kernel).
+//
+// best_approximate_match (algorithms.py:73-75, FLANN kd-tree in the reference) becomes
+// an EXACT 1-NN over the level database As[level] in two stages:
+//
+//  1. k_screen (MFMA-bound): e(q, a) = |a'|^2 - 2 a'.q' with a' = a - c, q' = q - c
+//     (c = screening centre), computed as ONE fp32 contraction of length 56 on
+//     v_mfma_f32_32x32x2_f32: DB row = [a'_0..a'_54, |a'|^2], query = [-2q'_0..-2q'_54, 1].
+//     Queries are the stationary operand (kept in VGPRs for the whole chunk), DB rows
+//     stream through in 32-row tiles.  Accumulator lane = query, registers = 16 DB rows,
+//     so each lane keeps its own top-K (K=4) of (e, row) over the rows it sees; the
+//     block merges 8 such lists per query through LDS and writes SCREEN_K candidates per
+//     (query, chunk).
+//  2. k_merge (latency-bound, one workgroup per query): e + |q'|^2 approximates the true
+//     distance D within eps_q = 70 u32 (2 Amax |q'| + Amax^2) (fp32 conversion of both
+//     operands + a 56-term fma chain, worst case; Amax = max row |a'|).  Every row whose
+//     D could be the minimum therefore has e <= e_min + 2 eps_q; all such rows are
+//     re-scored in fp64 with the oracle's exact pairwise-8 sum, gathering the row's 55
+//     features straight from the fp64 pyramids.  A chunk whose K-th candidate is itself
+//     inside the window may have dropped candidates: it is re-scanned exactly.  Ties
+//     break to the lowest row index (np.argmin).  The result is bit-identical to the
+//     oracle's brute force for any input.
+#include "ia_internal.h"
+
+#include <float.h>
+
+namespace ia {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// K = 4 sorted insert of (v, idx), v < t[3] known (branch-free).
+__device__ __forceinline__ void topk_insert(float (&t)[SCREEN_K], int (&ti)[SCREEN_K], float v,
+                                            int idx) {
+    const bool c0 = v < t[0], c1 = v < t[1], c2 = v < t[2];
+    const float n3 = c2 ? t[2] : v;
+    const int i3 = c2 ? ti[2] : idx;
+    const float n2 = c1 ? t[1] : (c2 ? v : t[2]);
+    const int i2 = c1 ? ti[1] : (c2 ? idx : ti[2]);
+    const float n1 = c0 ? t[0] : (c1 ? v : t[1]);
+    const int i1 = c0 ? ti[0] : (c1 ? idx : ti[1]);
+    t[0] = c0 ? v : t[0];
+    ti[0] = c0 ? idx : ti[0];
+    t[1] = n1; ti[1] = i1;
+    t[2] = n2; ti[2] = i2;
+    t[3] = n3; ti[3] = i3;
+}
+
+// grid: (nchunks rounded up to 8) x groups workgroups, XCD-aware: all query groups of a
+// chunk share blockIdx % 8 (one XCD under round-robin dispatch) so the chunk's rows are
+// fetched from HBM once and re-read from that XCD's L2.
+template <int NQ>
+__global__ __launch_bounds__(256) void k_screen(const float *__restrict__ db, int nchunks,
+                                                int ch, const float *__restrict__ qp, int M,
+                                                int groups, Cand *__restrict__ cand) {
+    __shared__ float le[NQ * 32][8][SCREEN_K];
+    __shared__ int li[NQ * 32][8][SCREEN_K];
+
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int j = lane & 31, h = lane >> 5;
+
+    // stationary query fragments: lane (j, h) holds B[k = 2s + h][col j], s = 0..27
+    float bq[NQ][28];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        const float4 *p = reinterpret_cast<const float4 *>(
+            qp + (long)((group * NQ + qt) * 32 + j) * IA_DP + h * 28);
+#pragma unroll
+        for (int v = 0; v < 7; ++v) {
+            const float4 x = p[v];
+            bq[qt][4 * v] = x.x; bq[qt][4 * v + 1] = x.y;
+            bq[qt][4 * v + 2] = x.z; bq[qt][4 * v + 3] = x.w;
+        }
+    }
+
+    float te[NQ][SCREEN_K];
+    int ti[NQ][SCREEN_K];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) { te[qt][k] = FLT_MAX; ti[qt][k] = -1; }
+
+    const int rows_per_wave = ch >> 2;
+    const int ntile = rows_per_wave >> 5;
+    const long row_begin = (long)chunk * ch + wv * rows_per_wave;
+    // lane (j, h) streams DB row (tile*32 + j), elements k = 2s + h
+    const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
+    constexpr int TILE_VEC = 32 * IA_DP / 4;   // float4s per 32-row tile
+
+    float4 an[7];
+#pragma unroll
+    for (int v = 0; v < 7; ++v) an[v] = dp[v];
+
+    for (int tile = 0; tile < ntile; ++tile) {
+        float4 a4[7];
+#pragma unroll
+        for (int v = 0; v < 7; ++v) a4[v] = an[v];
+        if (tile + 1 < ntile) {
+            const float4 *np_ = dp + (long)(tile + 1) * TILE_VEC;
+#pragma unroll
+            for (int v = 0; v < 7; ++v) an[v] = np_[v];
+        }
+        floatx16 acc[NQ];
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
+#pragma unroll
+        for (int v = 0; v < 7; ++v) {
+            const float av[4] = {a4[v].x, a4[v].y, a4[v].z, a4[v].w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt)
+                    acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bq[qt][4 * v + u],
+                                                                   acc[qt], 0, 0, 0);
+        }
+        // epilogue: C[row i][col j] at lane (j, h), reg r: i = (r&3) + 8(r>>2) + 4h
+        const int rbase = (int)(row_begin - (long)chunk * ch) + tile * 32 + 4 * h;
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt) {
+            float mn = acc[qt][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) mn = fminf(mn, acc[qt][r]);
+            if (mn < te[qt][SCREEN_K - 1]) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[qt][r];
+                    if (v < te[qt][SCREEN_K - 1])
+                        topk_insert(te[qt], ti[qt], v, rbase + (r & 3) + 8 * (r >> 2));
+                }
+            }
+        }
+    }
+
+    // merge the 8 per-lane lists of each query (4 waves x 2 row halves) through LDS
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) {
+            le[qt * 32 + j][wv * 2 + h][k] = te[qt][k];
+            li[qt * 32 + j][wv * 2 + h][k] = ti[qt][k];
+        }
+    __syncthreads();
+    if (tid < NQ * 32) {
+        const int qg = group * NQ * 32 + tid;
+        if (qg < M) {
+            float be[SCREEN_K];
+            int bi[SCREEN_K];
+#pragma unroll
+            for (int k = 0; k < SCREEN_K; ++k) { be[k] = FLT_MAX; bi[k] = -1; }
+            for (int l = 0; l < 8; ++l)
+#pragma unroll
+                for (int k = 0; k < SCREEN_K; ++k) {
+                    const float v = le[tid][l][k];
+                    if (v < be[SCREEN_K - 1]) topk_insert(be, bi, v, li[tid][l][k]);
+                }
+            Cand *o = cand + ((long)qg * nchunks + chunk) * SCREEN_K;
+            const int cbase = chunk * ch;
+#pragma unroll
+            for (int k = 0; k < SCREEN_K; ++k) o[k] = Cand{be[k], bi[k] < 0 ? -1 : cbase + bi[k]};
+        }
+    }
+}
+
+int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
+                  hipStream_t st) {
+    const int ch = db_chunk_rows(nrows);
+    const long nchunks = db_nchunks(nrows);
+    const QSplit qs = qsplit(M);
+    const long nblocks = ((nchunks + 7) / 8) * 8 * qs.groups;
+    IA_ARG(nblocks < (1L << 31), "screen grid too large");
+    switch (qs.nq) {
+#define IA_SCREEN_CASE(N)                                                                     \
+    case N:                                                                                   \
+        k_screen<N><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, qp, M, qs.groups, \
+                                                       cand);                                 \
+        break;
+        IA_SCREEN_CASE(1)
+        IA_SCREEN_CASE(2)
+        IA_SCREEN_CASE(3)
+#undef IA_SCREEN_CASE
+        default: set_error("bad query split"); return IA_E_ARG;
+    }
+    IA_LAUNCH_CHECK("k_screen");
+    return IA_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// exact merge / rescore: one 256-thread workgroup per query
+// ---------------------------------------------------------------------------------
+constexpr int MERGE_CAP = 2048;     // candidate rows held in LDS
+constexpr int MERGE_OCAP = 256;     // overflow chunks held in LDS
+
+__device__ __forceinline__ void best_update(double &bd, long long &bi, double d, long long i) {
+    if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
+}
+
+__global__ __launch_bounds__(256) void k_merge(DbSrc src, long row0, long nrows, int nchunks,
+                                               int ch, const Cand *__restrict__ cand,
+                                               const double *__restrict__ q64,
+                                               const double *__restrict__ nq,
+                                               const float *__restrict__ amax,
+                                               Best *__restrict__ best,
+                                               unsigned long long *stats) {
+    __shared__ int clist[MERGE_CAP];
+    __shared__ int olist[MERGE_OCAP];
+    __shared__ int ccount, ocount;
+    __shared__ float redf[4];
+    __shared__ double redd[4];
+    __shared__ long long redi[4];
+    __shared__ double qs[IA_DP];
+
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x;
+    const Cand *cq = cand + (long)q * nchunks * SCREEN_K;
+    if (tid < IA_DP) qs[tid] = q64[(long)q * IA_DP + tid];
+    if (tid == 0) { ccount = 0; ocount = 0; }
+
+    float emin = FLT_MAX;
+    for (int c = tid; c < nchunks; c += 256) emin = fminf(emin, cq[(long)c * SCREEN_K].e);
+    for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
+    if ((tid & 63) == 0) redf[tid >> 6] = emin;
+    __syncthreads();
+    emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
+
+    const double A = (double)amax[0];
+    const double nqq = nq[q];
+    const double eps = 70.0 * 5.9604644775390625e-08 * (2.0 * A * sqrt(nqq) + A * A);
+    const double T = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
+
+    for (int c = tid; c < nchunks; c += 256) {
+        const Cand *e = cq + (long)c * SCREEN_K;
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) {
+            if ((double)e[k].e <= T && e[k].idx >= 0 && e[k].idx < nrows) {
+                const int pos = atomicAdd(&ccount, 1);
+                if (pos < MERGE_CAP) clist[pos] = e[k].idx;
+            }
+        }
+        if ((double)e[SCREEN_K - 1].e <= T) {
+            const int pos = atomicAdd(&ocount, 1);
+            if (pos < MERGE_OCAP) olist[pos] = c;
+        }
+    }
+    __syncthreads();
+    const int nc = ccount, no = ocount;
+    const bool full = nc > MERGE_CAP || no > MERGE_OCAP;
+
+    double bd = INFINITY;
+    long long bi = 0x7fffffffffffffffLL;
+    if (full) {
+        for (long lr = tid; lr < nrows; lr += 256)
+            best_update(bd, bi, row_dist2(src, row0 + lr, qs), row0 + lr);
+    } else {
+        for (int i = tid; i < nc; i += 256) {
+            const long ix = row0 + clist[i];
+            best_update(bd, bi, row_dist2(src, ix, qs), ix);
+        }
+        for (int o = 0; o < no; ++o) {
+            const long lo = (long)olist[o] * ch;
+            const long hi = lo + ch < nrows ? lo + ch : nrows;
+            for (long lr = lo + tid; lr < hi; lr += 256)
+                best_update(bd, bi, row_dist2(src, row0 + lr, qs), row0 + lr);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o);
+        const long long oi = __shfl_xor(bi, o);
+        best_update(bd, bi, od, oi);
+    }
+    if ((tid & 63) == 0) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w) best_update(bd, bi, redd[w], redi[w]);
+        best[q] = Best{bd, bi};
+        if (stats) {
+            atomicAdd(&stats[0], (unsigned long long)nc);
+            atomicAdd(&stats[1], (unsigned long long)no);
+            atomicAdd(&stats[2], full ? 1ULL : 0ULL);
+        }
+    }
+}
+
+int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int M,
+                 const double *q64, const double *nq, const float *amax, Best *best,
+                 unsigned long long *stats, hipStream_t st) {
+    const int ch = db_chunk_rows(nrows);
+    const long nchunks = db_nchunks(nrows);
+    k_merge<<<M, 256, 0, st>>>(src, row0, nrows, (int)nchunks, ch, cand, q64, nq, amax, best,
+                               stats);
+    IA_LAUNCH_CHECK("k_merge");
+    return IA_OK;
+}
+
+__global__ void k_split_best(const Best *b, int M, int64_t *idx, double *dist) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    if (idx) idx[i] = b[i].idx;
+    if (dist) dist[i] = b[i].d;
+}
+
+// ---------------------------------------------------------------------------------
+// per-pixel API helpers (algorithms.py:92-135)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_coherence_pick(const double *rows, int n,
+                                                       const double *q, int32_t *out) {
+    double bd = INFINITY;
+    long long bi = 0x7fffffffffffffffLL;
+    for (int i = threadIdx.x; i < n; i += 64) {
+        Pw55 pw;
+#pragma unroll
+        for (int k = 0; k < IA_D; ++k) {
+            const double x = rows[(long)i * IA_D + k] - q[k];
+            pw.feed(k, x * x);
+        }
+        best_update(bd, bi, sqrt(pw.res), i);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o);
+        const long long oi = __shfl_xor(bi, o);
+        best_update(bd, bi, od, oi);
+    }
+    if (threadIdx.x == 0) out[0] = (int32_t)bi;
+}
+
+__global__ void k_wdist(const double *a, const double *q, const double *w, int n,
+                        double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Pw55 pw;
+#pragma unroll
+    for (int k = 0; k < IA_D; ++k) {
+        const double x = (a[(long)i * IA_D + k] - q[(long)i * IA_D + k]) * w[k];
+        pw.feed(k, x * x);
+    }
+    const double s = sqrt(pw.res);
+    out[i] = s * s;
+}
+
+}  // namespace ia
+
+using namespace ia;
+
+extern "C" {
+
+static constexpr int MATCH_BATCH = 384;
+
+size_t ia_match_workspace_bytes(int M, long nrows) {
+    const int mb = M < MATCH_BATCH ? M : MATCH_BATCH;
+    const int qr = qrows_alloc(mb);
+    size_t b = 0;
+    b += align_up((size_t)qr * IA_DP * sizeof(float), 256);                        // qp
+    b += align_up((size_t)qr * sizeof(double), 256);                               // nq
+    b += align_up((size_t)qr * db_nchunks(nrows) * SCREEN_K * sizeof(Cand), 256);  // cand
+    b += align_up((size_t)qr * sizeof(Best), 256);                                 // best
+    return b;
+}
+
+int ia_match_batch(const IaMatchArgs *a, void *stream) {
+    IA_ARG(a && a->db && a->q64 && a->center && a->amax && a->workspace && a->M >= 0 &&
+               a->nrows > 0,
+           "ia_match_batch: bad args");
+    if (a->M == 0) return IA_OK;
+    hipStream_t st = S(stream);
+    const int mb = a->M < MATCH_BATCH ? a->M : MATCH_BATCH;
+    const int qr = qrows_alloc(mb);
+    char *w = reinterpret_cast<char *>(a->workspace);
+    float *qp = reinterpret_cast<float *>(w);
+    w += align_up((size_t)qr * IA_DP * sizeof(float), 256);
+    double *nq = reinterpret_cast<double *>(w);
+    w += align_up((size_t)qr * sizeof(double), 256);
+    Cand *cand = reinterpret_cast<Cand *>(w);
+    w += align_up((size_t)qr * db_nchunks(a->nrows) * SCREEN_K * sizeof(Cand), 256);
+    Best *best = reinterpret_cast<Best *>(w);
+    IA_HIP(hipMemsetAsync(qp, 0, (size_t)qr * IA_DP * sizeof(float), st));
+    const DbSrc src = make_dbsrc(a->src);
+    for (int m0 = 0; m0 < a->M; m0 += MATCH_BATCH) {
+        const int M = a->M - m0 < MATCH_BATCH ? a->M - m0 : MATCH_BATCH;
+        const double *q = a->q64 + (long)m0 * IA_DP;
+        int rc;
+        if ((rc = launch_query_rows(q, M, a->center, qp, nq, st))) return rc;
+        if ((rc = launch_screen(a->db, a->nrows, qp, M, cand, st))) return rc;
+        if ((rc = launch_merge(src, a->row0, a->nrows, cand, M, q, nq, a->amax, best, nullptr,
+                               st)))
+            return rc;
+        k_split_best<<<(M + 255) / 256, 256, 0, st>>>(best, M, a->idx ? a->idx + m0 : nullptr,
+                                                      a->dist ? a->dist + m0 : nullptr);
+        IA_LAUNCH_CHECK("k_split_best");
+    }
+    return IA_OK;
+}
+
+int ia_coherence_pick(const double *rows, int n, const double *q, int32_t *out, void *stream) {
+    IA_ARG(rows && q && out && n > 0, "ia_coherence_pick: bad args");
+    k_coherence_pick<<<1, 64, 0, S(stream)>>>(rows, n, q, out);
+    IA_LAUNCH_CHECK("k_coherence_pick");
+    return IA_OK;
+}
+
+int ia_wdist_batch(const double *a, const double *q, const double *w, int n, double *out,
+                   void *stream) {
+    IA_ARG(a && q && w && out && n >= 0, "ia_wdist_batch: bad args");
+    if (n == 0) return IA_OK;
+    k_wdist<<<(n + 63) / 64, 64, 0, S(stream)>>>(a, q, w, n, out);
+    IA_LAUNCH_CHECK("k_wdist");
+    return IA_OK;
+}
+
+}  // extern "C"

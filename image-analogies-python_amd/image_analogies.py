@@ -1,0 +1,223 @@
+"""Image Analogies driver — drop-in for the reference's ``image_analogies`` module
+(reference image_analogies.py:17-268), running the whole B' synthesis on an MI355X.
+
+``image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False)`` keeps
+the reference's signature, parameters (``config`` module as ``c``), outputs
+(``level_%d_color.jpg`` per level and ``<name>.jpg``, ``metadata.txt``) and printed timings.
+Underneath, every level is synthesised by ``ia_synth_level`` (skewed wavefront,
+exact matcher) with the pyramids, databases and index maps resident in HBM.
+
+``synthesize_dev`` is the device-level entry used by bench.py and the parity tests:
+device pyramids in, per-level (s, im) index maps out, B' pyramid updated in place;
+with ``comm`` it shards every level's database over the ranks (RCCL all-gather per wave).
+"""
+import ctypes
+import os
+import time
+import warnings
+
+import numpy as np
+import torch
+
+import _ia
+import algorithms
+import img_preprocess as ip
+from config import save_metadata, setup_vars
+
+
+def kappa_factor(level, max_levels, k):
+    """1 + 2**(level - max_levels) * kappa (image_analogies.py:206)."""
+    return 1 + (2.0 ** (level - max_levels)) * k
+
+
+def shard_rows(N, rank, nranks):
+    """Contiguous row range of one rank: [N*r/G, N*(r+1)/G)."""
+    r0 = N * rank // nranks
+    return r0, N * (rank + 1) // nranks - r0
+
+
+def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
+                         comm=None, prof=None):
+    """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32."""
+    dev = B_lg.device
+    H, W = B_lg.shape
+    s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
+    im = torch.empty(H * W, dtype=torch.int32, device=dev)
+    nranks = _ia.lib().ia_comm_nranks(comm) if comm else 1
+    ws = _ia.workspace(_ia.lib().ia_synth_workspace_bytes(H, W, index.nrows, nranks))
+    a = _ia.IaSynthArgs()
+    a.src = index.src
+    a.db, a.row0, a.nrows, a.N_total = _ia.ptr(index.db).value, index.row0, index.nrows, index.N
+    a.center, a.amax = _ia.ptr(index.center).value, _ia.ptr(index.amax).value
+    a.B_sm, a.B_lg = _ia.ptr(B_sm).value, _ia.ptr(B_lg).value
+    a.B_hs, a.B_ws = B_sm.shape
+    a.H, a.W = H, W
+    a.Bp_sm, a.Bp_lg = _ia.ptr(Bp_sm).value, _ia.ptr(Bp_lg).value
+    a.weights = _ia.ptr(weights).value
+    a.kappa_factor = kappa_factor(level, max_levels, k)
+    a.s, a.im = _ia.ptr(s).value, _ia.ptr(im).value
+    a.workspace = _ia.ptr(ws).value
+    a.comm = comm
+    pbuf = None
+    if prof is not None:
+        pbuf = (ctypes.c_double * 8)()
+        a.prof = ctypes.cast(pbuf, ctypes.POINTER(ctypes.c_double))
+    _ia.check(_ia.lib().ia_synth_level(ctypes.byref(a), _ia.stream()), 'ia_synth_level')
+    if pbuf is not None:
+        prof.append({'level': level, 'screen_ms': pbuf[0], 'screens': int(pbuf[1]),
+                     'pairs': pbuf[2], 'candidates': int(pbuf[3]),
+                     'overflow_chunks': int(pbuf[4]), 'full_scans': int(pbuf[5]),
+                     'rows': index.nrows, 'pixels': H * W})
+    return s, im
+
+
+def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
+                   comm=None, rank=0, nranks=1, prof=None, levels=None):
+    """Synthesise levels 1..max_levels-1 (image_analogies.py:119-220) from device
+    pyramids.  Bp_pyr (list of device tensors) is updated in place.
+    Returns {level: (s, im)} device tensors."""
+    w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
+    row_range = None
+    if comm is not None:
+        row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
+    out = {}
+    for level in range(1, max_levels):
+        if levels is not None and level not in levels:
+            continue
+        index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range)
+        out[level] = synthesize_level_dev(level, max_levels, index, B_pyr[level - 1],
+                                          B_pyr[level], Bp_pyr[level - 1], Bp_pyr[level], w,
+                                          k, comm, prof)
+        del index
+    return out
+
+
+# ---- setup (image_analogies.py:17-94) ------------------------------------------------------
+
+def _read(fname):
+    """Decode an image file (host; file I/O is outside the device path).  An alpha
+    channel (RGBA PNG) is dropped — the reference's 3x3 YIQ einsum would reject it."""
+    import matplotlib.pyplot as plt
+    img = plt.imread(fname)
+    return img[..., :3] if img.ndim == 3 and img.shape[2] == 4 else img
+
+
+def setup_dev(A_orig, Ap_orig_list, B_orig, c):
+    """Numeric part of img_setup on device, from already-decoded images.
+    Returns device (A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list) and sets c.*."""
+    dev = _ia.require_device()
+    assert len(A_orig.shape) == len(B_orig.shape)
+    for Ap in Ap_orig_list:
+        assert A_orig.shape == Ap.shape
+    # scale to [0, 1]; the A' scale comes from the first row of the LAST A'
+    # (image_analogies.py:32-37 reads Ap_orig[0] after the loading loop)
+    scales = [255. if np.max(x) > 1.0 else 1.0
+              for x in (A_orig, B_orig, Ap_orig_list[-1][0])]
+    up = lambda x: torch.as_tensor(np.ascontiguousarray(x)).to(dev)  # noqa: E731
+    color_B = None
+    if c.convert:
+        _, A = ip.rgb_to_yiq_dev(up(A_orig), scales[0], want_yiq=False)
+        B_yiq, B = ip.rgb_to_yiq_dev(up(B_orig), scales[1], want_yiq=True)
+        Ap_list = [ip.rgb_to_yiq_dev(up(x), scales[2], want_yiq=False)[1] for x in Ap_orig_list]
+        color_B = B_yiq
+    else:
+        A = ip.scale_dev(up(A_orig), scales[0])
+        B = ip.scale_dev(up(B_orig), scales[1])
+        Ap_list = [ip.scale_dev(up(x), scales[2]) for x in Ap_orig_list]
+    if A.dim() != 2:
+        raise NotImplementedError('3-channel matching (convert=False on colour images) is not '
+                                  'supported by this build; use convert=True (YIQ luminance)')
+    if c.remap_lum:
+        A, Ap_list = ip.remap_luminance_dev(A, Ap_list, B)
+    levels = getattr(c, 'levels', None)
+    B_orig_pyr = None if c.init_rand else ip.gaussian_pyramid_dev(B, c.n_sm, levels)
+    A, B = ip.compress_values_dev(A, B, c.AB_weight)
+    c.num_ch, c.padding_sm, c.padding_lg, c.weights = setup_vars(A)
+    A_pyr = ip.gaussian_pyramid_dev(A, c.n_sm, levels)
+    B_pyr = ip.gaussian_pyramid_dev(B, c.n_sm, levels)
+    Ap_pyr_list = [ip.gaussian_pyramid_dev(Ap, c.n_sm, levels) for Ap in Ap_list]
+    if c.convert:
+        color_pyr_list = [ip.gaussian_pyramid_dev(color_B, c.n_sm, levels)]
+    else:
+        color_pyr_list = Ap_pyr_list
+    if len(A_pyr) != len(B_pyr):
+        c.max_levels = min(len(A_pyr), len(B_pyr))
+        warnings.warn('Warning: input images are very different sizes! The minimum number of '
+                      'levels will be used.')
+    else:
+        c.max_levels = len(B_pyr)
+    init = ip.initialize_Bp([p.cpu() for p in (B_pyr if c.init_rand else B_orig_pyr)],
+                            c.init_rand, getattr(c, 'seed', None))
+    Bp_pyr = [torch.as_tensor(np.ascontiguousarray(x)).to(dev) for x in init]
+    return A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list
+
+
+def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
+    """Read, convert, remap, compress and build pyramids (image_analogies.py:17-94).
+    Returns numpy pyramids like the reference."""
+    if not os.path.exists(out_path):
+        os.makedirs(out_path)
+    A_orig, B_orig = _read(A_fname), _read(B_fname)
+    Ap_orig_list = [_read(f) for f in Ap_fname_list]
+    dev_out = setup_dev(A_orig, Ap_orig_list, B_orig, c)
+    to_np = lambda pyr: [p.cpu().numpy() for p in pyr]  # noqa: E731
+    A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list = dev_out
+    return (to_np(A_pyr), [to_np(p) for p in Ap_pyr_list], to_np(B_pyr), to_np(Bp_pyr),
+            [to_np(p) for p in color_pyr_list], c)
+
+
+def color_output(level, Bp_lvl, s, im, color_pyr_list, c):
+    """Colour image of a level (image_analogies.py:216-217, 255-258): with convert, Y from
+    B' and I/Q from B's pyramid (the reference takes color_pyr_list[i] with the LAST
+    pixel's i; there is one colour pyramid then), clipped; otherwise the A' colour of each
+    pixel's source."""
+    H, W = Bp_lvl.shape
+    if c.convert:
+        yiq = torch.stack([Bp_lvl, color_pyr_list[0][level][:, :, 1], color_pyr_list[0][level][:, :, 2]], -1)
+        out = torch.empty_like(yiq)
+        _ia.check(_ia.lib().ia_yiq_to_rgb(_ia.ptr(yiq.contiguous()), H * W, _ia.ptr(out),
+                                          _ia.stream()), 'ia_yiq_to_rgb')
+        return out.clamp(0, 1).cpu().numpy()
+    src = torch.stack([p[level] for p in color_pyr_list])           # (nAp, h, w[, 3])
+    vals = src[im.long(), s[:, 0].long(), s[:, 1].long()]
+    vals = vals.reshape(H, W, *src.shape[3:])
+    if vals.dim() == 2:
+        vals = vals[..., None].expand(H, W, 3)
+    return vals.cpu().numpy()
+
+
+def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False):
+    """Full run (image_analogies.py:97-268): setup, per-level synthesis on device, colour
+    output images.  debug=True also saves each level's index maps as
+    ``%d_s.npy`` / ``%d_im.npy`` (the s / im lists of the reference's debug pickle)."""
+    import matplotlib.pyplot as plt
+    begin_time = start_time = time.time()
+    if not os.path.exists(out_path):
+        os.makedirs(out_path)
+    A_orig, B_orig = _read(A_fname), _read(B_fname)
+    Ap_orig_list = [_read(f) for f in Ap_fname_list]
+    A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list = setup_dev(A_orig, Ap_orig_list,
+                                                                  B_orig, c)
+    names = ['A_fname', 'Ap_fname_list', 'B_fname', 'c.convert', 'c.remap_lum', 'c.init_rand',
+             'c.AB_weight', 'c.k']
+    vals = [A_fname, Ap_fname_list, B_fname, c.convert, c.remap_lum, c.init_rand, c.AB_weight,
+            c.k]
+    save_metadata(out_path, names, vals)
+    torch.cuda.synchronize()
+    print('Environment Setup: %f' % (time.time() - start_time))
+    weights = _ia.to_dev(c.weights)
+    for level in range(1, c.max_levels):
+        start_time = time.time()
+        print('Computing level %d of %d' % (level, c.max_levels - 1))
+        index = algorithms.level_index(A_pyr, Ap_pyr_list, level)
+        s, im = synthesize_level_dev(level, c.max_levels, index, B_pyr[level - 1], B_pyr[level],
+                                     Bp_pyr[level - 1], Bp_pyr[level], weights, c.k)
+        color_im_out = color_output(level, Bp_pyr[level], s, im, color_pyr_list, c)
+        if debug:
+            np.save(out_path + '%d_s.npy' % level, s.cpu().numpy())
+            np.save(out_path + '%d_im.npy' % level, im.cpu().numpy())
+        plt.imsave(out_path + 'level_%d_color.jpg' % level, color_im_out)
+        plt.imsave(out_path + out_path.split('/')[-2] + '.jpg', color_im_out)
+        print('Level %d time: %f' % (level, time.time() - start_time))
+    print('Total time: %f' % (time.time() - begin_time))
+    return [p.cpu().numpy() for p in Bp_pyr]

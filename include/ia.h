@@ -1,0 +1,156 @@
+/* ia.h — C-ABI of the MI355X-native Image Analogies synthesis core (libia.so).
+ *
+ * Drop-in boundary for the reference's hot path (rubychen0611/image-analogies-python,
+ * SURVEY.md §8(b)).  Every entry point below names the reference interface it
+ * replaces.  Conventions:
+ *   - all array arguments are caller-owned DEVICE memory (row-major, element counts);
+ *     the library never allocates or frees caller memory; scratch comes in through a
+ *     `workspace` pointer sized by the matching *_workspace_bytes() query;
+ *   - `stream` is a hipStream_t passed as void* (no HIP/torch types in the ABI); work is
+ *     enqueued stream-ordered and the call returns without synchronising unless noted;
+ *   - return 0 on success, <0 on error (IA_E_*); ia_last_error() gives the message
+ *     (thread-local).  The Python host layer raises on any non-zero return.
+ *   - numerics: fp64 everywhere the reference computes in fp64, in the reference's
+ *     operation order (numpy pairwise-8 sums, no FMA contraction); the matcher screens in
+ *     fp32 MFMA and rescores candidates in fp64, so indices are exact.
+ */
+#ifndef IA_H
+#define IA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IA_OK 0
+#define IA_E_ARG (-1)       /* bad argument / shape                      */
+#define IA_E_HIP (-2)       /* HIP runtime error                         */
+#define IA_E_COMM (-3)      /* RCCL error                                */
+#define IA_E_UNSUPPORTED (-4)
+
+#define IA_D 55             /* feature length, 1 channel: 9 + 25 + 9 + 12          */
+#define IA_DP 56            /* padded row: 55 features + squared norm slot         */
+
+const char *ia_last_error(void);
+int ia_version(void);
+
+/* One pyramid level pair of the A / A' database (algorithms.py:50-70 inputs).
+ * A_sm/A_lg: A at levels l-1 (A_hs x A_ws) and l (Ah x Aw), fp64.
+ * Ap_sm/Ap_lg: nAp A' images stacked contiguously with the same shapes. */
+typedef struct {
+    const double *A_sm, *A_lg, *Ap_sm, *Ap_lg;
+    int A_hs, A_ws, Ah, Aw, nAp;
+} IaSrcLevel;
+
+/* ---- a1/a2: img_preprocess.py:6-13 convert_to_YIQ (+ image_analogies.py:32-50 scale).
+ * src: npix x 3 interleaved, dtype 0=uint8, 1=float32, 2=float64; x = src / div.
+ * yiq (npix x 3, nullable) and y (npix, nullable) receive the einsum result. */
+int ia_rgb_to_yiq(const void *src, int src_dtype, long npix, double div, double *yiq,
+                  double *y, void *stream);
+/* img_preprocess.py:16-22 convert_to_RGB: in npix x 3 -> out npix x 3. */
+int ia_yiq_to_rgb(const double *in, long npix, double *out, void *stream);
+/* scale only (convert=False path, image_analogies.py:51-56): out = src / div. */
+int ia_scale_to_f64(const void *src, int src_dtype, long n, double div, double *out,
+                    void *stream);
+/* a3/a4: img_preprocess.py:25-44.  mode 0: y = a*x (compress_values);
+ * mode 1: y = a*(x - m) + b (remap_luminance with a = s_B/s_A). */
+int ia_axpb_f64(const double *x, long n, int mode, double a, double m, double b,
+                double *y, void *stream);
+
+/* ---- a5: one skimage pyramid_reduce step (img_preprocess.py:56).
+ * src H x W -> dst h x w (h = ceil(H/2), w = ceil(W/2)); coef = (sx, tx, sy, ty) of
+ * skimage's estimated AffineTransform; taps = (w0, w1, w2, w3).
+ * workspace: ia_pyr_workspace_bytes(H, W). */
+size_t ia_pyr_workspace_bytes(int H, int W);
+int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w,
+                      const double coef[4], const double taps[4], void *workspace,
+                      void *stream);
+
+/* deterministic mean of n doubles (used for the screening centre). */
+size_t ia_mean_workspace_bytes(long n);
+int ia_mean_f64(const double *x, long n, double *out, void *workspace, void *stream);
+
+/* ---- a9: algorithms.py:11-47 compute_feature_array, one level, 1 channel.
+ * out: (h*w) x (full ? 34 : 21) fp64. */
+int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, int h, int w,
+                          int full, double *out, void *stream);
+
+/* ---- a10: algorithms.py:50-70 create_index — fp32 screening database for rows
+ * [row0, row0 + nrows) of As[level] (= A full | A'_i half).  Row layout (IA_DP floats):
+ * element k = 2s + h of (a - center, k < 55; |a - center|^2 at k = 55) stored at
+ * h*28 + s.  Rows are padded to ia_db_rows_padded(nrows) with sentinel rows.
+ * amax (device, 1 float) receives max_row |a - center| (atomic max; zero it first). */
+long ia_db_rows_padded(long nrows);
+int ia_db_chunk_rows(long nrows);
+int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                float *db, float *amax, void *stream);
+/* per-dimension screening centre: k < 34 -> mA, k >= 34 -> mAp (host scalars). */
+int ia_center_fill(double *center, double mA, double mAp, void *stream);
+
+/* ---- a11: algorithms.py:73-75 best_approximate_match, batched: exact 1-NN of M
+ * fp64 queries (M x 55, row stride IA_DP) over the DB rows built above (fp32 MFMA screen
+ * + fp64 rescore from the src pyramids).  Outputs idx (global row, int64) and the fp64
+ * distance (pairwise-8 sum of squares, the oracle's value). */
+typedef struct {
+    IaSrcLevel src;
+    const float *db;           /* ia_db_build output                       */
+    long row0, nrows;          /* this shard's global row range            */
+    const double *center;      /* 55 (device)                              */
+    const float *amax;         /* device scalar from ia_db_build           */
+    const double *q64;         /* M x IA_DP queries (device)               */
+    int M;
+    int64_t *idx;              /* out M                                    */
+    double *dist;              /* out M                                    */
+    void *workspace;
+} IaMatchArgs;
+size_t ia_match_workspace_bytes(int M, long nrows);
+int ia_match_batch(const IaMatchArgs *a, void *stream);
+
+/* ---- a13/a14: per-pixel helpers of algorithms.py:92-135 on device.
+ * ia_coherence_pick: argmin over n candidate rows of sqrt(pairwise8((a - q)^2)),
+ *   first minimum -> *out (device int32).  rows: n x 55, q: 55.
+ * ia_wdist_batch: out[i] = s*s, s = sqrt(pairwise8(((a_i - q_i) * w)^2)). */
+int ia_coherence_pick(const double *rows, int n, const double *q, int32_t *out,
+                      void *stream);
+int ia_wdist_batch(const double *a, const double *q, const double *w, int n, double *out,
+                   void *stream);
+
+/* ---- a12-a15: image_analogies.py:130-220 — synthesize one pyramid level on device,
+ * skewed wavefront t = x + 3y (exactly the scanline semantics).
+ * B_sm/B_lg: B at levels l-1 (B_hs x B_ws) and l (H x W); Bp_sm: B' level l-1;
+ * Bp_lg: B' level l (in: init, out: result); s: H*W*2 int32 (row, col) in A';
+ * im: H*W int32 A' image number.  weights: 55 fp64 (config.py:68-79);
+ * kappa_factor = 1 + 2**(level - max_levels) * k.
+ * comm: NULL (single GPU) or an ia_comm_init() communicator — the DB rows are then
+ * sharded (row0/nrows of this rank, N_total overall) and each wave exchanges the
+ * per-rank (dist, idx) winners with one RCCL all-gather. */
+typedef struct {
+    IaSrcLevel src;
+    const float *db; long row0, nrows, N_total;
+    const double *center; const float *amax;
+    const double *B_sm, *B_lg; int B_hs, B_ws, H, W;
+    const double *Bp_sm; double *Bp_lg;
+    const double *weights; double kappa_factor;
+    int32_t *s, *im;
+    void *workspace;
+    void *comm;
+    /* optional profiling: when non-NULL the call synchronises at the end and writes
+     * {sum screen-kernel ms, #screen launches, sum query-pixels x rows (pairs),
+     *  #candidates rescored, #overflow chunks, #full scans} */
+    double *prof;
+} IaSynthArgs;
+size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
+int ia_synth_level(const IaSynthArgs *a, void *stream);
+
+/* ---- multi-GPU: RCCL communicator over xGMI, one process per GPU. */
+int ia_comm_unique_id(uint8_t out[128]);
+int ia_comm_init(const uint8_t uid[128], int nranks, int rank, void **comm);
+int ia_comm_destroy(void *comm);
+int ia_comm_nranks(void *comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IA_H */

@@ -1,0 +1,196 @@
+"""Host-side logic of the product, CPU only: C-ABI exports, config parity, the skimage
+coefficient fit, the skewed-wavefront schedule, and the multi-rank sharding/exchange rule
+(gloo, world_size 2)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import ia_oracle as o
+from conftest import analogy_inputs, golden
+
+
+def test_libia_loads_and_exports_every_declared_symbol():
+    import _ia
+    lib = ctypes.CDLL(_ia.LIB_PATH)
+    names = _ia.declared_symbols()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_ia._SIGS) == set(names)      # every declared entry point is bound
+    assert _ia.lib().ia_version() == 1
+
+
+def test_product_config_matches_reference():
+    import config as c
+    g310 = golden('ref_weights_py310.npz')
+    assert np.array_equal(c.compute_weights(3, 5, 12, 1), g310['ch1'])
+    assert np.array_equal(c.compute_weights(3, 5, 12, 3), g310['ch3'])
+    num_ch, psm, plg, w = c.setup_vars(np.zeros((7, 9)))
+    assert (num_ch, psm, plg) == (1, 1, 2) and w.shape == (55,)
+    num_ch, psm, plg, w = c.setup_vars(np.zeros((7, 9, 3)))
+    assert num_ch == 3 and w.shape == (165,)
+    assert (c.n_half, c.pad_sm, c.pad_lg) == (12, 1, 2)
+
+
+def test_resize_coeffs_equal_skimage_fit():
+    """The product's host restatement of skimage's AffineTransform fit gives the same
+    coefficients as the oracle (which reproduces skimage's pyramids bit for bit)."""
+    import img_preprocess as ip
+    for H in range(2, 80):
+        for W in (H, H + 1, 2 * H + 3, max(2, H // 3)):
+            out = ((H + 1) // 2, (W + 1) // 2)
+            assert ip.resize_coeffs((H, W), out) == o.affine_coeffs((H, W), out), (H, W)
+    for shp in [(2048, 2048), (1024, 1024), (362, 638), (117, 180)]:
+        out = ((shp[0] + 1) // 2, (shp[1] + 1) // 2)
+        assert ip.resize_coeffs(shp, out) == o.affine_coeffs(shp, out)
+
+
+def test_num_layers_and_index_maps():
+    import img_preprocess as ip
+    for h, w in [(180, 117), (362, 638), (2048, 2048), (4, 4), (25, 40)]:
+        assert ip.num_layers(h, w, 3) == o.pyramid_num_layers(h, w, 3)
+        assert ip.num_layers(h, w, 3, 5) == o.pyramid_num_layers(h, w, 3, 5)
+    h, w = 7, 11
+    ix = np.arange(3 * h * w)
+    (px, img) = ip.Ap_ix2px(ix, h, w)
+    assert np.array_equal(ip.Ap_px2ix(px, img, h, w), ix)
+    assert np.array_equal(ip.px2ix(ip.ix2px(ix[:h * w], w), w), ix[:h * w])
+
+
+# ---- skewed wavefront t = x + 3y ---------------------------------------------------------------
+
+def wave_rows(t, H, W):
+    """y range of wave t — the formula of ia_synth_level's loop (ia_synth.hip)."""
+    lo_num = t - (W - 1)
+    y_lo = (lo_num + 2) // 3 if lo_num > 0 else 0
+    y_hi = min(t // 3, H - 1)
+    return y_lo, y_hi
+
+
+def read_set(y, x, H, W):
+    """Every B' fine-level position the query of (y, x) reads (image_analogies.py:166-168,
+    symmetric padding) plus the coherence window's s/im positions (algorithms.py:101-106)."""
+    pts = set()
+    for t in range(12):
+        pts.add((int(o.sym_index(y + t // 5 - 2, H)), int(o.sym_index(x + t % 5 - 2, W))))
+    for rr in range(max(0, y - 2), y + 1):
+        for cc in range(max(0, x - 2), min(W, x + 3)):
+            if rr * W + cc < y * W + x:
+                pts.add((rr, cc))
+    return pts
+
+
+@pytest.mark.parametrize('skew,ok', [(3, True), (2, False)])
+def test_wavefront_reads_equal_scanline_reads(skew, ok):
+    """For every H <= 23, W <= 30: a position read by q was written before q in scanline
+    order  <=>  its wave index is smaller.  Skew 3 holds everywhere, skew 2 does not."""
+    all_ok = True
+    for H in range(1, 24):
+        for W in range(1, 31):
+            for y in range(H):
+                for x in range(W):
+                    for (py, px) in read_set(y, x, H, W):
+                        before = py * W + px < y * W + x
+                        if before != (px + skew * py < x + skew * y):
+                            all_ok = False
+    assert all_ok == ok
+
+
+def test_wave_rows_cover_every_pixel_once():
+    for H in range(1, 20):
+        for W in range(1, 25):
+            seen = np.zeros((H, W), int)
+            for t in range((W - 1) + 3 * (H - 1) + 1):
+                y_lo, y_hi = wave_rows(t, H, W)
+                for y in range(y_lo, y_hi + 1):
+                    x = t - 3 * y
+                    assert 0 <= x < W
+                    seen[y, x] += 1
+            assert (seen == 1).all()
+
+
+def test_wavefront_synthesis_equals_scanline_oracle():
+    """The oracle run wave by wave (all queries of a wave read the state before the wave
+    writes) produces the scanline oracle's B', s and im exactly."""
+    A, Aps, B = analogy_inputs(11, (22, 27), (19, 24), n_ap=2)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=4)
+    Bp_w = [b.copy() for b in Bp_pyr]
+    ref = o.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, 1.0)
+    w = o.compute_weights(3, 5, 12, 1)
+    As = o.create_index(A_pyr, Ap_list, L)
+    for level in range(1, L):
+        H, W = Bp_w[level].shape
+        Ah, Aw = Ap_list[0][level].shape
+        Bf = o.level_features(B_pyr[level - 1], B_pyr[level], True)
+        f = o.kappa_factor(level, L, 1.0)
+        s = np.zeros((H * W, 2), np.int64)
+        im = np.zeros(H * W, np.int64)
+        for t in range((W - 1) + 3 * (H - 1) + 1):
+            y_lo, y_hi = wave_rows(t, H, W)
+            snap = Bp_w[level].copy()
+            upd = []
+            for y in range(y_lo, y_hi + 1):
+                x = t - 3 * y
+                q = np.hstack([Bf[y * W + x], o.extract_pixel_feature(Bp_w[level - 1], snap, (y, x), False)])
+                app = o.best_approximate_match(As[level], q)
+                p, i = o.Ap_ix2px(app, Ah, Aw)
+                if (y, x) != (0, 0):
+                    sl = [tuple(v) for v in s]
+                    pc, ic, _ = o.best_coherence_match(As[level], (Ah, Aw), q, sl, list(im), (y, x), W)
+                    if pc != (-1, -1):
+                        da = o.compute_distance(As[level][app], q, w)
+                        dc = o.compute_distance(As[level][o.Ap_px2ix(pc, ic, Ah, Aw)], q, w)
+                        if dc <= da * f:
+                            p, i = pc, ic
+                upd.append((y, x, p, i))
+            for y, x, p, i in upd:
+                Bp_w[level][y, x] = Ap_list[i][level][p[0], p[1]]
+                s[y * W + x] = p
+                im[y * W + x] = i
+        assert np.array_equal(Bp_w[level], ref[level][0])
+        assert np.array_equal(s, ref[level][1]) and np.array_equal(im, ref[level][2])
+
+
+# ---- sharded database: per-rank exact winners + lexicographic min (gloo, 2 ranks) -------------
+
+def _shard_worker(rank, world, port, N, Q, As, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from image_analogies import shard_rows
+    r0, nr = shard_rows(N, rank, world)
+    d = np.add.reduce((As[r0:r0 + nr][None, :, :] - Q[:, None, :]) ** 2, axis=2)
+    loc = np.argmin(d, axis=1)
+    mine = torch.tensor(np.stack([d[np.arange(len(Q)), loc], (loc + r0).astype(np.float64)], 1))
+    allw = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allw, mine)                      # the RCCL all-gather of ia_comm.hip
+    best = []
+    for qi in range(len(Q)):
+        cands = sorted((float(a[qi, 0]), int(a[qi, 1])) for a in allw)
+        best.append(cands[0][1])                     # (distance, lowest row) minimum
+    out[rank] = best
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_exchange_equals_global_argmin(world):
+    rs = np.random.RandomState(9)
+    N = 1001
+    As = np.round(rs.rand(N, 55) * 8) / 8      # coarse values: many exact ties across shards
+    Q = As[rs.randint(0, N, 40)] + (rs.rand(40, 55) < 0.1) / 8
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29500 + rs.randint(0, 2000)
+    mp.spawn(_shard_worker, args=(world, port, N, Q, As, out), nprocs=world, join=True)
+    ref = [o.best_approximate_match(As, q) for q in Q]
+    for r in range(world):
+        assert out[r] == ref
+    from image_analogies import shard_rows
+    spans = [shard_rows(N, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and sum(n for _, n in spans) == N
+    assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))

@@ -1,0 +1,187 @@
+"""Pin the CPU oracle against the reference: golden vectors produced by the reference's
+own modules (tests/golden/make_golden.py), the KATs of the reference's tests
+(algorithms_test.py, config_test.py, img_preprocess_test.py), and C-vs-numpy oracle
+agreement.  CPU only."""
+import numpy as np
+import pytest
+
+import ia_oracle as o
+import ia_oracle_c as oc
+from conftest import analogy_inputs, golden
+
+
+# ---- config.py ----------------------------------------------------------------------------
+
+def test_weights_match_reference_goldens():
+    g = golden()
+    g310 = golden('ref_weights_py310.npz')
+    for ch, key in ((1, 'ch1'), (3, 'ch3')):
+        w = o.compute_weights(3, 5, 12, ch)
+        # reference config.py under this interpreter's numpy: bit-exact
+        assert np.array_equal(w, g310[key])
+        # under the skimage-era numpy 1.26.4: np.exp differs by <= 1 ulp
+        assert np.allclose(w, g['weights_%s' % key], rtol=1e-15, atol=0)
+
+
+def test_compute_weights_kat():
+    """config_test.py:5-62 restated."""
+    for ch in (1, 3):
+        gs = o.matlab_style_gauss2D((3, 3), 0.5)
+        gl = o.matlab_style_gauss2D((5, 5), 1)
+        w_sm = np.repeat(((1. / 9) * gs).flatten(), ch)
+        w_lg = np.repeat(((1. / 25) * gl).flatten(), ch)
+        w_half = np.repeat(((1. / 12) * gl.flatten()[:12]), ch)
+        assert len(w_sm) == 9 * ch and len(w_lg) == 25 * ch and len(w_half) == 12 * ch
+        assert np.isclose(np.sum(w_sm), ch / 9.)
+        assert np.isclose(np.sum(w_lg), ch / 25.)
+        assert np.sum(w_half) < ch * 0.5 / 12
+        assert np.allclose(o.compute_weights(3, 5, 12, ch), np.hstack([w_sm, w_lg, w_sm, w_half]))
+
+
+# ---- img_preprocess.py -------------------------------------------------------------------------
+
+def test_yiq_rgb_match_reference():
+    g = golden()
+    assert np.array_equal(o.convert_to_YIQ(g['yiq_in']), g['yiq_out'])
+    assert np.array_equal(o.convert_to_RGB(g['yiq_out']), g['rgb_out'])
+    assert np.array_equal(o.convert_to_YIQ(g['yiq_u8_in'] / 255.), g['yiq_u8_out'])
+
+
+def test_yiq_einsum_order():
+    """The kernels' per-channel order (m0*x0 + m2*x2) + m1*x1 is numpy's einsum order."""
+    x = np.random.RandomState(3).rand(31, 17, 3)
+    e = o.convert_to_YIQ(x)
+    for i in range(3):
+        m = o.YIQ_M[i]
+        assert np.array_equal(e[..., i], (m[0] * x[..., 0] + m[2] * x[..., 2]) + m[1] * x[..., 1])
+
+
+def test_converts_roundtrip():
+    """img_preprocess_test.py:6-13."""
+    img = np.random.RandomState(0xba5eba11).rand(25, 25, 3)
+    assert np.allclose(o.convert_to_RGB(o.convert_to_YIQ(img)), img, atol=0.05)
+    for img in (np.ones((25, 25, 3)), np.zeros((25, 25, 3))):
+        assert np.allclose(o.convert_to_RGB(o.convert_to_YIQ(img)), img)
+
+
+def test_remap_luminance_matches_reference():
+    g = golden()
+    a, ap = o.remap_luminance(g['remap_A'], [g['remap_Ap']], g['remap_B'])
+    assert np.array_equal(a, g['remap_A_out']) and np.array_equal(ap[0], g['remap_Ap_out'])
+    # img_preprocess_test.py:16-26 intent (the reference test passes a bare array)
+    B = g['remap_B']
+    for X in (a, ap[0]):
+        assert np.isclose(np.mean(B), np.mean(X), atol=0.05)
+        assert np.isclose(np.std(B), np.std(X), atol=0.05)
+
+
+@pytest.mark.parametrize('k', range(9))
+def test_pyramid_bit_exact_vs_skimage(k):
+    """img_preprocess.py:47-63 -> skimage 0.18.3 pyramid_gaussian, every level bit-exact."""
+    g = golden()
+    img = g['pyr%d_in' % k]
+    n = int(g['pyr%d_n' % k])
+    pyr = o.compute_gaussian_pyramid(img, 3)
+    assert len(pyr) == n
+    for l in range(n):
+        assert np.array_equal(pyr[l], g['pyr%d_l%d' % (k, l)]), (k, l)
+
+
+def test_initialize_Bp():
+    """img_preprocess_test.py:29-42 intent, seeded."""
+    img = np.random.RandomState(0xba5eba11).rand(25, 40)
+    pyr = o.compute_gaussian_pyramid(img, 3)
+    for a, b in zip(pyr, o.initialize_Bp(pyr, init_rand=False)):
+        assert np.array_equal(a, b)
+    for a, b in zip(pyr, o.initialize_Bp(pyr, init_rand=True, seed=5)):
+        assert not np.allclose(a, b)
+    r1 = o.initialize_Bp(pyr, True, seed=5)
+    r2 = o.initialize_Bp(pyr, True, seed=5)
+    assert all(np.array_equal(a, b) for a, b in zip(r1, r2))
+
+
+# ---- algorithms.py KATs (algorithms_test.py:10-115) --------------------------------------------
+
+SM_0 = np.array([[0, 0, 0.5], [0, 0, 0.5], [0.5, 0.5, 0.5]])
+LG_0 = np.array([[0.3, 0.3, 0.3, 0.3, 0.3],
+                 [0.3, 1, 1, 0.3, 0.3],
+                 [0.3, 1, 1, 0.3, 0.3],
+                 [0.3, 0.3, 0.3, 0.3, 0.3],
+                 [0.3, 0.3, 0.3, 0.3, 0.3]])
+
+
+def kat_images():
+    sm = 0.5 * np.ones((4, 5)); sm[0, 0] = 0
+    lg = 0.3 * np.ones((7, 10)); lg[0, 0] = 1
+    return sm, lg
+
+
+def test_compute_feature_array_kat():
+    sm, lg = kat_images()
+    feat = o.compute_feature_array([sm, lg], True)
+    assert len(feat) == 2 and feat[0] == []
+    assert feat[1].shape == (70, 34)
+    assert np.allclose(feat[1][0], np.hstack([SM_0.flatten(), LG_0.flatten()]))
+    feat = o.compute_feature_array([sm, lg], False)
+    assert feat[1].shape == (70, 21)
+    assert np.allclose(feat[1][0], np.hstack([SM_0.flatten(), LG_0.flatten()[:12]]))
+
+
+def test_extract_pixel_feature_kat():
+    sm, lg = kat_images()
+    assert np.allclose(o.extract_pixel_feature(sm, lg, (0, 0), True),
+                       np.hstack([SM_0.flatten(), LG_0.flatten()]))
+    assert np.allclose(o.extract_pixel_feature(sm, lg, (0, 0), False),
+                       np.hstack([SM_0.flatten(), LG_0.flatten()[:12]]))
+    # the index-map form equals explicit symmetric padding (algorithms.py:81-84)
+    psm, plg = o.pad_img_pair(sm, lg)
+    for r in range(7):
+        for c in range(10):
+            ref = np.hstack([psm[r // 2:r // 2 + 3, c // 2:c // 2 + 3].flatten(),
+                             plg[r:r + 5, c:c + 5].flatten()])
+            assert np.array_equal(o.extract_pixel_feature(sm, lg, (r, c), True), ref)
+
+
+def test_best_coherence_match_property():
+    """algorithms_test.py:158-207 restated with the current signature: with B = A and
+    s(q - (1,1)) = q - (1,1), coherence must return exactly q."""
+    A, Aps, _ = analogy_inputs(7, (40, 52), (8, 8))
+    A_pyr = o.compute_gaussian_pyramid(A, 3)
+    Ap_pyr = o.compute_gaussian_pyramid(Aps[0], 3)
+    As = o.create_index(A_pyr, [Ap_pyr], len(A_pyr))[-1]
+    imh, imw = A.shape
+    rs = np.random.RandomState(1)
+    for row, col in [(1, 1), (1, imw - 1), (imh - 1, 1), (imh - 1, imw - 1), (imh // 2, imw // 2)]:
+        num_px = row * imw + col
+        s = [(int(a), int(b)) for a, b in zip(rs.randint(0, imh, num_px), rs.randint(0, imw, num_px))]
+        s[(row - 1) * imw + col - 1] = (row - 1, col - 1)
+        im = [0] * num_px
+        q = As[row * imw + col]
+        p, i, r_star = o.best_coherence_match(As, (imh, imw), q, s, im, (row, col), imw)
+        assert p == (row, col) and i == 0
+
+
+def test_brute_force_is_first_min():
+    rs = np.random.RandomState(2)
+    As = rs.rand(500, 55)
+    As[300] = As[100]       # exact duplicate: the lower row must win
+    assert o.best_approximate_match(As, As[100] + 1e-9) == 100
+
+
+# ---- C oracle == numpy oracle (end to end) -------------------------------------------------------
+
+@pytest.mark.parametrize('case', [
+    dict(seed=0, A=(30, 40), B=(28, 33), n_ap=1, k=0.5, flat=False),
+    dict(seed=3, A=(26, 21), B=(17, 30), n_ap=2, k=5.0, flat=False),
+    dict(seed=5, A=(24, 24), B=(24, 24), n_ap=1, k=2.0, flat=True),
+])
+def test_c_oracle_equals_numpy_oracle(case):
+    A, Aps, B = analogy_inputs(case['seed'], case['A'], case['B'], case['n_ap'], case['flat'])
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=case['seed'])
+    Bp2 = [b.copy() for b in Bp_pyr]
+    r1 = o.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, case['k'])
+    r2 = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp2, L, case['k'], o.compute_weights(3, 5, 12, 1))
+    assert set(r1) == set(r2) == set(range(1, L))
+    for l in r1:
+        for a, b in zip(r1[l], r2[l]):
+            assert np.array_equal(a, b), l
