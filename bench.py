@@ -1,0 +1,275 @@
+"""Benchmark: B' synthesis throughput (B' pixels/s) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4]
+
+One STEP = the whole hot path over one synthetic analogy, from the luminance images
+resident in HBM to B' and the (s, im) index maps in HBM: Gaussian pyramids of A, A', B
+(5-level cap), per level the fp32 screening database, then the wavefront synthesis of
+every level (query build, MFMA screen, exact fp64 rescore, coherence + kappa, update).
+B' restarts from the same random initialisation each step.
+
+Workloads (BASELINE.json configs):
+    c1  180x117 A/A'/B, kappa 0.5           c2  same, kappa 5
+    c3  362x638, kappa 25, 5-level cap      c4  A = A' 2048x2048, B 1024x1024, 5-level cap
+    c5  independent 512x512 jobs (multi_script batch), --jobs per GPU
+Default: c4 — the configuration the metric and its 1/2/4/8-GPU scaling are quoted on.
+With N > 1 (torch.distributed.run, one process per GPU) c4 shards every level's database
+rows over the ranks with one RCCL all-gather per wave (strong scaling); c5 spreads jobs
+(weak scaling, no collective).  rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'image-analogies-python_amd'))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import _ia  # noqa: E402
+import config as cfg  # noqa: E402
+import image_analogies as ia  # noqa: E402
+import img_preprocess as ip  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),
+    'c2': dict(A=(180, 117), B=(180, 117), k=5.0, levels=None, name='freud-crop 180x117 kappa=5, brute force'),
+    'c3': dict(A=(362, 638), B=(362, 638), k=25.0, levels=5, name='texture transfer 362x638 kappa=25, 5-level'),
+    'c4': dict(A=(2048, 2048), B=(1024, 1024), k=0.5, levels=5, name='A/A\' 2048x2048 x B 1024x1024, 5-level, DB sharded'),
+    'c5': dict(A=(512, 512), B=(512, 512), k=0.5, levels=5, name='independent 512x512 analogies (multi_script batch)'),
+}
+
+
+def smooth_noise(seed, shape, sigma=2.0):
+    from scipy.ndimage import gaussian_filter
+    x = gaussian_filter(np.random.RandomState(seed).rand(*shape), sigma)
+    return (x - x.min()) / (x.max() - x.min())
+
+
+def make_inputs(conf, seed):
+    """SURVEY §8(d) synthetic blur-filter analogy: A smooth noise, A' = blur(A), B noise."""
+    from scipy.ndimage import gaussian_filter
+    A = smooth_noise(seed, conf['A'])
+    Ap = gaussian_filter(A, 1.5)
+    B = smooth_noise(seed + 1, conf['B'])
+    return A, Ap, B
+
+
+class Job:
+    """One analogy with its inputs resident in HBM."""
+
+    def __init__(self, conf, seed, dev):
+        A, Ap, B = make_inputs(conf, seed)
+        self.A, self.Ap, self.B = (torch.as_tensor(x).to(dev) for x in (A, Ap, B))
+        self.k, self.levels = conf['k'], conf['levels']
+        nB = ip.num_layers(B.shape[0], B.shape[1], cfg.n_sm, self.levels)
+        nA = ip.num_layers(A.shape[0], A.shape[1], cfg.n_sm, self.levels)
+        self.max_levels = min(nA, nB) + 1
+        shapes = [B.shape]
+        for _ in range(nB):
+            shapes.append(((shapes[-1][0] + 1) // 2, (shapes[-1][1] + 1) // 2))
+        shapes.reverse()
+        init = ip.initialize_Bp([np.empty(s) for s in shapes], True, seed + 2)
+        self.Bp_init = [torch.as_tensor(x).to(dev) for x in init]
+        self.Bp = [x.clone() for x in self.Bp_init]
+        self.weights = torch.as_tensor(cfg.compute_weights(3, 5, 12, 1)).to(dev)
+        self.pixels = sum(s[0] * s[1] for s in shapes[1:self.max_levels])
+
+    def step(self, comm=None, rank=0, nranks=1, prof=None):
+        A_pyr = ip.gaussian_pyramid_dev(self.A, cfg.n_sm, self.levels)
+        Ap_pyr = ip.gaussian_pyramid_dev(self.Ap, cfg.n_sm, self.levels)
+        B_pyr = ip.gaussian_pyramid_dev(self.B, cfg.n_sm, self.levels)
+        for dst, src in zip(self.Bp, self.Bp_init):
+            dst.copy_(src)
+        return ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, self.Bp, self.max_levels, self.k,
+                                 self.weights, comm=comm, rank=rank, nranks=nranks, prof=prof)
+
+    def algorithmic_pairs(self):
+        """sum over synthesized levels of q_l * N_l (the matcher's (query, row) pairs);
+        pyramids are aligned from the coarse end as in image_analogies.py:82-86."""
+        def shapes(img):
+            n = ip.num_layers(img.shape[0], img.shape[1], cfg.n_sm, self.levels)
+            out = [tuple(img.shape)]
+            for _ in range(n):
+                out.append(((out[-1][0] + 1) // 2, (out[-1][1] + 1) // 2))
+            return out[::-1]
+        bl, al = shapes(self.B), shapes(self.A)
+        return sum(bl[l][0] * bl[l][1] * al[l][0] * al[l][1] for l in range(1, self.max_levels))
+
+
+def cpu_baseline(job, seconds=20.0):
+    """The C oracle (exact brute force, 1 core) on a bounded sample of the same workload:
+    the first pixels of the FINEST level in scanline order against its full database;
+    extrapolated to the whole job by (query, row) pair count."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import ia_oracle_c as oc
+    A_pyr = [p.cpu().numpy() for p in ip.gaussian_pyramid_dev(job.A, cfg.n_sm, job.levels)]
+    Ap_pyr = [p.cpu().numpy() for p in ip.gaussian_pyramid_dev(job.Ap, cfg.n_sm, job.levels)]
+    B_pyr = [p.cpu().numpy() for p in ip.gaussian_pyramid_dev(job.B, cfg.n_sm, job.levels)]
+    Bp_pyr = [p.cpu().numpy() for p in job.Bp_init]
+    level = job.max_levels - 1
+    w = cfg.compute_weights(3, 5, 12, 1)
+    N = A_pyr[level].size
+    f = ia.kappa_factor(level, job.max_levels, job.k)
+    probe = oc.LevelJob(level, A_pyr, [Ap_pyr], B_pyr, Bp_pyr, w, f, max_pixels=2)
+    probe.build_db()
+    t0 = time.perf_counter()
+    probe.run()
+    per_px = max((time.perf_counter() - t0) / 2, 1e-6)
+    npx = int(max(2, min(B_pyr[level].size, seconds / per_px)))
+    job_s = oc.LevelJob(level, A_pyr, [Ap_pyr], B_pyr, Bp_pyr, w, f, max_pixels=npx)
+    job_s.db = probe.db
+    probe.db = None
+    t0 = time.perf_counter()
+    job_s.run()
+    dt = time.perf_counter() - t0
+    pairs_per_s = npx * N / dt
+    value = pairs_per_s * job.pixels / job.algorithmic_pairs()
+    return {'value': value, 'unit': "B' pixels/s", 'cores': 1, 'kind': 'port',
+            'sample': '%d B\' pixels (scanline) of the finest level (%dx%d) against its full '
+                      '%d-row database, %.1f s on 1 core of %d; extrapolated to the whole '
+                      'job by (query,row) pairs' % (npx, B_pyr[level].shape[0],
+                                                    B_pyr[level].shape[1], N, dt,
+                                                    os.cpu_count())}
+
+
+def init_comm(rank, world):
+    """RCCL communicator of libia (one per process/GPU); the unique id travels over the
+    gloo process group."""
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        buf = ctypes.create_string_buffer(128)
+        _ia.check(_ia.lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
+        uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+    dist.broadcast(uid, 0)
+    h = ctypes.c_void_p()
+    _ia.check(_ia.lib().ia_comm_init(uid.numpy().tobytes(), world, rank, ctypes.byref(h)),
+              'ia_comm_init')
+    return h
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
+    ap.add_argument('--jobs', type=int, default=4, help='c5: jobs per GPU per step')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('gloo')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    conf = CONFIGS[args.config]
+
+    comm = None
+    if world > 1 and args.config != 'c5':
+        comm = init_comm(rank, world)
+
+    if args.config == 'c5':
+        jobs = [Job(conf, 1000 + 3 * (rank + world * j), dev) for j in range(args.jobs)]
+    else:
+        jobs = [Job(conf, 0, dev)]
+
+    def run_step(prof=None):
+        for jb in jobs:
+            jb.step(comm, rank, world, prof)
+
+    for _ in range(args.warmup):
+        run_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step(prof)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # consistency of the result (outside the timed region): B' == A'[im][s] per level and
+    # identical replicas across ranks
+    out = jobs[0].step(comm, rank, world)
+    chk = 0.0
+    for l, (s, im) in out.items():
+        chk += float(jobs[0].Bp[l].sum().item()) + float(s.double().sum().item())
+    ct = torch.tensor([chk], dtype=torch.float64)
+    replicas_ok = True
+    if world > 1 and args.config != 'c5':
+        lo, hi = ct.clone(), ct.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        replicas_ok = bool(lo.item() == hi.item())
+
+    pixels_per_step = sum(jb.pixels for jb in jobs) * (world if args.config == 'c5' else 1)
+    value = pixels_per_step * args.steps / elapsed
+    screen_ms = sum(p['screen_ms'] for p in prof)
+    screens = sum(p['screens'] for p in prof)
+    pairs = sum(p['pairs'] for p in prof)
+    flops = 2.0 * 55 * pairs
+    achieved = flops / (screen_ms * 1e-3) / 1e12 if screen_ms > 0 else 0.0
+
+    result = {
+        'metric': "B' pixels/sec (brute-force match, 5-level pyramid) + MFMA util @1/2/4/8 GPU",
+        'value': value,
+        'unit': "B' pixels/s",
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak' if args.config == 'c5' else 'strong',
+        'vs_baseline': None,
+        'dtype': 'f32 (MFMA screen) + f64 (exact rescore, pyramids)',
+        'data': 'synthetic (gaussian-filtered noise; A\' = blur(A)); seeded',
+        'config': {'workload': args.config + ': ' + conf['name'],
+                   'A': list(conf['A']), 'B': list(conf['B']), 'kappa': conf['k'],
+                   'levels_cap': conf['levels'], 'jobs_per_gpu': len(jobs),
+                   'pixels_per_step': pixels_per_step,
+                   'parallelism': ('jobs%d' % world) if args.config == 'c5' else
+                                  ('db-shard%d' % world if world > 1 else 'single')},
+        'roofline': {'bound': 'mfma', 'kernel': 'k_screen', 'achieved': achieved,
+                     'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': None,
+                     'algorithmic': '2*55 flop per (query,row) pair; this rank: %.4g pairs '
+                                    'over %d launches' % (pairs, screens),
+                     'screen_avg_us': screen_ms * 1e3 / max(screens, 1)},
+        'matcher': {'candidates_rescored': sum(p['candidates'] for p in prof),
+                    'overflow_chunks': sum(p['overflow_chunks'] for p in prof),
+                    'full_scans': sum(p['full_scans'] for p in prof)},
+        'checks': {'replicas_identical': replicas_ok, 'checksum': chk},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline(jobs[0], args.cpu_seconds)
+    if comm is not None:
+        _ia.lib().ia_comm_destroy(comm)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

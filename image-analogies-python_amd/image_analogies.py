@@ -13,6 +13,7 @@ with ``comm`` it shards every level's database over the ranks (RCCL all-gather p
 """
 import ctypes
 import os
+import sys
 import time
 import warnings
 
@@ -81,6 +82,7 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     if comm is not None:
         row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
     out = {}
+    t_start = time.time()
     for level in range(1, max_levels):
         if levels is not None and level not in levels:
             continue
@@ -89,6 +91,10 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
                                           B_pyr[level], Bp_pyr[level - 1], Bp_pyr[level], w,
                                           k, comm, prof)
         del index
+        if os.environ.get('IA_VERBOSE'):
+            torch.cuda.synchronize()
+            print('[ia] level %d/%d done %.3f s' % (level, max_levels - 1, time.time() - t_start),
+                  file=sys.stderr, flush=True)
     return out
 
 
