@@ -35,14 +35,16 @@ struct Best {            // exact winner of a (query, shard): fp64 distance + gl
 struct QSplit {
     int nq, groups, rows_pad;
 };
-static inline QSplit qsplit(int M) {
+// T = ceil(M/32) query tiles in groups of nq <= maxnq tiles: fewest padded tiles, then
+// the largest nq (fewest re-reads of the database).
+static inline QSplit qsplit(int M, int maxnq) {
     const int T = (M + 31) / 32;
     QSplit s;
-    if (T <= 3) {
+    if (T <= maxnq) {
         s.nq = T; s.groups = 1;
     } else {
-        int bestnq = 3, bestpad = 1 << 30;
-        for (int nq = 3; nq >= 2; --nq) {
+        int bestnq = maxnq, bestpad = 1 << 30;
+        for (int nq = maxnq; nq >= 2; --nq) {
             int pad = (T + nq - 1) / nq * nq;
             if (pad < bestpad) { bestpad = pad; bestnq = nq; }
         }
@@ -51,7 +53,8 @@ static inline QSplit qsplit(int M) {
     s.rows_pad = s.nq * s.groups * 32;
     return s;
 }
-static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + 4) * 32; }
+constexpr int MAX_NQ = 6;
+static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + MAX_NQ) * 32; }
 
 // ---- launchers ------------------------------------------------------------------
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
@@ -60,8 +63,11 @@ int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int 
 int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
                       hipStream_t st);
 // screen of M queries (qp) against nrows DB rows -> cand[M][nchunks][SCREEN_K]
+// variant 0: queries in VGPRs (<= 3 tiles/wave); 1: queries in LDS (<= 6 tiles/wave)
 int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
                   hipStream_t st);
+int launch_screen_v(const float *db, long nrows, const float *qp, int M, Cand *cand,
+                    int variant, hipStream_t st);
 // exact rescore of the screen's candidates -> best[M]; stats[0..2] += (#cand, #overflow
 // chunks, #full scans) when stats != nullptr
 int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int M,

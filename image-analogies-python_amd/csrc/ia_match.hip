@@ -45,6 +45,86 @@ __device__ __forceinline__ void topk_insert(float (&t)[SCREEN_K], int (&ti)[SCRE
     t[3] = n3; ti[3] = i3;
 }
 
+constexpr int TILE_VEC = 32 * IA_DP / 4;   // float4s per 32-row DB tile
+
+// One 32-row DB tile against NQ query tiles: 28*NQ MFMAs, then the per-lane top-K
+// epilogue.  C[row i][col j] lands at lane (j, h), register r, i = (r&3) + 8(r>>2) + 4h.
+// B operands come from registers (bval) or, with FROM_LDS, from ds_read_b128 of the
+// staged query image (4 k-steps per read).
+template <int NQ, bool FROM_LDS, typename BV>
+__device__ __forceinline__ void screen_tile(const float4 (&a4)[7], BV &bval,
+                                            const float4 *qsh, int lane,
+                                            float (&te)[NQ][SCREEN_K], int (&ti)[NQ][SCREEN_K],
+                                            int rbase) {
+    floatx16 acc[NQ];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
+#pragma unroll
+    for (int v = 0; v < 7; ++v) {
+        const float av[4] = {a4[v].x, a4[v].y, a4[v].z, a4[v].w};
+        float4 bl[NQ];
+        if constexpr (FROM_LDS) {
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt) bl[qt] = qsh[(qt * 7 + v) * 64 + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt) {
+                float bv;
+                if constexpr (FROM_LDS)
+                    bv = u == 0 ? bl[qt].x : u == 1 ? bl[qt].y : u == 2 ? bl[qt].z : bl[qt].w;
+                else
+                    bv = bval(qt, v, u);
+                acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv, acc[qt], 0, 0, 0);
+            }
+    }
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        float mn = acc[qt][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mn = fminf(mn, acc[qt][r]);
+        if (mn < te[qt][SCREEN_K - 1]) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = acc[qt][r];
+                if (x < te[qt][SCREEN_K - 1])
+                    topk_insert(te[qt], ti[qt], x, rbase + (r & 3) + 8 * (r >> 2));
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void load_tile(float4 (&a)[7], const float4 *p) {
+#pragma unroll
+    for (int v = 0; v < 7; ++v) a[v] = p[v];
+}
+
+// A wave's stream over its ntile DB tiles with an explicit two-buffer ping-pong (the
+// loads of tile t+1 are in flight while tile t's 28*NQ MFMAs run; no register copies,
+// so the compiler's counted vmcnt waits only for the tile being consumed).
+template <int NQ, bool FROM_LDS, typename BV>
+__device__ __forceinline__ void stream_tiles(const float4 *dp, int ntile, int rbase0, BV &bval,
+                                             const float4 *qsh, int lane,
+                                             float (&te)[NQ][SCREEN_K],
+                                             int (&ti)[NQ][SCREEN_K]) {
+    float4 b0[7], b1[7];
+    load_tile(b0, dp);
+    int tile = 0;
+    for (; tile + 1 < ntile; tile += 2) {
+        load_tile(b1, dp + (long)(tile + 1) * TILE_VEC);
+        screen_tile<NQ, FROM_LDS>(b0, bval, qsh, lane, te, ti, rbase0 + tile * 32);
+        // unconditional (clamped) reload: a load under a branch makes the compiler's
+        // waitcnt at the join conservative and stalls the next tile on it
+        const int nxt = tile + 2 < ntile ? tile + 2 : ntile - 1;
+        load_tile(b0, dp + (long)nxt * TILE_VEC);
+        screen_tile<NQ, FROM_LDS>(b1, bval, qsh, lane, te, ti, rbase0 + (tile + 1) * 32);
+    }
+    if (tile < ntile) screen_tile<NQ, FROM_LDS>(b0, bval, qsh, lane, te, ti, rbase0 + tile * 32);
+}
+
 // grid: (nchunks rounded up to 8) x groups workgroups, XCD-aware: all query groups of a
 // chunk share blockIdx % 8 (one XCD under round-robin dispatch) so the chunk's rows are
 // fetched from HBM once and re-read from that XCD's L2.
@@ -91,53 +171,9 @@ __global__ __launch_bounds__(256) void k_screen(const float *__restrict__ db, in
     const long row_begin = (long)chunk * ch + wv * rows_per_wave;
     // lane (j, h) streams DB row (tile*32 + j), elements k = 2s + h
     const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
-    constexpr int TILE_VEC = 32 * IA_DP / 4;   // float4s per 32-row tile
-
-    float4 an[7];
-#pragma unroll
-    for (int v = 0; v < 7; ++v) an[v] = dp[v];
-
-    for (int tile = 0; tile < ntile; ++tile) {
-        float4 a4[7];
-#pragma unroll
-        for (int v = 0; v < 7; ++v) a4[v] = an[v];
-        if (tile + 1 < ntile) {
-            const float4 *np_ = dp + (long)(tile + 1) * TILE_VEC;
-#pragma unroll
-            for (int v = 0; v < 7; ++v) an[v] = np_[v];
-        }
-        floatx16 acc[NQ];
-#pragma unroll
-        for (int qt = 0; qt < NQ; ++qt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
-#pragma unroll
-        for (int v = 0; v < 7; ++v) {
-            const float av[4] = {a4[v].x, a4[v].y, a4[v].z, a4[v].w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int qt = 0; qt < NQ; ++qt)
-                    acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bq[qt][4 * v + u],
-                                                                   acc[qt], 0, 0, 0);
-        }
-        // epilogue: C[row i][col j] at lane (j, h), reg r: i = (r&3) + 8(r>>2) + 4h
-        const int rbase = (int)(row_begin - (long)chunk * ch) + tile * 32 + 4 * h;
-#pragma unroll
-        for (int qt = 0; qt < NQ; ++qt) {
-            float mn = acc[qt][0];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) mn = fminf(mn, acc[qt][r]);
-            if (mn < te[qt][SCREEN_K - 1]) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float v = acc[qt][r];
-                    if (v < te[qt][SCREEN_K - 1])
-                        topk_insert(te[qt], ti[qt], v, rbase + (r & 3) + 8 * (r >> 2));
-                }
-            }
-        }
-    }
+    const int rbase0 = (int)(row_begin - (long)chunk * ch) + 4 * h;
+    auto bval = [&](int qt, int v, int u) { return bq[qt][4 * v + u]; };
+    stream_tiles<NQ, false>(dp, ntile, rbase0, bval, nullptr, lane, te, ti);
 
     // merge the 8 per-lane lists of each query (4 waves x 2 row halves) through LDS
 #pragma unroll
@@ -169,27 +205,317 @@ __global__ __launch_bounds__(256) void k_screen(const float *__restrict__ db, in
     }
 }
 
-int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
-                  hipStream_t st) {
+// Variant with the query group staged once per block in LDS (shared by the 4 waves)
+// instead of 28*NQ VGPRs per wave: B operands come from ds_read_b128 (4 k-steps per
+// read), which frees registers for up to 6 query tiles per wave — fewer query groups,
+// so each DB chunk is re-read fewer times and each A fragment feeds 28*NQ MFMAs.
+template <int NQ>
+__global__ __launch_bounds__(256, NQ <= 3 ? 2 : 1) void k_screen_lds(const float *__restrict__ db, int nchunks,
+                                                    int ch, const float *__restrict__ qp, int M,
+                                                    int groups, Cand *__restrict__ cand) {
+    constexpr int QVEC = NQ * 7 * 64;                                  // float4s of queries
+    constexpr int LBYTES = NQ * 32 * 8 * SCREEN_K * 8;                 // merge lists
+    constexpr int SBYTES = (QVEC * 16 > LBYTES) ? QVEC * 16 : LBYTES;
+    __shared__ __attribute__((aligned(16))) char smem[SBYTES];
+    float4 *qsh = reinterpret_cast<float4 *>(smem);
+
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int j = lane & 31, h = lane >> 5;
+
+    // stage B fragments: qsh[(qt*7 + v)*64 + lane] = B[k = 2(4v+u) + h][col j], u = 0..3
+    for (int i = tid; i < QVEC; i += 256) {
+        const int qt = i / 448, rem = i - qt * 448;
+        const int v = rem >> 6, l = rem & 63;
+        qsh[i] = *reinterpret_cast<const float4 *>(
+            qp + (long)((group * NQ + qt) * 32 + (l & 31)) * IA_DP + (l >> 5) * 28 + 4 * v);
+    }
+    __syncthreads();
+
+    float te[NQ][SCREEN_K];
+    int ti[NQ][SCREEN_K];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) { te[qt][k] = FLT_MAX; ti[qt][k] = -1; }
+
+    const int rows_per_wave = ch >> 2;
+    const int ntile = rows_per_wave >> 5;
+    const long row_begin = (long)chunk * ch + wv * rows_per_wave;
+    const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
+    const int rbase0 = (int)(row_begin - (long)chunk * ch) + 4 * h;
+    auto bval = [](int, int, int) { return 0.f; };
+    stream_tiles<NQ, true>(dp, ntile, rbase0, bval, qsh, lane, te, ti);
+
+    __syncthreads();   // queries no longer needed: the LDS becomes the merge lists
+    float(*le)[8][SCREEN_K] = reinterpret_cast<float(*)[8][SCREEN_K]>(smem);
+    int(*li)[8][SCREEN_K] = reinterpret_cast<int(*)[8][SCREEN_K]>(smem + NQ * 32 * 8 * SCREEN_K * 4);
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) {
+            le[qt * 32 + j][wv * 2 + h][k] = te[qt][k];
+            li[qt * 32 + j][wv * 2 + h][k] = ti[qt][k];
+        }
+    __syncthreads();
+    for (int t = tid; t < NQ * 32; t += 256) {
+        const int qg = group * NQ * 32 + t;
+        if (qg < M) {
+            float be[SCREEN_K];
+            int bi[SCREEN_K];
+#pragma unroll
+            for (int k = 0; k < SCREEN_K; ++k) { be[k] = FLT_MAX; bi[k] = -1; }
+            for (int l = 0; l < 8; ++l)
+#pragma unroll
+                for (int k = 0; k < SCREEN_K; ++k) {
+                    const float v = le[t][l][k];
+                    if (v < be[SCREEN_K - 1]) topk_insert(be, bi, v, li[t][l][k]);
+                }
+            Cand *o = cand + ((long)qg * nchunks + chunk) * SCREEN_K;
+            const int cbase = chunk * ch;
+#pragma unroll
+            for (int k = 0; k < SCREEN_K; ++k) o[k] = Cand{be[k], bi[k] < 0 ? -1 : cbase + bi[k]};
+        }
+    }
+}
+
+// ---- variant 2: software-pipelined screen --------------------------------------------
+// Queries in LDS (as variant 1) plus two accumulator sets: while the 28*NQ MFMAs of tile
+// t+1 run into one set, the wave reduces tile t's set (accvgpr reads + v_min3) in the
+// issue gaps between them (sched_group_barrier interleave: 1 MFMA, 1 VALU), so the
+// MFMA pipe no longer idles through each tile's epilogue.  The rare top-K insertion
+// (some lane's tile minimum beats its K-th best) runs after the interleaved block.
+template <int NQ>
+__device__ __forceinline__ void mfma_tile_lds(const float4 (&a4)[7], const float4 *qsh, int lane,
+                                              floatx16 (&acc)[NQ]) {
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
+#pragma unroll
+    for (int v = 0; v < 7; ++v) {
+        const float av[4] = {a4[v].x, a4[v].y, a4[v].z, a4[v].w};
+        float4 bl[NQ];
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt) bl[qt] = qsh[(qt * 7 + v) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt) {
+                const float bv = u == 0 ? bl[qt].x : u == 1 ? bl[qt].y : u == 2 ? bl[qt].z : bl[qt].w;
+                acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv, acc[qt], 0, 0, 0);
+            }
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void min_tile(const floatx16 (&acc)[NQ], float (&mn)[NQ]) {
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        float m = fminf(acc[qt][0], acc[qt][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) m = fminf(m, fminf(acc[qt][r], acc[qt][r + 1]));
+        mn[qt] = m;
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void interleave_mark() {
+#pragma unroll
+    for (int i = 0; i < 28 * NQ; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // 1 VALU
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void insert_tile(const floatx16 (&acc)[NQ], const float (&mn)[NQ],
+                                            float (&te)[NQ][SCREEN_K], int (&ti)[NQ][SCREEN_K],
+                                            int rbase) {
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        if (mn[qt] < te[qt][SCREEN_K - 1]) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = acc[qt][r];
+                if (x < te[qt][SCREEN_K - 1])
+                    topk_insert(te[qt], ti[qt], x, rbase + (r & 3) + 8 * (r >> 2));
+            }
+        }
+    }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256, 2) void k_screen_pipe(const float *__restrict__ db, int nchunks,
+                                                        int ch, const float *__restrict__ qp,
+                                                        int M, int groups,
+                                                        Cand *__restrict__ cand) {
+    constexpr int QVEC = NQ * 7 * 64;
+    constexpr int LBYTES = NQ * 32 * 8 * SCREEN_K * 8;
+    constexpr int SBYTES = (QVEC * 16 > LBYTES) ? QVEC * 16 : LBYTES;
+    __shared__ __attribute__((aligned(16))) char smem[SBYTES];
+    float4 *qsh = reinterpret_cast<float4 *>(smem);
+
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int j = lane & 31, h = lane >> 5;
+    for (int i = tid; i < QVEC; i += 256) {
+        const int qt = i / 448, rem = i - qt * 448;
+        const int v = rem >> 6, l = rem & 63;
+        qsh[i] = *reinterpret_cast<const float4 *>(
+            qp + (long)((group * NQ + qt) * 32 + (l & 31)) * IA_DP + (l >> 5) * 28 + 4 * v);
+    }
+    __syncthreads();
+
+    float te[NQ][SCREEN_K];
+    int ti[NQ][SCREEN_K];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) { te[qt][k] = FLT_MAX; ti[qt][k] = -1; }
+
+    const int rows_per_wave = ch >> 2;
+    const int n = rows_per_wave >> 5;
+    const long row_begin = (long)chunk * ch + wv * rows_per_wave;
+    const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
+    const int rbase0 = (int)(row_begin - (long)chunk * ch) + 4 * h;
+    auto at = [&](int t) { return dp + (long)(t < n ? t : n - 1) * TILE_VEC; };
+
+    float4 bufA[7], bufB[7];
+    floatx16 accA[NQ], accB[NQ];
+    float mn[NQ];
+    load_tile(bufA, at(0));
+    load_tile(bufB, at(1));
+    mfma_tile_lds<NQ>(bufA, qsh, lane, accA);
+    load_tile(bufA, at(2));
+    for (int t = 0; t < n; t += 2) {
+        // accA = tile t, bufB = tile t+1, bufA = tile t+2 (in flight)
+        if (t + 1 < n) {
+            mfma_tile_lds<NQ>(bufB, qsh, lane, accB);
+            min_tile<NQ>(accA, mn);
+            interleave_mark<NQ>();
+        } else {
+            min_tile<NQ>(accA, mn);
+        }
+        insert_tile<NQ>(accA, mn, te, ti, rbase0 + t * 32);
+        load_tile(bufB, at(t + 3));
+        if (t + 1 >= n) break;
+        if (t + 2 < n) {
+            mfma_tile_lds<NQ>(bufA, qsh, lane, accA);
+            min_tile<NQ>(accB, mn);
+            interleave_mark<NQ>();
+        } else {
+            min_tile<NQ>(accB, mn);
+        }
+        insert_tile<NQ>(accB, mn, te, ti, rbase0 + (t + 1) * 32);
+        load_tile(bufA, at(t + 4));
+    }
+
+    __syncthreads();
+    float(*le)[8][SCREEN_K] = reinterpret_cast<float(*)[8][SCREEN_K]>(smem);
+    int(*li)[8][SCREEN_K] = reinterpret_cast<int(*)[8][SCREEN_K]>(smem + NQ * 32 * 8 * SCREEN_K * 4);
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+        for (int k = 0; k < SCREEN_K; ++k) {
+            le[qt * 32 + j][wv * 2 + h][k] = te[qt][k];
+            li[qt * 32 + j][wv * 2 + h][k] = ti[qt][k];
+        }
+    __syncthreads();
+    for (int t = tid; t < NQ * 32; t += 256) {
+        const int qg = group * NQ * 32 + t;
+        if (qg < M) {
+            float be[SCREEN_K];
+            int bi[SCREEN_K];
+#pragma unroll
+            for (int k = 0; k < SCREEN_K; ++k) { be[k] = FLT_MAX; bi[k] = -1; }
+            for (int l = 0; l < 8; ++l)
+#pragma unroll
+                for (int k = 0; k < SCREEN_K; ++k) {
+                    const float v = le[t][l][k];
+                    if (v < be[SCREEN_K - 1]) topk_insert(be, bi, v, li[t][l][k]);
+                }
+            Cand *o = cand + ((long)qg * nchunks + chunk) * SCREEN_K;
+            const int cbase = chunk * ch;
+#pragma unroll
+            for (int k = 0; k < SCREEN_K; ++k) o[k] = Cand{be[k], bi[k] < 0 ? -1 : cbase + bi[k]};
+        }
+    }
+}
+
+// Default screen: variant 0 (queries in VGPRs, <= 3 query tiles per wave) measured
+// fastest on MI355X (tools/screen_bench, profiles/).  IA_SCREEN_VARIANT selects another
+// for A/B runs (bits 0-3 kind, 4-7 tile cap).
+int screen_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("IA_SCREEN_VARIANT");
+        v = e ? atoi(e) : 0;
+        if (v < 0 || (v & 15) > 2) v = 0;
+    }
+    return v;
+}
+
+int launch_screen_v(const float *db, long nrows, const float *qp, int M, Cand *cand, int variant,
+                    hipStream_t st) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
-    const QSplit qs = qsplit(M);
+    const int kind = variant & 15, nq_cap = (variant >> 4) & 15;
+    int maxnq = kind == 0 ? 3 : kind == 1 ? MAX_NQ : 3;
+    if (nq_cap > 0 && nq_cap < maxnq) maxnq = nq_cap;
+    const QSplit qs = qsplit(M, maxnq);
     const long nblocks = ((nchunks + 7) / 8) * 8 * qs.groups;
     IA_ARG(nblocks < (1L << 31), "screen grid too large");
-    switch (qs.nq) {
-#define IA_SCREEN_CASE(N)                                                                     \
+#define IA_SCREEN_CASE(K, N)                                                                  \
     case N:                                                                                   \
-        k_screen<N><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, qp, M, qs.groups, \
-                                                       cand);                                 \
+        K<N><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, qp, M, qs.groups, cand); \
         break;
-        IA_SCREEN_CASE(1)
-        IA_SCREEN_CASE(2)
-        IA_SCREEN_CASE(3)
-#undef IA_SCREEN_CASE
-        default: set_error("bad query split"); return IA_E_ARG;
+    if (kind == 0) {
+        switch (qs.nq) {
+            IA_SCREEN_CASE(k_screen, 1)
+            IA_SCREEN_CASE(k_screen, 2)
+            IA_SCREEN_CASE(k_screen, 3)
+            default: set_error("bad query split"); return IA_E_ARG;
+        }
+    } else if (kind == 2) {
+        switch (qs.nq) {
+            IA_SCREEN_CASE(k_screen_pipe, 1)
+            IA_SCREEN_CASE(k_screen_pipe, 2)
+            IA_SCREEN_CASE(k_screen_pipe, 3)
+            IA_SCREEN_CASE(k_screen_pipe, 4)
+            default: set_error("bad query split"); return IA_E_ARG;
+        }
+    } else {
+        switch (qs.nq) {
+            IA_SCREEN_CASE(k_screen_lds, 1)
+            IA_SCREEN_CASE(k_screen_lds, 2)
+            IA_SCREEN_CASE(k_screen_lds, 3)
+            IA_SCREEN_CASE(k_screen_lds, 4)
+            IA_SCREEN_CASE(k_screen_lds, 5)
+            IA_SCREEN_CASE(k_screen_lds, 6)
+            default: set_error("bad query split"); return IA_E_ARG;
+        }
     }
+#undef IA_SCREEN_CASE
     IA_LAUNCH_CHECK("k_screen");
     return IA_OK;
+}
+
+int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
+                  hipStream_t st) {
+    return launch_screen_v(db, nrows, qp, M, cand, screen_variant(), st);
 }
 
 // ---------------------------------------------------------------------------------
@@ -411,6 +737,32 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
     k_wdist<<<(n + 63) / 64, 64, 0, S(stream)>>>(a, q, w, n, out);
     IA_LAUNCH_CHECK("k_wdist");
     return IA_OK;
+}
+
+}  // extern "C"
+
+// ---- diagnostic entry points (include/ia_diag.h) ----------------------------------
+#include "../../include/ia_diag.h"
+
+extern "C" {
+
+size_t ia_diag_cand_bytes(int M, long nrows) {
+    return (size_t)qrows_alloc(M) * db_nchunks(nrows) * SCREEN_K * sizeof(Cand);
+}
+
+int ia_diag_qp_rows(int M) { return qrows_alloc(M); }
+
+int ia_diag_query_rows(const double *q64, int M, const double *center, float *qp, double *nq,
+                       void *stream) {
+    IA_ARG(q64 && center && qp && nq && M > 0, "ia_diag_query_rows: bad args");
+    return launch_query_rows(q64, M, center, qp, nq, S(stream));
+}
+
+int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand, int variant,
+                   void *stream) {
+    IA_ARG(db && qp && cand && M > 0 && nrows > 0 && (variant & 15) <= 2,
+           "ia_diag_screen: bad args");
+    return launch_screen_v(db, nrows, qp, M, reinterpret_cast<Cand *>(cand), variant, S(stream));
 }
 
 }  // extern "C"

@@ -1,0 +1,29 @@
+/* ia_diag.h — diagnostic entry points of libia.so (NOT part of the reference boundary).
+ * Used by tools/screen_bench (kernel A/B timing and rocprofv3 PMC runs outside any
+ * Python/torch process) to drive the matcher's stages one at a time.  Same conventions
+ * as ia.h: device pointers, void* hipStream_t, 0 / IA_E_* return codes. */
+#ifndef IA_DIAG_H
+#define IA_DIAG_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* bytes of the screen's candidate buffer for M queries over nrows DB rows */
+size_t ia_diag_cand_bytes(int M, long nrows);
+/* rows of the fp32 query buffer qp (IA_DP floats each) a screen of M queries reads */
+int ia_diag_qp_rows(int M);
+/* fp64 queries (M x IA_DP) -> MFMA-ordered fp32 qp + |q - c|^2 */
+int ia_diag_query_rows(const double *q64, int M, const double *center, float *qp, double *nq,
+                       void *stream);
+/* one screen launch; variant bits 0-3: 0 = queries in VGPRs, 1 = queries in LDS;
+ * bits 4-7: cap on query tiles per wave (0 = default) */
+int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand,
+                   int variant, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
