@@ -86,11 +86,19 @@ _SIGS = {
 _lib = None
 
 
-def declared_symbols():
-    """Function names declared in include/ia.h (the C-ABI contract)."""
-    src = open(HEADER).read()
-    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
-    return sorted(set(re.findall(r'\b(ia_[a-z0-9_]+)\s*\(', src)))
+def declared_symbols(header=None):
+    """Function names declared in include/ia.h (the C-ABI contract), or in every header
+    under include/ when header == 'all' (ia.h + the diagnostic ia_diag.h)."""
+    inc = os.path.dirname(HEADER)
+    if header == 'all':
+        paths = [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith('.h')]
+    else:
+        paths = [header or HEADER]
+    names = set()
+    for p in paths:
+        src = re.sub(r'/\*.*?\*/', '', open(p).read(), flags=re.S)
+        names.update(re.findall(r'\b(ia_[a-z0-9_]+)\s*\(', src))
+    return sorted(names)
 
 
 def lib():
