@@ -256,9 +256,10 @@ def main():
                      'algorithmic': '2*55 flop per (query,row) pair; this rank: %.4g pairs '
                                     'over %d launches' % (pairs, screens),
                      'screen_avg_us': screen_ms * 1e3 / max(screens, 1)},
-        'matcher': {'candidates_rescored': sum(p['candidates'] for p in prof),
-                    'overflow_chunks': sum(p['overflow_chunks'] for p in prof),
-                    'full_scans': sum(p['full_scans'] for p in prof)},
+        'matcher': {'rows_rescored_fp64': sum(p['rows_rescored'] for p in prof),
+                    'candidate_segments': sum(p['candidate_segments'] for p in prof),
+                    'full_scans': sum(p['full_scans'] for p in prof),
+                    'queries': pixels_per_step * args.steps // (world if args.config == 'c5' else 1)},
         'checks': {'replicas_identical': replicas_ok, 'checksum': chk},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -59,13 +59,19 @@ __global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nro
         float m = fmaxf(fmaxf(redmax[0], redmax[1]), fmaxf(redmax[2], redmax[3]));
         atomicMax(reinterpret_cast<unsigned int *>(amax), __float_as_uint(m));
     }
-    // coalesced copy-out: rows [blockIdx*256, +256) are contiguous in db
+    // fragment-major copy-out (the screen's operand order, ia_match.hip load_tile):
+    // float4 (tile T, v, lane l) = row T*32 + (l & 31), positions (l >> 5)*28 + 4v..4v+3.
+    // The block's 256 rows are 8 whole tiles, written as one contiguous 57 KB range.
     const long base = (long)blockIdx.x * 256;
-    const long rows_here = npad - base < 256 ? npad - base : 256;
+    const long rows_here = npad - base < 256 ? npad - base : 256;   // multiple of 32
     const long nvec = rows_here * IA_DP / 4;
     float4 *dst = reinterpret_cast<float4 *>(db + base * IA_DP);
-    const float4 *srcv = reinterpret_cast<const float4 *>(tile);
-    for (long i = threadIdx.x; i < nvec; i += 256) dst[i] = srcv[i];
+    for (long i = threadIdx.x; i < nvec; i += 256) {
+        const int T = (int)(i / (7 * 64)), rem = (int)(i - (long)T * 7 * 64);
+        const int v = rem >> 6, l = rem & 63;
+        const float *s = tile + (T * 32 + (l & 31)) * IA_DP + (l >> 5) * 28 + 4 * v;
+        dst[i] = make_float4(s[0], s[1], s[2], s[3]);
+    }
 }
 
 __global__ void k_center_fill(double *c, double mA, double mAp) {

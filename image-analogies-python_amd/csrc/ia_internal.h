@@ -10,10 +10,11 @@ namespace ia {
 constexpr int SCREEN_K = 4;            // candidates kept per (query, chunk)
 constexpr int TARGET_CHUNKS = 1024;
 
+// tiles per wave: a power of two in [1, 64] (so screen segments divide it)
 static inline int db_chunk_rows(long nrows) {
-    long tpw = (nrows + (long)TARGET_CHUNKS * 128 - 1) / ((long)TARGET_CHUNKS * 128);
-    if (tpw < 1) tpw = 1;
-    if (tpw > 64) tpw = 64;
+    const long want = (nrows + (long)TARGET_CHUNKS * 128 - 1) / ((long)TARGET_CHUNKS * 128);
+    long tpw = 1;
+    while (tpw < want && tpw < 64) tpw <<= 1;
     return (int)(128 * tpw);
 }
 static inline long db_nchunks(long nrows) {
@@ -21,6 +22,12 @@ static inline long db_nchunks(long nrows) {
     return (nrows + ch - 1) / ch;
 }
 static inline long db_rows_padded(long nrows) { return db_nchunks(nrows) * db_chunk_rows(nrows); }
+// segment-minimum matcher: one running minimum per (query, segment) of <= 512 rows
+static inline int db_seg_rows(long nrows) {
+    const int rpw = db_chunk_rows(nrows) / 4;
+    return rpw < 512 ? rpw : 512;
+}
+static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_rows(nrows); }
 
 struct Cand {            // one screen candidate: fp32 screen value + local row
     float e;
@@ -73,5 +80,18 @@ int launch_screen_v(const float *db, long nrows, const float *qp, int M, Cand *c
 int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int M,
                  const double *q64, const double *nq, const float *amax, Best *best,
                  unsigned long long *stats, hipStream_t st);
+// the whole exact matcher (screen + exact stage) with the selected algorithm
+// (IA_MATCH_ALG: 1 segment minima [default], 0 per-lane top-K); scratch of
+// match_scratch_bytes(qrows_alloc(M), nrows).  stats (segment alg): rows rescored,
+// candidate segments, full scans.
+size_t match_scratch_bytes(int qrows, long nrows);
+// ev0 / ev1 (nullable) are recorded on st immediately before / after the screen launch.
+int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp, int M,
+                 const double *q64, const double *nq, const float *amax, void *scratch,
+                 Best *best, unsigned long long *stats, hipStream_t st,
+                 hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
+                      int maxnq, hipStream_t st);
+int screen_variant();
 
 }  // namespace ia

@@ -97,16 +97,24 @@ __device__ __forceinline__ void screen_tile(const float4 (&a4)[7], BV &bval,
     }
 }
 
+// DB tiles are fragment-major (ia_features.hip k_db_build): float4 (tile, v, lane) holds
+// lane (j, h)'s k-steps 4v..4v+3 of row tile*32 + j, so each of the 7 loads of a tile
+// is one contiguous 1 KiB wave access.  p = tile base + lane.
 __device__ __forceinline__ void load_tile(float4 (&a)[7], const float4 *p) {
 #pragma unroll
-    for (int v = 0; v < 7; ++v) a[v] = p[v];
+    for (int v = 0; v < 7; ++v) a[v] = p[v * 64];
+}
+
+// first float4 of this lane in the tile containing DB row `row` (a multiple of 32)
+__device__ __forceinline__ const float4 *tile_ptr(const float *db, long row, int lane) {
+    return reinterpret_cast<const float4 *>(db) + (row >> 5) * TILE_VEC + lane;
 }
 
 // A wave's stream over its ntile DB tiles with an explicit two-buffer ping-pong (the
 // loads of tile t+1 are in flight while tile t's 28*NQ MFMAs run; no register copies,
 // so the compiler's counted vmcnt waits only for the tile being consumed).
 template <int NQ, bool FROM_LDS, typename BV>
-__device__ __forceinline__ void stream_tiles(const float4 *dp, int ntile, int rbase0, BV &bval,
+__device__ __forceinline__ void stream_tiles(const float4 *dp, int ntile, long stride, int rbase0, BV &bval,
                                              const float4 *qsh, int lane,
                                              float (&te)[NQ][SCREEN_K],
                                              int (&ti)[NQ][SCREEN_K]) {
@@ -114,21 +122,46 @@ __device__ __forceinline__ void stream_tiles(const float4 *dp, int ntile, int rb
     load_tile(b0, dp);
     int tile = 0;
     for (; tile + 1 < ntile; tile += 2) {
-        load_tile(b1, dp + (long)(tile + 1) * TILE_VEC);
+        load_tile(b1, dp + (long)(tile + 1) * stride);
         screen_tile<NQ, FROM_LDS>(b0, bval, qsh, lane, te, ti, rbase0 + tile * 32);
         // unconditional (clamped) reload: a load under a branch makes the compiler's
         // waitcnt at the join conservative and stalls the next tile on it
         const int nxt = tile + 2 < ntile ? tile + 2 : ntile - 1;
-        load_tile(b0, dp + (long)nxt * TILE_VEC);
+        load_tile(b0, dp + (long)nxt * stride);
         screen_tile<NQ, FROM_LDS>(b1, bval, qsh, lane, te, ti, rbase0 + (tile + 1) * 32);
     }
     if (tile < ntile) screen_tile<NQ, FROM_LDS>(b0, bval, qsh, lane, te, ti, rbase0 + tile * 32);
 }
 
+// Three-buffer ring: tile t+2's loads are issued while tile t computes (prefetch
+// distance two tiles), for when one tile of MFMA work does not cover HBM latency.
+template <int NQ, bool FROM_LDS, typename BV>
+__device__ __forceinline__ void stream_tiles3(const float4 *dp, int ntile, long stride, int rbase0, BV &bval,
+                                              const float4 *qsh, int lane,
+                                              float (&te)[NQ][SCREEN_K],
+                                              int (&ti)[NQ][SCREEN_K]) {
+    float4 b0[7], b1[7], b2[7];
+    auto at = [&](int t) { return dp + (long)(t < ntile ? t : ntile - 1) * stride; };
+    load_tile(b0, at(0));
+    load_tile(b1, at(1));
+    int tile = 0;
+    for (; tile + 2 < ntile; tile += 3) {
+        load_tile(b2, at(tile + 2));
+        screen_tile<NQ, FROM_LDS>(b0, bval, qsh, lane, te, ti, rbase0 + tile * 32);
+        load_tile(b0, at(tile + 3));
+        screen_tile<NQ, FROM_LDS>(b1, bval, qsh, lane, te, ti, rbase0 + (tile + 1) * 32);
+        load_tile(b1, at(tile + 4));
+        screen_tile<NQ, FROM_LDS>(b2, bval, qsh, lane, te, ti, rbase0 + (tile + 2) * 32);
+    }
+    if (tile < ntile) screen_tile<NQ, FROM_LDS>(b0, bval, qsh, lane, te, ti, rbase0 + tile * 32);
+    if (tile + 1 < ntile)
+        screen_tile<NQ, FROM_LDS>(b1, bval, qsh, lane, te, ti, rbase0 + (tile + 1) * 32);
+}
+
 // grid: (nchunks rounded up to 8) x groups workgroups, XCD-aware: all query groups of a
 // chunk share blockIdx % 8 (one XCD under round-robin dispatch) so the chunk's rows are
 // fetched from HBM once and re-read from that XCD's L2.
-template <int NQ>
+template <int NQ, int MODE = 0>
 __global__ __launch_bounds__(256) void k_screen(const float *__restrict__ db, int nchunks,
                                                 int ch, const float *__restrict__ qp, int M,
                                                 int groups, Cand *__restrict__ cand) {
@@ -170,10 +203,13 @@ __global__ __launch_bounds__(256) void k_screen(const float *__restrict__ db, in
     const int ntile = rows_per_wave >> 5;
     const long row_begin = (long)chunk * ch + wv * rows_per_wave;
     // lane (j, h) streams DB row (tile*32 + j), elements k = 2s + h
-    const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
+    const float4 *dp = tile_ptr(db, row_begin, lane);
     const int rbase0 = (int)(row_begin - (long)chunk * ch) + 4 * h;
     auto bval = [&](int qt, int v, int u) { return bq[qt][4 * v + u]; };
-    stream_tiles<NQ, false>(dp, ntile, rbase0, bval, nullptr, lane, te, ti);
+    if constexpr (MODE == 0) stream_tiles<NQ, false>(dp, ntile, TILE_VEC, rbase0, bval, nullptr, lane, te, ti);
+    else if constexpr (MODE == 1) stream_tiles3<NQ, false>(dp, ntile, TILE_VEC, rbase0, bval, nullptr, lane, te, ti);
+    else if constexpr (MODE == 2) stream_tiles<NQ, false>(dp, ntile, 0, rbase0, bval, nullptr, lane, te, ti);
+    else stream_tiles3<NQ, false>(dp, ntile, 0, rbase0, bval, nullptr, lane, te, ti);
 
     // merge the 8 per-lane lists of each query (4 waves x 2 row halves) through LDS
 #pragma unroll
@@ -248,10 +284,10 @@ __global__ __launch_bounds__(256, NQ <= 3 ? 2 : 1) void k_screen_lds(const float
     const int rows_per_wave = ch >> 2;
     const int ntile = rows_per_wave >> 5;
     const long row_begin = (long)chunk * ch + wv * rows_per_wave;
-    const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
+    const float4 *dp = tile_ptr(db, row_begin, lane);
     const int rbase0 = (int)(row_begin - (long)chunk * ch) + 4 * h;
     auto bval = [](int, int, int) { return 0.f; };
-    stream_tiles<NQ, true>(dp, ntile, rbase0, bval, qsh, lane, te, ti);
+    stream_tiles<NQ, true>(dp, ntile, TILE_VEC, rbase0, bval, qsh, lane, te, ti);
 
     __syncthreads();   // queries no longer needed: the LDS becomes the merge lists
     float(*le)[8][SCREEN_K] = reinterpret_cast<float(*)[8][SCREEN_K]>(smem);
@@ -389,7 +425,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_pipe(const float *__restrict_
     const int rows_per_wave = ch >> 2;
     const int n = rows_per_wave >> 5;
     const long row_begin = (long)chunk * ch + wv * rows_per_wave;
-    const float4 *dp = reinterpret_cast<const float4 *>(db + (row_begin + j) * IA_DP + h * 28);
+    const float4 *dp = tile_ptr(db, row_begin, lane);
     const int rbase0 = (int)(row_begin - (long)chunk * ch) + 4 * h;
     auto at = [&](int t) { return dp + (long)(t < n ? t : n - 1) * TILE_VEC; };
 
@@ -463,7 +499,7 @@ int screen_variant() {
     if (v < 0) {
         const char *e = getenv("IA_SCREEN_VARIANT");
         v = e ? atoi(e) : 0;
-        if (v < 0 || (v & 15) > 2) v = 0;
+        if (v < 0 || (v & 15) > 3) v = 0;
     }
     return v;
 }
@@ -472,8 +508,12 @@ int launch_screen_v(const float *db, long nrows, const float *qp, int M, Cand *c
                     hipStream_t st) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
+    // kinds: 0 registers/2-deep, 1 LDS queries, 2 pipelined epilogue, 3 registers/3-deep;
+    // diagnostic only: 4 / 5 = kinds 0 / 3 re-reading ONE tile per wave (L2-hot, wrong
+    // results) to separate memory latency from issue limits.
     const int kind = variant & 15, nq_cap = (variant >> 4) & 15;
-    int maxnq = kind == 0 ? 3 : kind == 1 ? MAX_NQ : 3;
+    int maxnq = (kind == 1) ? MAX_NQ : 3;
+    if (kind == 3 || kind == 5) maxnq = 2;
     if (nq_cap > 0 && nq_cap < maxnq) maxnq = nq_cap;
     const QSplit qs = qsplit(M, maxnq);
     const long nblocks = ((nchunks + 7) / 8) * 8 * qs.groups;
@@ -482,13 +522,41 @@ int launch_screen_v(const float *db, long nrows, const float *qp, int M, Cand *c
     case N:                                                                                   \
         K<N><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, qp, M, qs.groups, cand); \
         break;
-    if (kind == 0) {
-        switch (qs.nq) {
-            IA_SCREEN_CASE(k_screen, 1)
-            IA_SCREEN_CASE(k_screen, 2)
-            IA_SCREEN_CASE(k_screen, 3)
-            default: set_error("bad query split"); return IA_E_ARG;
+#define IA_SCREEN_CASE_M(N, MODE)                                                             \
+    case N:                                                                                   \
+        k_screen<N, MODE><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, qp, M,     \
+                                                             qs.groups, cand);                \
+        break;
+    if (kind == 0 || kind == 3 || kind == 4 || kind == 5) {
+        const int mode = kind == 0 ? 0 : kind == 3 ? 1 : kind == 4 ? 2 : 3;
+        if (mode == 0) {
+            switch (qs.nq) {
+                IA_SCREEN_CASE_M(1, 0)
+                IA_SCREEN_CASE_M(2, 0)
+                IA_SCREEN_CASE_M(3, 0)
+                default: set_error("bad query split"); return IA_E_ARG;
+            }
+        } else if (mode == 1) {
+            switch (qs.nq) {
+                IA_SCREEN_CASE_M(1, 1)
+                IA_SCREEN_CASE_M(2, 1)
+                default: set_error("bad query split"); return IA_E_ARG;
+            }
+        } else if (mode == 2) {
+            switch (qs.nq) {
+                IA_SCREEN_CASE_M(1, 2)
+                IA_SCREEN_CASE_M(2, 2)
+                IA_SCREEN_CASE_M(3, 2)
+                default: set_error("bad query split"); return IA_E_ARG;
+            }
+        } else {
+            switch (qs.nq) {
+                IA_SCREEN_CASE_M(1, 3)
+                IA_SCREEN_CASE_M(2, 3)
+                default: set_error("bad query split"); return IA_E_ARG;
+            }
         }
+#undef IA_SCREEN_CASE_M
     } else if (kind == 2) {
         switch (qs.nq) {
             IA_SCREEN_CASE(k_screen_pipe, 1)
@@ -625,6 +693,276 @@ int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int 
     return IA_OK;
 }
 
+// =================================================================================
+// Segment-minimum matcher (default): the screen keeps NO per-row state, only the
+// running minimum of e per (query, 512-row segment) — 8 v_min3 per 16 values, branch
+// free — and the exact stage re-screens just the segments whose minimum lies inside the
+// error window.  Exactness: the oracle's winner r_o has e(r_o) <= e* + 2 eps_q (e* the
+// global minimum), so its segment's minimum is inside the window; inside a candidate
+// segment a VALU fp32 recomputation e'(r) obeys the same bound, so every row with
+// e'(r) <= e* + 2 eps_q (+ slack) is rescored in fp64 and r_o is among them.
+// =================================================================================
+template <int NQ>
+__global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db, int nchunks,
+                                                    int ch, int seg_rows,
+                                                    const float *__restrict__ qp, int M,
+                                                    int groups, float *__restrict__ segmin,
+                                                    long nseg) {
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int j = lane & 31, h = lane >> 5;
+
+    float bq[NQ][28];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        const float4 *p = reinterpret_cast<const float4 *>(
+            qp + (long)((group * NQ + qt) * 32 + j) * IA_DP + h * 28);
+#pragma unroll
+        for (int v = 0; v < 7; ++v) {
+            const float4 x = p[v];
+            bq[qt][4 * v] = x.x; bq[qt][4 * v + 1] = x.y;
+            bq[qt][4 * v + 2] = x.z; bq[qt][4 * v + 3] = x.w;
+        }
+    }
+    const int rows_per_wave = ch >> 2;
+    const int ntile = rows_per_wave >> 5;
+    const int tps = seg_rows >> 5;                          // tiles per segment
+    const long row_begin = (long)chunk * ch + wv * rows_per_wave;
+    const long seg_begin = row_begin / seg_rows;
+    const float4 *dp = tile_ptr(db, row_begin, lane);
+
+    float mn[NQ];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) mn[qt] = FLT_MAX;
+
+    auto tile_min = [&](const float4 (&a4)[7]) {
+        floatx16 acc[NQ];
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
+#pragma unroll
+        for (int v = 0; v < 7; ++v) {
+            const float av[4] = {a4[v].x, a4[v].y, a4[v].z, a4[v].w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt)
+                    acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bq[qt][4 * v + u],
+                                                                   acc[qt], 0, 0, 0);
+        }
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt) {
+            float m = mn[qt];
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) m = fminf(m, fminf(acc[qt][r], acc[qt][r + 1]));
+            mn[qt] = m;
+        }
+    };
+    auto flush = [&](int tile) {   // after the last tile of a segment
+        const long seg = seg_begin + tile / tps;
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt) {
+            const float m = fminf(mn[qt], __shfl_xor(mn[qt], 32));
+            const int qg = (group * NQ + qt) * 32 + j;
+            if (h == 0 && qg < M) segmin[(long)qg * nseg + seg] = m;
+            mn[qt] = FLT_MAX;
+        }
+    };
+
+    float4 b0[7], b1[7];
+    load_tile(b0, dp);
+    int tile = 0;
+    for (; tile + 1 < ntile; tile += 2) {
+        load_tile(b1, dp + (long)(tile + 1) * TILE_VEC);
+        tile_min(b0);
+        if ((tile + 1) % tps == 0) flush(tile);
+        const int nxt = tile + 2 < ntile ? tile + 2 : ntile - 1;
+        load_tile(b0, dp + (long)nxt * TILE_VEC);
+        tile_min(b1);
+        if ((tile + 2) % tps == 0) flush(tile + 1);
+    }
+    if (tile < ntile) {
+        tile_min(b0);
+        flush(tile);
+    }
+}
+
+constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
+
+// Exact stage of the segment-minimum matcher: one 256-thread workgroup per query.
+__global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrows, long nseg,
+                                                 int seg_rows, const float *__restrict__ segmin,
+                                                 const float *__restrict__ db,
+                                                 const float *__restrict__ qp,
+                                                 const double *__restrict__ q64,
+                                                 const double *__restrict__ nq,
+                                                 const float *__restrict__ amax,
+                                                 Best *__restrict__ best,
+                                                 unsigned long long *stats) {
+    __shared__ int slist[RESCORE_SEGCAP];
+    __shared__ int scount;
+    __shared__ float redf[4];
+    __shared__ double redd[4];
+    __shared__ long long redi[4];
+    __shared__ double qs[IA_DP];
+    __shared__ float qf[IA_DP];
+    __shared__ unsigned int nresc;
+
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (tid < IA_DP) {
+        qs[tid] = q64[(long)q * IA_DP + tid];
+        qf[tid] = qp[(long)q * IA_DP + tid];
+    }
+    if (tid == 0) { scount = 0; nresc = 0; }
+    const float *sq = segmin + (long)q * nseg;
+
+    float emin = FLT_MAX;
+    const float4 *sq4 = reinterpret_cast<const float4 *>(sq);
+    for (long i = tid; i < nseg / 4; i += 256) {
+        const float4 x = sq4[i];
+        emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
+    }
+    for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
+    if ((tid & 63) == 0) redf[tid >> 6] = emin;
+    __syncthreads();
+    emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
+
+    const double A = (double)amax[0];
+    const double nqq = nq[q];
+    const double eps = 70.0 * 5.9604644775390625e-08 * (2.0 * A * sqrt(nqq) + A * A);
+    const double T = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
+
+    for (long s = tid; s < nseg; s += 256) {
+        if ((double)sq[s] <= T) {
+            const int pos = atomicAdd(&scount, 1);
+            if (pos < RESCORE_SEGCAP) slist[pos] = (int)s;
+        }
+    }
+    __syncthreads();
+    const int ns = scount;
+    const bool full = ns > RESCORE_SEGCAP;
+    const long nscan = full ? nseg : ns;
+
+    double bd = INFINITY;
+    long long bi = 0x7fffffffffffffffLL;
+    unsigned int mine = 0;
+    for (long i = 0; i < nscan; ++i) {
+        const long seg = full ? i : slist[i];
+        for (int rr = tid; rr < seg_rows; rr += 256) {
+            const long lr = seg * seg_rows + rr;
+            if (lr >= nrows) continue;
+            // fp32 recomputation from the fragment-major DB (row lr = tile*32 + jj)
+            const float4 *t4 = reinterpret_cast<const float4 *>(db) + (lr >> 5) * TILE_VEC + (lr & 31);
+            float e = 0.f;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                for (int v = 0; v < 7; ++v) {
+                    const float4 x = t4[v * 64 + hh * 32];
+                    const float *qv = qf + hh * 28 + 4 * v;
+                    e = fmaf(x.x, qv[0], e);
+                    e = fmaf(x.y, qv[1], e);
+                    e = fmaf(x.z, qv[2], e);
+                    e = fmaf(x.w, qv[3], e);
+                }
+            if ((double)e <= T) {
+                ++mine;
+                best_update(bd, bi, row_dist2(src, row0 + lr, qs), row0 + lr);
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o);
+        const long long oi = __shfl_xor(bi, o);
+        best_update(bd, bi, od, oi);
+    }
+    if (mine) atomicAdd(&nresc, mine);
+    if ((tid & 63) == 0) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w) best_update(bd, bi, redd[w], redi[w]);
+        best[q] = Best{bd, bi};
+        if (stats) {
+            atomicAdd(&stats[0], (unsigned long long)nresc);
+            atomicAdd(&stats[1], (unsigned long long)ns);
+            atomicAdd(&stats[2], full ? 1ULL : 0ULL);
+        }
+    }
+}
+
+int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
+                      int maxnq, hipStream_t st) {
+    const int ch = db_chunk_rows(nrows);
+    const long nchunks = db_nchunks(nrows);
+    const int seg_rows = db_seg_rows(nrows);
+    const long nseg = db_nsegs(nrows);
+    const QSplit qs = qsplit(M, maxnq);
+    const long nblocks = ((nchunks + 7) / 8) * 8 * qs.groups;
+    IA_ARG(nblocks < (1L << 31), "screen grid too large");
+    switch (qs.nq) {
+#define IA_SEG_CASE(N)                                                                        \
+    case N:                                                                                   \
+        k_screen_seg<N><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, qp, \
+                                                           M, qs.groups, segmin, nseg);       \
+        break;
+        IA_SEG_CASE(1)
+        IA_SEG_CASE(2)
+        IA_SEG_CASE(3)
+#undef IA_SEG_CASE
+        default: set_error("bad query split"); return IA_E_ARG;
+    }
+    IA_LAUNCH_CHECK("k_screen_seg");
+    return IA_OK;
+}
+
+int match_alg() {
+    static int a = -1;
+    if (a < 0) {
+        const char *e = getenv("IA_MATCH_ALG");   // 0 = per-lane top-K, 1 = segment minima
+        a = e ? atoi(e) : 1;
+        if (a < 0 || a > 1) a = 1;
+    }
+    return a;
+}
+
+size_t match_scratch_bytes(int qrows, long nrows) {
+    const size_t a = (size_t)qrows * db_nchunks(nrows) * SCREEN_K * sizeof(Cand);
+    const size_t b = (size_t)qrows * db_nsegs(nrows) * sizeof(float);
+    return a > b ? a : b;
+}
+
+int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp, int M,
+                 const double *q64, const double *nq, const float *amax, void *scratch,
+                 Best *best, unsigned long long *stats, hipStream_t st, hipEvent_t ev0,
+                 hipEvent_t ev1) {
+    int rc;
+    if (ev0) IA_HIP(hipEventRecord(ev0, st));
+    if (match_alg() == 0) {
+        Cand *cand = reinterpret_cast<Cand *>(scratch);
+        if ((rc = launch_screen(db, nrows, qp, M, cand, st))) return rc;
+        if (ev1) IA_HIP(hipEventRecord(ev1, st));
+        return launch_merge(src, row0, nrows, cand, M, q64, nq, amax, best, stats, st);
+    }
+    float *segmin = reinterpret_cast<float *>(scratch);
+    const int nq_cap = (screen_variant() >> 4) & 15;
+    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, nq_cap > 0 && nq_cap < 3 ? nq_cap : 2,
+                                st)))
+        return rc;
+    if (ev1) IA_HIP(hipEventRecord(ev1, st));
+    k_rescore<<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows), segmin, db,
+                                 qp, q64, nq, amax, best, stats);
+    IA_LAUNCH_CHECK("k_rescore");
+    return IA_OK;
+}
+
 __global__ void k_split_best(const Best *b, int M, int64_t *idx, double *dist) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M) return;
@@ -684,7 +1022,7 @@ size_t ia_match_workspace_bytes(int M, long nrows) {
     size_t b = 0;
     b += align_up((size_t)qr * IA_DP * sizeof(float), 256);                        // qp
     b += align_up((size_t)qr * sizeof(double), 256);                               // nq
-    b += align_up((size_t)qr * db_nchunks(nrows) * SCREEN_K * sizeof(Cand), 256);  // cand
+    b += align_up(match_scratch_bytes(qr, nrows), 256);                           // screen out
     b += align_up((size_t)qr * sizeof(Best), 256);                                 // best
     return b;
 }
@@ -702,8 +1040,8 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
     w += align_up((size_t)qr * IA_DP * sizeof(float), 256);
     double *nq = reinterpret_cast<double *>(w);
     w += align_up((size_t)qr * sizeof(double), 256);
-    Cand *cand = reinterpret_cast<Cand *>(w);
-    w += align_up((size_t)qr * db_nchunks(a->nrows) * SCREEN_K * sizeof(Cand), 256);
+    void *scratch = w;
+    w += align_up(match_scratch_bytes(qr, a->nrows), 256);
     Best *best = reinterpret_cast<Best *>(w);
     IA_HIP(hipMemsetAsync(qp, 0, (size_t)qr * IA_DP * sizeof(float), st));
     const DbSrc src = make_dbsrc(a->src);
@@ -712,9 +1050,8 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
         const double *q = a->q64 + (long)m0 * IA_DP;
         int rc;
         if ((rc = launch_query_rows(q, M, a->center, qp, nq, st))) return rc;
-        if ((rc = launch_screen(a->db, a->nrows, qp, M, cand, st))) return rc;
-        if ((rc = launch_merge(src, a->row0, a->nrows, cand, M, q, nq, a->amax, best, nullptr,
-                               st)))
+        if ((rc = launch_match(src, a->row0, a->nrows, a->db, qp, M, q, nq, a->amax, scratch,
+                               best, nullptr, st)))
             return rc;
         k_split_best<<<(M + 255) / 256, 256, 0, st>>>(best, M, a->idx ? a->idx + m0 : nullptr,
                                                       a->dist ? a->dist + m0 : nullptr);
@@ -746,9 +1083,7 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
 
 extern "C" {
 
-size_t ia_diag_cand_bytes(int M, long nrows) {
-    return (size_t)qrows_alloc(M) * db_nchunks(nrows) * SCREEN_K * sizeof(Cand);
-}
+size_t ia_diag_cand_bytes(int M, long nrows) { return match_scratch_bytes(qrows_alloc(M), nrows); }
 
 int ia_diag_qp_rows(int M) { return qrows_alloc(M); }
 
@@ -760,8 +1095,13 @@ int ia_diag_query_rows(const double *q64, int M, const double *center, float *qp
 
 int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand, int variant,
                    void *stream) {
-    IA_ARG(db && qp && cand && M > 0 && nrows > 0 && (variant & 15) <= 2,
+    IA_ARG(db && qp && cand && M > 0 && nrows > 0 && (variant & 15) <= 6,
            "ia_diag_screen: bad args");
+    if ((variant & 15) == 6) {   // segment-minimum screen (the default matcher's stage 1)
+        const int cap = (variant >> 4) & 15;
+        return launch_screen_seg(db, nrows, qp, M, reinterpret_cast<float *>(cand),
+                                 cap > 0 && cap <= 3 ? cap : 2, S(stream));
+    }
     return launch_screen_v(db, nrows, qp, M, reinterpret_cast<Cand *>(cand), variant, S(stream));
 }
 

@@ -10,8 +10,8 @@
 // scanline loop reads (DESIGN.md gives the case analysis; tests/test_oracle.py checks it
 // exhaustively for small H, W).  Per wave:
 //   k_query_wave  -> q64 / qp / nq       (ia_features.hip)
-//   k_screen      -> cand                (ia_match.hip, MFMA)
-//   k_merge       -> best (this shard)   (ia_match.hip, exact fp64)
+//   k_screen_seg  -> segment minima     (ia_match.hip, MFMA)
+//   k_rescore     -> best (this shard)   (ia_match.hip, exact fp64)
 //   [RCCL all-gather of best over ranks when the DB is sharded]
 //   k_finish      -> coherence, kappa test, B'/s/im update (this file)
 #include "ia_internal.h"
@@ -113,7 +113,7 @@ struct SynthWs {
     double *q64;
     float *qp;
     double *nq;
-    Cand *cand;
+    void *scratch;           // screen output (candidates or segment minima)
     Best *best_local;
     Best *best_all;
     unsigned long long *stats;
@@ -133,7 +133,7 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     w.q64 = (double *)take((size_t)Mmax * IA_DP * sizeof(double));
     w.qp = (float *)take((size_t)qr * IA_DP * sizeof(float));
     w.nq = (double *)take((size_t)qr * sizeof(double));
-    w.cand = (Cand *)take((size_t)qr * db_nchunks(nrows) * SCREEN_K * sizeof(Cand));
+    w.scratch = take(match_scratch_bytes(qr, nrows));
     w.best_local = (Best *)take((size_t)Mmax * sizeof(Best));
     w.best_all = (Best *)take((size_t)Mmax * nranks * sizeof(Best));
     w.stats = (unsigned long long *)take(8 * sizeof(unsigned long long));
@@ -206,14 +206,13 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         int rc;
         if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, st)))
             return rc;
-        if (prof) IA_HIP(hipEventRecord(g_events.ev[2 * nscreen], st));
-        if ((rc = launch_screen(a->db, a->nrows, ws.qp, M, ws.cand, st))) return rc;
-        if (prof) IA_HIP(hipEventRecord(g_events.ev[2 * nscreen + 1], st));
+        hipEvent_t e0 = prof ? g_events.ev[2 * nscreen] : nullptr;
+        hipEvent_t e1 = prof ? g_events.ev[2 * nscreen + 1] : nullptr;
+        if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, M, ws.q64, ws.nq, a->amax,
+                               ws.scratch, ws.best_local, prof ? ws.stats : nullptr, st, e0, e1)))
+            return rc;
         ++nscreen;
         pairs += (double)M * (double)a->nrows;
-        if ((rc = launch_merge(src, a->row0, a->nrows, ws.cand, M, ws.q64, ws.nq, a->amax,
-                               ws.best_local, prof ? ws.stats : nullptr, st)))
-            return rc;
         const Best *ball = ws.best_local;
         if (nranks > 1) {
             if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, st))) return rc;

@@ -66,8 +66,8 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
     _ia.check(_ia.lib().ia_synth_level(ctypes.byref(a), _ia.stream()), 'ia_synth_level')
     if pbuf is not None:
         prof.append({'level': level, 'screen_ms': pbuf[0], 'screens': int(pbuf[1]),
-                     'pairs': pbuf[2], 'candidates': int(pbuf[3]),
-                     'overflow_chunks': int(pbuf[4]), 'full_scans': int(pbuf[5]),
+                     'pairs': pbuf[2], 'rows_rescored': int(pbuf[3]),
+                     'candidate_segments': int(pbuf[4]), 'full_scans': int(pbuf[5]),
                      'rows': index.nrows, 'pixels': H * W})
     return s, im
 

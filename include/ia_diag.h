@@ -18,7 +18,9 @@ int ia_diag_qp_rows(int M);
 /* fp64 queries (M x IA_DP) -> MFMA-ordered fp32 qp + |q - c|^2 */
 int ia_diag_query_rows(const double *q64, int M, const double *center, float *qp, double *nq,
                        void *stream);
-/* one screen launch; variant bits 0-3: 0 = queries in VGPRs, 1 = queries in LDS;
+/* one screen launch; variant bits 0-3: 0 = queries in VGPRs, 1 = queries in LDS,
+ * 2 = pipelined epilogue, 3 = 3-deep prefetch, 4/5 = L2-hot diagnostics,
+ * 6 = segment-minimum screen (default matcher);
  * bits 4-7: cap on query tiles per wave (0 = default) */
 int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand,
                    int variant, void *stream);
