@@ -214,7 +214,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         ++nscreen;
         pairs += (double)M * (double)a->nrows;
         const Best *ball = ws.best_local;
-        if (nranks > 1) {
+        if (a->comm) {   // also with one rank: the same RCCL path, exercised by the tests
             if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, st))) return rc;
             ball = ws.best_all;
         }

@@ -218,3 +218,60 @@ def test_full_pipeline_from_uint8_images(gpu, tmp_path):
     for l in range(1, L):
         assert np.array_equal(Bp[l], ref[l][0]), l
     assert (tmp_path / 'out' / 'level_1_color.jpg').exists()
+
+
+def test_synthesis_through_rccl_exchange(gpu):
+    """The multi-GPU path (DB shard + RCCL all-gather of per-rank winners + replicated
+    finish) with a 1-rank communicator on the box's single GPU: same kernels and the
+    same ncclAllGather call as the 2/4/8-GPU run, result must equal the oracle."""
+    import ctypes
+    import _ia
+    import image_analogies as ia
+    buf = ctypes.create_string_buffer(128)
+    _ia.check(_ia.lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
+    comm = ctypes.c_void_p()
+    _ia.check(_ia.lib().ia_comm_init(buf.raw, 1, 0, ctypes.byref(comm)), 'ia_comm_init')
+    try:
+        assert _ia.lib().ia_comm_nranks(comm) == 1
+        A, Aps, B = analogy_inputs(31, (40, 52), (33, 47), n_ap=2)
+        A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=31)
+        w = o.compute_weights(3, 5, 12, 1)
+        ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 1.0, w)
+        Bp_dev = [dev(b) for b in Bp_pyr]
+        out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                                [dev(p) for p in B_pyr], Bp_dev, L, 1.0, w, comm=comm, rank=0,
+                                nranks=1)
+        for l in ref:
+            assert np.array_equal(out[l][0].cpu().numpy(), ref[l][1]), l
+            assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
+    finally:
+        _ia.check(_ia.lib().ia_comm_destroy(comm), 'ia_comm_destroy')
+
+
+def test_sharded_level_index_rows(gpu):
+    """Per-rank shards: each rank's exact local winner, combined with the lexicographic
+    (distance, row) rule, equals the global exact winner (the rule k_finish applies to the
+    all-gathered winners)."""
+    import algorithms
+    from image_analogies import shard_rows
+    A, Aps, _ = analogy_inputs(33, (70, 90), (8, 8), n_ap=2, flat=True)
+    A_pyr = o.compute_gaussian_pyramid(A, 3)
+    Ap_pyr = [o.compute_gaussian_pyramid(x, 3) for x in Aps]
+    L = len(A_pyr)
+    As = o.create_index(A_pyr, Ap_pyr, L)[L - 1]
+    N = len(As)
+    rs = np.random.RandomState(8)
+    Q = np.vstack([As[rs.randint(0, N, 60)], rs.rand(40, 55)])
+    Ad = [dev(p) for p in A_pyr]
+    Apd = [[dev(p) for p in q] for q in Ap_pyr]
+    for G in (2, 3, 8):
+        per = []
+        for r in range(G):
+            idx = algorithms.level_index(Ad, Apd, L - 1, lambda lv, n: shard_rows(n, r, G))
+            i, d = idx.match(Q)
+            per.append((d.cpu().numpy(), i.cpu().numpy()))
+        for qi, q in enumerate(Q):
+            win = min((per[r][0][qi], per[r][1][qi]) for r in range(G))
+            dd = np.add.reduce((As - q) ** 2, axis=1)
+            j = int(np.argmin(dd))
+            assert win == (dd[j], j)
