@@ -702,18 +702,11 @@ int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int 
 // segment a VALU fp32 recomputation e'(r) obeys the same bound, so every row with
 // e'(r) <= e* + 2 eps_q (+ slack) is rescored in fp64 and r_o is among them.
 // =================================================================================
+// one workgroup's work: DB chunk `chunk` against query tiles [tile0, tile0 + NQ)
 template <int NQ>
-__global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db, int nchunks,
-                                                    int ch, int seg_rows,
-                                                    const float *__restrict__ qp, int M,
-                                                    int groups, float *__restrict__ segmin,
-                                                    long nseg) {
-    const int b = blockIdx.x;
-    const int slot = b >> 3;
-    const int chunk = (slot / groups) * 8 + (b & 7);
-    const int group = slot - (slot / groups) * groups;
-    if (chunk >= nchunks) return;
-
+__device__ __forceinline__ void seg_body(const float *__restrict__ db, int chunk, int ch,
+                                         int seg_rows, const float *__restrict__ qp, int M,
+                                         int tile0, float *__restrict__ segmin, long nseg) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
     const int j = lane & 31, h = lane >> 5;
@@ -722,7 +715,7 @@ __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db
 #pragma unroll
     for (int qt = 0; qt < NQ; ++qt) {
         const float4 *p = reinterpret_cast<const float4 *>(
-            qp + (long)((group * NQ + qt) * 32 + j) * IA_DP + h * 28);
+            qp + (long)((tile0 + qt) * 32 + j) * IA_DP + h * 28);
 #pragma unroll
         for (int v = 0; v < 7; ++v) {
             const float4 x = p[v];
@@ -770,7 +763,7 @@ __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db
 #pragma unroll
         for (int qt = 0; qt < NQ; ++qt) {
             const float m = fminf(mn[qt], __shfl_xor(mn[qt], 32));
-            const int qg = (group * NQ + qt) * 32 + j;
+            const int qg = (tile0 + qt) * 32 + j;
             if (h == 0 && qg < M) segmin[(long)qg * nseg + seg] = m;
             mn[qt] = FLT_MAX;
         }
@@ -792,6 +785,26 @@ __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db
         tile_min(b0);
         flush(tile);
     }
+}
+
+// grid: nchunks (rounded up to 8) x groups, XCD-aware as k_screen.  Groups hold NQ query
+// tiles; when NQT > 0 the LAST group holds the remaining NQT tiles, so a launch computes
+// exactly ceil(M/32) tiles (e.g. M = 342: 5 x 2 + 1 instead of 6 x 2).
+template <int NQ, int NQT>
+__global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db, int nchunks,
+                                                    int ch, int seg_rows,
+                                                    const float *__restrict__ qp, int M,
+                                                    int groups, float *__restrict__ segmin,
+                                                    long nseg) {
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+    if (NQT > 0 && group == groups - 1)
+        seg_body<(NQT > 0 ? NQT : 1)>(db, chunk, ch, seg_rows, qp, M, group * NQ, segmin, nseg);
+    else
+        seg_body<NQ>(db, chunk, ch, seg_rows, qp, M, group * NQ, segmin, nseg);
 }
 
 constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
@@ -904,23 +917,30 @@ int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
     const long nseg = db_nsegs(nrows);
-    const QSplit qs = qsplit(M, maxnq);
-    const long nblocks = ((nchunks + 7) / 8) * 8 * qs.groups;
+    const bool uniform = maxnq & 0x100;      // diagnostic: pad to whole groups instead
+    maxnq &= 0xff;
+    const int T = (M + 31) / 32;
+    const int nq = T < maxnq ? T : maxnq;
+    const int groups = (T + nq - 1) / nq;
+    const int tail = uniform ? 0 : T % nq;   // tiles of the last group when not nq
+    const long nblocks = ((nchunks + 7) / 8) * 8 * groups;
     IA_ARG(nblocks < (1L << 31), "screen grid too large");
-    switch (qs.nq) {
-#define IA_SEG_CASE(N)                                                                        \
-    case N:                                                                                   \
-        k_screen_seg<N><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, qp, \
-                                                           M, qs.groups, segmin, nseg);       \
-        break;
-        IA_SEG_CASE(1)
-        IA_SEG_CASE(2)
-        IA_SEG_CASE(3)
-#undef IA_SEG_CASE
-        default: set_error("bad query split"); return IA_E_ARG;
+#define IA_SEG_CASE(N, NT)                                                                    \
+    if (nq == N && tail == NT) {                                                              \
+        k_screen_seg<N, NT><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, \
+                                                               qp, M, groups, segmin, nseg);  \
+        IA_LAUNCH_CHECK("k_screen_seg");                                                      \
+        return IA_OK;                                                                         \
     }
-    IA_LAUNCH_CHECK("k_screen_seg");
-    return IA_OK;
+    IA_SEG_CASE(1, 0)
+    IA_SEG_CASE(2, 0)
+    IA_SEG_CASE(2, 1)
+    IA_SEG_CASE(3, 0)
+    IA_SEG_CASE(3, 1)
+    IA_SEG_CASE(3, 2)
+#undef IA_SEG_CASE
+    set_error("bad query split");
+    return IA_E_ARG;
 }
 
 int match_alg() {
@@ -1099,8 +1119,9 @@ int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *ca
            "ia_diag_screen: bad args");
     if ((variant & 15) == 6) {   // segment-minimum screen (the default matcher's stage 1)
         const int cap = (variant >> 4) & 15;
+        const int uniform = variant & 0x100;   // bit 8: pad to whole query groups
         return launch_screen_seg(db, nrows, qp, M, reinterpret_cast<float *>(cand),
-                                 cap > 0 && cap <= 3 ? cap : 2, S(stream));
+                                 (cap > 0 && cap <= 3 ? cap : 2) | uniform, S(stream));
     }
     return launch_screen_v(db, nrows, qp, M, reinterpret_cast<Cand *>(cand), variant, S(stream));
 }

@@ -9,6 +9,7 @@
 // flops, and checks that every variant returns identical candidates.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -68,13 +69,14 @@ static inline int symi(int i, int n) {
 }
 
 int main(int argc, char **argv) {
-    int S = 2048, reps = 5;
+    int S = 2048, reps = 3, rounds = 5;
     std::vector<int> Ms = {32, 64, 128, 256, 342}, vars = {0, 1};
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--A")) S = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--M")) Ms = parse_list(argv[i + 1]);
         else if (!strcmp(argv[i], "--variants")) vars = parse_list(argv[i + 1]);
         else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--rounds")) rounds = atoi(argv[i + 1]);
     }
     const int H = S, W = S, hs = (H + 1) / 2, ws = (W + 1) / 2;
     std::mt19937_64 rng(1234);
@@ -140,30 +142,41 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&cand, cb)); CK(hipMalloc(&cand_ref, cb));
     std::vector<char> h1(cb), h2(cb);
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    printf("N=%ld rows, DB %.1f MB\n", N, N * IA_DP * 4 / 1e6);
+    printf("N=%ld rows, DB %.1f MB; %d interleaved rounds x %d reps per variant\n", N,
+           N * IA_DP * 4 / 1e6, rounds, reps);
     for (int M : Ms) {
+        std::vector<std::vector<float>> t(vars.size());
+        for (size_t vi = 0; vi < vars.size(); ++vi)       // warm-up + result check
+            CI(ia_diag_screen(db, N, qp, M, vi == 0 ? cand_ref : cand, vars[vi], st));
+        for (int rd = 0; rd < rounds; ++rd)
+            for (size_t vi = 0; vi < vars.size(); ++vi) {
+                char *out = vi == 0 ? cand_ref : cand;
+                CK(hipEventRecord(e0, st));
+                for (int r = 0; r < reps; ++r) CI(ia_diag_screen(db, N, qp, M, out, vars[vi], st));
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                t[vi].push_back(ms / reps);
+            }
         for (size_t vi = 0; vi < vars.size(); ++vi) {
-            const int v = vars[vi];
-            char *out = vi == 0 ? cand_ref : cand;
-            CK(hipMemsetAsync(out, 0, cb, st));
-            CI(ia_diag_screen(db, N, qp, M, out, v, st));   // warm-up
-            CK(hipEventRecord(e0, st));
-            for (int r = 0; r < reps; ++r) CI(ia_diag_screen(db, N, qp, M, out, v, st));
-            CK(hipEventRecord(e1, st));
-            CK(hipEventSynchronize(e1));
-            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-            ms /= reps;
-            const double tf = 2.0 * 55 * M * (double)N / (ms * 1e-3) / 1e12;
+            std::vector<float> v = t[vi];
+            std::sort(v.begin(), v.end());
+            const float med = v[v.size() / 2], mn = v[0];
+            const double tf = 2.0 * 55 * M * (double)N / (med * 1e-3) / 1e12;
             long diff = 0;
-            if (vi > 0) {
+            if (vi > 0 && (vars[vi] & 15) == (vars[0] & 15)) {
+                CI(ia_diag_screen(db, N, qp, M, cand_ref, vars[0], st));
+                CI(ia_diag_screen(db, N, qp, M, cand, vars[vi], st));
+                CK(hipStreamSynchronize(st));
                 CK(hipMemcpy(h1.data(), cand_ref, cb, hipMemcpyDeviceToHost));
                 CK(hipMemcpy(h2.data(), cand, cb, hipMemcpyDeviceToHost));
-                for (size_t i = 0; i < cb; ++i) diff += h1[i] != h2[i];
+                const size_t used = (size_t)M * cb / ia_diag_qp_rows(Mmax);
+                for (size_t i = 0; i < used && i < cb; ++i) diff += h1[i] != h2[i];
             }
-            printf("variant 0x%02x M %4d  %9.1f us  %6.1f TFLOP/s  %5.1f%% of 157.3  cand-diff-bytes %ld\n",
-                   v, M, ms * 1e3, tf, 100 * tf / 157.3, diff);
-            fflush(stdout);
+            printf("variant 0x%03x M %4d  median %9.1f us  min %9.1f us  %6.1f TFLOP/s  %5.1f%% of 157.3  out-diff %ld\n",
+                   vars[vi], M, med * 1e3, mn * 1e3, tf, 100 * tf / 157.3, diff);
         }
+        fflush(stdout);
     }
     return 0;
 }
