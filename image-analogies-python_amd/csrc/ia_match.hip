@@ -787,24 +787,27 @@ __device__ __forceinline__ void seg_body(const float *__restrict__ db, int chunk
     }
 }
 
-// grid: nchunks (rounded up to 8) x groups, XCD-aware as k_screen.  Groups hold NQ query
-// tiles; when NQT > 0 the LAST group holds the remaining NQT tiles, so a launch computes
-// exactly ceil(M/32) tiles (e.g. M = 342: 5 x 2 + 1 instead of 6 x 2).
-template <int NQ, int NQT>
+// grid: nchunks (rounded up to 8) x groups, XCD-aware as k_screen.  The first nA groups
+// hold NQA query tiles, the rest NQB (< NQA) tiles, so a launch computes exactly
+// ceil(M/32) tiles with the largest groups that split them evenly (measured on MI355X:
+// 3-tile groups run ~15 % faster per tile than 2-tile ones, which beat 1-tile ones by
+// ~25 %; tools/screen_bench, profiles/r01_screen_bench_split.txt).
+template <int NQA, int NQB>
 __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db, int nchunks,
                                                     int ch, int seg_rows,
                                                     const float *__restrict__ qp, int M,
-                                                    int groups, float *__restrict__ segmin,
-                                                    long nseg) {
+                                                    int groups, int nA,
+                                                    float *__restrict__ segmin, long nseg) {
     const int b = blockIdx.x;
     const int slot = b >> 3;
     const int chunk = (slot / groups) * 8 + (b & 7);
     const int group = slot - (slot / groups) * groups;
     if (chunk >= nchunks) return;
-    if (NQT > 0 && group == groups - 1)
-        seg_body<(NQT > 0 ? NQT : 1)>(db, chunk, ch, seg_rows, qp, M, group * NQ, segmin, nseg);
+    if (NQB > 0 && group >= nA)
+        seg_body<(NQB > 0 ? NQB : 1)>(db, chunk, ch, seg_rows, qp, M,
+                                      nA * NQA + (group - nA) * NQB, segmin, nseg);
     else
-        seg_body<NQ>(db, chunk, ch, seg_rows, qp, M, group * NQ, segmin, nseg);
+        seg_body<NQA>(db, chunk, ch, seg_rows, qp, M, group * NQA, segmin, nseg);
 }
 
 constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
@@ -917,26 +920,36 @@ int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
     const long nseg = db_nsegs(nrows);
-    const bool uniform = maxnq & 0x100;      // diagnostic: pad to whole groups instead
+    const bool uniform = maxnq & 0x100;      // diagnostic: pad to whole groups of maxnq
     maxnq &= 0xff;
     const int T = (M + 31) / 32;
-    const int nq = T < maxnq ? T : maxnq;
-    const int groups = (T + nq - 1) / nq;
-    const int tail = uniform ? 0 : T % nq;   // tiles of the last group when not nq
+    int nqa, nqb, nA, groups;
+    if (uniform || maxnq < 3 || T < 3) {
+        nqa = T < maxnq ? T : maxnq;
+        nqb = 0;
+        groups = (T + nqa - 1) / nqa;
+        nA = groups;
+    } else {                                 // T = 3a + 2b with b in {0, 1, 2} minimal
+        const int b = (3 - T % 3) % 3;
+        nqa = 3;
+        nqb = b ? 2 : 0;
+        nA = (T - 2 * b) / 3;
+        groups = nA + b;
+        if (T == 4) { nqa = 2; nqb = 0; nA = 2; groups = 2; }
+    }
     const long nblocks = ((nchunks + 7) / 8) * 8 * groups;
     IA_ARG(nblocks < (1L << 31), "screen grid too large");
-#define IA_SEG_CASE(N, NT)                                                                    \
-    if (nq == N && tail == NT) {                                                              \
-        k_screen_seg<N, NT><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, \
-                                                               qp, M, groups, segmin, nseg);  \
+#define IA_SEG_CASE(NA, NB)                                                                   \
+    if (nqa == NA && nqb == NB) {                                                             \
+        k_screen_seg<NA, NB><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, \
+                                                                qp, M, groups, nA, segmin,    \
+                                                                nseg);                        \
         IA_LAUNCH_CHECK("k_screen_seg");                                                      \
         return IA_OK;                                                                         \
     }
     IA_SEG_CASE(1, 0)
     IA_SEG_CASE(2, 0)
-    IA_SEG_CASE(2, 1)
     IA_SEG_CASE(3, 0)
-    IA_SEG_CASE(3, 1)
     IA_SEG_CASE(3, 2)
 #undef IA_SEG_CASE
     set_error("bad query split");
@@ -973,7 +986,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
     }
     float *segmin = reinterpret_cast<float *>(scratch);
     const int nq_cap = (screen_variant() >> 4) & 15;
-    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, nq_cap > 0 && nq_cap < 3 ? nq_cap : 2,
+    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, nq_cap > 0 && nq_cap <= 3 ? nq_cap : 3,
                                 st)))
         return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
@@ -1121,7 +1134,7 @@ int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *ca
         const int cap = (variant >> 4) & 15;
         const int uniform = variant & 0x100;   // bit 8: pad to whole query groups
         return launch_screen_seg(db, nrows, qp, M, reinterpret_cast<float *>(cand),
-                                 (cap > 0 && cap <= 3 ? cap : 2) | uniform, S(stream));
+                                 (cap > 0 && cap <= 3 ? cap : 3) | uniform, S(stream));
     }
     return launch_screen_v(db, nrows, qp, M, reinterpret_cast<Cand *>(cand), variant, S(stream));
 }
