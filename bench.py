@@ -67,8 +67,9 @@ def make_inputs(conf, seed):
 class Job:
     """One analogy with its inputs resident in HBM."""
 
-    def __init__(self, conf, seed, dev):
+    def __init__(self, conf, seed, dev, lsh=None):
         A, Ap, B = make_inputs(conf, seed)
+        self.lsh = lsh
         self.A, self.Ap, self.B = (torch.as_tensor(x).to(dev) for x in (A, Ap, B))
         self.k, self.levels = conf['k'], conf['levels']
         nB = ip.num_layers(B.shape[0], B.shape[1], cfg.n_sm, self.levels)
@@ -91,7 +92,29 @@ class Job:
         for dst, src in zip(self.Bp, self.Bp_init):
             dst.copy_(src)
         return ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, self.Bp, self.max_levels, self.k,
-                                 self.weights, comm=comm, rank=rank, nranks=nranks, prof=prof)
+                                 self.weights, comm=comm, rank=rank, nranks=nranks, prof=prof,
+                                 lsh=self.lsh)
+
+    def lsh_quality(self):
+        """LSH vs exact on the same queries: the finest level's B / B' features (B' as
+        this job's last synthesis left it), matched by both matchers over one index."""
+        import algorithms
+        A_pyr = ip.gaussian_pyramid_dev(self.A, cfg.n_sm, self.levels)
+        Ap_pyr = ip.gaussian_pyramid_dev(self.Ap, cfg.n_sm, self.levels)
+        B_pyr = ip.gaussian_pyramid_dev(self.B, cfg.n_sm, self.levels)
+        level = self.max_levels - 1
+        index = algorithms.level_index(A_pyr, [Ap_pyr], level, lsh=self.lsh)
+        Q = torch.cat([algorithms.level_features_dev(B_pyr[level - 1], B_pyr[level], True),
+                       algorithms.level_features_dev(self.Bp[level - 1], self.Bp[level], False)],
+                      1)
+        li, ld = index.match(Q)
+        ei, ed = index.match(Q, exact=True)
+        return {'queries': int(Q.shape[0]), 'level': level,
+                'exact_frac': float((ld == ed).double().mean().item()),
+                'mean_dist_lsh': float(ld.mean().item()),
+                'mean_dist_exact': float(ed.mean().item()),
+                'mean_dist_ratio': float(ld.mean().item() / max(ed.mean().item(), 1e-300)),
+                'params': dict(self.lsh)}
 
     def algorithmic_pairs(self):
         """sum over synthesized levels of q_l * N_l (the matcher's (query, row) pairs);
@@ -166,6 +189,9 @@ def main():
     ap.add_argument('--jobs', type=int, default=4, help='c5: jobs per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--matcher', default='brute', choices=['brute', 'lsh'],
+                    help="lsh: the approximate E2LSH matcher (SURVEY §8(f)1, config c2)")
+    ap.add_argument('--lsh', default='16,4,1.0', help='tables,hashes,width for --matcher lsh')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -181,10 +207,14 @@ def main():
     if world > 1 and args.config != 'c5':
         comm = init_comm(rank, world)
 
+    lsh = None
+    if args.matcher == 'lsh':
+        t_, h_, w_ = args.lsh.split(',')
+        lsh = dict(tables=int(t_), hashes=int(h_), width=float(w_), seed=0)
     if args.config == 'c5':
-        jobs = [Job(conf, 1000 + 3 * (rank + world * j), dev) for j in range(args.jobs)]
+        jobs = [Job(conf, 1000 + 3 * (rank + world * j), dev, lsh) for j in range(args.jobs)]
     else:
-        jobs = [Job(conf, 0, dev)]
+        jobs = [Job(conf, 0, dev, lsh)]
 
     def run_step(prof=None):
         for jb in jobs:
@@ -230,9 +260,26 @@ def main():
     pairs = sum(p['pairs'] for p in prof)
     flops = 2.0 * 55 * pairs
     achieved = flops / (screen_ms * 1e-3) / 1e12 if screen_ms > 0 else 0.0
+    rescored = sum(p['rows_rescored'] for p in prof)
+    roof = {'bound': 'mfma', 'kernel': 'k_screen_seg', 'achieved': achieved,
+            'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': None,
+            'algorithmic': '2*55 flop per (query,row) pair; this rank: %.4g pairs '
+                           'over %d launches' % (pairs, screens),
+            'screen_avg_us': screen_ms * 1e3 / max(screens, 1)}
+    if lsh is not None:
+        # k_lsh_query is a gather: each examined row costs its 55 fp64 features (440 B)
+        gbs = rescored * 440.0 / (screen_ms * 1e-3) / 1e9 if screen_ms > 0 else 0.0
+        roof = {'bound': 'hbm', 'kernel': 'k_lsh_query', 'achieved': gbs,
+                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
+                'traffic': None,
+                'algorithmic': '440 B (55 fp64) per examined row; %d rows over %d launches'
+                               % (rescored, screens),
+                'screen_avg_us': screen_ms * 1e3 / max(screens, 1)}
 
     result = {
-        'metric': "B' pixels/sec (brute-force match, 5-level pyramid) + MFMA util @1/2/4/8 GPU",
+        'metric': "B' pixels/sec (brute-force match, 5-level pyramid) + MFMA util @1/2/4/8 GPU"
+                  + (' [LSH matcher]' if lsh is not None else ''),
         'value': value,
         'unit': "B' pixels/s",
         'n_gpus': world,
@@ -250,18 +297,16 @@ def main():
                    'pixels_per_step': pixels_per_step,
                    'parallelism': ('jobs%d' % world) if args.config == 'c5' else
                                   ('db-shard%d' % world if world > 1 else 'single')},
-        'roofline': {'bound': 'mfma', 'kernel': 'k_screen', 'achieved': achieved,
-                     'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': None,
-                     'algorithmic': '2*55 flop per (query,row) pair; this rank: %.4g pairs '
-                                    'over %d launches' % (pairs, screens),
-                     'screen_avg_us': screen_ms * 1e3 / max(screens, 1)},
-        'matcher': {'rows_rescored_fp64': sum(p['rows_rescored'] for p in prof),
+        'roofline': roof,
+        'matcher': {'kind': 'lsh' if lsh is not None else 'exact',
+                    'rows_rescored_fp64': rescored,
                     'candidate_segments': sum(p['candidate_segments'] for p in prof),
                     'full_scans': sum(p['full_scans'] for p in prof),
                     'queries': pixels_per_step * args.steps // (world if args.config == 'c5' else 1)},
         'checks': {'replicas_identical': replicas_ok, 'checksum': chk},
     }
+    if lsh is not None:
+        result['lsh_quality'] = jobs[0].lsh_quality()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(jobs[0], args.cpu_seconds)
     if comm is not None:

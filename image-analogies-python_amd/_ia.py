@@ -32,10 +32,16 @@ class IaSrcLevel(ctypes.Structure):
                 ('Aw', ctypes.c_int), ('nAp', ctypes.c_int)]
 
 
+class IaLsh(ctypes.Structure):
+    _fields_ = [('mem', _dp), ('proj', _dp), ('L', ctypes.c_int), ('k', ctypes.c_int),
+                ('w', ctypes.c_float)]
+
+
 class IaMatchArgs(ctypes.Structure):
     _fields_ = [('src', IaSrcLevel), ('db', _dp), ('row0', ctypes.c_long),
                 ('nrows', ctypes.c_long), ('center', _dp), ('amax', _dp), ('q64', _dp),
-                ('M', ctypes.c_int), ('idx', _dp), ('dist', _dp), ('workspace', _dp)]
+                ('M', ctypes.c_int), ('idx', _dp), ('dist', _dp), ('workspace', _dp),
+                ('lsh', ctypes.POINTER(IaLsh))]
 
 
 class IaSynthArgs(ctypes.Structure):
@@ -45,7 +51,8 @@ class IaSynthArgs(ctypes.Structure):
                 ('B_ws', ctypes.c_int), ('H', ctypes.c_int), ('W', ctypes.c_int),
                 ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
                 ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
-                ('workspace', _dp), ('comm', _dp), ('prof', ctypes.POINTER(ctypes.c_double))]
+                ('workspace', _dp), ('comm', _dp), ('prof', ctypes.POINTER(ctypes.c_double)),
+                ('lsh', ctypes.POINTER(IaLsh))]
 
 
 _SIGS = {
@@ -76,6 +83,8 @@ _SIGS = {
     'ia_synth_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long,
                                                    ctypes.c_int]),
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
+    'ia_lsh_build': (ctypes.c_int, [_dp, ctypes.c_long, ctypes.POINTER(IaLsh), _dp]),
     'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'ia_comm_init': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_void_p)]),

@@ -49,6 +49,25 @@ def compute_feature_array(im_pyr, c, full_feat):
 
 # ---- the level database (index) ---------------------------------------------------------------
 
+def lsh_projections(tables, hashes, width, seed=0):
+    """E2LSH parameters (host): (tables*hashes, 56) float32 rows, p ~ N(0, I_55) in
+    elements 0..54 and the offset b ~ U[0, width) in element 55."""
+    rs = np.random.RandomState(seed)
+    n = int(tables) * int(hashes)
+    P = np.zeros((n, _ia.IA_DP), dtype=np.float32)
+    P[:, :55] = rs.standard_normal((n, 55))
+    P[:, 55] = rs.uniform(0.0, width, n)
+    return P
+
+
+def lsh_params(c):
+    """LSH settings from the config namespace (None unless c.matcher == 'lsh')."""
+    if getattr(c, 'matcher', 'brute') != 'lsh':
+        return None
+    return dict(tables=getattr(c, 'lsh_tables', 16), hashes=getattr(c, 'lsh_hashes', 4),
+                width=getattr(c, 'lsh_width', 1.0), seed=getattr(c, 'lsh_seed', 0))
+
+
 class LevelIndex:
     """Device-resident As[level] for rows [row0, row0 + nrows) (a shard when sharded).
 
@@ -79,9 +98,37 @@ class LevelIndex:
         _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
                                   _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),
                                   st), 'ia_db_build')
+        self.lsh = None
 
-    def match(self, Q):
-        """Exact 1-NN rows (global index, fp64 distance) of queries Q (M x 55)."""
+    def build_lsh(self, tables=16, hashes=4, width=1.0, seed=0):
+        """Switch this index to the approximate LSH matcher (c.matcher = 'lsh', SURVEY
+        §8(f)1): ``tables`` x ``hashes`` Gaussian projections drawn from
+        RandomState(seed), bucket width ``width`` x the RMS per-dimension spread of the
+        centred rows (estimated from the A / A' pixel variances)."""
+        dev = self.A_lg.device
+        L, k = int(tables), int(hashes)
+        if not (1 <= L and 1 <= k and L * k <= 64):
+            raise ValueError('LSH needs 1 <= tables * hashes <= 64')
+        var = (34 * float(self.A_lg.var()) + 21 * float(self.Ap_lg.var())) / 55.0
+        w = float(width) * max(np.sqrt(var), 1e-6)
+        self.lsh_proj_host = lsh_projections(L, k, w, seed)
+        self.lsh_proj = torch.as_tensor(self.lsh_proj_host).to(dev)
+        lib = _ia.lib()
+        self.lsh_mem = _ia.workspace(lib.ia_lsh_bytes(self.nrows, L))
+        h = _ia.IaLsh()
+        h.mem, h.proj, h.L, h.k, h.w = (_ia.ptr(self.lsh_mem).value, _ia.ptr(self.lsh_proj).value,
+                                        L, k, w)
+        _ia.check(lib.ia_lsh_build(_ia.ptr(self.db), self.nrows, ctypes.byref(h), _ia.stream()),
+                  'ia_lsh_build')
+        self.lsh = h
+        return self
+
+    def lsh_ptr(self):
+        return ctypes.pointer(self.lsh) if self.lsh is not None else None
+
+    def match(self, Q, exact=None):
+        """1-NN rows (global index, fp64 distance) of queries Q (M x 55): exact, or from
+        the LSH buckets when build_lsh() was called (``exact=True`` forces exact)."""
         dev = self.A_lg.device
         Q = torch.as_tensor(Q, dtype=torch.float64)
         if Q.dim() == 1:
@@ -98,6 +145,8 @@ class LevelIndex:
         a.center, a.amax, a.q64, a.M = (_ia.ptr(self.center).value, _ia.ptr(self.amax).value,
                                         _ia.ptr(q).value, M)
         a.idx, a.dist, a.workspace = _ia.ptr(idx).value, _ia.ptr(dist).value, _ia.ptr(ws).value
+        if not exact and self.lsh is not None:
+            a.lsh = self.lsh_ptr()
         _ia.check(_ia.lib().ia_match_batch(ctypes.byref(a), _ia.stream()), 'ia_match_batch')
         return idx, dist
 
@@ -125,19 +174,24 @@ class _LazyAs(list):
         return cur
 
 
-def level_index(A_pyr, Ap_pyr_list, level, row_range=None):
+def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None):
     """Device index of one level from device pyramids.  row_range(level, N) ->
-    (row0, nrows) selects this rank's shard of the rows."""
+    (row0, nrows) selects this rank's shard of the rows; lsh (dict of build_lsh
+    arguments) switches it to the LSH matcher."""
     Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list])
     Ap_lg = torch.stack([p[level] for p in Ap_pyr_list])
     N = Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2]
     r0, nr = (0, N) if row_range is None else row_range(level, N)
-    return LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr)
+    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr)
+    if lsh is not None:
+        index.build_lsh(**lsh)
+    return index
 
 
-def create_index_dev(A_pyr, Ap_pyr_list, max_levels, row_range=None):
+def create_index_dev(A_pyr, Ap_pyr_list, max_levels, row_range=None, lsh=None):
     """Device index per level 1..max_levels-1 (entry 0 unused)."""
-    return [None] + [level_index(A_pyr, Ap_pyr_list, l, row_range) for l in range(1, max_levels)]
+    return [None] + [level_index(A_pyr, Ap_pyr_list, l, row_range, lsh)
+                     for l in range(1, max_levels)]
 
 
 def create_index(A_pyr, Ap_pyr_list, c):
@@ -147,9 +201,13 @@ def create_index(A_pyr, Ap_pyr_list, c):
     dev = _ia.require_device()
     A_dev = [_ia.to_dev(p) for p in A_pyr]
     Ap_dev = [[_ia.to_dev(p) for p in pyr] for pyr in Ap_pyr_list]
-    index = create_index_dev(A_dev, Ap_dev, c.max_levels)
-    params = [[]] + [{'algorithm': 'brute', 'exact': True, 'device': str(dev)}
-                     for _ in range(1, c.max_levels)]
+    lsh = lsh_params(c)
+    index = create_index_dev(A_dev, Ap_dev, c.max_levels, lsh=lsh)
+    if lsh is None:
+        desc = {'algorithm': 'brute', 'exact': True, 'device': str(dev)}
+    else:
+        desc = dict(lsh, algorithm='lsh', exact=False, device=str(dev))
+    params = [[]] + [dict(desc) for _ in range(1, c.max_levels)]
     As_size = [[]] + [index[l].shape for l in range(1, c.max_levels)]
     return index, params, _LazyAs(index), As_size
 

@@ -8,7 +8,10 @@ longer accepts as indices).  Fields added by this build (SURV
 
     levels   cap on pyramid halvings (skimage ``max_layer``); None = reference rule
     seed     seed of the B' random initialisation (the reference draws unseeded)
-    matcher  'brute': exact 1-NN (fp32 MFMA screen + fp64 rescore) — the only matcher
+    matcher  'brute': exact 1-NN (fp32 MFMA screen + fp64 rescore), the default;
+             'lsh': approximate E2LSH matcher with
+             lsh_tables x lsh_hashes projections, bucket width lsh_width (in units of
+             the rows' RMS per-dimension spread) and projection seed lsh_seed
 """
 import numpy as np
 
@@ -36,6 +39,10 @@ weights = None
 levels = None
 seed = 0
 matcher = 'brute'
+lsh_tables = 16
+lsh_hashes = 4
+lsh_width = 1.0
+lsh_seed = 0
 
 
 def setup_vars(img):

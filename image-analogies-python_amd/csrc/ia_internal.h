@@ -93,5 +93,9 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
                       int maxnq, hipStream_t st);
 int screen_variant();
+// approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query
+int launch_lsh_match(const IaLsh *lsh, const DbSrc &src, long row0, long nrows, int M,
+                     const double *q64, const double *center, Best *best,
+                     unsigned long long *stats, hipStream_t st);
 
 }  // namespace ia

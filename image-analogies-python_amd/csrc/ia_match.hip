@@ -1082,10 +1082,16 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
         const int M = a->M - m0 < MATCH_BATCH ? a->M - m0 : MATCH_BATCH;
         const double *q = a->q64 + (long)m0 * IA_DP;
         int rc;
-        if ((rc = launch_query_rows(q, M, a->center, qp, nq, st))) return rc;
-        if ((rc = launch_match(src, a->row0, a->nrows, a->db, qp, M, q, nq, a->amax, scratch,
-                               best, nullptr, st)))
-            return rc;
+        if (a->lsh) {
+            if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, q, a->center, best,
+                                       nullptr, st)))
+                return rc;
+        } else {
+            if ((rc = launch_query_rows(q, M, a->center, qp, nq, st))) return rc;
+            if ((rc = launch_match(src, a->row0, a->nrows, a->db, qp, M, q, nq, a->amax,
+                                   scratch, best, nullptr, st)))
+                return rc;
+        }
         k_split_best<<<(M + 255) / 256, 256, 0, st>>>(best, M, a->idx ? a->idx + m0 : nullptr,
                                                       a->dist ? a->dist + m0 : nullptr);
         IA_LAUNCH_CHECK("k_split_best");

@@ -208,9 +208,17 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
             return rc;
         hipEvent_t e0 = prof ? g_events.ev[2 * nscreen] : nullptr;
         hipEvent_t e1 = prof ? g_events.ev[2 * nscreen + 1] : nullptr;
-        if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, M, ws.q64, ws.nq, a->amax,
-                               ws.scratch, ws.best_local, prof ? ws.stats : nullptr, st, e0, e1)))
+        if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
+            if (e0) IA_HIP(hipEventRecord(e0, st));
+            if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
+                                       ws.best_local, prof ? ws.stats : nullptr, st)))
+                return rc;
+            if (e1) IA_HIP(hipEventRecord(e1, st));
+        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, M, ws.q64, ws.nq,
+                                      a->amax, ws.scratch, ws.best_local,
+                                      prof ? ws.stats : nullptr, st, e0, e1))) {
             return rc;
+        }
         ++nscreen;
         pairs += (double)M * (double)a->nrows;
         const Best *ball = ws.best_local;

@@ -5,7 +5,7 @@
 the reference's signature, parameters (``config`` module as ``c``), outputs
 (``level_%d_color.jpg`` per level and ``<name>.jpg``, ``metadata.txt``) and printed timings.
 Underneath, every level is synthesised by ``ia_synth_level`` (skewed wavefront,
-exact matcher) with the pyramids, databases and index maps resident in HBM.
+exact matcher, or the LSH matcher with ``c.matcher = 'lsh'``) with the pyramids, databases and index maps resident in HBM.
 
 ``synthesize_dev`` is the device-level entry used by bench.py and the parity tests:
 device pyramids in, per-level (s, im) index maps out, B' pyramid updated in place;
@@ -59,6 +59,7 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
     a.s, a.im = _ia.ptr(s).value, _ia.ptr(im).value
     a.workspace = _ia.ptr(ws).value
     a.comm = comm
+    a.lsh = index.lsh_ptr()
     pbuf = None
     if prof is not None:
         pbuf = (ctypes.c_double * 8)()
@@ -73,9 +74,10 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
 
 
 def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
-                   comm=None, rank=0, nranks=1, prof=None, levels=None):
+                   comm=None, rank=0, nranks=1, prof=None, levels=None, lsh=None):
     """Synthesise levels 1..max_levels-1 (image_analogies.py:119-220) from device
-    pyramids.  Bp_pyr (list of device tensors) is updated in place.
+    pyramids.  Bp_pyr (list of device tensors) is updated in place.  lsh: None (exact
+    matcher) or LevelIndex.build_lsh arguments (approximate matcher).
     Returns {level: (s, im)} device tensors."""
     w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
     row_range = None
@@ -86,7 +88,7 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     for level in range(1, max_levels):
         if levels is not None and level not in levels:
             continue
-        index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range)
+        index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range, lsh)
         out[level] = synthesize_level_dev(level, max_levels, index, B_pyr[level - 1],
                                           B_pyr[level], Bp_pyr[level - 1], Bp_pyr[level], w,
                                           k, comm, prof)
@@ -215,7 +217,8 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
     for level in range(1, c.max_levels):
         start_time = time.time()
         print('Computing level %d of %d' % (level, c.max_levels - 1))
-        index = algorithms.level_index(A_pyr, Ap_pyr_list, level)
+        index = algorithms.level_index(A_pyr, Ap_pyr_list, level,
+                                       lsh=algorithms.lsh_params(c))
         s, im = synthesize_level_dev(level, c.max_levels, index, B_pyr[level - 1], B_pyr[level],
                                      Bp_pyr[level - 1], Bp_pyr[level], weights, c.k)
         color_im_out = color_output(level, Bp_pyr[level], s, im, color_pyr_list, c)

@@ -78,9 +78,11 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
                           int full, double *out, void *stream);
 
 /* ---- a10: algorithms.py:50-70 create_index — fp32 screening database for rows
- * [row0, row0 + nrows) of As[level] (= A full | A'_i half).  Row layout (IA_DP floats):
- * element k = 2s + h of (a - center, k < 55; |a - center|^2 at k = 55) stored at
- * h*28 + s.  Rows are padded to ia_db_rows_padded(nrows) with sentinel rows.
+ * [row0, row0 + nrows) of As[level] (= A full | A'_i half).  Each row holds IA_DP floats:
+ * element k = 2s + h of (a - center, k < 55; |a - center|^2 at k = 55) at position
+ * p = h*28 + s.  Storage is fragment-major for the 32x32x2 MFMA: float4 number
+ * (tile*7 + v)*64 + lane holds row tile*32 + (lane & 31), positions (lane >> 5)*28 + 4v
+ * .. +3.  Rows are padded to ia_db_rows_padded(nrows) with sentinel rows.
  * amax (device, 1 float) receives max_row |a - center| (atomic max; zero it first). */
 long ia_db_rows_padded(long nrows);
 int ia_db_chunk_rows(long nrows);
@@ -89,10 +91,27 @@ int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *cent
 /* per-dimension screening centre: k < 34 -> mA, k >= 34 -> mAp (host scalars). */
 int ia_center_fill(double *center, double mA, double mAp, void *stream);
 
+/* ---- §8(f)1: approximate matcher (config matcher='lsh', the reference's
+ * output/freud-crop-filt-lsh.jpg variant; no reference code exists for it).  E2LSH over
+ * the centred DB rows: L tables of k hashes h = floor((p . a' + b) / w); proj is
+ * L*k rows of IA_DP floats on device (p in elements 0..54, b in element 55).
+ * mem: ia_lsh_bytes(nrows, L) bytes of device memory, filled by ia_lsh_build from the
+ * ia_db_build output.  A query returns the exact-distance (fp64) best of up to 32 rows
+ * per table bucket it falls in (lexicographic (distance, row) minimum). */
+typedef struct {
+    void *mem;
+    const float *proj;
+    int L, k;
+    float w;
+} IaLsh;
+size_t ia_lsh_bytes(long nrows, int L);
+int ia_lsh_build(const float *db, long nrows, const IaLsh *lsh, void *stream);
+
 /* ---- a11: algorithms.py:73-75 best_approximate_match, batched: exact 1-NN of M
  * fp64 queries (M x 55, row stride IA_DP) over the DB rows built above (fp32 MFMA screen
  * + fp64 rescore from the src pyramids).  Outputs idx (global row, int64) and the fp64
- * distance (pairwise-8 sum of squares, the oracle's value). */
+ * distance (pairwise-8 sum of squares, the oracle's value).  lsh (nullable): use the
+ * approximate LSH matcher over the same rows instead. */
 typedef struct {
     IaSrcLevel src;
     const float *db;           /* ia_db_build output                       */
@@ -104,6 +123,7 @@ typedef struct {
     int64_t *idx;              /* out M                                    */
     double *dist;              /* out M                                    */
     void *workspace;
+    const IaLsh *lsh;          /* NULL: exact matcher                      */
 } IaMatchArgs;
 size_t ia_match_workspace_bytes(int M, long nrows);
 int ia_match_batch(const IaMatchArgs *a, void *stream);
@@ -140,6 +160,7 @@ typedef struct {
      * {sum screen-kernel ms, #screen launches, sum query-pixels x rows (pairs),
      *  #candidates rescored, #overflow chunks, #full scans} */
     double *prof;
+    const IaLsh *lsh;   /* NULL: exact matcher; else LSH tables of this shard's rows */
 } IaSynthArgs;
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);

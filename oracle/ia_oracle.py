@@ -419,9 +419,11 @@ def kappa_factor(level, max_levels, k):
 # ----------------------------------------------------------------------------------
 
 def synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, As_level,
-                     weights, k):
+                     weights, k, matcher=None):
     """image_analogies.py:130-220 for ONE level, scanline order, luminance only.
-    Updates Bp_pyr[level] in place; returns (s, im) as int arrays (H*W, 2), (H*W,)."""
+    Updates Bp_pyr[level] in place; returns (s, im) as int arrays (H*W, 2), (H*W,).
+    matcher: q -> row (default: the exact best_approximate_match; an LshIndex's match
+    for the LSH variant)."""
     imh, imw = Bp_pyr[level].shape[:2]
     A_h, A_w = Ap_pyr_list[0][level].shape[:2]
     Bfeat = level_features(B_pyr[level - 1], B_pyr[level], True)
@@ -432,7 +434,8 @@ def synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, As_le
             q = np.hstack([Bfeat[row * imw + col],
                            extract_pixel_feature(Bp_pyr[level - 1], Bp_pyr[level],
                                                  (row, col), False)])
-            p_app_ix = best_approximate_match(As_level, q)
+            p_app_ix = (best_approximate_match(As_level, q) if matcher is None
+                        else int(matcher(q)))
             p_app, i_app = Ap_ix2px(p_app_ix, A_h, A_w)
             if len(s) < 1:
                 p, i = p_app, i_app
@@ -484,3 +487,74 @@ def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, levels=None):
                                  As[level], weights, k)
         out[level] = (Bp_pyr[level].copy(), s, im)
     return out
+
+
+# ----------------------------------------------------------------------------------
+# LSH matcher.  The reference snapshot holds no LSH code (only the
+# artefact output/freud-crop-filt-lsh.jpg), so this restates THIS BUILD's definition
+# (image-analogies-python_amd/csrc/ia_lsh.hip) to check the HIP kernels: E2LSH keys of
+# the centred fp32 rows, a stable sort per table, and the exact pairwise-8 distance of
+# the first LSH_CAP rows of each bucket the query falls in.  Parity unpinned against
+# any reference (there is none); bit-exact against the HIP path up to fp32 double-
+# rounding ties of the emulated FMA chain (measure zero; the test tolerates 1%).
+LSH_CAP = 32
+
+
+def _fma32(a, b, c):
+    """fp32 fused multiply-add: the product of two fp32 values is exact in fp64."""
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+
+
+def lsh_hash_keys(X32, proj, L, k, w):
+    """(n, L) uint32 keys of centred fp32 rows X32 (n, 55): per table the wrapped sum of
+    mix(floor((p . x + b) / w), i), top bit cleared (ia_lsh.hip k_lsh_keys)."""
+    n = X32.shape[0]
+    w = np.float32(w)
+    d = np.broadcast_to(proj[:, 55][None, :], (n, L * k)).astype(np.float32)
+    for e in range(55):
+        d = _fma32(proj[None, :, e], X32[:, e:e + 1], d)
+    h = np.floor(d / w).astype(np.int64) & 0xffffffff
+    i = np.arange(L * k, dtype=np.int64) % k
+    mix = (h * ((0x9E3779B1 + 2 * i) & 0xffffffff) + 0x7F4A7C15 * i) & 0xffffffff
+    keys = mix.reshape(n, L, k).sum(axis=2) & 0x7fffffff
+    return keys.astype(np.uint32)
+
+
+class LshIndex:
+    """The LSH tables of rows As_level (N, 55) centred by ``center`` (55,)."""
+
+    def __init__(self, As_level, center, proj, L, k, w, cap=LSH_CAP):
+        self.As, self.center, self.proj = As_level, center, proj
+        self.L, self.k, self.w, self.cap = L, k, w, cap
+        keys = lsh_hash_keys((As_level - center[None, :]).astype(np.float32), proj, L, k, w)
+        self.order = [np.argsort(keys[:, t], kind='stable') for t in range(L)]
+        self.sorted_keys = [keys[self.order[t], t] for t in range(L)]
+
+    def match(self, Q):
+        """(idx, dist): lexicographic (distance, row) minimum over the query's buckets."""
+        Q = np.atleast_2d(Q)
+        N = self.As.shape[0]
+        qk = lsh_hash_keys((Q - self.center[None, :]).astype(np.float32), self.proj, self.L,
+                           self.k, self.w)
+        idx = np.empty(len(Q), dtype=np.int64)
+        dist = np.empty(len(Q))
+        for m in range(len(Q)):
+            cand = []
+            for t in range(self.L):
+                key = int(qk[m, t])
+                lo = int(np.searchsorted(self.sorted_keys[t], key, 'left'))
+                hi = int(np.searchsorted(self.sorted_keys[t], key + 1, 'left'))
+                if lo == hi:   # empty bucket: neighbouring entries of the sorted table
+                    lo = max(lo - 2, 0)
+                    hi = min(lo + 4, N)
+                cand.append(self.order[t][lo:min(hi, lo + self.cap)])
+            cand = np.unique(np.concatenate(cand))
+            d = np.add.reduce((self.As[cand] - Q[m]) ** 2, axis=1)
+            j = np.lexsort((cand, d))[0]
+            idx[m], dist[m] = cand[j], d[j]
+        return idx, dist
+
+
+def lsh_match(As_level, center, proj, L, k, w, Q, cap=LSH_CAP):
+    """(idx, dist) of queries Q (M, 55) under the LSH matcher over rows As_level."""
+    return LshIndex(As_level, center, proj, L, k, w, cap).match(Q)

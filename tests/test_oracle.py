@@ -185,3 +185,52 @@ def test_c_oracle_equals_numpy_oracle(case):
     for l in r1:
         for a, b in zip(r1[l], r2[l]):
             assert np.array_equal(a, b), l
+
+
+# ---- LSH restatement (this build's definition, no reference code) -------
+
+def test_lsh_keys_kat():
+    """One table, one axis-aligned projection, b = 0, w = 1: key = floor(x0) * golden."""
+    proj = np.zeros((1, 56), np.float32)
+    proj[0, 0] = 1.0
+    X = np.zeros((4, 55), np.float32)
+    X[:, 0] = [0.5, 1.5, -0.5, 7.0]
+    keys = o.lsh_hash_keys(X, proj, 1, 1, 1.0)[:, 0]
+    want = [(h * 0x9E3779B1) & 0x7fffffff for h in (0, 1, 0xffffffff, 7)]
+    assert keys.tolist() == want
+
+
+def test_lsh_single_bucket_is_bruteforce():
+    """A bucket wider than the data holds every row: with N <= cap the LSH matcher is the
+    exact first-minimum brute force."""
+    rs = np.random.RandomState(0)
+    As = rs.rand(30, 55)
+    proj = np.zeros((2, 56), np.float32)
+    proj[:, :55] = rs.randn(2, 55)
+    proj[:, 55] = 5e5      # offset b = w / 2 keeps every |p . x| << w in bucket 0
+    Q = np.vstack([As[:5], rs.rand(20, 55)])
+    idx, dist = o.lsh_match(As, As.mean(0), proj, 1, 2, 1e6, Q)
+    for q, i, d in zip(Q, idx, dist):
+        dd = np.add.reduce((As - q) ** 2, axis=1)
+        assert i == np.argmin(dd) and d == dd.min()
+
+
+def test_lsh_recall_on_perturbed_rows():
+    """Sanity of the definition: near-duplicate queries find their row (or an equally
+    close one) in most cases with the default 16 x 4 tables."""
+    A, Aps, _ = analogy_inputs(4, (40, 50), (8, 8))
+    pyr = o.compute_gaussian_pyramid(A, 3)
+    ppyr = o.compute_gaussian_pyramid(Aps[0], 3)
+    As = o.create_index(pyr, [ppyr], len(pyr))[-1]
+    c = As.mean(0)
+    rs = np.random.RandomState(1)
+    sigma = np.sqrt(((As - c) ** 2).mean())
+    P = np.zeros((64, 56), np.float32)
+    P[:, :55] = rs.standard_normal((64, 55))
+    P[:, 55] = rs.uniform(0, sigma, 64)
+    rows = rs.randint(0, len(As), 200)
+    Q = As[rows] + rs.randn(200, 55) * 1e-3 * sigma
+    idx, dist = o.lsh_match(As, c, P, 16, 4, sigma, Q)
+    exact = np.array([np.add.reduce((As - q) ** 2, axis=1).min() for q in Q])
+    assert np.all(dist >= exact)
+    assert np.mean(dist == exact) > 0.9
