@@ -40,6 +40,16 @@ __device__ __forceinline__ int symi(int i, int n) {
     return i >= n ? p - 1 - i : i;
 }
 
+// symi for i in [-2, n + 1] and n >= 1 (the feature windows), branch-free: three
+// selects (reflect low, high, low) equal the period-2n map on that range.  Keeping the
+// gathers of a 55-feature row in one basic block lets all 55 loads issue before the
+// first use (a branchy index map serialises them: one memory round trip per feature).
+__device__ __forceinline__ int symi2(int i, int n) {
+    i = i < 0 ? -1 - i : i;
+    i = i >= n ? 2 * n - 1 - i : i;
+    return i < 0 ? -1 - i : i;
+}
+
 // skimage _warp_fast mode 'R' (mirror about the edge sample).
 __device__ __forceinline__ long mirrori(long c, long n) {
     long cmax = n - 1;
@@ -67,13 +77,13 @@ __device__ __forceinline__ void emit_pixel(const ImgPair &p, int r, int c, int k
     const int rs = r >> 1, cs = c >> 1;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-        const int rr = symi(rs + t / 3 - 1, p.hs), cc = symi(cs + t % 3 - 1, p.ws);
+        const int rr = symi2(rs + t / 3 - 1, p.hs), cc = symi2(cs + t % 3 - 1, p.ws);
         f(k0 + t, p.sm[(long)rr * p.ws + cc]);
     }
     constexpr int NF = FULL ? 25 : 12;
 #pragma unroll
     for (int t = 0; t < NF; ++t) {
-        const int rr = symi(r + t / 5 - 2, p.h), cc = symi(c + t % 5 - 2, p.w);
+        const int rr = symi2(r + t / 5 - 2, p.h), cc = symi2(c + t % 5 - 2, p.w);
         f(k0 + 9 + t, p.lg[(long)rr * p.w + cc]);
     }
 }

@@ -95,13 +95,13 @@ __global__ __launch_bounds__(64) void k_query_wave(ImgPair B, ImgPair Bp, int t,
     if (lane < 34) {
         const bool coarse = lane < 9;
         const int tt = coarse ? lane : lane - 9;
-        v = coarse ? B.sm[(long)symi((y >> 1) + tt / 3 - 1, B.hs) * B.ws + symi((x >> 1) + tt % 3 - 1, B.ws)]
-                   : B.lg[(long)symi(y + tt / 5 - 2, B.h) * B.w + symi(x + tt % 5 - 2, B.w)];
+        v = coarse ? B.sm[(long)symi2((y >> 1) + tt / 3 - 1, B.hs) * B.ws + symi2((x >> 1) + tt % 3 - 1, B.ws)]
+                   : B.lg[(long)symi2(y + tt / 5 - 2, B.h) * B.w + symi2(x + tt % 5 - 2, B.w)];
     } else if (lane < 55) {
         const bool coarse = lane < 43;
         const int tt = coarse ? lane - 34 : lane - 43;
-        v = coarse ? Bp.sm[(long)symi((y >> 1) + tt / 3 - 1, Bp.hs) * Bp.ws + symi((x >> 1) + tt % 3 - 1, Bp.ws)]
-                   : Bp.lg[(long)symi(y + tt / 5 - 2, Bp.h) * Bp.w + symi(x + tt % 5 - 2, Bp.w)];
+        v = coarse ? Bp.sm[(long)symi2((y >> 1) + tt / 3 - 1, Bp.hs) * Bp.ws + symi2((x >> 1) + tt % 3 - 1, Bp.ws)]
+                   : Bp.lg[(long)symi2(y + tt / 5 - 2, Bp.h) * Bp.w + symi2(x + tt % 5 - 2, Bp.w)];
     }
     double d = 0.0;
     if (lane < 55) {

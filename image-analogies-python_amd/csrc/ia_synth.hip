@@ -90,9 +90,8 @@ __global__ __launch_bounds__(64) void k_finish(DbSrc src, const Best *__restrict
             const long wix = __shfl(cix, win);
             const int wr = __shfl(cr, win), wc = __shfl(cc, win), wim = __shfl(cim, win);
             // kappa test (image_analogies.py:200-211), lane 0: d_app, lane 1: d_coh
-            double d = 0.0;
-            if (lane == 0) d = row_wdist(src, app, qs, weights);
-            if (lane == 1) d = row_wdist(src, wix, qs, weights);
+            double d = 0.0;   // one inlined copy of the gather (instruction-cache footprint)
+            if (lane < 2) d = row_wdist(src, lane == 0 ? app : wix, qs, weights);
             const double d_app = __shfl(d, 0), d_coh = __shfl(d, 1);
             if (d_coh <= d_app * kappa_factor) {
                 pr = wr; pc = wc; img = wim;

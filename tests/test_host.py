@@ -194,3 +194,15 @@ def test_sharded_exchange_equals_global_argmin(world):
     spans = [shard_rows(N, r, world) for r in range(world)]
     assert spans[0][0] == 0 and sum(n for _, n in spans) == N
     assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def test_branch_free_symmetric_index_equals_period_map():
+    """ia_common.h symi2 (three selects, used by every feature gather) equals the
+    period-2n symmetric map on its domain i in [-2, n + 1], n >= 1."""
+    def symi2(i, n):
+        i = -1 - i if i < 0 else i
+        i = 2 * n - 1 - i if i >= n else i
+        return -1 - i if i < 0 else i
+    for n in range(1, 12):
+        for i in range(-2, n + 2):
+            assert symi2(i, n) == o.sym_index(i, n), (i, n)
