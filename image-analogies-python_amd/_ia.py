@@ -52,8 +52,10 @@ class IaSynthArgs(ctypes.Structure):
                 ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
                 ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
                 ('workspace', _dp), ('comm', _dp), ('prof', ctypes.POINTER(ctypes.c_double)),
-                ('lsh', ctypes.POINTER(IaLsh))]
+                ('lsh', ctypes.POINTER(IaLsh)), ('flags', ctypes.c_int)]
 
+
+IA_SYNTH_EAGER = 1
 
 _SIGS = {
     'ia_last_error': (ctypes.c_char_p, []),
@@ -85,6 +87,7 @@ _SIGS = {
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
     'ia_lsh_build': (ctypes.c_int, [_dp, ctypes.c_long, ctypes.POINTER(IaLsh), _dp]),
+    'ia_lsh_bits': (ctypes.c_int, [ctypes.c_long]),
     'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'ia_comm_init': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_void_p)]),

@@ -8,11 +8,14 @@ namespace ia {
 // A screen workgroup owns one chunk of CH rows: 4 waves x (CH/4) rows, 32-row tiles.
 // CH is chosen so a DB produces ~1024 chunks (>= 4 workgroups per CU per query group).
 constexpr int SCREEN_K = 4;            // candidates kept per (query, chunk)
-constexpr int TARGET_CHUNKS = 1024;
+// ~chunks per database: IA_TARGET_CHUNKS (read once per process, default 1024; a
+// tuning knob for tools/screen_bench — the DB build and the screen must agree on it)
+int target_chunks();
 
 // tiles per wave: a power of two in [1, 64] (so screen segments divide it)
 static inline int db_chunk_rows(long nrows) {
-    const long want = (nrows + (long)TARGET_CHUNKS * 128 - 1) / ((long)TARGET_CHUNKS * 128);
+    const long tc = target_chunks();
+    const long want = (nrows + tc * 128 - 1) / (tc * 128);
     long tpw = 1;
     while (tpw < want && tpw < 64) tpw <<= 1;
     return (int)(128 * tpw);
@@ -63,6 +66,25 @@ static inline QSplit qsplit(int M, int maxnq) {
 constexpr int MAX_NQ = 6;
 static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + MAX_NQ) * 32; }
 
+// the level state one wave of the per-pixel tail updates (ia_finish.h)
+struct FinishArgs {
+    int t, y_lo, W;
+    long N_total;
+    const double *weights;
+    double kappa_factor;
+    double *Bp_lg;
+    int32_t *s, *im;
+};
+
+// matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS
+// cache lines so that the atomics of a wave's M queries do not serialise on one address;
+// the host sums the slots.
+constexpr int STATS_SLOTS = 64, STATS_LINE = 8;
+constexpr size_t STATS_BYTES = (size_t)STATS_SLOTS * STATS_LINE * sizeof(unsigned long long);
+__device__ __forceinline__ unsigned long long *stats_slot(unsigned long long *s, int q) {
+    return s + (q & (STATS_SLOTS - 1)) * STATS_LINE;
+}
+
 // ---- launchers ------------------------------------------------------------------
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
                       const double *center, double *q64, float *qp, double *nq,
@@ -86,10 +108,15 @@ int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int 
 // candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);
 // ev0 / ev1 (nullable) are recorded on st immediately before / after the screen launch.
+// fin (nullable, single shard only): the exact stage also runs the per-pixel tail of the
+// wave (coherence, kappa, B'/s/im update) in the same kernel.
 int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp, int M,
                  const double *q64, const double *nq, const float *amax, void *scratch,
                  Best *best, unsigned long long *stats, hipStream_t st,
-                 hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                 hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                 const FinishArgs *fin = nullptr);
+int fuse_finish();    // IA_FUSE_FINISH: 0 off, 1 levels <= 2^20 rows [default], 2 on
+int match_alg();      // IA_MATCH_ALG (default 1: segment minima)
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
                       int maxnq, hipStream_t st);
 int screen_variant();

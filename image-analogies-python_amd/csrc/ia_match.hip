@@ -20,7 +20,7 @@
 //     inside the window may have dropped candidates: it is re-scanned exactly.  Ties
 //     break to the lowest row index (np.argmin).  The result is bit-identical to the
 //     oracle's brute force for any input.
-#include "ia_internal.h"
+#include "ia_finish.h"
 
 #include <float.h>
 
@@ -675,9 +675,10 @@ __global__ __launch_bounds__(256) void k_merge(DbSrc src, long row0, long nrows,
         for (int w = 1; w < 4; ++w) best_update(bd, bi, redd[w], redi[w]);
         best[q] = Best{bd, bi};
         if (stats) {
-            atomicAdd(&stats[0], (unsigned long long)nc);
-            atomicAdd(&stats[1], (unsigned long long)no);
-            atomicAdd(&stats[2], full ? 1ULL : 0ULL);
+            unsigned long long *sl = stats_slot(stats, q);
+            atomicAdd(&sl[0], (unsigned long long)nc);
+            atomicAdd(&sl[1], (unsigned long long)no);
+            atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
 }
@@ -810,9 +811,30 @@ __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db
         seg_body<NQA>(db, chunk, ch, seg_rows, qp, M, group * NQA, segmin, nseg);
 }
 
+// Phase probes (tools/rescore_probe only: built with -DIA_PROBE into a separate library):
+// lane 0 of every wave of the first 64 workgroups stores wall_clock64() at each mark
+// (slot [block][wave][mark], 64 x 4 x 16).
+#ifdef IA_PROBE
+__device__ unsigned long long *g_probe;
+#define IA_PROBE_MARK(i)                                                                    \
+    do {                                                                                    \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 64 && g_probe)                           \
+            g_probe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (i)] = wall_clock64();     \
+    } while (0)
+#else
+#define IA_PROBE_MARK(i) \
+    do {                 \
+    } while (0)
+#endif
+
 constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
+constexpr int RESCORE_REG = 8;         // float4s of segment minima per thread kept in VGPRs
+constexpr int RESCORE_RPT = 2;         // candidate rows per thread per step
 
 // Exact stage of the segment-minimum matcher: one 256-thread workgroup per query.
+// FIN: single shard — wave 0 then runs the per-pixel tail of the synthesis step
+// (ia_finish.h) on the winner, saving a launch and a round trip per wave.
+template <bool FIN>
 __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrows, long nseg,
                                                  int seg_rows, const float *__restrict__ segmin,
                                                  const float *__restrict__ db,
@@ -821,8 +843,9 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
                                                  const double *__restrict__ nq,
                                                  const float *__restrict__ amax,
                                                  Best *__restrict__ best,
-                                                 unsigned long long *stats) {
+                                                 unsigned long long *stats, FinishArgs fa) {
     __shared__ int slist[RESCORE_SEGCAP];
+    __shared__ long long win;
     __shared__ int scount;
     __shared__ float redf[4];
     __shared__ double redd[4];
@@ -833,36 +856,68 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
 
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
+    IA_PROBE_MARK(0);
     if (tid < IA_DP) {
         qs[tid] = q64[(long)q * IA_DP + tid];
         qf[tid] = qp[(long)q * IA_DP + tid];
     }
     if (tid == 0) { scount = 0; nresc = 0; }
     const float *sq = segmin + (long)q * nseg;
+    const double A = (double)amax[0];   // issued with the segment-minimum loads
+    const double nqq = nq[q];
 
-    float emin = FLT_MAX;
+    // segment minima of this query: the first RESCORE_REG*256 float4s stay in registers
+    // between the two passes (all loads of a pass in flight at once); nseg is a multiple
+    // of 4 (>= 4 segments per chunk)
+    const long n4 = nseg / 4;
     const float4 *sq4 = reinterpret_cast<const float4 *>(sq);
-    for (long i = tid; i < nseg / 4; i += 256) {
+    float4 v[RESCORE_REG];
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j) {
+        const long i = tid + (long)j * 256;
+        v[j] = i < n4 ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+    }
+    float emin = FLT_MAX;
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j)
+        emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
+    for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
         const float4 x = sq4[i];
         emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
     }
     for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
     if ((tid & 63) == 0) redf[tid >> 6] = emin;
+    IA_PROBE_MARK(1);
     __syncthreads();
+    IA_PROBE_MARK(2);
     emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
 
-    const double A = (double)amax[0];
-    const double nqq = nq[q];
     const double eps = 70.0 * 5.9604644775390625e-08 * (2.0 * A * sqrt(nqq) + A * A);
     const double T = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
 
-    for (long s = tid; s < nseg; s += 256) {
-        if ((double)sq[s] <= T) {
+    auto push = [&](float e, long s) {
+        if ((double)e <= T) {
             const int pos = atomicAdd(&scount, 1);
             if (pos < RESCORE_SEGCAP) slist[pos] = (int)s;
         }
+    };
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j) {
+        const long i = tid + (long)j * 256;
+        push(v[j].x, 4 * i);
+        push(v[j].y, 4 * i + 1);
+        push(v[j].z, 4 * i + 2);
+        push(v[j].w, 4 * i + 3);
+    }
+    for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
+        const float4 x = sq4[i];
+        push(x.x, 4 * i);
+        push(x.y, 4 * i + 1);
+        push(x.z, 4 * i + 2);
+        push(x.w, 4 * i + 3);
     }
     __syncthreads();
+    IA_PROBE_MARK(3);
     const int ns = scount;
     const bool full = ns > RESCORE_SEGCAP;
     const long nscan = full ? nseg : ns;
@@ -870,28 +925,41 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
     unsigned int mine = 0;
-    for (long i = 0; i < nscan; ++i) {
-        const long seg = full ? i : slist[i];
-        for (int rr = tid; rr < seg_rows; rr += 256) {
-            const long lr = seg * seg_rows + rr;
-            if (lr >= nrows) continue;
-            // fp32 recomputation from the fragment-major DB (row lr = tile*32 + jj)
-            const float4 *t4 = reinterpret_cast<const float4 *>(db) + (lr >> 5) * TILE_VEC + (lr & 31);
-            float e = 0.f;
+    // rows of the candidate segments, RESCORE_RPT per thread per step with all their DB
+    // loads issued together (seg_rows <= 512 = RESCORE_RPT * 256: one step per segment)
+    const long nrs = nscan * seg_rows;
+    for (long base = 0; base < nrs; base += RESCORE_RPT * 256) {
+        float e[RESCORE_RPT];
+        long lr[RESCORE_RPT];
+#pragma unroll
+        for (int u = 0; u < RESCORE_RPT; ++u) {
+            const long k = base + u * 256 + tid;
+            const long seg = k < nrs ? (full ? k / seg_rows : slist[k / seg_rows]) : 0;
+            lr[u] = k < nrs ? seg * seg_rows + k % seg_rows : nrows;
+            // fp32 recomputation from the fragment-major DB (row lr = tile*32 + jj);
+            // out-of-range rows read row 0 and are discarded below
+            const long r = lr[u] < nrows ? lr[u] : 0;
+            const float4 *t4 = reinterpret_cast<const float4 *>(db) + (r >> 5) * TILE_VEC + (r & 31);
+            float acc = 0.f;
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
                 for (int v = 0; v < 7; ++v) {
                     const float4 x = t4[v * 64 + hh * 32];
                     const float *qv = qf + hh * 28 + 4 * v;
-                    e = fmaf(x.x, qv[0], e);
-                    e = fmaf(x.y, qv[1], e);
-                    e = fmaf(x.z, qv[2], e);
-                    e = fmaf(x.w, qv[3], e);
+                    acc = fmaf(x.x, qv[0], acc);
+                    acc = fmaf(x.y, qv[1], acc);
+                    acc = fmaf(x.z, qv[2], acc);
+                    acc = fmaf(x.w, qv[3], acc);
                 }
-            if ((double)e <= T) {
+            e[u] = acc;
+        }
+        IA_PROBE_MARK(8);
+#pragma unroll
+        for (int u = 0; u < RESCORE_RPT; ++u) {
+            if (lr[u] < nrows && (double)e[u] <= T) {
                 ++mine;
-                best_update(bd, bi, row_dist2(src, row0 + lr, qs), row0 + lr);
+                best_update(bd, bi, row_dist2(src, row0 + lr[u], qs), row0 + lr[u]);
             }
         }
     }
@@ -902,16 +970,34 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     }
     if (mine) atomicAdd(&nresc, mine);
     if ((tid & 63) == 0) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
+    IA_PROBE_MARK(4);
     __syncthreads();
+    IA_PROBE_MARK(5);
     if (tid == 0) {
         for (int w = 1; w < 4; ++w) best_update(bd, bi, redd[w], redi[w]);
         best[q] = Best{bd, bi};
+        win = bi;
         if (stats) {
-            atomicAdd(&stats[0], (unsigned long long)nresc);
-            atomicAdd(&stats[1], (unsigned long long)ns);
-            atomicAdd(&stats[2], full ? 1ULL : 0ULL);
+            unsigned long long *sl = stats_slot(stats, q);
+            atomicAdd(&sl[0], (unsigned long long)nresc);
+            atomicAdd(&sl[1], (unsigned long long)ns);
+            atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
+    if (FIN) {
+        __syncthreads();
+        if (tid < 64) finish_pixel(src, win, q, fa, qs, tid);
+        IA_PROBE_MARK(6);
+    }
+}
+
+int fuse_finish() {
+    static int f = -1;
+    if (f < 0) {
+        const char *e = getenv("IA_FUSE_FINISH");
+        f = e ? atoi(e) : 1;
+    }
+    return f;
 }
 
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
@@ -975,9 +1061,10 @@ size_t match_scratch_bytes(int qrows, long nrows) {
 int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp, int M,
                  const double *q64, const double *nq, const float *amax, void *scratch,
                  Best *best, unsigned long long *stats, hipStream_t st, hipEvent_t ev0,
-                 hipEvent_t ev1) {
+                 hipEvent_t ev1, const FinishArgs *fin) {
     int rc;
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
+    IA_ARG(!fin || match_alg() == 1, "launch_match: the fused tail needs the segment matcher");
     if (match_alg() == 0) {
         Cand *cand = reinterpret_cast<Cand *>(scratch);
         if ((rc = launch_screen(db, nrows, qp, M, cand, st))) return rc;
@@ -990,8 +1077,13 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
                                 st)))
         return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
-    k_rescore<<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows), segmin, db,
-                                 qp, q64, nq, amax, best, stats);
+    if (fin)
+        k_rescore<true><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows),
+                                           segmin, db, qp, q64, nq, amax, best, stats, *fin);
+    else
+        k_rescore<false><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows),
+                                            segmin, db, qp, q64, nq, amax, best, stats,
+                                            FinishArgs{});
     IA_LAUNCH_CHECK("k_rescore");
     return IA_OK;
 }
@@ -1146,3 +1238,11 @@ int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *ca
 }
 
 }  // extern "C"
+
+#ifdef IA_PROBE
+// diagnostic: route the phase marks to buf (device, 64 x 4 x 16 uint64) or disable (NULL)
+extern "C" int ia_probe_set(unsigned long long *buf) {
+    IA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ia::g_probe), &buf, sizeof(buf)));
+    return IA_OK;
+}
+#endif

@@ -11,6 +11,17 @@
 
 namespace ia {
 
+int target_chunks() {
+    static int tc = -1;
+    if (tc < 0) {
+        const char *e = getenv("IA_TARGET_CHUNKS");
+        tc = e ? atoi(e) : 1024;
+        if (tc < 64 || tc > 65536) tc = 1024;
+    }
+    return tc;
+}
+
+
 thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 int hip_fail(hipError_t e, const char *what) {

@@ -14,7 +14,7 @@
 //   k_rescore     -> best (this shard)   (ia_match.hip, exact fp64)
 //   [RCCL all-gather of best over ranks when the DB is sharded]
 //   k_finish      -> coherence, kappa test, B'/s/im update (this file)
-#include "ia_internal.h"
+#include "ia_finish.h"
 
 #include <vector>
 
@@ -22,89 +22,23 @@
 
 namespace ia {
 
-__device__ __forceinline__ void best_upd(double &bd, long long &bi, double d, long long i) {
-    if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
-}
-
-// one wave per query pixel
+// one wave per query pixel: the lexicographic (dist, row) minimum over the shards'
+// exact winners, then the shared per-pixel tail (ia_finish.h)
 __global__ __launch_bounds__(64) void k_finish(DbSrc src, const Best *__restrict__ best_all,
-                                               int nranks, int M, int t, int y_lo, int W,
-                                               long N_total,
-                                               const double *__restrict__ q64,
-                                               const double *__restrict__ weights,
-                                               double kappa_factor,
-                                               double *__restrict__ Bp_lg,
-                                               int32_t *__restrict__ s,
-                                               int32_t *__restrict__ im) {
+                                               int nranks, int M, FinishArgs f,
+                                               const double *__restrict__ q64) {
     __shared__ double qs[IA_DP];
     const int m = blockIdx.x;
-    const int y = y_lo + m, x = t - 3 * y;
     const int lane = threadIdx.x;
     if (lane < IA_DP) qs[lane] = q64[(long)m * IA_DP + lane];
     __syncthreads();
-
-    // p_app: lexicographic (dist, row) minimum over the shards' exact winners
     double ad = INFINITY;
     long long app = 0x7fffffffffffffffLL;
     for (int g = 0; g < nranks; ++g) {
         const Best b = best_all[(long)g * M + m];
-        best_upd(ad, app, b.d, b.idx);
+        fin_best(ad, app, b.d, b.idx);
     }
-    const int Ah = src.A.h, Aw = src.A.w;
-    const long hw = src.hw;
-    if (app < 0 || app >= N_total) app = 0;   // unreachable: every merge has a winner
-    long img = app / hw;
-    long rem = app - img * hw;
-    int pr = (int)(rem / Aw), pc = (int)(rem - (long)(rem / Aw) * Aw);
-
-    if (y != 0 || x != 0) {
-        // best_coherence_match (algorithms.py:92-130): lanes 0..14 = 3x5 causal window,
-        // row-major = the reference's product(rows, cols) order
-        double cd = INFINITY;
-        long long cl = 0x7fffffffffffffffLL;
-        long cix = -1;
-        int cr = 0, cc = 0, cim = 0;
-        if (lane < 15) {
-            const int rr = y - 2 + lane / 5, rc = x - 2 + lane % 5;
-            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
-                const long sidx = (long)rr * W + rc;
-                const int sr = s[2 * sidx] + y - rr, sc = s[2 * sidx + 1] + x - rc;
-                if (sr >= 0 && sr < Ah && sc >= 0 && sc < Aw) {
-                    const int simg = im[sidx];
-                    cix = ((long)Ah * simg + sr) * Aw + sc;
-                    cr = sr; cc = sc; cim = simg;
-                    cd = sqrt(row_dist2(src, cix, qs));
-                    cl = lane;
-                }
-            }
-        }
-        double bd = cd;
-        long long bl = cl;
-        for (int o = 32; o > 0; o >>= 1) {
-            const double od = __shfl_xor(bd, o);
-            const long long ol = __shfl_xor(bl, o);
-            best_upd(bd, bl, od, ol);
-        }
-        if (bl != 0x7fffffffffffffffLL) {
-            const int win = (int)bl;
-            const long wix = __shfl(cix, win);
-            const int wr = __shfl(cr, win), wc = __shfl(cc, win), wim = __shfl(cim, win);
-            // kappa test (image_analogies.py:200-211), lane 0: d_app, lane 1: d_coh
-            double d = 0.0;   // one inlined copy of the gather (instruction-cache footprint)
-            if (lane < 2) d = row_wdist(src, lane == 0 ? app : wix, qs, weights);
-            const double d_app = __shfl(d, 0), d_coh = __shfl(d, 1);
-            if (d_coh <= d_app * kappa_factor) {
-                pr = wr; pc = wc; img = wim;
-            }
-        }
-    }
-    if (lane == 0) {
-        const long q = (long)y * W + x;
-        Bp_lg[q] = src.Ap.lg[img * hw + (long)pr * Aw + pc];
-        s[2 * q] = pr;
-        s[2 * q + 1] = pc;
-        im[q] = (int32_t)img;
-    }
+    finish_pixel(src, app, m, f, qs, lane);
 }
 
 // -------------------------------- workspace ----------------------------------------
@@ -135,7 +69,7 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     w.scratch = take(match_scratch_bytes(qr, nrows));
     w.best_local = (Best *)take((size_t)Mmax * sizeof(Best));
     w.best_all = (Best *)take((size_t)Mmax * nranks * sizeof(Best));
-    w.stats = (unsigned long long *)take(8 * sizeof(unsigned long long));
+    w.stats = (unsigned long long *)take(STATS_BYTES);
     if (ws) *ws = w;
     return off;
 }
@@ -152,6 +86,39 @@ struct EventPool {
     }
 };
 static thread_local EventPool g_events;
+
+// executable graphs stay alive until their launch has completed (destroyed lazily at the
+// next capture, after an event wait)
+struct GraphKeeper {
+    hipStream_t cap = nullptr;
+    hipGraphExec_t exec = nullptr;
+    hipEvent_t done = nullptr;
+    hipError_t retire() {
+        if (!exec) return hipSuccess;
+        hipError_t e = hipEventSynchronize(done);
+        if (e == hipSuccess) e = hipGraphExecDestroy(exec);
+        exec = nullptr;
+        return e;
+    }
+    hipError_t hold(hipGraphExec_t x, hipStream_t st) {
+        exec = x;
+        if (!done) {
+            hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        return hipEventRecord(done, st);
+    }
+};
+static thread_local GraphKeeper g_graphs;
+
+static int graph_mode() {
+    static int g = -1;
+    if (g < 0) {
+        const char *e = getenv("IA_GRAPH");
+        g = e ? atoi(e) : 1;
+    }
+    return g;
+}
 
 int comm_allgather_best(void *comm, const Best *send, Best *recv, int M, hipStream_t st);
 int comm_nranks(void *comm);
@@ -186,7 +153,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     carve(&ws, reinterpret_cast<char *>(a->workspace), H, W, a->nrows, nranks);
     const int Mmax = wave_max_queries(H, W);
     IA_HIP(hipMemsetAsync(ws.qp, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
-    IA_HIP(hipMemsetAsync(ws.stats, 0, 8 * sizeof(unsigned long long), st));
+    IA_HIP(hipMemsetAsync(ws.stats, 0, STATS_BYTES, st));
 
     const DbSrc src = make_dbsrc(a->src);
     const ImgPair B{a->B_sm, a->B_lg, a->B_hs, a->B_ws, H, W};
@@ -196,6 +163,8 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     if (prof && g_events.get(2 * (size_t)nw)) { set_error("hipEventCreate failed"); return IA_E_HIP; }
     double pairs = 0.0;
     int nscreen = 0;
+    bool timed = prof;
+    auto enqueue_waves = [&](hipStream_t sq) -> int {
     for (int t = 0; t < nw; ++t) {
         const int lo_num = t - (W - 1);
         const int y_lo = lo_num > 0 ? (lo_num + 2) / 3 : 0;
@@ -203,48 +172,92 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         const int M = y_hi - y_lo + 1;
         if (M <= 0) continue;
         int rc;
-        if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, st)))
+        if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, sq)))
             return rc;
-        hipEvent_t e0 = prof ? g_events.ev[2 * nscreen] : nullptr;
-        hipEvent_t e1 = prof ? g_events.ev[2 * nscreen + 1] : nullptr;
+        hipEvent_t e0 = timed ? g_events.ev[2 * nscreen] : nullptr;
+        hipEvent_t e1 = timed ? g_events.ev[2 * nscreen + 1] : nullptr;
+        const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
+                            a->im};
+        // fused tail (one launch + one round trip less per wave): measured faster for
+        // launch-bound levels, ~0.5 % slower on the 4M-row c4 finest level
+        const int fm = fuse_finish();
+        const bool fused = !a->comm && !a->lsh && match_alg() == 1 &&
+                           (fm == 2 || (fm == 1 && a->nrows <= (1L << 20)));
         if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
-            if (e0) IA_HIP(hipEventRecord(e0, st));
+            if (e0) IA_HIP(hipEventRecord(e0, sq));
             if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
-                                       ws.best_local, prof ? ws.stats : nullptr, st)))
+                                       ws.best_local, prof ? ws.stats : nullptr, sq)))
                 return rc;
-            if (e1) IA_HIP(hipEventRecord(e1, st));
+            if (e1) IA_HIP(hipEventRecord(e1, sq));
         } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, M, ws.q64, ws.nq,
                                       a->amax, ws.scratch, ws.best_local,
-                                      prof ? ws.stats : nullptr, st, e0, e1))) {
+                                      prof ? ws.stats : nullptr, sq, e0, e1,
+                                      fused ? &fa : nullptr))) {
             return rc;
         }
         ++nscreen;
         pairs += (double)M * (double)a->nrows;
+        if (fused) continue;   // the exact stage already ran the per-pixel tail
         const Best *ball = ws.best_local;
         if (a->comm) {   // also with one rank: the same RCCL path, exercised by the tests
-            if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, st))) return rc;
+            if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, sq))) return rc;
             ball = ws.best_all;
         }
-        k_finish<<<M, 64, 0, st>>>(src, ball, nranks, M, t, y_lo, W, a->N_total, ws.q64, a->weights,
-                                   a->kappa_factor, a->Bp_lg, a->s, a->im);
+        k_finish<<<M, 64, 0, sq>>>(src, ball, nranks, M, fa, ws.q64);
         IA_LAUNCH_CHECK("k_finish");
+    }
+    return IA_OK;
+    };
+    // Small levels are launch-bound (a few us of work per wave): capture the whole wave
+    // loop into one HIP graph and launch it once (IA_GRAPH: 0 off, 1 levels of <= 2^18
+    // rows [default], 2 always).  Sharded levels stay eager (RCCL calls per wave).
+    // Kernel events cannot be timed inside a graph: captured launches are not timed.
+    const int gm = graph_mode();
+    const bool use_graph = !a->comm && !(a->flags & IA_SYNTH_EAGER) &&
+                           (gm == 2 || (gm == 1 && a->nrows <= (1L << 18)));
+    if (!use_graph) {
+        int rc = enqueue_waves(st);
+        if (rc) return rc;
+    } else {
+        // capture on a private stream (the legacy default stream cannot capture)
+        timed = false;
+        IA_HIP(g_graphs.retire());
+        if (!g_graphs.cap) IA_HIP(hipStreamCreateWithFlags(&g_graphs.cap, hipStreamNonBlocking));
+        IA_HIP(hipStreamBeginCapture(g_graphs.cap, hipStreamCaptureModeThreadLocal));
+        const int rc = enqueue_waves(g_graphs.cap);
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = hipStreamEndCapture(g_graphs.cap, &graph);
+        if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+        IA_HIP(ec);
+        hipGraphExec_t exec = nullptr;
+        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        IA_HIP(ei);
+        IA_HIP(hipGraphLaunch(exec, st));
+        IA_HIP(g_graphs.hold(exec, st));
     }
     if (prof) {
         IA_HIP(hipStreamSynchronize(st));
         double ms = 0.0;
-        for (int i = 0; i < nscreen; ++i) {
+        const int ntimed = timed ? nscreen : 0;
+        for (int i = 0; i < ntimed; ++i) {
             float e = 0.f;
             IA_HIP(hipEventElapsedTime(&e, g_events.ev[2 * i], g_events.ev[2 * i + 1]));
             ms += e;
         }
-        unsigned long long st_h[8];
-        IA_HIP(hipMemcpy(st_h, ws.stats, sizeof(st_h), hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> slots(STATS_SLOTS * STATS_LINE);
+        IA_HIP(hipMemcpy(slots.data(), ws.stats, STATS_BYTES, hipMemcpyDeviceToHost));
+        unsigned long long st_h[STATS_LINE] = {};
+        for (int sl = 0; sl < STATS_SLOTS; ++sl)
+            for (int i = 0; i < STATS_LINE; ++i) st_h[i] += slots[sl * STATS_LINE + i];
         a->prof[0] = ms;
         a->prof[1] = nscreen;
         a->prof[2] = pairs;
         a->prof[3] = (double)st_h[0];
         a->prof[4] = (double)st_h[1];
         a->prof[5] = (double)st_h[2];
+        a->prof[6] = ntimed;
+        a->prof[7] = timed ? pairs : 0.0;
     }
     return IA_OK;
 }

@@ -38,8 +38,10 @@ def shard_rows(N, rank, nranks):
 
 
 def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
-                         comm=None, prof=None):
-    """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32."""
+                         comm=None, prof=None, eager=False):
+    """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32.
+    eager=True: never capture the level's wave loop into a HIP graph (every screen launch
+    is then timed when prof is given)."""
     dev = B_lg.device
     H, W = B_lg.shape
     s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
@@ -60,6 +62,7 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
     a.workspace = _ia.ptr(ws).value
     a.comm = comm
     a.lsh = index.lsh_ptr()
+    a.flags = _ia.IA_SYNTH_EAGER if eager else 0
     pbuf = None
     if prof is not None:
         pbuf = (ctypes.c_double * 8)()
@@ -69,12 +72,13 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
         prof.append({'level': level, 'screen_ms': pbuf[0], 'screens': int(pbuf[1]),
                      'pairs': pbuf[2], 'rows_rescored': int(pbuf[3]),
                      'candidate_segments': int(pbuf[4]), 'full_scans': int(pbuf[5]),
+                     'timed_screens': int(pbuf[6]), 'timed_pairs': pbuf[7],
                      'rows': index.nrows, 'pixels': H * W})
     return s, im
 
 
 def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
-                   comm=None, rank=0, nranks=1, prof=None, levels=None, lsh=None):
+                   comm=None, rank=0, nranks=1, prof=None, levels=None, lsh=None, eager=False):
     """Synthesise levels 1..max_levels-1 (image_analogies.py:119-220) from device
     pyramids.  Bp_pyr (list of device tensors) is updated in place.  lsh: None (exact
     matcher) or LevelIndex.build_lsh arguments (approximate matcher).
@@ -91,7 +95,7 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range, lsh)
         out[level] = synthesize_level_dev(level, max_levels, index, B_pyr[level - 1],
                                           B_pyr[level], Bp_pyr[level - 1], Bp_pyr[level], w,
-                                          k, comm, prof)
+                                          k, comm, prof, eager)
         del index
         if os.environ.get('IA_VERBOSE'):
             torch.cuda.synchronize()

@@ -97,7 +97,8 @@ int ia_center_fill(double *center, double mA, double mAp, void *stream);
  * L*k rows of IA_DP floats on device (p in elements 0..54, b in element 55).
  * mem: ia_lsh_bytes(nrows, L) bytes of device memory, filled by ia_lsh_build from the
  * ia_db_build output.  A query returns the exact-distance (fp64) best of up to 32 rows
- * per table bucket it falls in (lexicographic (distance, row) minimum). */
+ * per table bucket it falls in (lexicographic (distance, row) minimum; an empty bucket
+ * contributes the 4 entries around its position in the sorted table). */
 typedef struct {
     void *mem;
     const float *proj;
@@ -106,6 +107,8 @@ typedef struct {
 } IaLsh;
 size_t ia_lsh_bytes(long nrows, int L);
 int ia_lsh_build(const float *db, long nrows, const IaLsh *lsh, void *stream);
+/* bucket keys are masked to ia_lsh_bits(nrows) = ceil(log2(nrows)) + 1 bits (<= 30). */
+int ia_lsh_bits(long nrows);
 
 /* ---- a11: algorithms.py:73-75 best_approximate_match, batched: exact 1-NN of M
  * fp64 queries (M x 55, row stride IA_DP) over the DB rows built above (fp32 MFMA screen
@@ -156,12 +159,18 @@ typedef struct {
     int32_t *s, *im;
     void *workspace;
     void *comm;
-    /* optional profiling: when non-NULL the call synchronises at the end and writes
-     * {sum screen-kernel ms, #screen launches, sum query-pixels x rows (pairs),
-     *  #candidates rescored, #overflow chunks, #full scans} */
+    /* optional profiling: when non-NULL the call synchronises at the end and writes 8
+     * doubles {sum screen-kernel ms over the timed launches, #screen launches, sum
+     * query-pixels x rows (pairs), #rows rescored, #candidate segments, #full scans,
+     * #timed launches, pairs of the timed launches}.  Launches inside a captured graph
+     * (see flags) are not timed. */
     double *prof;
     const IaLsh *lsh;   /* NULL: exact matcher; else LSH tables of this shard's rows */
+    /* IA_SYNTH_EAGER: never capture the wave loop into a HIP graph.  By default a level
+     * of <= 2^18 rows on one GPU (launch-bound) is captured and launched as one graph. */
+    int flags;
 } IaSynthArgs;
+#define IA_SYNTH_EAGER 1
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);
 

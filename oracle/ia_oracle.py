@@ -505,9 +505,17 @@ def _fma32(a, b, c):
     return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
 
 
-def lsh_hash_keys(X32, proj, L, k, w):
+def lsh_bits(N):
+    """Key bits for N rows: ceil(log2(N)) + 1, at most 30 (ia_lsh.hip lsh_bits)."""
+    b = 1
+    while b < 29 and (1 << b) < N:
+        b += 1
+    return b + 1
+
+
+def lsh_hash_keys(X32, proj, L, k, w, bits=31):
     """(n, L) uint32 keys of centred fp32 rows X32 (n, 55): per table the wrapped sum of
-    mix(floor((p . x + b) / w), i), top bit cleared (ia_lsh.hip k_lsh_keys)."""
+    mix(floor((p . x + b) / w), i), masked to ``bits`` bits (ia_lsh.hip k_lsh_keys)."""
     n = X32.shape[0]
     w = np.float32(w)
     d = np.broadcast_to(proj[:, 55][None, :], (n, L * k)).astype(np.float32)
@@ -516,7 +524,7 @@ def lsh_hash_keys(X32, proj, L, k, w):
     h = np.floor(d / w).astype(np.int64) & 0xffffffff
     i = np.arange(L * k, dtype=np.int64) % k
     mix = (h * ((0x9E3779B1 + 2 * i) & 0xffffffff) + 0x7F4A7C15 * i) & 0xffffffff
-    keys = mix.reshape(n, L, k).sum(axis=2) & 0x7fffffff
+    keys = mix.reshape(n, L, k).sum(axis=2) & ((1 << bits) - 1)
     return keys.astype(np.uint32)
 
 
@@ -526,7 +534,9 @@ class LshIndex:
     def __init__(self, As_level, center, proj, L, k, w, cap=LSH_CAP):
         self.As, self.center, self.proj = As_level, center, proj
         self.L, self.k, self.w, self.cap = L, k, w, cap
-        keys = lsh_hash_keys((As_level - center[None, :]).astype(np.float32), proj, L, k, w)
+        self.bits = lsh_bits(As_level.shape[0])
+        keys = lsh_hash_keys((As_level - center[None, :]).astype(np.float32), proj, L, k, w,
+                             self.bits)
         self.order = [np.argsort(keys[:, t], kind='stable') for t in range(L)]
         self.sorted_keys = [keys[self.order[t], t] for t in range(L)]
 
@@ -535,7 +545,7 @@ class LshIndex:
         Q = np.atleast_2d(Q)
         N = self.As.shape[0]
         qk = lsh_hash_keys((Q - self.center[None, :]).astype(np.float32), self.proj, self.L,
-                           self.k, self.w)
+                           self.k, self.w, self.bits)
         idx = np.empty(len(Q), dtype=np.int64)
         dist = np.empty(len(Q))
         for m in range(len(Q)):

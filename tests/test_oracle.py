@@ -197,6 +197,7 @@ def test_lsh_keys_kat():
     X[:, 0] = [0.5, 1.5, -0.5, 7.0]
     keys = o.lsh_hash_keys(X, proj, 1, 1, 1.0)[:, 0]
     want = [(h * 0x9E3779B1) & 0x7fffffff for h in (0, 1, 0xffffffff, 7)]
+    assert [o.lsh_bits(n) for n in (1, 2, 3, 1024, 1025, 1 << 40)] == [2, 2, 3, 11, 12, 30]
     assert keys.tolist() == want
 
 

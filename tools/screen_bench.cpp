@@ -20,6 +20,9 @@
 
 #include "../include/ia.h"
 #include "../include/ia_diag.h"
+#ifdef IA_PROBE
+extern "C" int ia_probe_set(unsigned long long *buf);
+#endif
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -137,6 +140,55 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&qp, sizeof(float) * IA_DP * qrows)); CK(hipMemset(qp, 0, sizeof(float) * IA_DP * qrows));
     CK(hipMalloc(&dnq, sizeof(double) * qrows));
     CI(ia_diag_query_rows(dq, Mmax, dc, qp, dnq, st));
+#ifdef IA_PROBE
+    {   // rescore_probe: phase timestamps of the exact stage (k_rescore) for M queries
+        unsigned long long *probe;
+        const int NS = 64 * 4 * 16;
+        CK(hipMalloc(&probe, NS * 8));
+        const int M = Ms.back();
+        void *mw; CK(hipMalloc(&mw, ia_match_workspace_bytes(M, N)));
+        int64_t *idx; double *dist;
+        CK(hipMalloc(&idx, 8 * M)); CK(hipMalloc(&dist, 8 * M));
+        IaMatchArgs a{};
+        a.src = src; a.db = db; a.row0 = 0; a.nrows = N; a.center = dc; a.amax = amax;
+        a.q64 = dq; a.M = M; a.idx = idx; a.dist = dist; a.workspace = mw; a.lsh = nullptr;
+        for (int rep = 0; rep < reps + 1; ++rep) {
+            CK(hipMemset(probe, 0, NS * 8));
+            CI(ia_probe_set(probe));
+            CI(ia_match_batch(&a, st));
+            CK(hipStreamSynchronize(st));
+            CI(ia_probe_set(nullptr));
+            std::vector<unsigned long long> h(NS);
+            CK(hipMemcpy(h.data(), probe, h.size() * 8, hipMemcpyDeviceToHost));
+            if (rep == 0) continue;   // warm-up
+            const int nb = M < 64 ? M : 64;
+            unsigned long long t0 = ~0ULL;
+            for (int b = 0; b < nb; ++b) if (h[b * 64]) t0 = std::min(t0, h[b * 64]);
+            printf("M=%d rep %d: wall_clock64 @100 MHz; us after the block's wave-0 mark 0; "
+                   "mean / max over %d blocks\n", M, rep, nb);
+            for (int i = 1; i < 16; ++i) {
+                printf("  mark %2d:", i);
+                bool any = false;
+                for (int w = 0; w < 4; ++w) {
+                    double sum = 0, mx = 0; int n = 0;
+                    for (int b = 0; b < nb; ++b) {
+                        const unsigned long long x = h[(b * 4 + w) * 16 + i], s0 = h[b * 64];
+                        if (!x || !s0) continue;
+                        const double d = ((double)x - (double)s0) / 100.0;
+                        sum += d; mx = std::max(mx, d); ++n;
+                    }
+                    if (n) { printf("  w%d %6.2f/%6.2f", w, sum / n, mx); any = true; }
+                    else printf("  w%d      -/     -", w);
+                }
+                printf("%s\n", any ? "" : "  (unused)");
+            }
+            double sk = 0;
+            for (int b = 0; b < nb; ++b) sk = std::max(sk, (h[b * 64] - t0) / 100.0);
+            printf("  block start skew: %.2f us\n", sk);
+        }
+        return 0;
+    }
+#endif
     const size_t cb = ia_diag_cand_bytes(Mmax, N);
     char *cand, *cand_ref;
     CK(hipMalloc(&cand, cb)); CK(hipMalloc(&cand_ref, cb));
