@@ -74,6 +74,7 @@ _SIGS = {
     'ia_level_features_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, _dp, _dp]),
     'ia_db_rows_padded': (ctypes.c_long, [ctypes.c_long]),
+    'ia_db_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_db_chunk_rows': (ctypes.c_int, [ctypes.c_long]),
     'ia_db_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
                                    _dp, _dp, _dp, _dp]),
@@ -93,6 +94,12 @@ _SIGS = {
                                     ctypes.POINTER(ctypes.c_void_p)]),
     'ia_comm_destroy': (ctypes.c_int, [_dp]),
     'ia_comm_nranks': (ctypes.c_int, [_dp]),
+    # diagnostics (include/ia_diag.h)
+    'ia_diag_set_match_alg': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
+    'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, ctypes.c_int,
+                                        _dp]),
 }
 
 _lib = None
@@ -128,6 +135,12 @@ def lib():
             fn.argtypes = args
         _lib = l
     return _lib
+
+
+def match_alg(alg=-1):
+    """Select the exact matcher's screen for this process (0 per-lane top-K, 1 f32-MFMA
+    segment minima, 2 split-f16 segment minima [default]); returns the previous value."""
+    return lib().ia_diag_set_match_alg(int(alg))
 
 
 def check(rc, what):

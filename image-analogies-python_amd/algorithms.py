@@ -92,8 +92,9 @@ class LevelIndex:
         mAp = _ia.mean_dev(self.Ap_lg)
         self.center = torch.empty(55, dtype=torch.float64, device=dev)
         _ia.check(lib.ia_center_fill(_ia.ptr(self.center), mA, mAp, st), 'ia_center_fill')
-        npad = lib.ia_db_rows_padded(self.nrows)
-        self.db = torch.empty((npad, _ia.IA_DP), dtype=torch.float32, device=dev)
+        nbytes = lib.ia_db_bytes(self.nrows)      # fp32 rows + their split-f16 copy
+        self.db = torch.empty((nbytes // (4 * _ia.IA_DP), _ia.IA_DP), dtype=torch.float32,
+                              device=dev)
         self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
         _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
                                   _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),

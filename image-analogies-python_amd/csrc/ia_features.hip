@@ -8,6 +8,7 @@
 // screen, whose error bound is accounted for in ia_match.hip.
 #include "ia_common.h"
 #include "ia_internal.h"
+#include "ia_split16.h"
 
 namespace ia {
 
@@ -74,6 +75,52 @@ __global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nro
     }
 }
 
+// Split-f16 copy of the fp32 DB (ia_split16.h): one wave per 32-row tile, the tile
+// un-permuted through LDS, then lane (j, h) emits its 7 half8 register groups; output
+// half8 (tile, g, lane) at (tile * 7 + g) * 64 + lane, so each of the screen's 7 loads
+// per tile is one contiguous 1 KiB wave access.  Padding rows (>= nrows) are zero (the
+// screen masks them).  Runs after k_db_build on the same stream (needs the final amax).
+__global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, long nrows,
+                                                  const float *__restrict__ amax,
+                                                  half8 *__restrict__ db16) {
+    constexpr int LD = IA_DP + 1;
+    __shared__ float t[4][32 * LD];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j = lane & 31, h = lane >> 5;
+    const long T = (long)blockIdx.x * 4 + wv;
+    const float4 *src = reinterpret_cast<const float4 *>(db) + T * (7 * 64) + lane;
+    float *tr = t[wv] + j * LD;
+#pragma unroll
+    for (int v = 0; v < 7; ++v) {   // positions h*28 + 4v + c = element 2(4v + c) + h
+        const float4 x = src[v * 64];
+        tr[2 * (4 * v + 0) + h] = x.x;
+        tr[2 * (4 * v + 1) + h] = x.y;
+        tr[2 * (4 * v + 2) + h] = x.z;
+        tr[2 * (4 * v + 3) + h] = x.w;
+    }
+    __syncthreads();
+    const Split16Db s = split16_db_scale(amax[0]);
+    const bool real = T * 32 + j < nrows;
+    auto val = [&](int k) { return k < 55 ? ldexpf(tr[k], s.ea) : ldexpf(tr[55], s.ea - s.R); };
+    half8 *out = db16 + T * (DB16_GROUPS * 64) + lane;
+#pragma unroll
+    for (int g = 0; g < DB16_GROUPS; ++g) {
+        // (h, g) -> 8 features k0..k0+7, hi or lo part (ia_split16.h table)
+        int k0;
+        bool hi;
+        if (h == 0) { hi = g < 4; k0 = hi ? 8 * g : 8 * (g - 4); }
+        else { hi = g >= 1 && g <= 3; k0 = g == 0 ? 24 : (hi ? 32 + 8 * (g - 1) : 32 + 8 * (g - 4)); }
+        half8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            _Float16 xh, xl;
+            split16f(val(k0 + e), xh, xl);
+            o[e] = real ? (hi ? xh : xl) : (_Float16)0.f;
+        }
+        out[g * 64] = o;
+    }
+}
+
 __global__ void k_center_fill(double *c, double mA, double mAp) {
     const int k = threadIdx.x;
     if (k < IA_D) c[k] = k < 34 ? mA : mAp;
@@ -86,7 +133,9 @@ __global__ __launch_bounds__(64) void k_query_wave(ImgPair B, ImgPair Bp, int t,
                                                    const double *__restrict__ center,
                                                    double *__restrict__ q64,
                                                    float *__restrict__ qp,
-                                                   double *__restrict__ nq) {
+                                                   double *__restrict__ nq,
+                                                   const float *__restrict__ amax,
+                                                   _Float16 *__restrict__ q16) {
     const int m = blockIdx.x;
     const int y = y_lo + m, x = t - 3 * y;
     const int lane = threadIdx.x;
@@ -113,15 +162,18 @@ __global__ __launch_bounds__(64) void k_query_wave(ImgPair B, ImgPair Bp, int t,
         qp[(long)m * IA_DP + perm56(55)] = 1.0f;
     }
     double d2 = d * d;
-    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
     if (lane == 0) nq[m] = d2;
+    if (q16) split16_write_query(q16 + (long)m * Q16_ROW * 8, lane, d, d2, amax[0]);
 }
 
 // Query rows from caller-provided fp64 features (ia_match_batch).
 __global__ __launch_bounds__(64) void k_query_rows(const double *__restrict__ qin, int M,
                                                    const double *__restrict__ center,
                                                    float *__restrict__ qp,
-                                                   double *__restrict__ nq) {
+                                                   double *__restrict__ nq,
+                                                   const float *__restrict__ amax,
+                                                   _Float16 *__restrict__ q16) {
     const int m = blockIdx.x;
     const int lane = threadIdx.x;
     double d = 0.0;
@@ -132,21 +184,22 @@ __global__ __launch_bounds__(64) void k_query_rows(const double *__restrict__ qi
         qp[(long)m * IA_DP + perm56(55)] = 1.0f;
     }
     double d2 = d * d;
-    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
     if (lane == 0) nq[m] = d2;
+    if (q16) split16_write_query(q16 + (long)m * Q16_ROW * 8, lane, d, d2, amax[0]);
 }
 
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
                       const double *center, double *q64, float *qp, double *nq,
-                      hipStream_t st) {
-    k_query_wave<<<M, 64, 0, st>>>(B, Bp, t, y_lo, center, q64, qp, nq);
+                      const float *amax, _Float16 *q16, hipStream_t st) {
+    k_query_wave<<<M, 64, 0, st>>>(B, Bp, t, y_lo, center, q64, qp, nq, amax, q16);
     IA_LAUNCH_CHECK("k_query_wave");
     return IA_OK;
 }
 
 int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
-                      hipStream_t st) {
-    k_query_rows<<<M, 64, 0, st>>>(qin, M, center, qp, nq);
+                      const float *amax, _Float16 *q16, hipStream_t st) {
+    k_query_rows<<<M, 64, 0, st>>>(qin, M, center, qp, nq, amax, q16);
     IA_LAUNCH_CHECK("k_query_rows");
     return IA_OK;
 }
@@ -169,6 +222,7 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
 
 int ia_db_chunk_rows(long nrows) { return db_chunk_rows(nrows); }
 long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
+size_t ia_db_bytes(long nrows) { return db_bytes(nrows); }
 
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 float *db, float *amax, void *stream) {
@@ -179,6 +233,8 @@ int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *cent
     k_db_build<<<(unsigned)((npad + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, npad,
                                                                      center, db, amax);
     IA_LAUNCH_CHECK("k_db_build");
+    k_db_split<<<(unsigned)(npad / 128), 256, 0, S(stream)>>>(db, nrows, amax, reinterpret_cast<half8 *>(db16_of(db, nrows)));
+    IA_LAUNCH_CHECK("k_db_split");
     return IA_OK;
 }
 

@@ -25,6 +25,13 @@ static inline long db_nchunks(long nrows) {
     return (nrows + ch - 1) / ch;
 }
 static inline long db_rows_padded(long nrows) { return db_nchunks(nrows) * db_chunk_rows(nrows); }
+// one DB buffer = the fp32 screening rows (npad x IA_DP floats, fragment-major) followed
+// by their split-f16 copy (npad x 112 halves, ia_split16.h): 2 x 224 B per padded row
+static inline size_t db_bytes(long nrows) { return (size_t)db_rows_padded(nrows) * IA_DP * 4 * 2; }
+template <typename T>
+static inline T *db16_of(T *db, long nrows) {
+    return db + (size_t)db_rows_padded(nrows) * IA_DP * 4 / sizeof(T);
+}
 // segment-minimum matcher: one running minimum per (query, segment) of <= 512 rows
 static inline int db_seg_rows(long nrows) {
     const int rpw = db_chunk_rows(nrows) / 4;
@@ -86,11 +93,12 @@ __device__ __forceinline__ unsigned long long *stats_slot(unsigned long long *s,
 }
 
 // ---- launchers ------------------------------------------------------------------
+// q16 (nullable): the split-f16 query rows (Q16_ROW half8 each, ia_split16.h)
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
                       const double *center, double *q64, float *qp, double *nq,
-                      hipStream_t st);
+                      const float *amax, _Float16 *q16, hipStream_t st);
 int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
-                      hipStream_t st);
+                      const float *amax, _Float16 *q16, hipStream_t st);
 // screen of M queries (qp) against nrows DB rows -> cand[M][nchunks][SCREEN_K]
 // variant 0: queries in VGPRs (<= 3 tiles/wave); 1: queries in LDS (<= 6 tiles/wave)
 int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
@@ -110,15 +118,17 @@ size_t match_scratch_bytes(int qrows, long nrows);
 // ev0 / ev1 (nullable) are recorded on st immediately before / after the screen launch.
 // fin (nullable, single shard only): the exact stage also runs the per-pixel tail of the
 // wave (coherence, kappa, B'/s/im update) in the same kernel.
-int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp, int M,
-                 const double *q64, const double *nq, const float *amax, void *scratch,
-                 Best *best, unsigned long long *stats, hipStream_t st,
+int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp,
+                 const _Float16 *q16, int M, const double *q64, const double *nq,
+                 const float *amax, void *scratch, Best *best, unsigned long long *stats,
+                 hipStream_t st,
                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                  const FinishArgs *fin = nullptr);
 int fuse_finish();    // IA_FUSE_FINISH: 0 off, 1 levels <= 2^20 rows [default], 2 on
-int match_alg();      // IA_MATCH_ALG (default 1: segment minima)
+int match_alg();      // IA_MATCH_ALG (default 2: segment minima, split-f16 screen)
+// q16 != nullptr: the split-f16 screen (k_screen_h16) over db16_of(db)
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
-                      int maxnq, hipStream_t st);
+                      int maxnq, hipStream_t st, const _Float16 *q16 = nullptr);
 int screen_variant();
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query
 int launch_lsh_match(const IaLsh *lsh, const DbSrc &src, long row0, long nrows, int M,

@@ -21,6 +21,7 @@
 //     break to the lowest row index (np.argmin).  The result is bit-identical to the
 //     oracle's brute force for any input.
 #include "ia_finish.h"
+#include "ia_split16.h"
 
 #include <float.h>
 
@@ -811,6 +812,119 @@ __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db
         seg_body<NQA>(db, chunk, ch, seg_rows, qp, M, group * NQA, segmin, nseg);
 }
 
+// =================================================================================
+// Split-f16 segment screen (IA_MATCH_ALG=2, ia_split16.h): the same segment minima as
+// k_screen_seg, from 11 v_mfma_f32_32x32x16_f16 per 32x32 tile instead of 28
+// v_mfma_f32_32x32x2_f32 (352 vs 1792 MFMA cycles per tile and wave).  Values are in
+// the scaled units sa * sq_j * e; rows >= nrows (padding) are masked to FLT_MAX.
+// =================================================================================
+__device__ __forceinline__ void load_tile16(half8 (&a)[DB16_GROUPS], const half8 *p) {
+#pragma unroll
+    for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+}
+
+template <int NQ>
+__device__ __forceinline__ void seg16_body(const half8 *__restrict__ db16, int chunk, int ch,
+                                           int seg_rows, long nrows,
+                                           const half8 *__restrict__ q16, int M, int tile0,
+                                           float *__restrict__ segmin, long nseg) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int j = lane & 31, h = lane >> 5;
+
+    half8 bq[NQ][Q16_GROUPS];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        const half8 *p = q16 + (long)((tile0 + qt) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m) bq[qt][m] = p[m];
+    }
+    const int rows_per_wave = ch >> 2;
+    const int ntile = rows_per_wave >> 5;
+    const int tps = seg_rows >> 5;
+    const long row_begin = (long)chunk * ch + wv * rows_per_wave;
+    const long seg_begin = row_begin / seg_rows;
+    const half8 *dp = db16 + (row_begin >> 5) * (DB16_GROUPS * 64) + lane;
+
+    float mn[NQ];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) mn[qt] = FLT_MAX;
+
+    auto tile_min = [&](const half8 (&a)[DB16_GROUPS], int tile) {
+        floatx16 acc[NQ];
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m)
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt)
+                acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m < 7 ? m : m - 7], bq[qt][m],
+                                                                 acc[qt], 0, 0, 0);
+        const long r0 = row_begin + (long)tile * 32;
+        if (r0 + 32 > nrows) {   // tail tile of the last chunk: mask padding rows
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (r0 + (r & 3) + 8 * (r >> 2) + 4 * h >= nrows) acc[qt][r] = FLT_MAX;
+        }
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt) {
+            float m = mn[qt];
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) m = fminf(m, fminf(acc[qt][r], acc[qt][r + 1]));
+            mn[qt] = m;
+        }
+    };
+    auto flush = [&](int tile) {
+        const long seg = seg_begin + tile / tps;
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt) {
+            const float m = fminf(mn[qt], __shfl_xor(mn[qt], 32));
+            const int qg = (tile0 + qt) * 32 + j;
+            if (h == 0 && qg < M) segmin[(long)qg * nseg + seg] = m;
+            mn[qt] = FLT_MAX;
+        }
+    };
+
+    half8 b0[DB16_GROUPS], b1[DB16_GROUPS];
+    load_tile16(b0, dp);
+    int tile = 0;
+    for (; tile + 1 < ntile; tile += 2) {
+        load_tile16(b1, dp + (long)(tile + 1) * (DB16_GROUPS * 64));
+        tile_min(b0, tile);
+        if ((tile + 1) % tps == 0) flush(tile);
+        const int nxt = tile + 2 < ntile ? tile + 2 : ntile - 1;
+        load_tile16(b0, dp + (long)nxt * (DB16_GROUPS * 64));
+        tile_min(b1, tile + 1);
+        if ((tile + 2) % tps == 0) flush(tile + 1);
+    }
+    if (tile < ntile) {
+        tile_min(b0, tile);
+        flush(tile);
+    }
+}
+
+template <int NQA, int NQB>
+__global__ __launch_bounds__(256) void k_screen_h16(const half8 *__restrict__ db16, int nchunks,
+                                                    int ch, int seg_rows, long nrows,
+                                                    const half8 *__restrict__ q16, int M,
+                                                    int groups, int nA,
+                                                    float *__restrict__ segmin, long nseg) {
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+    if (NQB > 0 && group >= nA)
+        seg16_body<(NQB > 0 ? NQB : 1)>(db16, chunk, ch, seg_rows, nrows, q16, M,
+                                        nA * NQA + (group - nA) * NQB, segmin, nseg);
+    else
+        seg16_body<NQA>(db16, chunk, ch, seg_rows, nrows, q16, M, group * NQA, segmin, nseg);
+}
+
 // Phase probes (tools/rescore_probe only: built with -DIA_PROBE into a separate library):
 // lane 0 of every wave of the first 64 workgroups stores wall_clock64() at each mark
 // (slot [block][wave][mark], 64 x 4 x 16).
@@ -834,7 +948,7 @@ constexpr int RESCORE_RPT = 2;         // candidate rows per thread per step
 // Exact stage of the segment-minimum matcher: one 256-thread workgroup per query.
 // FIN: single shard — wave 0 then runs the per-pixel tail of the synthesis step
 // (ia_finish.h) on the winner, saving a launch and a round trip per wave.
-template <bool FIN>
+template <bool FIN, bool SPLIT>
 __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrows, long nseg,
                                                  int seg_rows, const float *__restrict__ segmin,
                                                  const float *__restrict__ db,
@@ -892,11 +1006,30 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     IA_PROBE_MARK(2);
     emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
 
-    const double eps = 70.0 * 5.9604644775390625e-08 * (2.0 * A * sqrt(nqq) + A * A);
-    const double T = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
+    constexpr double U32 = 5.9604644775390625e-08;
+    const double eps = 70.0 * U32 * (2.0 * A * sqrt(nqq) + A * A);
+    // Tseg: segment-minimum threshold (screen units), Trow: re-screen threshold (fp32
+    // VALU recomputation, unscaled).  f32 screen: both e* + 2 eps.  Split-f16 screen
+    // (minima in units of sa * sq): e* = emin / (sa sq) exactly, Tseg = e* + 2 eps16,
+    // Trow = e* + eps16 + eps.
+    double Tseg, Trow;
+    bool force_full = false;
+    if (SPLIT) {
+        const Split16Db sc = split16_db_scale(amax[0]);
+        const int eq = split16_q_scale(nqq, sc.R);
+        const int e2 = sc.ea + eq;
+        const double em = ldexp((double)emin, -e2);
+        const double eps16 = U32 * (300.0 * A * sqrt(nqq) + 50.0 * A * A);
+        const double slack = 1e-12 * (fabs(em) + nqq + A * A);
+        Tseg = ldexp(em + 2.0 * eps16 + slack, e2);
+        Trow = em + eps16 + eps + slack;
+        force_full = eq + sc.R < -10;   // |q'| > 2^24 Amax: the norm slot nears f16 flush
+    } else {
+        Tseg = Trow = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
+    }
 
     auto push = [&](float e, long s) {
-        if ((double)e <= T) {
+        if ((double)e <= Tseg) {
             const int pos = atomicAdd(&scount, 1);
             if (pos < RESCORE_SEGCAP) slist[pos] = (int)s;
         }
@@ -919,7 +1052,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     __syncthreads();
     IA_PROBE_MARK(3);
     const int ns = scount;
-    const bool full = ns > RESCORE_SEGCAP;
+    const bool full = ns > RESCORE_SEGCAP || force_full;
     const long nscan = full ? nseg : ns;
 
     double bd = INFINITY;
@@ -957,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
         IA_PROBE_MARK(8);
 #pragma unroll
         for (int u = 0; u < RESCORE_RPT; ++u) {
-            if (lr[u] < nrows && (double)e[u] <= T) {
+            if (lr[u] < nrows && (double)e[u] <= Trow) {
                 ++mine;
                 best_update(bd, bi, row_dist2(src, row0 + lr[u], qs), row0 + lr[u]);
             }
@@ -1001,7 +1134,7 @@ int fuse_finish() {
 }
 
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
-                      int maxnq, hipStream_t st) {
+                      int maxnq, hipStream_t st, const _Float16 *q16) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -1025,7 +1158,16 @@ int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float
     }
     const long nblocks = ((nchunks + 7) / 8) * 8 * groups;
     IA_ARG(nblocks < (1L << 31), "screen grid too large");
+    const half8 *db16 = reinterpret_cast<const half8 *>(db16_of(db, nrows));
+    const half8 *q16v = reinterpret_cast<const half8 *>(q16);
 #define IA_SEG_CASE(NA, NB)                                                                   \
+    if (nqa == NA && nqb == NB && q16) {                                                      \
+        k_screen_h16<NA, NB><<<(unsigned)nblocks, 256, 0, st>>>(db16, (int)nchunks, ch,       \
+                                                                seg_rows, nrows, q16v, M,     \
+                                                                groups, nA, segmin, nseg);    \
+        IA_LAUNCH_CHECK("k_screen_h16");                                                      \
+        return IA_OK;                                                                         \
+    }                                                                                         \
     if (nqa == NA && nqb == NB) {                                                             \
         k_screen_seg<NA, NB><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, \
                                                                 qp, M, groups, nA, segmin,    \
@@ -1042,12 +1184,14 @@ int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float
     return IA_E_ARG;
 }
 
+static int g_match_alg = -1;
 int match_alg() {
-    static int a = -1;
+    int &a = g_match_alg;
     if (a < 0) {
-        const char *e = getenv("IA_MATCH_ALG");   // 0 = per-lane top-K, 1 = segment minima
-        a = e ? atoi(e) : 1;
-        if (a < 0 || a > 1) a = 1;
+        // 0 = per-lane top-K, 1 = segment minima (f32 MFMA), 2 = segment minima (split f16)
+        const char *e = getenv("IA_MATCH_ALG");
+        a = e ? atoi(e) : 2;
+        if (a < 0 || a > 2) a = 2;
     }
     return a;
 }
@@ -1058,13 +1202,14 @@ size_t match_scratch_bytes(int qrows, long nrows) {
     return a > b ? a : b;
 }
 
-int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp, int M,
-                 const double *q64, const double *nq, const float *amax, void *scratch,
-                 Best *best, unsigned long long *stats, hipStream_t st, hipEvent_t ev0,
-                 hipEvent_t ev1, const FinishArgs *fin) {
+int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp,
+                 const _Float16 *q16, int M, const double *q64, const double *nq,
+                 const float *amax, void *scratch, Best *best, unsigned long long *stats,
+                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, const FinishArgs *fin) {
     int rc;
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
-    IA_ARG(!fin || match_alg() == 1, "launch_match: the fused tail needs the segment matcher");
+    IA_ARG(!fin || match_alg() >= 1, "launch_match: the fused tail needs the segment matcher");
+    IA_ARG(match_alg() != 2 || q16, "launch_match: split-f16 screen without q16 rows");
     if (match_alg() == 0) {
         Cand *cand = reinterpret_cast<Cand *>(scratch);
         if ((rc = launch_screen(db, nrows, qp, M, cand, st))) return rc;
@@ -1073,17 +1218,22 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
     }
     float *segmin = reinterpret_cast<float *>(scratch);
     const int nq_cap = (screen_variant() >> 4) & 15;
-    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, nq_cap > 0 && nq_cap <= 3 ? nq_cap : 3,
-                                st)))
+    const bool split = match_alg() == 2;
+    // default query tiles per wave: 3 (f32: profiles/r01_screen_bench_split.txt), 2 (split
+    // f16: profiles/r01_screen_bench_h16.txt)
+    const int cap = nq_cap > 0 && nq_cap <= 3 ? nq_cap : (split ? 2 : 3);
+    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, cap, st, split ? q16 : nullptr)))
         return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
-    if (fin)
-        k_rescore<true><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows),
-                                           segmin, db, qp, q64, nq, amax, best, stats, *fin);
-    else
-        k_rescore<false><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows),
-                                            segmin, db, qp, q64, nq, amax, best, stats,
-                                            FinishArgs{});
+    const FinishArgs fa = fin ? *fin : FinishArgs{};
+#define IA_RESCORE(F, SP)                                                                      \
+    k_rescore<F, SP><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows), \
+                                        segmin, db, qp, q64, nq, amax, best, stats, fa)
+    if (fin && split) IA_RESCORE(true, true);
+    else if (fin) IA_RESCORE(true, false);
+    else if (split) IA_RESCORE(false, true);
+    else IA_RESCORE(false, false);
+#undef IA_RESCORE
     IA_LAUNCH_CHECK("k_rescore");
     return IA_OK;
 }
@@ -1146,6 +1296,7 @@ size_t ia_match_workspace_bytes(int M, long nrows) {
     const int qr = qrows_alloc(mb);
     size_t b = 0;
     b += align_up((size_t)qr * IA_DP * sizeof(float), 256);                        // qp
+    b += align_up((size_t)qr * Q16_ROW * sizeof(half8), 256);                      // q16
     b += align_up((size_t)qr * sizeof(double), 256);                               // nq
     b += align_up(match_scratch_bytes(qr, nrows), 256);                           // screen out
     b += align_up((size_t)qr * sizeof(Best), 256);                                 // best
@@ -1163,12 +1314,15 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
     char *w = reinterpret_cast<char *>(a->workspace);
     float *qp = reinterpret_cast<float *>(w);
     w += align_up((size_t)qr * IA_DP * sizeof(float), 256);
+    _Float16 *q16 = reinterpret_cast<_Float16 *>(w);
+    w += align_up((size_t)qr * Q16_ROW * sizeof(half8), 256);
     double *nq = reinterpret_cast<double *>(w);
     w += align_up((size_t)qr * sizeof(double), 256);
     void *scratch = w;
     w += align_up(match_scratch_bytes(qr, a->nrows), 256);
     Best *best = reinterpret_cast<Best *>(w);
     IA_HIP(hipMemsetAsync(qp, 0, (size_t)qr * IA_DP * sizeof(float), st));
+    IA_HIP(hipMemsetAsync(q16, 0, (size_t)qr * Q16_ROW * sizeof(half8), st));
     const DbSrc src = make_dbsrc(a->src);
     for (int m0 = 0; m0 < a->M; m0 += MATCH_BATCH) {
         const int M = a->M - m0 < MATCH_BATCH ? a->M - m0 : MATCH_BATCH;
@@ -1179,8 +1333,8 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
                                        nullptr, st)))
                 return rc;
         } else {
-            if ((rc = launch_query_rows(q, M, a->center, qp, nq, st))) return rc;
-            if ((rc = launch_match(src, a->row0, a->nrows, a->db, qp, M, q, nq, a->amax,
+            if ((rc = launch_query_rows(q, M, a->center, qp, nq, a->amax, q16, st))) return rc;
+            if ((rc = launch_match(src, a->row0, a->nrows, a->db, qp, q16, M, q, nq, a->amax,
                                    scratch, best, nullptr, st)))
                 return rc;
         }
@@ -1221,7 +1375,29 @@ int ia_diag_qp_rows(int M) { return qrows_alloc(M); }
 int ia_diag_query_rows(const double *q64, int M, const double *center, float *qp, double *nq,
                        void *stream) {
     IA_ARG(q64 && center && qp && nq && M > 0, "ia_diag_query_rows: bad args");
-    return launch_query_rows(q64, M, center, qp, nq, S(stream));
+    return launch_query_rows(q64, M, center, qp, nq, nullptr, nullptr, S(stream));
+}
+
+int ia_diag_query_rows16(const double *q64, int M, const double *center, const float *amax,
+                         float *qp, void *q16, double *nq, void *stream) {
+    IA_ARG(q64 && center && amax && qp && q16 && nq && M > 0, "ia_diag_query_rows16: bad args");
+    return launch_query_rows(q64, M, center, qp, nq, amax, reinterpret_cast<_Float16 *>(q16),
+                             S(stream));
+}
+
+int ia_diag_set_match_alg(int alg) {
+    const int prev = match_alg();
+    if (alg >= 0 && alg <= 2) g_match_alg = alg;
+    return prev;
+}
+
+int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
+                     int maxnq, void *stream) {
+    IA_ARG(db && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16: bad args");
+    const int cap = maxnq & 15;
+    return launch_screen_seg(db, nrows, nullptr, M, segmin,
+                             (cap > 0 && cap <= 3 ? cap : 3) | (maxnq & 0x100), S(stream),
+                             reinterpret_cast<const _Float16 *>(q16));
 }
 
 int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand, int variant,

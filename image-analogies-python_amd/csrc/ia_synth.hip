@@ -15,6 +15,7 @@
 //   [RCCL all-gather of best over ranks when the DB is sharded]
 //   k_finish      -> coherence, kappa test, B'/s/im update (this file)
 #include "ia_finish.h"
+#include "ia_split16.h"
 
 #include <vector>
 
@@ -45,6 +46,7 @@ __global__ __launch_bounds__(64) void k_finish(DbSrc src, const Best *__restrict
 struct SynthWs {
     double *q64;
     float *qp;
+    _Float16 *q16;
     double *nq;
     void *scratch;           // screen output (candidates or segment minima)
     Best *best_local;
@@ -65,6 +67,7 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     SynthWs w;
     w.q64 = (double *)take((size_t)Mmax * IA_DP * sizeof(double));
     w.qp = (float *)take((size_t)qr * IA_DP * sizeof(float));
+    w.q16 = (_Float16 *)take((size_t)qr * Q16_ROW * 16);
     w.nq = (double *)take((size_t)qr * sizeof(double));
     w.scratch = take(match_scratch_bytes(qr, nrows));
     w.best_local = (Best *)take((size_t)Mmax * sizeof(Best));
@@ -153,6 +156,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     carve(&ws, reinterpret_cast<char *>(a->workspace), H, W, a->nrows, nranks);
     const int Mmax = wave_max_queries(H, W);
     IA_HIP(hipMemsetAsync(ws.qp, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
+    IA_HIP(hipMemsetAsync(ws.q16, 0, (size_t)qrows_alloc(Mmax) * Q16_ROW * 16, st));
     IA_HIP(hipMemsetAsync(ws.stats, 0, STATS_BYTES, st));
 
     const DbSrc src = make_dbsrc(a->src);
@@ -172,7 +176,8 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         const int M = y_hi - y_lo + 1;
         if (M <= 0) continue;
         int rc;
-        if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, sq)))
+        if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
+                                    match_alg() == 2 ? ws.q16 : nullptr, sq)))
             return rc;
         hipEvent_t e0 = timed ? g_events.ev[2 * nscreen] : nullptr;
         hipEvent_t e1 = timed ? g_events.ev[2 * nscreen + 1] : nullptr;
@@ -181,7 +186,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         // fused tail (one launch + one round trip less per wave): measured faster for
         // launch-bound levels, ~0.5 % slower on the 4M-row c4 finest level
         const int fm = fuse_finish();
-        const bool fused = !a->comm && !a->lsh && match_alg() == 1 &&
+        const bool fused = !a->comm && !a->lsh && match_alg() >= 1 &&
                            (fm == 2 || (fm == 1 && a->nrows <= (1L << 20)));
         if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
             if (e0) IA_HIP(hipEventRecord(e0, sq));
@@ -189,7 +194,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
                                        ws.best_local, prof ? ws.stats : nullptr, sq)))
                 return rc;
             if (e1) IA_HIP(hipEventRecord(e1, sq));
-        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, M, ws.q64, ws.nq,
+        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, ws.q16, M, ws.q64, ws.nq,
                                       a->amax, ws.scratch, ws.best_local,
                                       prof ? ws.stats : nullptr, sq, e0, e1,
                                       fused ? &fa : nullptr))) {

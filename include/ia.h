@@ -85,6 +85,10 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
  * .. +3.  Rows are padded to ia_db_rows_padded(nrows) with sentinel rows.
  * amax (device, 1 float) receives max_row |a - center| (atomic max; zero it first). */
 long ia_db_rows_padded(long nrows);
+/* bytes of the db buffer ia_db_build fills: the fp32 rows above (ia_db_rows_padded x
+ * IA_DP floats) followed by their split-f16 copy for the default screen (the same size
+ * again). */
+size_t ia_db_bytes(long nrows);
 int ia_db_chunk_rows(long nrows);
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 float *db, float *amax, void *stream);

@@ -25,6 +25,19 @@ int ia_diag_query_rows(const double *q64, int M, const double *center, float *qp
 int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand,
                    int variant, void *stream);
 
+/* split-f16 screen (the default matcher's stage 1): query rows in both
+ * forms (qp as ia_diag_query_rows, q16 = ia_diag_qp_rows(M) x 352 B, zeroed by the caller;
+ * amax from ia_db_build), and one k_screen_h16 launch -> segment minima (screen units).
+ * maxnq: bits 0-3 cap on query tiles per wave (0 = default), bit 8 uniform groups. */
+int ia_diag_query_rows16(const double *q64, int M, const double *center, const float *amax,
+                         float *qp, void *q16, double *nq, void *stream);
+/* select the exact matcher's screen for this process (overrides IA_MATCH_ALG): 0 per-lane
+ * top-K (f32), 1 segment minima (f32 MFMA), 2 segment minima (split-f16 MFMA, default);
+ * returns the previous value (a negative alg only queries it). */
+int ia_diag_set_match_alg(int alg);
+int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
+                     int maxnq, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,146 @@
+"""The split-f16 screen on the GPU: its segment minima stay inside the
+error bound eps16 the exact stage relies on, and the whole matcher / synthesis stays
+bit-exact with either screen (IA_MATCH_ALG 1 = f32 MFMA, 2 = split-f16 MFMA)."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import ia_oracle as o
+import ia_oracle_c as oc
+from conftest import analogy_inputs
+
+pytestmark = pytest.mark.gpu
+
+U32 = 2.0 ** -24
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a)).to('cuda', dtype=dtype)
+
+
+def _ilogb(x):
+    return math.frexp(x)[1] - 1
+
+
+def _scales(amax, nq):
+    """Host restatement of split16_db_scale / split16_q_scale (ia_split16.h)."""
+    e = _ilogb(amax) if amax > 0 else 0
+    e = max(-60, min(60, e))
+    ea, R = 13 - e, e + 1
+    eq = 15 - R
+    if nq > 0:
+        eq = min(eq, 12 - _ilogb(math.sqrt(nq)))
+    return ea, R, max(eq, -120)
+
+
+@pytest.fixture
+def alg():
+    import _ia
+    prev = _ia.match_alg()
+    yield _ia.match_alg
+    _ia.match_alg(prev)
+
+
+def _index(A, Aps):
+    import algorithms
+    A_pyr = o.compute_gaussian_pyramid(A, 3)
+    Ap_pyr = [o.compute_gaussian_pyramid(x, 3) for x in Aps]
+    L = len(A_pyr)
+    idx = algorithms.level_index([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_pyr],
+                                 L - 1)
+    return idx, o.create_index(A_pyr, Ap_pyr, L)[L - 1]
+
+
+def _queries(As, rs):
+    n = len(As)
+    return np.vstack([As[rs.randint(0, n, 64)],                              # exact rows
+                      As[rs.randint(0, n, 64)] + rs.randn(64, 55) * 1e-7,    # near ties
+                      As[rs.randint(0, n, 64)] + rs.randn(64, 55) * 0.02,
+                      rs.rand(40, 55) * As.max(),                            # far queries
+                      np.full((1, 55), As.mean())])                          # ~ the centre
+
+
+@pytest.mark.parametrize('scale', [1.0, 1e3, 1e-3])
+def test_split16_segment_minima_within_bound(gpu, scale):
+    import _ia
+    lib = _ia.lib()
+    A, Aps, _ = analogy_inputs(41, (90, 117), (8, 8), n_ap=2)
+    A, Aps = A * scale, [x * scale for x in Aps]
+    idx, As = _index(A, Aps)
+    rs = np.random.RandomState(2)
+    Q = _queries(As, rs)
+    M, N = len(Q), len(As)
+    qrows = lib.ia_diag_qp_rows(M)
+    q64 = torch.zeros((M, _ia.IA_DP), dtype=torch.float64, device='cuda')
+    q64[:, :55] = dev(Q)
+    qp = torch.zeros((qrows, _ia.IA_DP), dtype=torch.float32, device='cuda')
+    q16 = torch.zeros((qrows, 176), dtype=torch.float16, device='cuda')
+    nq = torch.zeros(qrows, dtype=torch.float64, device='cuda')
+    st = _ia.stream()
+    _ia.check(lib.ia_diag_query_rows16(_ia.ptr(q64), M, _ia.ptr(idx.center), _ia.ptr(idx.amax),
+                                       _ia.ptr(qp), _ia.ptr(q16), _ia.ptr(nq), st),
+              'ia_diag_query_rows16')
+    npad = lib.ia_db_rows_padded(N)
+    seg = min(lib.ia_db_chunk_rows(N) // 4, 512)
+    nseg = npad // seg
+    segmin = torch.zeros((qrows, nseg), dtype=torch.float32, device='cuda')
+    _ia.check(lib.ia_diag_screen16(_ia.ptr(idx.db), N, _ia.ptr(q16), M, _ia.ptr(segmin), 0, st),
+              'ia_diag_screen16')
+    torch.cuda.synchronize()
+    got = segmin[:M].cpu().numpy().astype(np.float64)
+    amax = float(idx.amax.item())
+    c = idx.center.cpu().numpy()
+    a = As - c
+    na = np.einsum('ij,ij->i', a, a)
+    assert np.sqrt(na.max()) <= amax * (1 + 1e-6)
+    worst = 0.0
+    for m in range(M):
+        qq = Q[m] - c
+        nqm = float(nq[m].item())
+        assert nqm == pytest.approx(float(qq @ qq), rel=1e-12)
+        ea, R, eq = _scales(amax, nqm)
+        e = na - 2.0 * (a @ qq)                              # |a'|^2 - 2 a'.q', fp64
+        e = np.concatenate([e, np.full(npad - N, np.inf)])
+        true = np.ldexp(e.reshape(nseg, seg).min(axis=1), ea + eq)
+        eps = np.ldexp(U32 * (300 * amax * math.sqrt(nqm) + 50 * amax * amax), ea + eq)
+        real = np.isfinite(true)
+        assert np.all(got[m][~real] == np.finfo(np.float32).max)
+        err = np.abs(got[m][real] - true[real]).max()
+        worst = max(worst, err / eps)
+    print('split16 screen: worst |segmin - exact| / eps16 = %.3g' % worst)
+    assert worst < 1.0
+
+
+@pytest.mark.parametrize('which', [1, 2])
+@pytest.mark.parametrize('scale', [1.0, 1e3, 1e-3])
+def test_match_exact_with_either_screen(gpu, alg, which, scale):
+    alg(which)
+    A, Aps, _ = analogy_inputs(42, (70, 101), (8, 8), n_ap=2, flat=(scale == 1.0))
+    idx, As = _index(A * scale, [x * scale for x in Aps])
+    Q = _queries(As, np.random.RandomState(4))
+    gi, gd = idx.match(Q)
+    gi, gd = gi.cpu().numpy(), gd.cpu().numpy()
+    for q, i, d in zip(Q, gi, gd):
+        dd = np.add.reduce((As - q) ** 2, axis=1)
+        j = int(np.argmin(dd))
+        assert i == j and d == dd[j]
+
+
+@pytest.mark.parametrize('which', [1, 2])
+def test_synthesis_bit_exact_with_either_screen(gpu, alg, which):
+    import image_analogies as ia
+    alg(which)
+    A, Aps, B = analogy_inputs(44, (48, 61), (41, 50), n_ap=2)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=44)
+    w = o.compute_weights(3, 5, 12, 1)
+    ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 1.5, w)
+    Bp_dev = [dev(b) for b in Bp_pyr]
+    out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                            [dev(p) for p in B_pyr], Bp_dev, L, 1.5, w)
+    for l in ref:
+        assert np.array_equal(out[l][0].cpu().numpy(), ref[l][1]), l
+        assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
+        assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l

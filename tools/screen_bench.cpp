@@ -113,7 +113,7 @@ int main(int argc, char **argv) {
     IaSrcLevel src{dAs, dA, dAps, dAp, hs, ws, H, W, 1};
     const long N = (long)H * W;
     float *db, *amax;
-    CK(hipMalloc(&db, sizeof(float) * IA_DP * ia_db_rows_padded(N)));
+    CK(hipMalloc(&db, ia_db_bytes(N)));
     CK(hipMalloc(&amax, sizeof(float))); CK(hipMemset(amax, 0, sizeof(float)));
     CI(ia_db_build(&src, 0, N, dc, db, amax, st));
 
@@ -139,7 +139,16 @@ int main(int argc, char **argv) {
     const int qrows = ia_diag_qp_rows(Mmax);
     CK(hipMalloc(&qp, sizeof(float) * IA_DP * qrows)); CK(hipMemset(qp, 0, sizeof(float) * IA_DP * qrows));
     CK(hipMalloc(&dnq, sizeof(double) * qrows));
-    CI(ia_diag_query_rows(dq, Mmax, dc, qp, dnq, st));
+    void *q16;
+    CK(hipMalloc(&q16, (size_t)352 * qrows)); CK(hipMemset(q16, 0, (size_t)352 * qrows));
+    CI(ia_diag_query_rows16(dq, Mmax, dc, amax, qp, q16, dnq, st));
+    // variant 7 (bits 4-7 cap, bit 8 uniform): the split-f16 screen
+    auto screen = [&](int M, void *out, int v) {
+        if ((v & 15) == 7)
+            CI(ia_diag_screen16(db, N, q16, M, reinterpret_cast<float *>(out), ((v >> 4) & 15) | (v & 0x100), st));
+        else
+            CI(ia_diag_screen(db, N, qp, M, out, v, st));
+    };
 #ifdef IA_PROBE
     {   // rescore_probe: phase timestamps of the exact stage (k_rescore) for M queries
         unsigned long long *probe;
@@ -199,12 +208,12 @@ int main(int argc, char **argv) {
     for (int M : Ms) {
         std::vector<std::vector<float>> t(vars.size());
         for (size_t vi = 0; vi < vars.size(); ++vi)       // warm-up + result check
-            CI(ia_diag_screen(db, N, qp, M, vi == 0 ? cand_ref : cand, vars[vi], st));
+            screen(M, vi == 0 ? cand_ref : cand, vars[vi]);
         for (int rd = 0; rd < rounds; ++rd)
             for (size_t vi = 0; vi < vars.size(); ++vi) {
                 char *out = vi == 0 ? cand_ref : cand;
                 CK(hipEventRecord(e0, st));
-                for (int r = 0; r < reps; ++r) CI(ia_diag_screen(db, N, qp, M, out, vars[vi], st));
+                for (int r = 0; r < reps; ++r) screen(M, out, vars[vi]);
                 CK(hipEventRecord(e1, st));
                 CK(hipEventSynchronize(e1));
                 float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -217,8 +226,8 @@ int main(int argc, char **argv) {
             const double tf = 2.0 * 55 * M * (double)N / (med * 1e-3) / 1e12;
             long diff = 0;
             if (vi > 0 && (vars[vi] & 15) == (vars[0] & 15)) {
-                CI(ia_diag_screen(db, N, qp, M, cand_ref, vars[0], st));
-                CI(ia_diag_screen(db, N, qp, M, cand, vars[vi], st));
+                screen(M, cand_ref, vars[0]);
+                screen(M, cand, vars[vi]);
                 CK(hipStreamSynchronize(st));
                 CK(hipMemcpy(h1.data(), cand_ref, cb, hipMemcpyDeviceToHost));
                 CK(hipMemcpy(h2.data(), cand, cb, hipMemcpyDeviceToHost));
