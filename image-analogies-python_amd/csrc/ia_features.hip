@@ -78,8 +78,10 @@ __global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nro
 // Split-f16 copy of the fp32 DB (ia_split16.h): one wave per 32-row tile, the tile
 // un-permuted through LDS, then lane (j, h) emits its 7 half8 register groups; output
 // half8 (tile, g, lane) at (tile * 7 + g) * 64 + lane, so each of the screen's 7 loads
-// per tile is one contiguous 1 KiB wave access.  Padding rows (>= nrows) are zero (the
-// screen masks them).  Runs after k_db_build on the same stream (needs the final amax).
+// per tile is one contiguous 1 KiB wave access.  Padding rows (>= nrows) repeat row
+// nrows - 1: their screen values are those of a real row, so the segment minima need no
+// masking (the exact stage never rescores a row >= nrows).  Runs after k_db_build on the
+// same stream (needs the final amax).
 __global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, long nrows,
                                                   const float *__restrict__ amax,
                                                   half8 *__restrict__ db16) {
@@ -88,7 +90,9 @@ __global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, 
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = lane & 31, h = lane >> 5;
     const long T = (long)blockIdx.x * 4 + wv;
-    const float4 *src = reinterpret_cast<const float4 *>(db) + T * (7 * 64) + lane;
+    const long rr = T * 32 + j < nrows ? T * 32 + j : nrows - 1;   // source row
+    const float4 *src = reinterpret_cast<const float4 *>(db) + (rr >> 5) * (7 * 64) + h * 32 +
+                        (rr & 31);
     float *tr = t[wv] + j * LD;
 #pragma unroll
     for (int v = 0; v < 7; ++v) {   // positions h*28 + 4v + c = element 2(4v + c) + h
@@ -100,7 +104,6 @@ __global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, 
     }
     __syncthreads();
     const Split16Db s = split16_db_scale(amax[0]);
-    const bool real = T * 32 + j < nrows;
     auto val = [&](int k) { return k < 55 ? ldexpf(tr[k], s.ea) : ldexpf(tr[55], s.ea - s.R); };
     half8 *out = db16 + T * (DB16_GROUPS * 64) + lane;
 #pragma unroll
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, 
         for (int e = 0; e < 8; ++e) {
             _Float16 xh, xl;
             split16f(val(k0 + e), xh, xl);
-            o[e] = real ? (hi ? xh : xl) : (_Float16)0.f;
+            o[e] = hi ? xh : xl;
         }
         out[g * 64] = o;
     }

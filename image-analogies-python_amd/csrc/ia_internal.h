@@ -71,7 +71,8 @@ static inline QSplit qsplit(int M, int maxnq) {
     return s;
 }
 constexpr int MAX_NQ = 6;
-static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + MAX_NQ) * 32; }
+// query rows allocated for Mmax queries: the screens read up to 2 * MAX_NQ padding tiles
+static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + 2 * MAX_NQ) * 32; }
 
 // the level state one wave of the per-pixel tail updates (ia_finish.h)
 struct FinishArgs {
@@ -130,6 +131,11 @@ int match_alg();      // IA_MATCH_ALG (default 2: segment minima, split-f16 scre
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
                       int maxnq, hipStream_t st, const _Float16 *q16 = nullptr);
 int screen_variant();
+// split-f16 segment screen (ia_screen16.hip) over db16_of(db): flags bits
+// 0-3 cap on query tiles per wave (0 = shape rule), bit 8 per-wave kernel (no LDS sharing),
+// bit 9 no software-pipelined epilogue
+int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
+                    int flags, hipStream_t st);
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query
 int launch_lsh_match(const IaLsh *lsh, const DbSrc &src, long row0, long nrows, int M,
                      const double *q64, const double *center, Best *best,

@@ -812,119 +812,6 @@ __global__ __launch_bounds__(256) void k_screen_seg(const float *__restrict__ db
         seg_body<NQA>(db, chunk, ch, seg_rows, qp, M, group * NQA, segmin, nseg);
 }
 
-// =================================================================================
-// Split-f16 segment screen (IA_MATCH_ALG=2, ia_split16.h): the same segment minima as
-// k_screen_seg, from 11 v_mfma_f32_32x32x16_f16 per 32x32 tile instead of 28
-// v_mfma_f32_32x32x2_f32 (352 vs 1792 MFMA cycles per tile and wave).  Values are in
-// the scaled units sa * sq_j * e; rows >= nrows (padding) are masked to FLT_MAX.
-// =================================================================================
-__device__ __forceinline__ void load_tile16(half8 (&a)[DB16_GROUPS], const half8 *p) {
-#pragma unroll
-    for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
-}
-
-template <int NQ>
-__device__ __forceinline__ void seg16_body(const half8 *__restrict__ db16, int chunk, int ch,
-                                           int seg_rows, long nrows,
-                                           const half8 *__restrict__ q16, int M, int tile0,
-                                           float *__restrict__ segmin, long nseg) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
-    const int j = lane & 31, h = lane >> 5;
-
-    half8 bq[NQ][Q16_GROUPS];
-#pragma unroll
-    for (int qt = 0; qt < NQ; ++qt) {
-        const half8 *p = q16 + (long)((tile0 + qt) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
-#pragma unroll
-        for (int m = 0; m < Q16_GROUPS; ++m) bq[qt][m] = p[m];
-    }
-    const int rows_per_wave = ch >> 2;
-    const int ntile = rows_per_wave >> 5;
-    const int tps = seg_rows >> 5;
-    const long row_begin = (long)chunk * ch + wv * rows_per_wave;
-    const long seg_begin = row_begin / seg_rows;
-    const half8 *dp = db16 + (row_begin >> 5) * (DB16_GROUPS * 64) + lane;
-
-    float mn[NQ];
-#pragma unroll
-    for (int qt = 0; qt < NQ; ++qt) mn[qt] = FLT_MAX;
-
-    auto tile_min = [&](const half8 (&a)[DB16_GROUPS], int tile) {
-        floatx16 acc[NQ];
-#pragma unroll
-        for (int qt = 0; qt < NQ; ++qt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
-#pragma unroll
-        for (int m = 0; m < Q16_GROUPS; ++m)
-#pragma unroll
-            for (int qt = 0; qt < NQ; ++qt)
-                acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m < 7 ? m : m - 7], bq[qt][m],
-                                                                 acc[qt], 0, 0, 0);
-        const long r0 = row_begin + (long)tile * 32;
-        if (r0 + 32 > nrows) {   // tail tile of the last chunk: mask padding rows
-#pragma unroll
-            for (int qt = 0; qt < NQ; ++qt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (r0 + (r & 3) + 8 * (r >> 2) + 4 * h >= nrows) acc[qt][r] = FLT_MAX;
-        }
-#pragma unroll
-        for (int qt = 0; qt < NQ; ++qt) {
-            float m = mn[qt];
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) m = fminf(m, fminf(acc[qt][r], acc[qt][r + 1]));
-            mn[qt] = m;
-        }
-    };
-    auto flush = [&](int tile) {
-        const long seg = seg_begin + tile / tps;
-#pragma unroll
-        for (int qt = 0; qt < NQ; ++qt) {
-            const float m = fminf(mn[qt], __shfl_xor(mn[qt], 32));
-            const int qg = (tile0 + qt) * 32 + j;
-            if (h == 0 && qg < M) segmin[(long)qg * nseg + seg] = m;
-            mn[qt] = FLT_MAX;
-        }
-    };
-
-    half8 b0[DB16_GROUPS], b1[DB16_GROUPS];
-    load_tile16(b0, dp);
-    int tile = 0;
-    for (; tile + 1 < ntile; tile += 2) {
-        load_tile16(b1, dp + (long)(tile + 1) * (DB16_GROUPS * 64));
-        tile_min(b0, tile);
-        if ((tile + 1) % tps == 0) flush(tile);
-        const int nxt = tile + 2 < ntile ? tile + 2 : ntile - 1;
-        load_tile16(b0, dp + (long)nxt * (DB16_GROUPS * 64));
-        tile_min(b1, tile + 1);
-        if ((tile + 2) % tps == 0) flush(tile + 1);
-    }
-    if (tile < ntile) {
-        tile_min(b0, tile);
-        flush(tile);
-    }
-}
-
-template <int NQA, int NQB>
-__global__ __launch_bounds__(256) void k_screen_h16(const half8 *__restrict__ db16, int nchunks,
-                                                    int ch, int seg_rows, long nrows,
-                                                    const half8 *__restrict__ q16, int M,
-                                                    int groups, int nA,
-                                                    float *__restrict__ segmin, long nseg) {
-    const int b = blockIdx.x;
-    const int slot = b >> 3;
-    const int chunk = (slot / groups) * 8 + (b & 7);
-    const int group = slot - (slot / groups) * groups;
-    if (chunk >= nchunks) return;
-    if (NQB > 0 && group >= nA)
-        seg16_body<(NQB > 0 ? NQB : 1)>(db16, chunk, ch, seg_rows, nrows, q16, M,
-                                        nA * NQA + (group - nA) * NQB, segmin, nseg);
-    else
-        seg16_body<NQA>(db16, chunk, ch, seg_rows, nrows, q16, M, group * NQA, segmin, nseg);
-}
-
 // Phase probes (tools/rescore_probe only: built with -DIA_PROBE into a separate library):
 // lane 0 of every wave of the first 64 workgroups stores wall_clock64() at each mark
 // (slot [block][wave][mark], 64 x 4 x 16).
@@ -1135,6 +1022,7 @@ int fuse_finish() {
 
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
                       int maxnq, hipStream_t st, const _Float16 *q16) {
+    if (q16) return launch_screen16(db, nrows, q16, M, segmin, maxnq, st);
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -1158,16 +1046,7 @@ int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float
     }
     const long nblocks = ((nchunks + 7) / 8) * 8 * groups;
     IA_ARG(nblocks < (1L << 31), "screen grid too large");
-    const half8 *db16 = reinterpret_cast<const half8 *>(db16_of(db, nrows));
-    const half8 *q16v = reinterpret_cast<const half8 *>(q16);
 #define IA_SEG_CASE(NA, NB)                                                                   \
-    if (nqa == NA && nqb == NB && q16) {                                                      \
-        k_screen_h16<NA, NB><<<(unsigned)nblocks, 256, 0, st>>>(db16, (int)nchunks, ch,       \
-                                                                seg_rows, nrows, q16v, M,     \
-                                                                groups, nA, segmin, nseg);    \
-        IA_LAUNCH_CHECK("k_screen_h16");                                                      \
-        return IA_OK;                                                                         \
-    }                                                                                         \
     if (nqa == NA && nqb == NB) {                                                             \
         k_screen_seg<NA, NB><<<(unsigned)nblocks, 256, 0, st>>>(db, (int)nchunks, ch, seg_rows, \
                                                                 qp, M, groups, nA, segmin,    \
@@ -1219,10 +1098,11 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
     float *segmin = reinterpret_cast<float *>(scratch);
     const int nq_cap = (screen_variant() >> 4) & 15;
     const bool split = match_alg() == 2;
-    // default query tiles per wave: 3 (f32: profiles/r01_screen_bench_split.txt), 2 (split
-    // f16: profiles/r01_screen_bench_h16.txt)
-    const int cap = nq_cap > 0 && nq_cap <= 3 ? nq_cap : (split ? 2 : 3);
-    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, cap, st, split ? q16 : nullptr)))
+    // f32: up to 3 query tiles per wave (profiles/r01_screen_bench_split.txt); split f16:
+    // the shape rule of launch_screen16
+    const int cap = nq_cap > 0 && nq_cap <= 3 ? nq_cap : 3;
+    if ((rc = launch_screen_seg(db, nrows, qp, M, segmin, split ? 0 : cap, st,
+                                split ? q16 : nullptr)))
         return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
@@ -1394,10 +1274,8 @@ int ia_diag_set_match_alg(int alg) {
 int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
                      int maxnq, void *stream) {
     IA_ARG(db && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16: bad args");
-    const int cap = maxnq & 15;
-    return launch_screen_seg(db, nrows, nullptr, M, segmin,
-                             (cap > 0 && cap <= 3 ? cap : 3) | (maxnq & 0x100), S(stream),
-                             reinterpret_cast<const _Float16 *>(q16));
+    return launch_screen16(db, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin, maxnq,
+                           S(stream));
 }
 
 int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *cand, int variant,
