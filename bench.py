@@ -38,7 +38,15 @@ import image_analogies as ia  # noqa: E402
 import img_preprocess as ip  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+# f16 MFMA dense peak: 32x32x16 = 32768 flop / 32 cycles / SIMD -> 4096 flop/clk/CU x 256 CU
+# x 2.4 GHz (MI355X_MICROARCH.md: ~2.5 PF dense)
+F16_MFMA_PEAK_TFLOPS = 4096 * 256 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
+# HBM traffic of one finest-level screen launch, from rocprofv3 PMC (FETCH_SIZE x 2 on
+# gfx950 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench at M = 342 queries
+# against the 4,194,304-row c4 database (profiles/r01_screen_h16s_pmc_m342.txt)
+SCREEN_PMC = {'fetch_kb': 4.604e5, 'write_kb': 8.754e4, 'M': 342, 'rows': 4194304,
+              'source': 'profiles/r01_screen_h16s_pmc_m342.txt'}
 
 CONFIGS = {
     'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),
@@ -267,15 +275,42 @@ def main():
     screen_ms = sum(p['screen_ms'] for p in rprof)
     screens = sum(p['timed_screens'] for p in rprof)
     pairs = sum(p['timed_pairs'] for p in rprof)
-    flops = 2.0 * 55 * pairs
-    achieved = flops / (screen_ms * 1e-3) / 1e12 if screen_ms > 0 else 0.0
     rescored = sum(p['rows_rescored'] for p in prof)
-    roof = {'bound': 'mfma', 'kernel': 'k_screen_seg', 'achieved': achieved,
-            'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': None,
-            'algorithmic': '2*55 flop per (query,row) pair; this rank: %.4g pairs '
-                           'over %d launches' % (pairs, screens),
-            'screen_avg_us': screen_ms * 1e3 / max(screens, 1), 'source': rsource}
+    # the dominant kernel: the screen at the finest level (most timed screen time)
+    by_level = {}
+    for p in rprof:
+        d = by_level.setdefault(p['level'], [0.0, 0, 0.0])
+        d[0] += p['screen_ms']; d[1] += p['timed_screens']; d[2] += p['timed_pairs']
+    dom = max(by_level, key=lambda l: by_level[l][0]) if by_level else None
+    d_ms, d_n, d_pairs = by_level[dom] if dom is not None else (0.0, 0, 0.0)
+    split = _ia.match_alg() == 2
+    if split:
+        # split-f16 screen: 3 f16 products (a_h q_h + a_h q_l + a_l q_h) of 2 flop per
+        # feature per (query, row) pair on v_mfma_f32_32x32x16_f16
+        per_pair, peak, kname = 3 * 2 * 55, F16_MFMA_PEAK_TFLOPS, 'k_screen_h16s'
+    else:
+        per_pair, peak, kname = 2 * 55, FP32_MFMA_PEAK_TFLOPS, 'k_screen_seg'
+    achieved = per_pair * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
+    fp32eq = 2.0 * 55 * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
+    traffic = None
+    if split and args.config == 'c4' and world == 1:
+        traffic = (SCREEN_PMC['fetch_kb'] * 2 + SCREEN_PMC['write_kb']) * 1024
+    roof = {'bound': 'mfma', 'kernel': kname, 'achieved': achieved, 'peak': peak,
+            'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': traffic,
+            'algorithmic': '%d flop per (query,row) pair; level %s: %.4g pairs over %d launches'
+                           % (per_pair, dom, d_pairs, d_n),
+            'screen_avg_us': d_ms * 1e3 / max(d_n, 1), 'source': rsource,
+            'fp32_equivalent_tflops': fp32eq,
+            'fp32_equivalent_frac_of_fp32_mfma_peak': fp32eq / FP32_MFMA_PEAK_TFLOPS,
+            'all_levels': {'launches': screens, 'pairs': pairs,
+                           'screen_avg_us': screen_ms * 1e3 / max(screens, 1),
+                           'fp32_equivalent_tflops':
+                               2.0 * 55 * pairs / (screen_ms * 1e-3) / 1e12 if screen_ms else 0.0}}
+    if traffic is not None:
+        roof['traffic_note'] = ('HBM bytes of one M=%d finest-level launch (PMC FETCH_SIZE x 2 + '
+                                'WRITE_SIZE, %s); algorithmic: %.0f MB split-f16 DB read once'
+                                % (SCREEN_PMC['M'], SCREEN_PMC['source'],
+                                   SCREEN_PMC['rows'] * 224 / 1e6))
     if lsh is not None:
         # k_lsh_query is a gather: each examined row costs its 55 fp64 features (440 B)
         # (rows counted over the same launches the events timed)
@@ -301,7 +336,8 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak' if args.config == 'c5' else 'strong',
         'vs_baseline': None,
-        'dtype': 'f32 (MFMA screen) + f64 (exact rescore, pyramids)',
+        'dtype': ('f16x3 split (MFMA screen, f32 accumulate)' if split else
+                  'f32 (MFMA screen)') + ' + f64 (exact rescore, pyramids)',
         'data': 'synthetic (gaussian-filtered noise; A\' = blur(A)); seeded',
         'config': {'workload': args.config + ': ' + conf['name'],
                    'A': list(conf['A']), 'B': list(conf['B']), 'kappa': conf['k'],

@@ -5,8 +5,9 @@
 // v_mfma_f32_32x32x16_f16 per 32x32 (rows x queries) tile from the split-f16 operands of
 // ia_split16.h.  Queries are the stationary operand (VGPRs), DB rows stream through.
 // Padding rows of the DB's last chunk repeat its last real row (k_db_split), so the
-// minima need no masking.  Built with -fno-honor-nans: the min-reductions then need no
-// NaN canonicalisation (inputs are finite by construction).
+// minima need no masking.  Built with -fno-honor-nans (the min-reductions need no NaN
+// canonicalisation: inputs are finite by construction) and -amdgpu-mfma-vgpr-form (MFMA
+// results in VGPRs: the reductions read them without v_accvgpr_read copies).
 //
 // Two forms:
 //  * k_screen_h16 (per-wave): each wave streams its own quarter of a chunk straight into
@@ -45,14 +46,17 @@ __device__ __forceinline__ void tile_mfma(const half8 (&a)[DB16_GROUPS],
                                                              acc[qt], 0, 0, 0);
 }
 
+// running minimum over a tile: 8 v_min3_f32 per query tile, dependency depth 3
 template <int NQ>
 __device__ __forceinline__ void tile_min(const floatx16 (&acc)[NQ], float (&mn)[NQ]) {
 #pragma unroll
     for (int qt = 0; qt < NQ; ++qt) {
-        float m = mn[qt];
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) m = fminf(m, fminf(acc[qt][r], acc[qt][r + 1]));
-        mn[qt] = m;
+        const floatx16 &x = acc[qt];
+        const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+        const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+        const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+        const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+        mn[qt] = fminf(fminf(mn[qt], u0), u1);
     }
 }
 
@@ -261,13 +265,16 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
     const half8 *q = reinterpret_cast<const half8 *>(q16);
     const int T = (M + 31) / 32;
     const int cap = flags & 15;
-    const bool pipe = !(flags & 0x200);
+    bool pipe = !(flags & 0x200);
     if (h16_shared() && !(flags & 0x100) && T >= 2) {
         // query tiles per block WQ x NQ: T >= 9 -> 4 x 3, 5..8 -> 4 x 2, 3..4 -> 4 x 1,
         // 2 -> 2 x 1 (fewest padded tiles, then the most sharing)
         int wq = 4, nq = T >= 9 ? 3 : (T >= 5 ? 2 : 1);
         if (T == 2) wq = 2;
         if (cap > 0 && cap < nq) nq = cap;
+        // the pipelined epilogue's second accumulator set costs NQ = 3 its second wave per
+        // SIMD (measured slower: profiles/r01_screen_bench_h16s.txt)
+        if (nq == 3) pipe = false;
         const int g = (T + wq * nq - 1) / (wq * nq);
         const long nb = ((nchunks + 7) / 8) * 8 * g;
         IA_ARG(nb < (1L << 31), "screen grid too large");
@@ -280,7 +287,6 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
             IA_LAUNCH_CHECK("k_screen_h16s");                                                   \
             return IA_OK;                                                                       \
         }
-        IA_H16S_CASE(3, 4, true)
         IA_H16S_CASE(2, 4, true)
         IA_H16S_CASE(1, 4, true)
         IA_H16S_CASE(1, 2, true)
