@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, 
         int k0;
         bool hi;
         if (h == 0) { hi = g < 4; k0 = hi ? 8 * g : 8 * (g - 4); }
-        else { hi = g >= 1 && g <= 3; k0 = g == 0 ? 24 : (hi ? 32 + 8 * (g - 1) : 32 + 8 * (g - 4)); }
+        else { hi = g < 3; k0 = hi ? 32 + 8 * g : (g == 3 ? 24 : 32 + 8 * (g - 4)); }
         half8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {

@@ -131,9 +131,11 @@ int match_alg();      // IA_MATCH_ALG (default 2: segment minima, split-f16 scre
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
                       int maxnq, hipStream_t st, const _Float16 *q16 = nullptr);
 int screen_variant();
-// split-f16 segment screen (ia_screen16.hip) over db16_of(db): flags bits
-// 0-3 cap on query tiles per wave (0 = shape rule), bit 8 per-wave kernel (no LDS sharing),
-// bit 9 no software-pipelined epilogue
+// split-f16 segment screen (ia_screen16.hip) over db16_of(db): flags bits 0-3 cap on
+// query tiles per wave (0 = shape rule), bit 8 per-wave kernel (no LDS sharing), bit 9 no
+// pipelined epilogue, bit 10 fragment-prefetch form, bit 11 keep the epilogue at
+// NQ = 3, bit 12 spanning form (bits 13 / 15: its no-copy diagnostics), bit 14 uneven
+// query shares
 int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
                     int flags, hipStream_t st);
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query

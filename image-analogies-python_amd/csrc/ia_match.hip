@@ -844,7 +844,8 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
                                                  const double *__restrict__ nq,
                                                  const float *__restrict__ amax,
                                                  Best *__restrict__ best,
-                                                 unsigned long long *stats, FinishArgs fa) {
+                                                 unsigned long long *stats, FinishArgs fa,
+                                                 int probe) {
     __shared__ int slist[RESCORE_SEGCAP];
     __shared__ long long win;
     __shared__ int scount;
@@ -935,6 +936,41 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
         push(x.y, 4 * i + 1);
         push(x.z, 4 * i + 2);
         push(x.w, 4 * i + 3);
+    }
+    if (SPLIT && probe && stats) {
+        // diagnostic (IA_PRUNE_PROBE): how many segments a coarser screen would leave to the
+        // exact stage.  Coarse f16 forms, error bounds in unscaled units: a_h q_h (4 MFMAs)
+        // eps4 = 2^-9 A|q'| + 2^-11 A^2, a_h (q_h + q_l) (8 MFMAs) eps8 = 2^-10 A|q'| + 2^-11 A^2
+        // (+ 2^-8 relative and 2^-18 (2A|q'| + A^2) accumulation allowances); counts of
+        // segments with minimum <= e* + 2 eps4, e* + 4 eps4, e* + 2 eps8.
+        const Split16Db sc = split16_db_scale(amax[0]);
+        const int e2 = sc.ea + split16_q_scale(nqq, sc.R);
+        const double em = ldexp((double)emin, -e2);
+        const double aq = A * sqrt(nqq), acc = 0x1p-18 * (2.0 * aq + A * A);
+        const double e4 = (0x1p-9 * aq + 0x1p-11 * A * A) * (1.0 + 0x1p-8) + acc;
+        const double e8 = (0x1p-10 * aq + 0x1p-11 * A * A) * (1.0 + 0x1p-8) + acc;
+        const double t42 = ldexp(em + 2.0 * e4, e2), t44 = ldexp(em + 4.0 * e4, e2);
+        const double t82 = ldexp(em + 2.0 * e8, e2);
+        unsigned int c42 = 0, c44 = 0, c82 = 0;
+        for (long i = tid; i < nseg; i += 256) {
+            const double x = (double)sq[i];
+            c42 += x <= t42; c44 += x <= t44; c82 += x <= t82;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            c42 += __shfl_xor(c42, o); c44 += __shfl_xor(c44, o); c82 += __shfl_xor(c82, o);
+        }
+        __shared__ unsigned int pc[3];
+        if (tid == 0) { pc[0] = 0; pc[1] = 0; pc[2] = 0; }
+        __syncthreads();
+        if ((tid & 63) == 0) { atomicAdd(&pc[0], c42); atomicAdd(&pc[1], c44); atomicAdd(&pc[2], c82); }
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long *sl = stats_slot(stats, q);
+            atomicAdd(&sl[3], (unsigned long long)pc[0]);
+            atomicAdd(&sl[4], (unsigned long long)pc[1]);
+            atomicAdd(&sl[5], (unsigned long long)pc[2]);
+            atomicMax(&sl[6], (unsigned long long)pc[0]);
+        }
     }
     __syncthreads();
     IA_PROBE_MARK(3);
@@ -1106,9 +1142,10 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
         return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
+    static const int probe = getenv("IA_PRUNE_PROBE") ? atoi(getenv("IA_PRUNE_PROBE")) : 0;
 #define IA_RESCORE(F, SP)                                                                      \
     k_rescore<F, SP><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows), \
-                                        segmin, db, qp, q64, nq, amax, best, stats, fa)
+                                        segmin, db, qp, q64, nq, amax, best, stats, fa, probe)
     if (fin && split) IA_RESCORE(true, true);
     else if (fin) IA_RESCORE(true, false);
     else if (split) IA_RESCORE(false, true);

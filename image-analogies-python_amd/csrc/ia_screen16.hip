@@ -3,7 +3,7 @@
 // Stage 1 of the exact matcher (ia_match.hip): for every (query, DB segment of <= 512
 // rows) the minimum of the screen value sa * sq_j * (|a'|^2 - 2 a'.q'), computed as 11
 // v_mfma_f32_32x32x16_f16 per 32x32 (rows x queries) tile from the split-f16 operands of
-// ia_split16.h.  Queries are the stationary operand (VGPRs), DB rows stream through.
+// ia_split16.h (7 DB and 8 query register groups per lane).  Queries are the stationary operand (VGPRs), DB rows stream through.
 // Padding rows of the DB's last chunk repeat its last real row (k_db_split), so the
 // minima need no masking.  Built with -fno-honor-nans (the min-reductions need no NaN
 // canonicalisation: inputs are finite by construction) and -amdgpu-mfma-vgpr-form (MFMA
@@ -39,10 +39,10 @@ __device__ __forceinline__ void tile_mfma(const half8 (&a)[DB16_GROUPS],
     for (int qt = 0; qt < NQ; ++qt)
         acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[qt][0], zero, 0, 0, 0);
 #pragma unroll
-    for (int m = 1; m < Q16_GROUPS; ++m)
+    for (int m = 1; m < MFMA16; ++m)
 #pragma unroll
         for (int qt = 0; qt < NQ; ++qt)
-            acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m < 7 ? m : m - 7], bq[qt][m],
+            acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[qt][mfma_b(m)],
                                                              acc[qt], 0, 0, 0);
 }
 
@@ -147,7 +147,10 @@ __global__ __launch_bounds__(256) void k_screen_h16(const half8 *__restrict__ db
 // ---------------------------------------------------------------------------------
 // shared-tile form
 // ---------------------------------------------------------------------------------
-template <int NQ, int WQ, bool PIPE>
+// MODE 0: plain; 1: pipelined epilogue (two accumulator sets); 2: fragment prefetch (the
+// next tile's LDS groups re-read into each register group right after its last MFMA use,
+// barrier at the start of each stage's last tile, two stages of global_load_lds in flight)
+template <int NQ, int WQ, int MODE>
 __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ db16, int nchunks,
                                                      int ch, int seg_rows,
                                                      const half8 *__restrict__ q16, int M,
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
                                                      long nseg) {
     constexpr int WR = 4 / WQ;
     constexpr int TPW = STAGE_TILES / WR;      // tiles per wave per stage (4, 2 or 1)
-    static_assert(!PIPE || TPW % 2 == 0, "pipelined epilogue needs an even tile count");
+    static_assert(MODE != 1 || TPW % 2 == 0, "pipelined epilogue needs an even tile count");
     __shared__ half8 sbuf[2][STAGE_H8];
     const int b = blockIdx.x;
     const int slot = b >> 3;
@@ -189,6 +192,13 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
                                              (void *)&sbuf[buf][k * 256 + wv * 64], 16, 0, 0);
         }
     };
+    // every wave's global_load_lds of the next stage retired, then the barrier: the
+    // compiler's own wait before __syncthreads() is not reliable here (hipcc 7.2 dropped it
+    // in the loop of MODE 2, letting waves read a stage before it landed)
+    auto stage_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
     auto read_tile = [&](half8 (&a)[DB16_GROUPS], const half8 *sb, int u) {
         const half8 *p = sb + (u * WR + wr) * TILE_H8 + lane;
 #pragma unroll
@@ -203,8 +213,46 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
     };
 
     issue(0, 0);
-    __syncthreads();
-    if (!PIPE) {
+    if (MODE == 2) {
+        if (nstage > 1) issue(1, 1);
+        stage_barrier();
+        half8 a[DB16_GROUPS];
+        read_tile(a, sbuf[0], 0);
+        const floatx16 zero = {};
+        for (int s = 0; s < nstage; ++s) {
+            const half8 *sb = sbuf[s & 1];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                const half8 *np;      // where the next tile's groups come from
+                if (u + 1 < TPW) {
+                    np = sb + ((u + 1) * WR + wr) * TILE_H8 + lane;
+                } else {
+                    // stage s+1 landed and every wave is done reading stage s-1's buffer
+                    stage_barrier();
+                    if (s + 2 < nstage) issue(s + 2, s & 1);
+                    np = (s + 1 < nstage ? sbuf[(s + 1) & 1] + wr * TILE_H8 : sb) + lane;
+                }
+                floatx16 acc[NQ];
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt)
+                    acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[qt][0], zero, 0, 0, 0);
+#pragma unroll
+                for (int m = 1; m < MFMA16; ++m) {
+                    const int g = mfma_a(m);
+#pragma unroll
+                    for (int qt = 0; qt < NQ; ++qt)
+                        acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[g], bq[qt][mfma_b(m)],
+                                                                         acc[qt], 0, 0, 0);
+                    if (m >= 4) a[g] = np[g * 64];   // last use of group g in this tile
+                }
+                tile_min<NQ>(acc, mn);
+                close(s * TPW + u);
+            }
+        }
+        return;
+    }
+    stage_barrier();
+    if (MODE == 0) {
         for (int s = 0; s < nstage; ++s) {
             if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
             const half8 *sb = sbuf[s & 1];
@@ -217,7 +265,7 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
                 tile_min<NQ>(acc, mn);
                 close(s * TPW + u);
             }
-            __syncthreads();   // stage s+1 landed (vmcnt(0)) and stage s is free again
+            stage_barrier();   // stage s+1 landed and stage s is free again
         }
         return;
     }
@@ -240,10 +288,199 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
             tile_min<NQ>(accX, mn);
             close(i);
         }
-        __syncthreads();
+        stage_barrier();
     }
     tile_min<NQ>(accY, mn);
     close(nstage * TPW - 1);
+}
+
+// ---------------------------------------------------------------------------------
+// spanning form (flag 0x1000): 512 threads = 2 row parts x 4 query parts, three stage
+// buffers (84 KiB, one array).  Stage s+2 is copied while stage s is computed, and the
+// barrier before stage s+1 waits only for stage s+1's copies: a counted vmcnt (loads retire
+// in order, so later stores only make the wait stricter) and a raw s_barrier, since
+// __syncthreads()' fence would also drain the copies still in flight
+// (cdna_hip_programming.md, "Pipelining across barriers").  MODE 1 / 2 (diagnostics, flags
+// 0x2000 / 0x8000): stage 0 only is copied and every stage re-reads it, with / without the
+// per-stage barriers — the ceiling of the same instruction stream.
+// ---------------------------------------------------------------------------------
+constexpr int SPAN_WAVES = 8;
+constexpr int SPAN_LOADS = STAGE_TILES * DB16_GROUPS;     // 1 KiB wave-loads per stage (28)
+
+template <int NQ, int MODE>
+__global__ __launch_bounds__(512) void k_screen_h16p(const half8 *__restrict__ db16, int nchunks,
+                                                     int ch, int seg_rows,
+                                                     const half8 *__restrict__ q16, int M,
+                                                     int groups, float *__restrict__ segmin,
+                                                     long nseg) {
+    constexpr bool DRY = MODE != 0;
+    constexpr int WQ = 4, WR = 2, TPW = STAGE_TILES / WR;
+    __shared__ half8 sbuf[3 * STAGE_H8];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;   // uniform over the block, before any barrier
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+    const int wr = wv >> 2, wq = wv & 3;
+    const int tile0 = (group * WQ + wq) * NQ;
+
+    half8 bq[NQ][Q16_GROUPS];
+    load_queries<NQ>(bq, q16, tile0, j, h);
+    const int tpc = ch >> 5;
+    const int tpp = tpc / WR;
+    const int tps = seg_rows >> 5;
+    const int nstage = tpc / STAGE_TILES;
+    const long ctile0 = (long)chunk * tpc;
+    const long seg0 = (ctile0 + (long)wr * tpp) * 32 / seg_rows;
+
+    // wave-load k (0..27) of stage s: group k % 7 of virtual tile k / 7 (part v % WR,
+    // index v / WR); waves 0-3 issue 4 loads per stage, waves 4-7 issue 3
+    auto issue = [&](int s, int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = wv + i * SPAN_WAVES;
+            if (k < SPAN_LOADS) {
+                const int tt = k / DB16_GROUPS, g = k - tt * DB16_GROUPS;
+                const int v = s * STAGE_TILES + tt;
+                const long gt = ctile0 + (long)(v % WR) * tpp + v / WR;
+                __builtin_amdgcn_global_load_lds((const void *)(db16 + gt * TILE_H8 + g * 64 + lane),
+                                                 (void *)(sbuf + buf * STAGE_H8 + k * 64), 16, 0,
+                                                 0);
+            }
+        }
+    };
+    // this wave's copies of the next stage retired (ahead: the next-but-one stage's copies,
+    // issued later, may still be in flight)
+    auto wait_stage = [&](bool ahead) {
+        if (!ahead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (wv < SPAN_LOADS - 3 * SPAN_WAVES) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    };
+    auto barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+    float mn[NQ];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) mn[qt] = FLT_MAX;
+    issue(0, 0);
+    if (!DRY && nstage > 1) issue(1, 1);
+    wait_stage(!DRY && nstage > 1);
+    barrier();
+    int buf = 0;
+    for (int s = 0; s < nstage; ++s) {
+        if (!DRY && s + 2 < nstage) issue(s + 2, buf == 0 ? 2 : buf - 1);
+        const half8 *sb = sbuf + buf * STAGE_H8;
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            half8 a[DB16_GROUPS];
+            const half8 *p = sb + (u * WR + wr) * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+            floatx16 acc[NQ];
+            tile_mfma<NQ>(a, bq, acc);
+            tile_min<NQ>(acc, mn);
+            const int i = s * TPW + u;
+            if ((i + 1) % tps == 0) seg_flush<NQ>(mn, tile0, j, h, M, segmin, nseg, seg0 + i / tps);
+        }
+        if (MODE != 2) {
+            wait_stage(!DRY && s + 2 < nstage);
+            barrier();
+        }
+        if (!DRY) buf = buf == 2 ? 0 : buf + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// uneven-share form (flag 0x4000): a block's G (4..12) query tiles are split over its 4
+// waves as evenly as possible (G = 11: 3 + 3 + 3 + 2; G = 6: 2 + 2 + 1 + 1) instead of
+// padding every wave to the same count (M = 342: 11 tiles computed, not 12); which wave
+// takes a short share rotates from block to block, so that the SIMDs of a CU (one wave
+// of each resident block) carry equal work on average.  Each wave runs the plain stage
+// loop at its own tile count; every wave copies its part of each stage and meets every
+// barrier.
+// ---------------------------------------------------------------------------------
+template <int NQ>
+__device__ __forceinline__ void uneven_body(const half8 *__restrict__ db16, half8 *sbuf,
+                                            long ctile0, int nstage, int tps, long seg0,
+                                            const half8 *__restrict__ q16, int M, int tile0,
+                                            float *__restrict__ segmin, long nseg) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int j = lane & 31, h = lane >> 5;
+    half8 bq[NQ][Q16_GROUPS];
+    load_queries<NQ>(bq, q16, tile0, j, h);
+    // one row part: stage s = the 4 consecutive tiles 4s..4s+3, one contiguous 28 KiB
+    auto issue = [&](int s, int buf) {
+        const half8 *src = db16 + (ctile0 + (long)s * STAGE_TILES) * TILE_H8 + tid;
+#pragma unroll
+        for (int k = 0; k < DB16_GROUPS; ++k)
+            __builtin_amdgcn_global_load_lds((const void *)(src + k * 256),
+                                             (void *)(sbuf + buf * STAGE_H8 + k * 256 + wv * 64),
+                                             16, 0, 0);
+    };
+    auto stage_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    float mn[NQ];
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) mn[qt] = FLT_MAX;
+    issue(0, 0);
+    stage_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        const half8 *sb = sbuf + (s & 1) * STAGE_H8;
+#pragma unroll
+        for (int u = 0; u < STAGE_TILES; ++u) {
+            half8 a[DB16_GROUPS];
+            const half8 *p = sb + u * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+            floatx16 acc[NQ];
+            tile_mfma<NQ>(a, bq, acc);
+            tile_min<NQ>(acc, mn);
+            const int i = s * STAGE_TILES + u;
+            if ((i + 1) % tps == 0) seg_flush<NQ>(mn, tile0, j, h, M, segmin, nseg, seg0 + i / tps);
+        }
+        stage_barrier();
+    }
+}
+
+// grid: nchunks (rounded up to 8) x groups; the T query tiles split over the groups as
+// evenly as possible (each 4..12 tiles: the launcher takes groups = ceil(T / 12), T >= 4)
+__global__ __launch_bounds__(256) void k_screen_h16u(const half8 *__restrict__ db16, int nchunks,
+                                                     int ch, int seg_rows,
+                                                     const half8 *__restrict__ q16, int M, int T,
+                                                     int groups, float *__restrict__ segmin,
+                                                     long nseg) {
+    __shared__ half8 sbuf[2 * STAGE_H8];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+    const int tpc = ch >> 5;
+    const long ctile0 = (long)chunk * tpc;
+    const int per = T / groups, rem = T - per * groups;
+    const int G = per + (group < rem ? 1 : 0);
+    const int first = group * per + (group < rem ? group : rem);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = (wv + slot) & 3;                 // share index, rotated per block
+    const int base = G >> 2, extra = G & 3;
+    const int nqw = base + (r < extra ? 1 : 0);
+    const int tile0 = first + r * base + (r < extra ? r : extra);
+    const int nstage = tpc / STAGE_TILES;
+    const int tps = seg_rows >> 5;
+    const long seg0 = ctile0 * 32 / seg_rows;
+    if (nqw >= 3)
+        uneven_body<3>(db16, sbuf, ctile0, nstage, tps, seg0, q16, M, tile0, segmin, nseg);
+    else if (nqw == 2)
+        uneven_body<2>(db16, sbuf, ctile0, nstage, tps, seg0, q16, M, tile0, segmin, nseg);
+    else
+        uneven_body<1>(db16, sbuf, ctile0, nstage, tps, seg0, q16, M, tile0, segmin, nseg);
 }
 
 static int h16_shared() {
@@ -265,7 +502,44 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
     const half8 *q = reinterpret_cast<const half8 *>(q16);
     const int T = (M + 31) / 32;
     const int cap = flags & 15;
+    if ((flags & 0x1000) && T >= 2) {   // spanning form (A/B)
+        const int nq = T >= 9 ? 3 : (T >= 5 ? 2 : 1);
+        const int g = (T + 4 * nq - 1) / (4 * nq);
+        const long nb = ((nchunks + 7) / 8) * 8 * g;
+        IA_ARG(nb < (1L << 31), "screen grid too large");
+        IA_ARG(g * 4 * nq <= T + 2 * MAX_NQ, "screen: query tiles exceed the padded rows");
+        const int md = (flags & 0x8000) ? 2 : ((flags & 0x2000) ? 1 : 0);
+#define IA_H16P_CASE(NQ, MD)                                                                    \
+        if (nq == NQ && md == MD) {                                                             \
+            k_screen_h16p<NQ, MD><<<(unsigned)nb, 512, 0, st>>>(db16, (int)nchunks, ch, seg_rows, \
+                                                               q, M, g, segmin, nseg);          \
+            IA_LAUNCH_CHECK("k_screen_h16p");                                                   \
+            return IA_OK;                                                                       \
+        }
+        IA_H16P_CASE(3, 0)
+        IA_H16P_CASE(2, 0)
+        IA_H16P_CASE(1, 0)
+        IA_H16P_CASE(3, 1)
+        IA_H16P_CASE(2, 1)
+        IA_H16P_CASE(1, 1)
+        IA_H16P_CASE(3, 2)
+        IA_H16P_CASE(2, 2)
+        IA_H16P_CASE(1, 2)
+#undef IA_H16P_CASE
+        set_error("launch_screen16: bad span split");
+        return IA_E_ARG;
+    }
+    if ((flags & 0x4000) && T >= 4) {   // uneven query shares (A/B)
+        const int g = (T + 11) / 12;
+        const long nb = ((nchunks + 7) / 8) * 8 * g;
+        IA_ARG(nb < (1L << 31), "screen grid too large");
+        k_screen_h16u<<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M, T, g,
+                                                    segmin, nseg);
+        IA_LAUNCH_CHECK("k_screen_h16u");
+        return IA_OK;
+    }
     bool pipe = !(flags & 0x200);
+    const bool pf = flags & 0x400;    // fragment-prefetch form (A/B)
     if (h16_shared() && !(flags & 0x100) && T >= 2) {
         // query tiles per block WQ x NQ: T >= 9 -> 4 x 3, 5..8 -> 4 x 2, 3..4 -> 4 x 1,
         // 2 -> 2 x 1 (fewest padded tiles, then the most sharing)
@@ -274,26 +548,32 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
         if (cap > 0 && cap < nq) nq = cap;
         // the pipelined epilogue's second accumulator set costs NQ = 3 its second wave per
         // SIMD (measured slower: profiles/r01_screen_bench_h16s.txt)
-        if (nq == 3) pipe = false;
+        if (nq == 3 && !(flags & 0x800)) pipe = false;   // bit 11: keep it (A/B)
         const int g = (T + wq * nq - 1) / (wq * nq);
         const long nb = ((nchunks + 7) / 8) * 8 * g;
         IA_ARG(nb < (1L << 31), "screen grid too large");
         IA_ARG(g * wq * nq <= T + 2 * MAX_NQ, "screen: query tiles exceed the padded rows");
-#define IA_H16S_CASE(NQ, WQ, P)                                                                 \
-        if (nq == NQ && wq == WQ && pipe == P) {                                                \
-            k_screen_h16s<NQ, WQ, P><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch,      \
-                                                                   seg_rows, q, M, g, segmin,   \
-                                                                   nseg);                       \
+        const int mode = pf ? 2 : (pipe ? 1 : 0);
+#define IA_H16S_CASE(NQ, WQ, MD)                                                                \
+        if (nq == NQ && wq == WQ && mode == MD) {                                               \
+            k_screen_h16s<NQ, WQ, MD><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch,     \
+                                                                    seg_rows, q, M, g, segmin,  \
+                                                                    nseg);                      \
             IA_LAUNCH_CHECK("k_screen_h16s");                                                   \
             return IA_OK;                                                                       \
         }
-        IA_H16S_CASE(2, 4, true)
-        IA_H16S_CASE(1, 4, true)
-        IA_H16S_CASE(1, 2, true)
-        IA_H16S_CASE(3, 4, false)
-        IA_H16S_CASE(2, 4, false)
-        IA_H16S_CASE(1, 4, false)
-        IA_H16S_CASE(1, 2, false)
+        IA_H16S_CASE(3, 4, 1)
+        IA_H16S_CASE(2, 4, 1)
+        IA_H16S_CASE(1, 4, 1)
+        IA_H16S_CASE(1, 2, 1)
+        IA_H16S_CASE(3, 4, 0)
+        IA_H16S_CASE(2, 4, 0)
+        IA_H16S_CASE(1, 4, 0)
+        IA_H16S_CASE(1, 2, 0)
+        IA_H16S_CASE(3, 4, 2)
+        IA_H16S_CASE(2, 4, 2)
+        IA_H16S_CASE(1, 4, 2)
+        IA_H16S_CASE(1, 2, 2)
 #undef IA_H16S_CASE
         set_error("launch_screen16: bad shared split");
         return IA_E_ARG;

@@ -5,7 +5,7 @@
 // the f32 MFMA rate, so each operand x is carried as two f16 values, x = x_h + x_l
 // (x_h = f16(x), x_l = f16(x - x_h)), and the product as a_h q_h + a_h q_l + a_l q_h
 // (the a_l q_l term, ~2^-22 relative, is dropped): 21 groups of 8 products, packed into
-// 11 v_mfma_f32_32x32x16_f16 per 32x32 tile with f32 accumulation.  Both operands are
+// 11 v_mfma_f32_32x32x16_f16 per 32x32 tile with f32 accumulation (one 8-slot group zero).  Both operands are
 // scaled by powers of two first (exact), so that every f16 value is far from the f16
 // overflow and flush thresholds:
 //   DB     alpha_k = sa * a'_k, alpha_55 = sa * 2^-R * |a'|^2,  sa = 2^ea
@@ -15,16 +15,20 @@
 //
 // Lane layout of one MFMA (lane l: row/col l & 31, half h = l >> 5 supplies k-slots
 // 8h..8h+7 of both operands).  Groups of 8 features: [8g, 8g+8).  The DB lane (row, h)
-// holds 7 register groups G0..G6, the query lane (col, h) 11 groups Q0..Q10, and MFMA m
-// multiplies G[m < 7 ? m : m - 7] by Q[m]:
+// holds 7 register groups G0..G6, the query lane (col, h) 8 groups Q0..Q7, and MFMA m
+// multiplies G[MA[m]] by Q[MB[m]] (tables below):
 //   h = 0: G0..G3 = a_h[0..31], G4..G6 = a_l[0..23]
-//          Q0..Q3 = q_l[0..31], Q4..Q6 = q_h[0..23], Q7..Q10 = q_h[0..31]
-//   h = 1: G0 = a_l[24..31], G1..G3 = a_h[32..55], G4..G6 = a_l[32..55]
-//          Q0 = q_h[24..31], Q1..Q3 = q_l[32..55], Q4..Q6 = q_h[32..55],
-//          Q7 = 0, Q8..Q10 = q_h[32..55]
+//          Q0..Q3 = q_l[0..31], Q4..Q7 = q_h[0..31]
+//   h = 1: G0..G2 = a_h[32..55], G3 = a_l[24..31], G4..G6 = a_l[32..55]
+//          Q0..Q2 = q_l[32..55], Q3 = q_h[24..31], Q4..Q6 = q_h[32..55], Q7 = 0
+//   m      0  1  2  3  4  5  6  7  8  9 10
+//   MA     0  1  2  3  4  5  6  0  1  3  2
+//   MB     0  1  2  3  4  5  6  4  5  7  6
 // MFMAs 0-6 carry only cross terms (a_h q_l, a_l q_h: ~2^-11 of the main terms) and
-// 7-10 the main terms a_h q_h, the norm slot (55) in the last one; the error bound of
-// DESIGN.md §4b uses that order.
+// 7-10 the main terms a_h q_h (h = 1 adds a_l[24..31] x 0 at m = 9), with the norm slot
+// (55) in the last one; the error bound of DESIGN.md §4b uses that order.  The query
+// groups q_h[0..23] / q_h[32..55] serve both a cross and a main term, so a query tile
+// costs 8 half8 = 32 VGPRs.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -32,9 +36,12 @@ namespace ia {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
-constexpr int Q16_GROUPS = 11;                   // half8 groups per query lane half
-constexpr int Q16_ROW = 2 * Q16_GROUPS;          // half8 per query row (352 B)
+constexpr int Q16_GROUPS = 8;                    // half8 groups per query lane half
+constexpr int Q16_ROW = 2 * Q16_GROUPS;          // half8 per query row (256 B)
 constexpr int DB16_GROUPS = 7;                   // half8 groups per DB lane half (224 B/row)
+constexpr int MFMA16 = 11;                       // MFMAs per 32x32 tile
+__host__ __device__ constexpr int mfma_a(int m) { return m < 7 ? m : (m == 9 ? 3 : (m == 10 ? 2 : m - 7)); }
+__host__ __device__ constexpr int mfma_b(int m) { return m < 7 ? m : (m == 9 ? 7 : (m == 10 ? 6 : m - 3)); }
 
 // DB scale exponents from amax = max row |a'| (fp32): sa * Amax in [2^13, 2^14),
 // 2^R >= Amax, so |alpha_k| < 2^14 and alpha_55 <= 2^14.
@@ -69,30 +76,20 @@ __device__ __forceinline__ void split16d(double x, _Float16 &h, _Float16 &l) {
     l = (_Float16)(float)(x - (double)h);  // x - h exact in f64
 }
 
-// query slot positions of feature k (0..55): hi value goes to up to two (h, m) slots,
-// lo value to one.  Returns the slot indices h * 11 + m (or -1); element = k & 7.
+// query slots of feature k (0..55), as h * 8 + group: the hi value goes to one or two
+// slots (hi1 = -1: none), the lo value to one; element = k & 7.
 __device__ __forceinline__ void split16_q_slots(int k, int &lo, int &hi0, int &hi1) {
-    if (k < 24) {
-        lo = k >> 3; hi0 = 4 + (k >> 3); hi1 = 7 + (k >> 3);
-    } else if (k < 32) {
-        lo = 3; hi0 = Q16_GROUPS + 0; hi1 = 10;
+    if (k < 32) {
+        lo = k >> 3; hi0 = 4 + (k >> 3); hi1 = k >= 24 ? Q16_GROUPS + 3 : -1;
     } else {
         const int g = (k - 32) >> 3;
-        lo = Q16_GROUPS + 1 + g; hi0 = Q16_GROUPS + 4 + g; hi1 = Q16_GROUPS + 8 + g;
+        lo = Q16_GROUPS + g; hi0 = Q16_GROUPS + 4 + g; hi1 = -1;
     }
-}
-// DB register group holding feature k's hi / lo value, as (h, g) -> h * 7 + g
-__device__ __forceinline__ void split16_db_slots(int k, int &hi, int &lo) {
-    if (k < 32) hi = k >> 3;
-    else hi = DB16_GROUPS + 1 + ((k - 32) >> 3);
-    if (k < 24) lo = 4 + (k >> 3);
-    else if (k < 32) lo = DB16_GROUPS + 0;
-    else lo = DB16_GROUPS + 4 + ((k - 32) >> 3);
 }
 
 // lane k (0..63) of a query wave writes its feature's split values into the query's
-// 11 x 2 half8 groups (d = q'_k in fp64, k < 55; slot 55 = sq 2^R; lanes 56..63 zero
-// the h = 1, m = 7 group).  nq = |q'|^2 (same value in every lane).
+// 8 x 2 half8 groups (d = q'_k in fp64, k < 55; slot 55 = sq 2^R; lanes 56..63 zero
+// the h = 1 group 7).  nq = |q'|^2 (same value in every lane).
 __device__ __forceinline__ void split16_write_query(_Float16 *row, int k, double d, double nq,
                                                     float amax) {
     const Split16Db s = split16_db_scale(amax);
@@ -110,7 +107,7 @@ __device__ __forceinline__ void split16_write_query(_Float16 *row, int k, double
         const int e = k & 7;
         row[lo * 8 + e] = l;
         row[hi0 * 8 + e] = h;
-        row[hi1 * 8 + e] = h;
+        if (hi1 >= 0) row[hi1 * 8 + e] = h;
     } else {
         row[(Q16_GROUPS + 7) * 8 + (k & 7)] = (_Float16)0.f;
     }

@@ -17,6 +17,8 @@
 #include "ia_finish.h"
 #include "ia_split16.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -121,6 +123,12 @@ static int graph_mode() {
         g = e ? atoi(e) : 1;
     }
     return g;
+}
+
+static unsigned long long slots_max(const std::vector<unsigned long long> &s, int i) {
+    unsigned long long m = 0;
+    for (int sl = 0; sl < STATS_SLOTS; ++sl) m = s[sl * STATS_LINE + i] > m ? s[sl * STATS_LINE + i] : m;
+    return m;
 }
 
 int comm_allgather_best(void *comm, const Best *send, Best *recv, int M, hipStream_t st);
@@ -263,6 +271,10 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         a->prof[5] = (double)st_h[2];
         a->prof[6] = ntimed;
         a->prof[7] = timed ? pairs : 0.0;
+        if (getenv("IA_PRUNE_PROBE"))   // diagnostic: see k_rescore
+            fprintf(stderr, "prune-probe nrows %ld queries %.0f segs %llu rows %llu c4x2 %llu c4x4 %llu "
+                    "c8x2 %llu c4x2max %llu\n", a->nrows, pairs / (double)a->nrows, st_h[1], st_h[0],
+                    st_h[3], st_h[4], st_h[5], slots_max(slots, 6));
     }
     return IA_OK;
 }

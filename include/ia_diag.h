@@ -26,7 +26,7 @@ int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *ca
                    int variant, void *stream);
 
 /* split-f16 screen (the default matcher's stage 1): query rows in both
- * forms (qp as ia_diag_query_rows, q16 = ia_diag_qp_rows(M) x 352 B, zeroed by the caller;
+ * forms (qp as ia_diag_query_rows, q16 = ia_diag_qp_rows(M) x 256 B, zeroed by the caller;
  * amax from ia_db_build), and one k_screen_h16 launch -> segment minima (screen units).
  * maxnq: bits 0-3 cap on query tiles per wave (0 = default), bit 8 uniform groups. */
 int ia_diag_query_rows16(const double *q64, int M, const double *center, const float *amax,

@@ -15,6 +15,7 @@ from conftest import analogy_inputs
 pytestmark = pytest.mark.gpu
 
 U32 = 2.0 ** -24
+Q16_HALVES = 128          # split-f16 query row: 16 half8 groups (ia_split16.h Q16_ROW)
 
 
 def dev(a, dtype=torch.float64):
@@ -77,7 +78,7 @@ def test_split16_segment_minima_within_bound(gpu, scale):
     q64 = torch.zeros((M, _ia.IA_DP), dtype=torch.float64, device='cuda')
     q64[:, :55] = dev(Q)
     qp = torch.zeros((qrows, _ia.IA_DP), dtype=torch.float32, device='cuda')
-    q16 = torch.zeros((qrows, 176), dtype=torch.float16, device='cuda')
+    q16 = torch.zeros((qrows, Q16_HALVES), dtype=torch.float16, device='cuda')
     nq = torch.zeros(qrows, dtype=torch.float64, device='cuda')
     st = _ia.stream()
     _ia.check(lib.ia_diag_query_rows16(_ia.ptr(q64), M, _ia.ptr(idx.center), _ia.ptr(idx.amax),
@@ -110,6 +111,50 @@ def test_split16_segment_minima_within_bound(gpu, scale):
         worst = max(worst, err / eps)
     print('split16 screen: worst |segmin - exact| / eps16 = %.3g' % worst)
     assert worst < 1.0
+
+
+def test_split16_screen_forms_agree(gpu):
+    """Every form of the split-f16 screen (per-wave, LDS-shared with and without the
+    pipelined epilogue, fragment prefetch, spanning stages, uneven query shares; each
+    query-tile cap) runs the same MFMA chain per tile and takes exact minima, so their
+    segment minima agree bitwise, on a 1M-row level (many stages per chunk) at query
+    counts that hit every shape of the launcher."""
+    import _ia
+    import algorithms
+    lib = _ia.lib()
+    A, Aps, _ = analogy_inputs(45, (1024, 1024), (8, 8), n_ap=1)
+    A_pyr = o.compute_gaussian_pyramid(A, 3, cap=2)
+    Ap_pyr = o.compute_gaussian_pyramid(Aps[0], 3, cap=2)
+    L = len(A_pyr)
+    idx = algorithms.level_index([dev(p) for p in A_pyr], [[dev(p) for p in Ap_pyr]], L - 1)
+    N = idx.nrows
+    Mmax = 342
+    rs = np.random.RandomState(7)
+    qrows = lib.ia_diag_qp_rows(Mmax)
+    q64 = torch.zeros((Mmax, _ia.IA_DP), dtype=torch.float64, device='cuda')
+    q64[:, :55] = dev(rs.rand(Mmax, 55))
+    qp = torch.zeros((qrows, _ia.IA_DP), dtype=torch.float32, device='cuda')
+    q16 = torch.zeros((qrows, Q16_HALVES), dtype=torch.float16, device='cuda')
+    nq = torch.zeros(qrows, dtype=torch.float64, device='cuda')
+    st = _ia.stream()
+    _ia.check(lib.ia_diag_query_rows16(_ia.ptr(q64), Mmax, _ia.ptr(idx.center),
+                                       _ia.ptr(idx.amax), _ia.ptr(qp), _ia.ptr(q16),
+                                       _ia.ptr(nq), st), 'ia_diag_query_rows16')
+    npad = lib.ia_db_rows_padded(N)
+    nseg = npad // min(lib.ia_db_chunk_rows(N) // 4, 512)
+    segmin = torch.empty((qrows, nseg), dtype=torch.float32, device='cuda')
+    for M in (1, 20, 64, 100, 128, 192, 256, 342):
+        outs = {}
+        for flags in (0x100, 0x000, 0x200, 0x400, 0x800, 0x001, 0x002, 0x003, 0x1000, 0x4000):
+            segmin.fill_(float('nan'))
+            _ia.check(lib.ia_diag_screen16(_ia.ptr(idx.db), N, _ia.ptr(q16), M,
+                                           _ia.ptr(segmin), flags, st), 'ia_diag_screen16')
+            torch.cuda.synchronize()
+            outs[flags] = segmin[:M].cpu().numpy().copy()
+            assert np.isfinite(outs[flags]).all(), (M, hex(flags))
+        ref = outs[0x100]
+        for flags, got in outs.items():
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (M, hex(flags))
 
 
 @pytest.mark.parametrize('which', [1, 2])

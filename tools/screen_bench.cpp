@@ -140,12 +140,12 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&qp, sizeof(float) * IA_DP * qrows)); CK(hipMemset(qp, 0, sizeof(float) * IA_DP * qrows));
     CK(hipMalloc(&dnq, sizeof(double) * qrows));
     void *q16;
-    CK(hipMalloc(&q16, (size_t)352 * qrows)); CK(hipMemset(q16, 0, (size_t)352 * qrows));
+    CK(hipMalloc(&q16, (size_t)256 * qrows)); CK(hipMemset(q16, 0, (size_t)256 * qrows));
     CI(ia_diag_query_rows16(dq, Mmax, dc, amax, qp, q16, dnq, st));
     // variant 7 (bits 4-7 cap, bit 8 uniform): the split-f16 screen
     auto screen = [&](int M, void *out, int v) {
         if ((v & 15) == 7)
-            CI(ia_diag_screen16(db, N, q16, M, reinterpret_cast<float *>(out), ((v >> 4) & 15) | (v & 0x300), st));
+            CI(ia_diag_screen16(db, N, q16, M, reinterpret_cast<float *>(out), ((v >> 4) & 15) | (v & 0xff00), st));
         else
             CI(ia_diag_screen(db, N, qp, M, out, v, st));
     };
