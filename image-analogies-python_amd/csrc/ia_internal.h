@@ -47,6 +47,14 @@ struct Best {            // exact winner of a (query, shard): fp64 distance + gl
     double d;
     long long idx;
 };
+struct WItem {           // one (query, candidate segment) of the work-list exact stage
+    int q, seg;
+    double trow;         // the query's fp32 re-screen threshold
+};
+struct QSel {            // per-query record of k_select: re-screen threshold, items
+    double trow;
+    int base, count;
+};
 
 // query-group split of M queries (32-query tiles, NQ tiles per group)
 struct QSplit {
@@ -125,7 +133,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
                  hipStream_t st,
                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                  const FinishArgs *fin = nullptr);
-int fuse_finish();    // IA_FUSE_FINISH: 0 off, 1 levels <= 2^20 rows [default], 2 on
+int fuse_finish();    // IA_FUSE_FINISH: 0 off, 1 levels <= 2^20 rows, 2 on [default]
 int match_alg();      // IA_MATCH_ALG (default 2: segment minima, split-f16 screen)
 // q16 != nullptr: the split-f16 screen (k_screen_h16) over db16_of(db)
 int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
@@ -135,7 +143,7 @@ int screen_variant();
 // query tiles per wave (0 = shape rule), bit 8 per-wave kernel (no LDS sharing), bit 9 no
 // pipelined epilogue, bit 10 fragment-prefetch form, bit 11 keep the epilogue at
 // NQ = 3, bit 12 spanning form (bits 13 / 15: its no-copy diagnostics), bit 14 uneven
-// query shares
+// query shares, bit 16 double-buffered fragment registers
 int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
                     int flags, hipStream_t st);
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query

@@ -828,9 +828,37 @@ __device__ unsigned long long *g_probe;
     } while (0)
 #endif
 
+// Thresholds of the exact stage from the minimum segment minimum emin:
+// Tseg for segment minima (screen units), Trow for the fp32 VALU re-screen (unscaled).
+// f32 screen: both e* + 2 eps.  Split-f16 screen (minima in units of sa * sq): e* = emin /
+// (sa sq) exactly, Tseg = e* + 2 eps16, Trow = e* + eps16 + eps; force_full when the
+// query's norm slot nears the f16 floor (|q'| > 2^24 Amax).
+template <bool SPLIT>
+__device__ __forceinline__ void rescore_thresholds(float emin, float amax0, double nqq,
+                                                   double &Tseg, double &Trow, bool &force_full) {
+    constexpr double U32 = 5.9604644775390625e-08;
+    const double A = (double)amax0;
+    const double eps = 70.0 * U32 * (2.0 * A * sqrt(nqq) + A * A);
+    force_full = false;
+    if (SPLIT) {
+        const Split16Db sc = split16_db_scale(amax0);
+        const int eq = split16_q_scale(nqq, sc.R);
+        const int e2 = sc.ea + eq;
+        const double em = ldexp((double)emin, -e2);
+        const double eps16 = U32 * (300.0 * A * sqrt(nqq) + 50.0 * A * A);
+        const double slack = 1e-12 * (fabs(em) + nqq + A * A);
+        Tseg = ldexp(em + 2.0 * eps16 + slack, e2);
+        Trow = em + eps16 + eps + slack;
+        force_full = eq + sc.R < -10;
+    } else {
+        Tseg = Trow = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
+    }
+}
+
 constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
 constexpr int RESCORE_REG = 8;         // float4s of segment minima per thread kept in VGPRs
 constexpr int RESCORE_RPT = 2;         // candidate rows per thread per step
+constexpr int RESCORE_ROWCAP = 512;    // rows to rescore held in LDS per query
 
 // Exact stage of the segment-minimum matcher: one 256-thread workgroup per query.
 // FIN: single shard — wave 0 then runs the per-pixel tail of the synthesis step
@@ -855,6 +883,8 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     __shared__ double qs[IA_DP];
     __shared__ float qf[IA_DP];
     __shared__ unsigned int nresc;
+    __shared__ long rlist[RESCORE_ROWCAP];
+    __shared__ int rcount;
 
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
@@ -863,7 +893,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
         qs[tid] = q64[(long)q * IA_DP + tid];
         qf[tid] = qp[(long)q * IA_DP + tid];
     }
-    if (tid == 0) { scount = 0; nresc = 0; }
+    if (tid == 0) { scount = 0; nresc = 0; rcount = 0; }
     const float *sq = segmin + (long)q * nseg;
     const double A = (double)amax[0];   // issued with the segment-minimum loads
     const double nqq = nq[q];
@@ -894,27 +924,9 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     IA_PROBE_MARK(2);
     emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
 
-    constexpr double U32 = 5.9604644775390625e-08;
-    const double eps = 70.0 * U32 * (2.0 * A * sqrt(nqq) + A * A);
-    // Tseg: segment-minimum threshold (screen units), Trow: re-screen threshold (fp32
-    // VALU recomputation, unscaled).  f32 screen: both e* + 2 eps.  Split-f16 screen
-    // (minima in units of sa * sq): e* = emin / (sa sq) exactly, Tseg = e* + 2 eps16,
-    // Trow = e* + eps16 + eps.
     double Tseg, Trow;
-    bool force_full = false;
-    if (SPLIT) {
-        const Split16Db sc = split16_db_scale(amax[0]);
-        const int eq = split16_q_scale(nqq, sc.R);
-        const int e2 = sc.ea + eq;
-        const double em = ldexp((double)emin, -e2);
-        const double eps16 = U32 * (300.0 * A * sqrt(nqq) + 50.0 * A * A);
-        const double slack = 1e-12 * (fabs(em) + nqq + A * A);
-        Tseg = ldexp(em + 2.0 * eps16 + slack, e2);
-        Trow = em + eps16 + eps + slack;
-        force_full = eq + sc.R < -10;   // |q'| > 2^24 Amax: the norm slot nears f16 flush
-    } else {
-        Tseg = Trow = (double)emin + 2.0 * eps + 1e-12 * (fabs((double)emin) + nqq + A * A);
-    }
+    bool force_full;
+    rescore_thresholds<SPLIT>(emin, amax[0], nqq, Tseg, Trow, force_full);
 
     auto push = [&](float e, long s) {
         if ((double)e <= Tseg) {
@@ -1011,13 +1023,23 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
             e[u] = acc;
         }
         IA_PROBE_MARK(8);
+        // rows within Trow go to a list rescored one per thread after the loop (one round
+        // of feature gathers); a list overflow is rescored in place
 #pragma unroll
         for (int u = 0; u < RESCORE_RPT; ++u) {
             if (lr[u] < nrows && (double)e[u] <= Trow) {
                 ++mine;
-                best_update(bd, bi, row_dist2(src, row0 + lr[u], qs), row0 + lr[u]);
+                const int pos = atomicAdd(&rcount, 1);
+                if (pos < RESCORE_ROWCAP) rlist[pos] = lr[u];
+                else best_update(bd, bi, row_dist2(src, row0 + lr[u], qs), row0 + lr[u]);
             }
         }
+    }
+    __syncthreads();
+    {
+        const int nl = rcount < RESCORE_ROWCAP ? rcount : RESCORE_ROWCAP;
+        for (int i = tid; i < nl; i += 256)
+            best_update(bd, bi, row_dist2(src, row0 + rlist[i], qs), row0 + rlist[i]);
     }
     for (int o = 32; o > 0; o >>= 1) {
         const double od = __shfl_xor(bd, o);
@@ -1047,11 +1069,223 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Work-list exact stage: the same thresholds and the same rows as
+// k_rescore, but the candidate segments of all queries become items of one list, so a
+// query with many candidate segments spreads over many workgroups instead of serialising
+// in one (k_rescore's time is that of its heaviest query).
+//   k_select  one workgroup per query: e*, thresholds, candidate segments -> items
+//   k_items   one workgroup per item (grid-stride): fp32 re-screen of the segment's rows,
+//             exact rescore of those <= Trow -> the item's (distance, row) minimum
+//   k_gather  one wave per query: the lexicographic minimum over its items [+ the
+//             per-pixel tail]; also empties the list for the next call
+// ---------------------------------------------------------------------------------
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void k_select(long nseg, const float *__restrict__ segmin,
+                                                const double *__restrict__ nq,
+                                                const float *__restrict__ amax, int *ctr,
+                                                WItem *__restrict__ items, QSel *__restrict__ sel,
+                                                unsigned long long *stats) {
+    __shared__ int slist[RESCORE_SEGCAP];
+    __shared__ int scount, sbase;
+    __shared__ float redf[4];
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (tid == 0) scount = 0;
+    const float *sq = segmin + (long)q * nseg;
+    const double nqq = nq[q];
+    const long n4 = nseg / 4;
+    const float4 *sq4 = reinterpret_cast<const float4 *>(sq);
+    float4 v[RESCORE_REG];
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j) {
+        const long i = tid + (long)j * 256;
+        v[j] = i < n4 ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+    }
+    float emin = FLT_MAX;
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j)
+        emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
+    for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
+        const float4 x = sq4[i];
+        emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
+    }
+    for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
+    if ((tid & 63) == 0) redf[tid >> 6] = emin;
+    __syncthreads();
+    emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
+    double Tseg, Trow;
+    bool force_full;
+    rescore_thresholds<SPLIT>(emin, amax[0], nqq, Tseg, Trow, force_full);
+    auto push = [&](float e, long s) {
+        if ((double)e <= Tseg) {
+            const int pos = atomicAdd(&scount, 1);
+            if (pos < RESCORE_SEGCAP) slist[pos] = (int)s;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j) {
+        const long i = tid + (long)j * 256;
+        push(v[j].x, 4 * i);
+        push(v[j].y, 4 * i + 1);
+        push(v[j].z, 4 * i + 2);
+        push(v[j].w, 4 * i + 3);
+    }
+    for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
+        const float4 x = sq4[i];
+        push(x.x, 4 * i);
+        push(x.y, 4 * i + 1);
+        push(x.z, 4 * i + 2);
+        push(x.w, 4 * i + 3);
+    }
+    __syncthreads();
+    const int ns = scount;
+    const bool full = ns > RESCORE_SEGCAP || force_full;
+    const int cnt = full ? (int)nseg : ns;
+    if (tid == 0) {
+        sbase = atomicAdd(ctr, cnt);
+        sel[q] = QSel{Trow, sbase, cnt};
+        if (stats) {
+            unsigned long long *sl = stats_slot(stats, q);
+            atomicAdd(&sl[1], (unsigned long long)ns);
+            atomicAdd(&sl[2], full ? 1ULL : 0ULL);
+        }
+    }
+    __syncthreads();
+    const int base = sbase;
+    for (int i = tid; i < cnt; i += 256) items[base + i] = WItem{q, full ? i : slist[i], Trow};
+}
+
+__global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows, int seg_rows,
+                                               const WItem *__restrict__ items,
+                                               const int *__restrict__ ctr,
+                                               const float *__restrict__ db,
+                                               const float *__restrict__ qp,
+                                               const double *__restrict__ q64,
+                                               Best *__restrict__ ibest,
+                                               unsigned long long *stats) {
+    __shared__ double qs[IA_DP];
+    __shared__ float qf[IA_DP];
+    __shared__ double redd[4];
+    __shared__ long long redi[4];
+    __shared__ int plist[RESCORE_RPT * 256];
+    __shared__ int pcount;
+    IA_PROBE_MARK(0);
+    const int n = *ctr;
+    const int tid = threadIdx.x;
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+        const WItem w = items[it];
+        // this thread's rows of the segment (fragment-major fp32 DB, as k_rescore), issued
+        // before the query is staged so that the two round trips overlap
+        float4 x[RESCORE_RPT][14];
+        long lr[RESCORE_RPT];
+#pragma unroll
+        for (int u = 0; u < RESCORE_RPT; ++u) {
+            const int k = u * 256 + tid;
+            lr[u] = k < seg_rows ? (long)w.seg * seg_rows + k : nrows;
+            const long r = lr[u] < nrows ? lr[u] : 0;
+            const float4 *t4 = reinterpret_cast<const float4 *>(db) + (r >> 5) * TILE_VEC + (r & 31);
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                for (int v = 0; v < 7; ++v) x[u][hh * 7 + v] = t4[v * 64 + hh * 32];
+        }
+        __syncthreads();                       // the previous item's LDS reads are done
+        if (tid < IA_DP) {
+            qs[tid] = q64[(long)w.q * IA_DP + tid];
+            qf[tid] = qp[(long)w.q * IA_DP + tid];
+        }
+        if (tid == 0) pcount = 0;
+        __syncthreads();
+        IA_PROBE_MARK(1);
+        // fp32 re-screen; rows within Trow go to one list, rescored one per thread below
+        // (a single round of feature gathers, however the passing rows fall over lanes)
+#pragma unroll
+        for (int u = 0; u < RESCORE_RPT; ++u) {
+            float acc = 0.f;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                for (int v = 0; v < 7; ++v) {
+                    const float4 xv = x[u][hh * 7 + v];
+                    const float *qv = qf + hh * 28 + 4 * v;
+                    acc = fmaf(xv.x, qv[0], acc);
+                    acc = fmaf(xv.y, qv[1], acc);
+                    acc = fmaf(xv.z, qv[2], acc);
+                    acc = fmaf(xv.w, qv[3], acc);
+                }
+            if (lr[u] < nrows && (double)acc <= w.trow) plist[atomicAdd(&pcount, 1)] = u * 256 + tid;
+        }
+        __syncthreads();
+        IA_PROBE_MARK(2);
+        const int np = pcount;
+        double bd = INFINITY;
+        long long bi = 0x7fffffffffffffffLL;
+        for (int i = tid; i < np; i += 256) {
+            const long row = row0 + (long)w.seg * seg_rows + plist[i];
+            best_update(bd, bi, row_dist2(src, row, qs), row);
+        }
+        IA_PROBE_MARK(3);
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o);
+            const long long oi = __shfl_xor(bi, o);
+            best_update(bd, bi, od, oi);
+        }
+        if ((tid & 63) == 0) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
+        __syncthreads();
+        IA_PROBE_MARK(4);
+        if (tid == 0) {
+            for (int wv = 1; wv < 4; ++wv) best_update(bd, bi, redd[wv], redi[wv]);
+            ibest[it] = Best{bd, bi};
+            if (stats) atomicAdd(&stats_slot(stats, w.q)[0], (unsigned long long)np);
+        }
+    }
+}
+
+template <bool FIN>
+__global__ __launch_bounds__(64) void k_gather(DbSrc src, const QSel *__restrict__ sel,
+                                               const Best *__restrict__ ibest, int *ctr,
+                                               Best *__restrict__ best, FinishArgs fa,
+                                               const double *__restrict__ q64) {
+    __shared__ double qs[IA_DP];
+    const int m = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (FIN && lane < IA_DP) qs[lane] = q64[(long)m * IA_DP + lane];
+    const QSel r = sel[m];
+    double bd = INFINITY;
+    long long bi = 0x7fffffffffffffffLL;
+    for (int i = lane; i < r.count; i += 64) {
+        const Best b = ibest[r.base + i];
+        best_update(bd, bi, b.d, b.idx);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o);
+        const long long oi = __shfl_xor(bi, o);
+        best_update(bd, bi, od, oi);
+    }
+    if (m == 0 && lane == 0) *ctr = 0;   // every k_items block has read it
+    if (FIN) {
+        __syncthreads();
+        finish_pixel(src, bi, m, fa, qs, lane);
+    } else if (lane == 0) {
+        best[m] = Best{bd, bi};
+    }
+}
+
+static int rescore_mode() {
+    static int v = -2;
+    if (v == -2) {
+        const char *e = getenv("IA_RESCORE");   // 0: per-query k_rescore, 1: work list
+        v = e ? atoi(e) : -1;                   // default: see launch_match
+    }
+    return v;
+}
+
 int fuse_finish() {
     static int f = -1;
     if (f < 0) {
         const char *e = getenv("IA_FUSE_FINISH");
-        f = e ? atoi(e) : 1;
+        f = e ? atoi(e) : 2;
     }
     return f;
 }
@@ -1111,9 +1345,33 @@ int match_alg() {
     return a;
 }
 
+// segment matcher scratch: [list counter | segment minima | items | item winners | per-query
+// records]; the counter sits at a fixed offset (it carries over between calls, emptied by
+// k_gather)
+static constexpr size_t WL_HEAD = 256;
+struct SegWs {
+    int *ctr;
+    float *segmin;
+    WItem *items;
+    Best *ibest;
+    QSel *sel;
+};
+static SegWs seg_ws(void *scratch, int M, long nrows) {
+    char *p = reinterpret_cast<char *>(scratch);
+    const size_t n = (size_t)M * db_nsegs(nrows);
+    SegWs w;
+    w.ctr = reinterpret_cast<int *>(p);
+    w.segmin = reinterpret_cast<float *>(p + WL_HEAD);
+    w.items = reinterpret_cast<WItem *>(p + WL_HEAD + align_up(n * sizeof(float), 256));
+    w.ibest = reinterpret_cast<Best *>(reinterpret_cast<char *>(w.items) + align_up(n * sizeof(WItem), 256));
+    w.sel = reinterpret_cast<QSel *>(reinterpret_cast<char *>(w.ibest) + align_up(n * sizeof(Best), 256));
+    return w;
+}
 size_t match_scratch_bytes(int qrows, long nrows) {
     const size_t a = (size_t)qrows * db_nchunks(nrows) * SCREEN_K * sizeof(Cand);
-    const size_t b = (size_t)qrows * db_nsegs(nrows) * sizeof(float);
+    const size_t n = (size_t)qrows * db_nsegs(nrows);
+    const size_t b = WL_HEAD + align_up(n * sizeof(float), 256) + align_up(n * sizeof(WItem), 256) +
+                     align_up(n * sizeof(Best), 256) + align_up((size_t)qrows * sizeof(QSel), 256);
     return a > b ? a : b;
 }
 
@@ -1131,7 +1389,8 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
         if (ev1) IA_HIP(hipEventRecord(ev1, st));
         return launch_merge(src, row0, nrows, cand, M, q64, nq, amax, best, stats, st);
     }
-    float *segmin = reinterpret_cast<float *>(scratch);
+    const SegWs ws = seg_ws(scratch, M, nrows);
+    float *segmin = ws.segmin;
     const int nq_cap = (screen_variant() >> 4) & 15;
     const bool split = match_alg() == 2;
     // f32: up to 3 query tiles per wave (profiles/r01_screen_bench_split.txt); split f16:
@@ -1142,6 +1401,27 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
         return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
+    const int rm = rescore_mode();
+    // default: the work list for levels above 2^20 rows (where k_rescore's per-query
+    // serialisation costs most) and wherever the tail runs separately
+    if (rm == 1 || (rm < 0 && (!fin || nrows > (1L << 20)))) {
+        const long nseg = db_nsegs(nrows);
+        if (split)
+            k_select<true><<<M, 256, 0, st>>>(nseg, segmin, nq, amax, ws.ctr, ws.items, ws.sel, stats);
+        else
+            k_select<false><<<M, 256, 0, st>>>(nseg, segmin, nq, amax, ws.ctr, ws.items, ws.sel, stats);
+        IA_LAUNCH_CHECK("k_select");
+        const int grid = 2 * M + 64;
+        k_items<<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr, db, qp,
+                                      q64, ws.ibest, stats);
+        IA_LAUNCH_CHECK("k_items");
+        if (fin)
+            k_gather<true><<<M, 64, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+        else
+            k_gather<false><<<M, 64, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+        IA_LAUNCH_CHECK("k_gather");
+        return IA_OK;
+    }
     static const int probe = getenv("IA_PRUNE_PROBE") ? atoi(getenv("IA_PRUNE_PROBE")) : 0;
 #define IA_RESCORE(F, SP)                                                                      \
     k_rescore<F, SP><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows), \
@@ -1240,6 +1520,7 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
     Best *best = reinterpret_cast<Best *>(w);
     IA_HIP(hipMemsetAsync(qp, 0, (size_t)qr * IA_DP * sizeof(float), st));
     IA_HIP(hipMemsetAsync(q16, 0, (size_t)qr * Q16_ROW * sizeof(half8), st));
+    IA_HIP(hipMemsetAsync(scratch, 0, WL_HEAD, st));   // empty work list
     const DbSrc src = make_dbsrc(a->src);
     for (int m0 = 0; m0 < a->M; m0 += MATCH_BATCH) {
         const int M = a->M - m0 < MATCH_BATCH ? a->M - m0 : MATCH_BATCH;

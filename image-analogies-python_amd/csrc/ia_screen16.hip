@@ -20,6 +20,7 @@
 #include "ia_split16.h"
 
 #include <float.h>
+#include <cstdlib>
 
 namespace ia {
 
@@ -147,11 +148,12 @@ __global__ __launch_bounds__(256) void k_screen_h16(const half8 *__restrict__ db
 // ---------------------------------------------------------------------------------
 // shared-tile form
 // ---------------------------------------------------------------------------------
-// MODE 0: plain; 1: pipelined epilogue (two accumulator sets); 2: fragment prefetch (the
+// MODE 0: plain; 1: pipelined epilogue (two accumulator sets); 3: double-buffered fragment
+// registers (below); 2: fragment prefetch (the
 // next tile's LDS groups re-read into each register group right after its last MFMA use,
 // barrier at the start of each stage's last tile, two stages of global_load_lds in flight)
-template <int NQ, int WQ, int MODE>
-__global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ db16, int nchunks,
+template <int NQ, int WQ, int MODE, bool NT = false>
+__global__ __launch_bounds__(256, 2) void k_screen_h16s(const half8 *__restrict__ db16, int nchunks,
                                                      int ch, int seg_rows,
                                                      const half8 *__restrict__ q16, int M,
                                                      int groups, float *__restrict__ segmin,
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
             const int v = s * STAGE_TILES + tt;
             const long gt = ctile0 + (long)(v % WR) * tpp + v / WR;
             __builtin_amdgcn_global_load_lds((const void *)(db16 + gt * TILE_H8 + rem),
-                                             (void *)&sbuf[buf][k * 256 + wv * 64], 16, 0, 0);
+                                             (void *)&sbuf[buf][k * 256 + wv * 64], 16, 0, NT ? 2 : 0);
         }
     };
     // every wave's global_load_lds of the next stage retired, then the barrier: the
@@ -213,6 +215,37 @@ __global__ __launch_bounds__(256) void k_screen_h16s(const half8 *__restrict__ d
     };
 
     issue(0, 0);
+    if (MODE == 3) {
+        // double-buffered fragments: tile i+1's ds_reads go into the other register set
+        // before tile i's MFMAs, so no tile starts on an LDS round trip; the barrier sits at
+        // the start of each stage's last tile (stage s+1 landed, stage s fully read), after
+        // which stage s+2's copies and the reads of stage s+1's first tile are issued
+        static_assert(TPW % 2 == 0, "register double buffering needs an even tile count");
+        half8 ra[DB16_GROUPS], rb[DB16_GROUPS];
+        if (nstage > 1) issue(1, 1);
+        stage_barrier();
+        read_tile(ra, sbuf[0], 0);
+        for (int s = 0; s < nstage; ++s) {
+            const half8 *sb = sbuf[s & 1];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                half8 (&cur)[DB16_GROUPS] = (u & 1) ? rb : ra;
+                half8 (&nxt)[DB16_GROUPS] = (u & 1) ? ra : rb;
+                if (u + 1 < TPW) {
+                    read_tile(nxt, sb, u + 1);
+                } else {
+                    stage_barrier();
+                    if (s + 2 < nstage) issue(s + 2, s & 1);
+                    if (s + 1 < nstage) read_tile(nxt, sbuf[(s + 1) & 1], 0);
+                }
+                floatx16 acc[NQ];
+                tile_mfma<NQ>(cur, bq, acc);
+                tile_min<NQ>(acc, mn);
+                close(s * TPW + u);
+            }
+        }
+        return;
+    }
     if (MODE == 2) {
         if (nstage > 1) issue(1, 1);
         stage_barrier();
@@ -553,7 +586,24 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
         const long nb = ((nchunks + 7) / 8) * 8 * g;
         IA_ARG(nb < (1L << 31), "screen grid too large");
         IA_ARG(g * wq * nq <= T + 2 * MAX_NQ, "screen: query tiles exceed the padded rows");
-        const int mode = pf ? 2 : (pipe ? 1 : 0);
+        const int mode = (flags & 0x10000) ? 3 : (pf ? 2 : (pipe ? 1 : 0));
+        // bit 17 / IA_SCREEN_NT (default 1): the DB stream copied with non-temporal loads (it
+        // is read once per launch and never fits the caches)
+        static const int nt_env = getenv("IA_SCREEN_NT") ? atoi(getenv("IA_SCREEN_NT")) : 1;
+        const bool nt = (flags & 0x20000) || nt_env;
+#define IA_H16S_NT_CASE(NQ, WQ, MD)                                                             \
+        if (nt && nq == NQ && wq == WQ && mode == MD) {                                         \
+            k_screen_h16s<NQ, WQ, MD, true><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, \
+                                                                          seg_rows, q, M, g,    \
+                                                                          segmin, nseg);        \
+            IA_LAUNCH_CHECK("k_screen_h16s");                                                   \
+            return IA_OK;                                                                       \
+        }
+        IA_H16S_NT_CASE(3, 4, 0)
+        IA_H16S_NT_CASE(2, 4, 1)
+        IA_H16S_NT_CASE(1, 4, 1)
+        IA_H16S_NT_CASE(1, 2, 1)
+#undef IA_H16S_NT_CASE
 #define IA_H16S_CASE(NQ, WQ, MD)                                                                \
         if (nq == NQ && wq == WQ && mode == MD) {                                               \
             k_screen_h16s<NQ, WQ, MD><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch,     \
@@ -574,6 +624,10 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
         IA_H16S_CASE(2, 4, 2)
         IA_H16S_CASE(1, 4, 2)
         IA_H16S_CASE(1, 2, 2)
+        IA_H16S_CASE(3, 4, 3)
+        IA_H16S_CASE(2, 4, 3)
+        IA_H16S_CASE(1, 4, 3)
+        IA_H16S_CASE(1, 2, 3)
 #undef IA_H16S_CASE
         set_error("launch_screen16: bad shared split");
         return IA_E_ARG;

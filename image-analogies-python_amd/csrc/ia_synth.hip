@@ -166,6 +166,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     IA_HIP(hipMemsetAsync(ws.qp, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
     IA_HIP(hipMemsetAsync(ws.q16, 0, (size_t)qrows_alloc(Mmax) * Q16_ROW * 16, st));
     IA_HIP(hipMemsetAsync(ws.stats, 0, STATS_BYTES, st));
+    IA_HIP(hipMemsetAsync(ws.scratch, 0, 256, st));   // the exact stage's empty work list
 
     const DbSrc src = make_dbsrc(a->src);
     const ImgPair B{a->B_sm, a->B_lg, a->B_hs, a->B_ws, H, W};
@@ -191,8 +192,8 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         hipEvent_t e1 = timed ? g_events.ev[2 * nscreen + 1] : nullptr;
         const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
                             a->im};
-        // fused tail (one launch + one round trip less per wave): measured faster for
-        // launch-bound levels, ~0.5 % slower on the 4M-row c4 finest level
+        // fused tail (one launch + one round trip less per wave): the exact stage's last
+        // kernel (k_rescore, or k_gather of the work list) runs the per-pixel tail
         const int fm = fuse_finish();
         const bool fused = !a->comm && !a->lsh && match_alg() >= 1 &&
                            (fm == 2 || (fm == 1 && a->nrows <= (1L << 20)));
