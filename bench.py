@@ -45,8 +45,8 @@ HBM_PEAK_GBS = 8000.0
 # HBM traffic of one finest-level screen launch, from rocprofv3 PMC (FETCH_SIZE x 2 on
 # gfx950 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench at M = 342 queries
 # against the 4,194,304-row c4 database (profiles/r01_screen_h16s_pmc_m342.txt)
-SCREEN_PMC = {'fetch_kb': 4.604e5, 'write_kb': 8.754e4, 'M': 342, 'rows': 4194304,
-              'source': 'profiles/r01_screen_h16s_pmc_m342.txt'}
+SCREEN_PMC = {'fetch_kb': 4.592e5, 'write_kb': 5.503e4, 'M': 342, 'rows': 4194304,
+              'source': 'profiles/r01_screen_h16s_pmc_m342_nt.txt'}
 
 CONFIGS = {
     'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),

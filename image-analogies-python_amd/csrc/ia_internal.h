@@ -143,7 +143,8 @@ int screen_variant();
 // query tiles per wave (0 = shape rule), bit 8 per-wave kernel (no LDS sharing), bit 9 no
 // pipelined epilogue, bit 10 fragment-prefetch form, bit 11 keep the epilogue at
 // NQ = 3, bit 12 spanning form (bits 13 / 15: its no-copy diagnostics), bit 14 uneven
-// query shares, bit 16 double-buffered fragment registers
+// query shares, bit 16 double-buffered fragment registers,
+// bit 17 non-temporal DB stream, bit 18 balanced query shares
 int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
                     int flags, hipStream_t st);
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query

@@ -516,6 +516,158 @@ __global__ __launch_bounds__(256) void k_screen_h16u(const half8 *__restrict__ d
         uneven_body<1>(db16, sbuf, ctile0, nstage, tps, seg0, q16, M, tile0, segmin, nseg);
 }
 
+// ---------------------------------------------------------------------------------
+// balanced form (flag 0x40000): a block's G query tiles (4A <= G <= 4A + 4, A = 1, 2) as
+// A tiles owned by each wave plus G - 4A extra tiles shared out by row quarters: in
+// quarter r of the chunk, wave w also takes extra tile (w + r) & 3 when that index is
+// below G - 4A.  Every (extra tile, quarter) is covered once and every wave carries
+// A + (G - 4A) / 4 tiles of work, so M = 342 computes 11 tiles (not 12) with the SIMDs
+// still evenly loaded (the uneven form above loses that balance).  Quarters hold whole
+// segments (seg_rows = min(ch / 4, 512)), so the extra tile's minima close inside them;
+// the next quarter's extra tile is prefetched into spare registers.
+// ---------------------------------------------------------------------------------
+template <int NQ, int NB>
+__device__ __forceinline__ void tile_mfma_n(const half8 (&a)[DB16_GROUPS],
+                                            const half8 (&bq)[NB][Q16_GROUPS],
+                                            floatx16 (&acc)[NB]) {
+    const floatx16 zero = {};
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt)
+        acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[qt][0], zero, 0, 0, 0);
+#pragma unroll
+    for (int m = 1; m < MFMA16; ++m)
+#pragma unroll
+        for (int qt = 0; qt < NQ; ++qt)
+            acc[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[qt][mfma_b(m)],
+                                                             acc[qt], 0, 0, 0);
+}
+template <int NQ, int NB>
+__device__ __forceinline__ void tile_min_n(const floatx16 (&acc)[NB], float (&mn)[NB]) {
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        const floatx16 &x = acc[qt];
+        const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+        const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+        const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+        const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+        mn[qt] = fminf(fminf(mn[qt], u0), u1);
+    }
+}
+template <int NQ, int NB>
+__device__ __forceinline__ void seg_flush_n(float (&mn)[NB], const int (&qtile)[NB], int j, int h,
+                                            int M, float *__restrict__ segmin, long nseg,
+                                            long seg) {
+#pragma unroll
+    for (int qt = 0; qt < NQ; ++qt) {
+        const float m = fminf(mn[qt], __shfl_xor(mn[qt], 32));
+        const int qg = qtile[qt] * 32 + j;
+        if (h == 0 && qg < M) segmin[(long)qg * nseg + seg] = m;
+        mn[qt] = FLT_MAX;
+    }
+}
+
+template <int A>
+__global__ __launch_bounds__(256, 2) void k_screen_h16b(const half8 *__restrict__ db16, int nchunks,
+                                                        int ch, int seg_rows,
+                                                        const half8 *__restrict__ q16, int M,
+                                                        int T, int groups,
+                                                        float *__restrict__ segmin, long nseg) {
+    constexpr int NB = A + 1;
+    __shared__ half8 sbuf[2][STAGE_H8];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+    const int per = T / groups, rem = T - per * groups;
+    const int G = per + (group < rem ? 1 : 0);
+    const int first = group * per + (group < rem ? group : rem);
+    const int bx = G - 4 * A;                  // 0..4 extra tiles
+    auto extra_of = [&](int qr) {
+        const int e = (wv + qr) & 3;
+        return e < bx ? first + 4 * A + e : -1;
+    };
+    auto load_tile = [&](half8 (&dst)[Q16_GROUPS], int t) {
+        const half8 *p = q16 + (long)(t * 32 + j) * Q16_ROW + h * Q16_GROUPS;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m) dst[m] = p[m];
+    };
+    int qtile[NB];
+    half8 bq[NB][Q16_GROUPS];
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+        qtile[k] = first + wv * A + k;
+        load_tile(bq[k], qtile[k]);
+    }
+    half8 bn[Q16_GROUPS];
+    int ecur = extra_of(0), enext = extra_of(1);
+    if (ecur >= 0) load_tile(bq[A], ecur);
+    if (enext >= 0) load_tile(bn, enext);
+    qtile[A] = ecur;
+
+    const int tpc = ch >> 5;
+    const int tq = tpc >> 2;                   // tiles per row quarter
+    const int tps = seg_rows >> 5;
+    const int nstage = tpc / STAGE_TILES;
+    const long ctile0 = (long)chunk * tpc;
+    const long seg0 = ctile0 * 32 / seg_rows;
+    auto issue = [&](int s, int buf) {
+        const half8 *src = db16 + (ctile0 + (long)s * STAGE_TILES) * TILE_H8 + tid;
+#pragma unroll
+        for (int k = 0; k < DB16_GROUPS; ++k)
+            __builtin_amdgcn_global_load_lds((const void *)(src + k * 256),
+                                             (void *)&sbuf[buf][k * 256 + wv * 64], 16, 0, 2);
+    };
+    auto stage_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    float mn[NB];
+#pragma unroll
+    for (int qt = 0; qt < NB; ++qt) mn[qt] = FLT_MAX;
+    issue(0, 0);
+    stage_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        const half8 *sb = sbuf[s & 1];
+#pragma unroll
+        for (int u = 0; u < STAGE_TILES; ++u) {
+            const int i = s * STAGE_TILES + u;
+            if (i > 0 && i % tq == 0) {        // next row quarter: rotate the extra tile
+                const int qr = i / tq;
+                ecur = enext;
+                if (ecur >= 0) {
+#pragma unroll
+                    for (int m = 0; m < Q16_GROUPS; ++m) bq[A][m] = bn[m];
+                }
+                qtile[A] = ecur;
+                enext = qr + 1 < 4 ? extra_of(qr + 1) : -1;
+                if (enext >= 0) load_tile(bn, enext);
+            }
+            half8 a[DB16_GROUPS];
+            const half8 *p = sb + u * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+            floatx16 acc[NB];
+            const bool close = (i + 1) % tps == 0;
+            if (ecur >= 0) {
+                tile_mfma_n<NB, NB>(a, bq, acc);
+                tile_min_n<NB, NB>(acc, mn);
+                if (close) seg_flush_n<NB, NB>(mn, qtile, j, h, M, segmin, nseg, seg0 + i / tps);
+            } else {
+                tile_mfma_n<A, NB>(a, bq, acc);
+                tile_min_n<A, NB>(acc, mn);
+                if (close) seg_flush_n<A, NB>(mn, qtile, j, h, M, segmin, nseg, seg0 + i / tps);
+            }
+        }
+        stage_barrier();
+    }
+}
+
 static int h16_shared() {
     static int v = -1;
     if (v < 0) {
@@ -561,6 +713,22 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
 #undef IA_H16P_CASE
         set_error("launch_screen16: bad span split");
         return IA_E_ARG;
+    }
+    if ((flags & 0x40000) && T >= 4) {   // balanced shares (A/B)
+        const int g = (T + 11) / 12;
+        const int A = (T / g) / 4;
+        if (A == 1 || A == 2) {
+            const long nb = ((nchunks + 7) / 8) * 8 * g;
+            IA_ARG(nb < (1L << 31), "screen grid too large");
+            if (A == 1)
+                k_screen_h16b<1><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M,
+                                                               T, g, segmin, nseg);
+            else
+                k_screen_h16b<2><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M,
+                                                               T, g, segmin, nseg);
+            IA_LAUNCH_CHECK("k_screen_h16b");
+            return IA_OK;
+        }
     }
     if ((flags & 0x4000) && T >= 4) {   // uneven query shares (A/B)
         const int g = (T + 11) / 12;

@@ -145,7 +145,7 @@ int main(int argc, char **argv) {
     // variant 7 (bits 4-7 cap, bit 8 uniform): the split-f16 screen
     auto screen = [&](int M, void *out, int v) {
         if ((v & 15) == 7)
-            CI(ia_diag_screen16(db, N, q16, M, reinterpret_cast<float *>(out), ((v >> 4) & 15) | (v & 0xff00), st));
+            CI(ia_diag_screen16(db, N, q16, M, reinterpret_cast<float *>(out), ((v >> 4) & 15) | (v & 0xfff00), st));
         else
             CI(ia_diag_screen(db, N, qp, M, out, v, st));
     };
