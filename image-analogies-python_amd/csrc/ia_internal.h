@@ -144,7 +144,8 @@ int screen_variant();
 // pipelined epilogue, bit 10 fragment-prefetch form, bit 11 keep the epilogue at
 // NQ = 3, bit 12 spanning form (bits 13 / 15: its no-copy diagnostics), bit 14 uneven
 // query shares, bit 16 double-buffered fragment registers,
-// bit 17 non-temporal DB stream, bit 18 balanced query shares
+// bit 17 non-temporal DB stream, bit 18 balanced query shares, bit 19
+// chain-balanced stages (9..11 query tiles)
 int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
                     int flags, hipStream_t st);
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query

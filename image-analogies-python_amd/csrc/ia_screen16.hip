@@ -21,6 +21,7 @@
 
 #include <float.h>
 #include <cstdlib>
+#include <type_traits>
 
 namespace ia {
 
@@ -668,6 +669,158 @@ __global__ __launch_bounds__(256, 2) void k_screen_h16b(const half8 *__restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------
+// chain-balanced form (default for G = 5..7 and 9..11 query tiles, flag 0x80000; one block
+// per chunk holds all G of them):
+// the 4G (query tile t, stage tile u) MFMA chains of a stage, in the order 4t + u, are
+// cut into 4 runs of G, one per wave.  Every wave issues the same G chains per stage, so
+// the per-stage barrier never waits for a lighter wave, and M = 342 computes 11 query
+// tiles instead of 12 (M = 171: 6 instead of 8).  A query tile cut between two waves has its per-segment minimum
+// combined through LDS (ordered-int ds_min, two copies alternating by segment); chunks
+// need segments of whole stages (tps >= 4).
+// ---------------------------------------------------------------------------------
+__host__ __device__ constexpr int bal_t0(int G, int W) { return (G * W) / 4; }
+__host__ __device__ constexpr int bal_ns(int G, int W) { return (G * W + G - 1) / 4 - (G * W) / 4 + 1; }
+__host__ __device__ constexpr bool bal_on(int G, int W, int k, int u) {
+    return 4 * (bal_t0(G, W) + k) + u >= G * W && 4 * (bal_t0(G, W) + k) + u < G * W + G;
+}
+__host__ __device__ constexpr bool bal_owner(int G, int W, int t) { return (4 * t) / G == W; }
+
+template <int K, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (K < N) {
+        f(std::integral_constant<int, K>{});
+        static_for<K + 1, N>(f);
+    }
+}
+__device__ __forceinline__ int fkey(float x) {
+    const int b = __float_as_int(x);
+    return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float fkey_inv(int b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
+
+template <int G, int W>
+__device__ __forceinline__ void bal_body(const half8 *__restrict__ db16, half8 *sbuf, int *xred,
+                                         long ctile0, int nstage, int tps, long seg0,
+                                         const half8 *__restrict__ q16, int M,
+                                         float *__restrict__ segmin, long nseg) {
+    constexpr int T0 = bal_t0(G, W), NS = bal_ns(G, W);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    half8 bq[NS][Q16_GROUPS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const half8 *p = q16 + (long)((T0 + k) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m) bq[k][m] = p[m];
+    }
+    auto issue = [&](int s, int buf) {
+        const half8 *src = db16 + (ctile0 + (long)s * STAGE_TILES) * TILE_H8 + tid;
+#pragma unroll
+        for (int k = 0; k < DB16_GROUPS; ++k)
+            __builtin_amdgcn_global_load_lds((const void *)(src + k * 256),
+                                             (void *)(sbuf + buf * STAGE_H8 + k * 256 + W * 64),
+                                             16, 0, 2);
+    };
+    auto stage_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    float mn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    const floatx16 zero = {};
+    issue(0, 0);
+    stage_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        const half8 *sb = sbuf + (s & 1) * STAGE_H8;
+        static_for<0, STAGE_TILES>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            half8 a[DB16_GROUPS];
+            const half8 *p = sb + u * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+            floatx16 acc[NS];
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u))
+                    acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[k][0], zero, 0, 0, 0);
+            });
+#pragma unroll
+            for (int m = 1; m < MFMA16; ++m)
+                static_for<0, NS>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (bal_on(G, W, k, u))
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[k][mfma_b(m)],
+                                                                         acc[k], 0, 0, 0);
+                });
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u)) {
+                    const floatx16 &x = acc[k];
+                    const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+                    const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+                    const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+                    const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+                    mn[k] = fminf(fminf(mn[k], u0), u1);
+                }
+            });
+        });
+        const int done = (s + 1) * STAGE_TILES;
+        const bool close = done % tps == 0;
+        const int sg = done / tps - 1;                 // segment (within the chunk) just closed
+        int *xr = xred + (sg & 1) * (G * 32);
+        if (close) {
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
+                if (h == 0) atomicMin(&xr[(T0 + k) * 32 + j], fkey(m));
+                mn[k] = FLT_MAX;
+            }
+        }
+        stage_barrier();
+        if (close) {
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_owner(G, W, T0 + k)) {
+                    if (h == 0) {
+                        const int at = (T0 + k) * 32 + j;
+                        const float m = fkey_inv(xr[at]);
+                        xr[at] = 0x7fffffff;
+                        const int qg = (T0 + k) * 32 + j;
+                        if (qg < M) segmin[(long)qg * nseg + seg0 + sg] = m;
+                    }
+                }
+            });
+        }
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(256, 2) void k_screen_h16c(const half8 *__restrict__ db16, int nchunks,
+                                                        int ch, int seg_rows,
+                                                        const half8 *__restrict__ q16, int M,
+                                                        float *__restrict__ segmin, long nseg) {
+    __shared__ half8 sbuf[2 * STAGE_H8];
+    __shared__ int xred[2 * G * 32];
+    const int b = blockIdx.x;
+    const int chunk = (b >> 3) * 8 + (b & 7);
+    if (chunk >= nchunks) return;
+    for (int i = threadIdx.x; i < 2 * G * 32; i += 256) xred[i] = 0x7fffffff;
+    const int tpc = ch >> 5;
+    const long ctile0 = (long)chunk * tpc;
+    const int nstage = tpc / STAGE_TILES;
+    const int tps = seg_rows >> 5;
+    const long seg0 = ctile0 * 32 / seg_rows;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) bal_body<G, 0>(db16, sbuf, xred, ctile0, nstage, tps, seg0, q16, M, segmin, nseg);
+    else if (wv == 1) bal_body<G, 1>(db16, sbuf, xred, ctile0, nstage, tps, seg0, q16, M, segmin, nseg);
+    else if (wv == 2) bal_body<G, 2>(db16, sbuf, xred, ctile0, nstage, tps, seg0, q16, M, segmin, nseg);
+    else bal_body<G, 3>(db16, sbuf, xred, ctile0, nstage, tps, seg0, q16, M, segmin, nseg);
+}
+
 static int h16_shared() {
     static int v = -1;
     if (v < 0) {
@@ -713,6 +866,27 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
 #undef IA_H16P_CASE
         set_error("launch_screen16: bad span split");
         return IA_E_ARG;
+    }
+    // chain-balanced form: the default for 5..7 and 9..11 query tiles (IA_SCREEN_BAL=0 turns
+    // it off; 8 and 12 split evenly anyway)
+    static const int bal_env = getenv("IA_SCREEN_BAL") ? atoi(getenv("IA_SCREEN_BAL")) : 1;
+    if (((flags & 0x80000) || (bal_env && flags == 0)) && T >= 5 && T <= 11 && T != 8 &&
+        seg_rows >= 4 * STAGE_TILES * 32) {
+        const long nb = ((nchunks + 7) / 8) * 8;
+#define IA_H16C_CASE(GG)                                                                        \
+        if (T == GG) {                                                                          \
+            k_screen_h16c<GG><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M, \
+                                                             segmin, nseg);                     \
+            IA_LAUNCH_CHECK("k_screen_h16c");                                                   \
+            return IA_OK;                                                                       \
+        }
+        IA_H16C_CASE(5)
+        IA_H16C_CASE(6)
+        IA_H16C_CASE(7)
+        IA_H16C_CASE(9)
+        IA_H16C_CASE(10)
+        IA_H16C_CASE(11)
+#undef IA_H16C_CASE
     }
     if ((flags & 0x40000) && T >= 4) {   // balanced shares (A/B)
         const int g = (T + 11) / 12;

@@ -145,7 +145,7 @@ def test_split16_screen_forms_agree(gpu):
     segmin = torch.empty((qrows, nseg), dtype=torch.float32, device='cuda')
     for M in (1, 20, 64, 100, 128, 192, 256, 342):
         outs = {}
-        for flags in (0x100, 0x000, 0x200, 0x400, 0x800, 0x001, 0x002, 0x003, 0x1000, 0x4000, 0x10000, 0x40000):
+        for flags in (0x100, 0x000, 0x200, 0x400, 0x800, 0x001, 0x002, 0x003, 0x1000, 0x4000, 0x10000, 0x40000, 0x80000):
             segmin.fill_(float('nan'))
             _ia.check(lib.ia_diag_screen16(_ia.ptr(idx.db), N, _ia.ptr(q16), M,
                                            _ia.ptr(segmin), flags, st), 'ia_diag_screen16')
