@@ -96,6 +96,7 @@ _SIGS = {
     'ia_comm_nranks': (ctypes.c_int, [_dp]),
     # diagnostics (include/ia_diag.h)
     'ia_diag_set_match_alg': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, ctypes.c_int,
@@ -141,6 +142,12 @@ def match_alg(alg=-1):
     """Select the exact matcher's screen for this process (0 per-lane top-K, 1 f32-MFMA
     segment minima, 2 split-f16 segment minima [default]); returns the previous value."""
     return lib().ia_diag_set_match_alg(int(alg))
+
+
+def rescore_mode(mode=-2):
+    """Select the exact stage's form for this process (0 per-query workgroups, 1 work list,
+    -1 default); returns the previous value."""
+    return lib().ia_diag_set_rescore_mode(int(mode))
 
 
 def check(rc, what):

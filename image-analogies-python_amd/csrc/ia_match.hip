@@ -1272,8 +1272,9 @@ __global__ __launch_bounds__(64) void k_gather(DbSrc src, const QSel *__restrict
     }
 }
 
+static int g_rescore_mode = -2;
 static int rescore_mode() {
-    static int v = -2;
+    int &v = g_rescore_mode;
     if (v == -2) {
         const char *e = getenv("IA_RESCORE");   // 0: per-query k_rescore, 1: work list
         v = e ? atoi(e) : -1;                   // default: see launch_match
@@ -1586,6 +1587,12 @@ int ia_diag_query_rows16(const double *q64, int M, const double *center, const f
 int ia_diag_set_match_alg(int alg) {
     const int prev = match_alg();
     if (alg >= 0 && alg <= 2) g_match_alg = alg;
+    return prev;
+}
+
+int ia_diag_set_rescore_mode(int mode) {
+    const int prev = rescore_mode();
+    if (mode >= -1 && mode <= 1) g_rescore_mode = mode;
     return prev;
 }
 

@@ -27,14 +27,23 @@ int ia_diag_screen(const float *db, long nrows, const float *qp, int M, void *ca
 
 /* split-f16 screen (the default matcher's stage 1): query rows in both
  * forms (qp as ia_diag_query_rows, q16 = ia_diag_qp_rows(M) x 256 B, zeroed by the caller;
- * amax from ia_db_build), and one k_screen_h16 launch -> segment minima (screen units).
- * maxnq: bits 0-3 cap on query tiles per wave (0 = default), bit 8 uniform groups. */
+ * amax from ia_db_build), and one split-f16 screen launch (ia_diag_screen16) -> segment
+ * minima (screen units).  Its flags select the form (0 = the default shape rule): bits 0-3
+ * cap on query tiles per wave, 0x100 per-wave form, 0x200 no pipelined epilogue, 0x400
+ * fragment prefetch, 0x800 pipelined epilogue at 3 tiles, 0x1000 spanning form (0x2000 /
+ * 0x8000 its no-copy diagnostics), 0x4000 uneven shares, 0x10000 double-buffered fragment
+ * registers, 0x20000 non-temporal DB stream, 0x40000 balanced shares, 0x80000 chain-balanced
+ * stages.  Every form writes bitwise the same minima (tests/test_gpu_split16.py). */
 int ia_diag_query_rows16(const double *q64, int M, const double *center, const float *amax,
                          float *qp, void *q16, double *nq, void *stream);
 /* select the exact matcher's screen for this process (overrides IA_MATCH_ALG): 0 per-lane
  * top-K (f32), 1 segment minima (f32 MFMA), 2 segment minima (split-f16 MFMA, default);
  * returns the previous value (a negative alg only queries it). */
 int ia_diag_set_match_alg(int alg);
+/* exact stage form for this process: 0 one workgroup per query (k_rescore), 1 the work list
+ * (k_select / k_items / k_gather), -1 the default (work list above 2^20 rows or when the
+ * per-pixel tail runs separately); other values leave it; returns the previous value */
+int ia_diag_set_rescore_mode(int mode);
 int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
                      int maxnq, void *stream);
 

@@ -172,6 +172,34 @@ def test_match_exact_with_either_screen(gpu, alg, which, scale):
         assert i == j and d == dd[j]
 
 
+@pytest.fixture
+def rescore():
+    import _ia
+    prev = _ia.rescore_mode()
+    yield _ia.rescore_mode
+    _ia.rescore_mode(prev)
+
+
+@pytest.mark.parametrize('mode', [0, 1])
+def test_synthesis_bit_exact_with_either_exact_stage(gpu, rescore, mode):
+    """Both forms of the exact stage (one workgroup per query with the fused tail, or the
+    work list k_select / k_items / k_gather with the tail in k_gather) give the oracle's
+    B', s and im."""
+    import image_analogies as ia
+    rescore(mode)
+    A, Aps, B = analogy_inputs(46, (52, 67), (44, 47), n_ap=2, flat=True)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=46)
+    w = o.compute_weights(3, 5, 12, 1)
+    ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 2.0, w)
+    Bp_dev = [dev(b) for b in Bp_pyr]
+    out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                            [dev(p) for p in B_pyr], Bp_dev, L, 2.0, w)
+    for l in ref:
+        assert np.array_equal(out[l][0].cpu().numpy(), ref[l][1]), l
+        assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
+        assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l
+
+
 @pytest.mark.parametrize('which', [1, 2])
 def test_synthesis_bit_exact_with_either_screen(gpu, alg, which):
     import image_analogies as ia
