@@ -97,6 +97,7 @@ _SIGS = {
     # diagnostics (include/ia_diag.h)
     'ia_diag_set_match_alg': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_graph_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, ctypes.c_int,
@@ -148,6 +149,12 @@ def rescore_mode(mode=-2):
     """Select the exact stage's form for this process (0 per-query workgroups, 1 work list,
     -1 default); returns the previous value."""
     return lib().ia_diag_set_rescore_mode(int(mode))
+
+
+def graph_mode(mode=-1):
+    """HIP-graph capture of the synthesis wave loop for this process (0 off [default],
+    1 levels <= 2^18 rows, 2 all single-GPU levels); returns the previous value."""
+    return lib().ia_diag_set_graph_mode(int(mode))
 
 
 def check(rc, what):

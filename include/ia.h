@@ -170,8 +170,10 @@ typedef struct {
      * (see flags) are not timed. */
     double *prof;
     const IaLsh *lsh;   /* NULL: exact matcher; else LSH tables of this shard's rows */
-    /* IA_SYNTH_EAGER: never capture the wave loop into a HIP graph.  By default a level
-     * of <= 2^18 rows on one GPU (launch-bound) is captured and launched as one graph. */
+    /* IA_SYNTH_EAGER: never capture the wave loop into a HIP graph.  Capture is off by
+     * default (a graph's instantiation costs more than it saves on every c4 level); the
+     * environment variable IA_GRAPH=1 captures levels of <= 2^18 rows on one GPU, =2 every
+     * single-GPU level. */
     int flags;
 } IaSynthArgs;
 #define IA_SYNTH_EAGER 1

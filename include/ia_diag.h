@@ -44,6 +44,10 @@ int ia_diag_set_match_alg(int alg);
  * (k_select / k_items / k_gather), -1 the default (work list above 2^20 rows or when the
  * per-pixel tail runs separately); other values leave it; returns the previous value */
 int ia_diag_set_rescore_mode(int mode);
+/* HIP-graph capture of ia_synth_level's wave loop for this process (overrides IA_GRAPH):
+ * 0 off, 1 levels of <= 2^18 rows, 2 every single-GPU level; other values leave it;
+ * returns the previous value */
+int ia_diag_set_graph_mode(int mode);
 int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
                      int maxnq, void *stream);
 

@@ -180,13 +180,23 @@ def rescore():
     _ia.rescore_mode(prev)
 
 
+@pytest.fixture
+def graph():
+    import _ia
+    prev = _ia.graph_mode()
+    yield _ia.graph_mode
+    _ia.graph_mode(prev)
+
+
+@pytest.mark.parametrize('gmode', [0, 2])
 @pytest.mark.parametrize('mode', [0, 1])
-def test_synthesis_bit_exact_with_either_exact_stage(gpu, rescore, mode):
+def test_synthesis_bit_exact_with_either_exact_stage(gpu, rescore, graph, mode, gmode):
     """Both forms of the exact stage (one workgroup per query with the fused tail, or the
-    work list k_select / k_items / k_gather with the tail in k_gather) give the oracle's
-    B', s and im."""
+    work list k_select / k_items / k_gather with the tail in k_gather), launched eagerly or
+    from a captured HIP graph, give the oracle's B', s and im."""
     import image_analogies as ia
     rescore(mode)
+    graph(gmode)
     A, Aps, B = analogy_inputs(46, (52, 67), (44, 47), n_ap=2, flat=True)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=46)
     w = o.compute_weights(3, 5, 12, 1)
