@@ -6,63 +6,88 @@
 
 namespace ia {
 
+// the coherence candidate of one query pixel (coh_pick)
+struct CohSel {
+    long long wix;       // winning candidate's DB row
+    int wr, wc, wim;     // its pixel and A' image
+    int valid;           // 0: no candidate (first pixel of the level, or none in range)
+    double dcoh;         // its weighted distance to the query
+};
+
 __device__ __forceinline__ void fin_best(double &bd, long long &bi, double d, long long i) {
     if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
 }
 
-// Executed by ONE 64-lane wave for query pixel m of wave t, given the exact approximate-
-// match winner app (global row) and the query in qs (LDS, IA_DP doubles):
-// best_coherence_match (algorithms.py:92-130) over the causal 3x5 window (lanes 0..14 =
-// the reference's product(rows, cols) order), the kappa test (image_analogies.py:200-211)
-// and the B' / s / im update (:213-217).
-__device__ __forceinline__ void finish_pixel(const DbSrc &src, long long app, int m,
-                                             const FinishArgs &f, const double *qs, int lane) {
+// Coherence half of the tail, executed by ONE 64-lane wave for query pixel m of wave t
+// (query in qs, LDS): best_coherence_match (algorithms.py:92-130) over the causal 3x5
+// window (lanes 0..14 = the reference's product(rows, cols) order) and the weighted
+// distance of its winner (algorithms.py:133-135).  Needs only s / im of earlier waves.
+// Result valid in every lane.
+__device__ __forceinline__ CohSel coh_pick(const DbSrc &src, int m, const FinishArgs &f,
+                                           const double *qs, int lane) {
+    CohSel r{0, 0, 0, 0, 0, 0.0};
     const int y = f.y_lo + m, x = f.t - 3 * y;
+    if (y == 0 && x == 0) return r;
     const int W = f.W;
     const int Ah = src.A.h, Aw = src.A.w;
+    double cd = INFINITY;
+    long long cl = 0x7fffffffffffffffLL;
+    long cix = -1;
+    int cr = 0, cc = 0, cim = 0;
+    if (lane < 15) {
+        const int rr = y - 2 + lane / 5, rc = x - 2 + lane % 5;
+        if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
+            const long sidx = (long)rr * W + rc;
+            const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
+            if (sr >= 0 && sr < Ah && sc >= 0 && sc < Aw) {
+                const int simg = f.im[sidx];
+                cix = ((long)Ah * simg + sr) * Aw + sc;
+                cr = sr; cc = sc; cim = simg;
+                cd = sqrt(row_dist2(src, cix, qs));
+                cl = lane;
+            }
+        }
+    }
+    double bd = cd;
+    long long bl = cl;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o);
+        const long long ol = __shfl_xor(bl, o);
+        fin_best(bd, bl, od, ol);
+    }
+    if (bl == 0x7fffffffffffffffLL) return r;
+    const int win = (int)bl;
+    r.wix = __shfl(cix, win);
+    r.wr = __shfl(cr, win);
+    r.wc = __shfl(cc, win);
+    r.wim = __shfl(cim, win);
+    r.valid = 1;
+    double d = 0.0;
+    if (lane == 1) d = row_wdist(src, r.wix, qs, f.weights);
+    r.dcoh = __shfl(d, 1);
+    return r;
+}
+
+// The rest of the tail for the exact-match winner app (global row): the kappa test
+// (image_analogies.py:200-211) against the coherence candidate c, and the B' / s / im
+// update (:213-217).
+__device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, int m,
+                                             const FinishArgs &f, const CohSel &c,
+                                             const double *qs, int lane) {
+    const int y = f.y_lo + m, x = f.t - 3 * y;
+    const int W = f.W;
+    const int Aw = src.A.w;
     const long hw = src.hw;
     if (app < 0 || app >= f.N_total) app = 0;   // unreachable: every search has a winner
     long img = app / hw;
     long rem = app - img * hw;
     int pr = (int)(rem / Aw), pc = (int)(rem - (long)(rem / Aw) * Aw);
-
-    if (y != 0 || x != 0) {
-        double cd = INFINITY;
-        long long cl = 0x7fffffffffffffffLL;
-        long cix = -1;
-        int cr = 0, cc = 0, cim = 0;
-        if (lane < 15) {
-            const int rr = y - 2 + lane / 5, rc = x - 2 + lane % 5;
-            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
-                const long sidx = (long)rr * W + rc;
-                const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
-                if (sr >= 0 && sr < Ah && sc >= 0 && sc < Aw) {
-                    const int simg = f.im[sidx];
-                    cix = ((long)Ah * simg + sr) * Aw + sc;
-                    cr = sr; cc = sc; cim = simg;
-                    cd = sqrt(row_dist2(src, cix, qs));
-                    cl = lane;
-                }
-            }
-        }
-        double bd = cd;
-        long long bl = cl;
-        for (int o = 32; o > 0; o >>= 1) {
-            const double od = __shfl_xor(bd, o);
-            const long long ol = __shfl_xor(bl, o);
-            fin_best(bd, bl, od, ol);
-        }
-        if (bl != 0x7fffffffffffffffLL) {
-            const int win = (int)bl;
-            const long wix = __shfl(cix, win);
-            const int wr = __shfl(cr, win), wc = __shfl(cc, win), wim = __shfl(cim, win);
-            // lane 0: d_app, lane 1: d_coh (one inlined copy of the gather)
-            double d = 0.0;
-            if (lane < 2) d = row_wdist(src, lane == 0 ? app : wix, qs, f.weights);
-            const double d_app = __shfl(d, 0), d_coh = __shfl(d, 1);
-            if (d_coh <= d_app * f.kappa_factor) {
-                pr = wr; pc = wc; img = wim;
-            }
+    if (c.valid) {
+        double d = 0.0;
+        if (lane == 0) d = row_wdist(src, app, qs, f.weights);
+        const double d_app = __shfl(d, 0);
+        if (c.dcoh <= d_app * f.kappa_factor) {
+            pr = c.wr; pc = c.wc; img = c.wim;
         }
     }
     if (lane == 0) {
@@ -72,6 +97,15 @@ __device__ __forceinline__ void finish_pixel(const DbSrc &src, long long app, in
         f.s[2 * q + 1] = pc;
         f.im[q] = (int32_t)img;
     }
+}
+
+// The whole tail for query pixel m (one wave).  (Picking the coherence candidate ahead, on a
+// side stream beside the screen, measured 5 % slower on c4: the per-wave cross-stream
+// event waits cost more than the two gather rounds they hide.)
+__device__ __forceinline__ void finish_pixel(const DbSrc &src, long long app, int m,
+                                             const FinishArgs &f, const double *qs, int lane) {
+    const CohSel c = coh_pick(src, m, f, qs, lane);
+    finish_apply(src, app, m, f, c, qs, lane);
 }
 
 }  // namespace ia

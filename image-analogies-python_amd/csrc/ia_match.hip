@@ -1242,32 +1242,44 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
     }
 }
 
+// FIN: two waves — wave 1 picks the coherence candidate (two gather rounds that need only
+// s / im of earlier waves) while wave 0 reduces the items; then wave 0 finishes the pixel
 template <bool FIN>
-__global__ __launch_bounds__(64) void k_gather(DbSrc src, const QSel *__restrict__ sel,
-                                               const Best *__restrict__ ibest, int *ctr,
-                                               Best *__restrict__ best, FinishArgs fa,
-                                               const double *__restrict__ q64) {
+__global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restrict__ sel,
+                                                const Best *__restrict__ ibest, int *ctr,
+                                                Best *__restrict__ best, FinishArgs fa,
+                                                const double *__restrict__ q64) {
     __shared__ double qs[IA_DP];
+    __shared__ CohSel cs;
     const int m = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (FIN && lane < IA_DP) qs[lane] = q64[(long)m * IA_DP + lane];
-    const QSel r = sel[m];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (FIN) {
+        if (threadIdx.x < IA_DP) qs[threadIdx.x] = q64[(long)m * IA_DP + threadIdx.x];
+        __syncthreads();
+        if (wv == 1) {
+            const CohSel c = coh_pick(src, m, fa, qs, lane);
+            if (lane == 0) cs = c;
+        }
+    }
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
-    for (int i = lane; i < r.count; i += 64) {
-        const Best b = ibest[r.base + i];
-        best_update(bd, bi, b.d, b.idx);
+    if (wv == 0) {
+        const QSel r = sel[m];
+        for (int i = lane; i < r.count; i += 64) {
+            const Best b = ibest[r.base + i];
+            best_update(bd, bi, b.d, b.idx);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o);
+            const long long oi = __shfl_xor(bi, o);
+            best_update(bd, bi, od, oi);
+        }
+        if (m == 0 && lane == 0) *ctr = 0;   // every k_items block has read it
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const double od = __shfl_xor(bd, o);
-        const long long oi = __shfl_xor(bi, o);
-        best_update(bd, bi, od, oi);
-    }
-    if (m == 0 && lane == 0) *ctr = 0;   // every k_items block has read it
     if (FIN) {
         __syncthreads();
-        finish_pixel(src, bi, m, fa, qs, lane);
-    } else if (lane == 0) {
+        if (wv == 0) finish_apply(src, bi, m, fa, cs, qs, lane);
+    } else if (wv == 0 && lane == 0) {
         best[m] = Best{bd, bi};
     }
 }
@@ -1417,7 +1429,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
                                       q64, ws.ibest, stats);
         IA_LAUNCH_CHECK("k_items");
         if (fin)
-            k_gather<true><<<M, 64, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+            k_gather<true><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
         else
             k_gather<false><<<M, 64, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
         IA_LAUNCH_CHECK("k_gather");

@@ -25,23 +25,31 @@
 
 namespace ia {
 
-// one wave per query pixel: the lexicographic (dist, row) minimum over the shards'
-// exact winners, then the shared per-pixel tail (ia_finish.h)
-__global__ __launch_bounds__(64) void k_finish(DbSrc src, const Best *__restrict__ best_all,
-                                               int nranks, int M, FinishArgs f,
-                                               const double *__restrict__ q64) {
+// two waves per query pixel: wave 1 picks the coherence candidate while wave 0 takes the
+// lexicographic (dist, row) minimum over the shards' exact winners; then wave 0 runs the
+// rest of the shared per-pixel tail (ia_finish.h)
+__global__ __launch_bounds__(128) void k_finish(DbSrc src, const Best *__restrict__ best_all,
+                                                int nranks, int M, FinishArgs f,
+                                                const double *__restrict__ q64) {
     __shared__ double qs[IA_DP];
+    __shared__ CohSel cs;
     const int m = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (lane < IA_DP) qs[lane] = q64[(long)m * IA_DP + lane];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x < IA_DP) qs[threadIdx.x] = q64[(long)m * IA_DP + threadIdx.x];
     __syncthreads();
     double ad = INFINITY;
     long long app = 0x7fffffffffffffffLL;
-    for (int g = 0; g < nranks; ++g) {
-        const Best b = best_all[(long)g * M + m];
-        fin_best(ad, app, b.d, b.idx);
+    if (wv == 1) {
+        const CohSel c = coh_pick(src, m, f, qs, lane);
+        if (lane == 0) cs = c;
+    } else {
+        for (int g = 0; g < nranks; ++g) {
+            const Best b = best_all[(long)g * M + m];
+            fin_best(ad, app, b.d, b.idx);
+        }
     }
-    finish_pixel(src, app, m, f, qs, lane);
+    __syncthreads();
+    if (wv == 0) finish_apply(src, app, m, f, cs, qs, lane);
 }
 
 // -------------------------------- workspace ----------------------------------------
@@ -226,7 +234,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
             if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, sq))) return rc;
             ball = ws.best_all;
         }
-        k_finish<<<M, 64, 0, sq>>>(src, ball, nranks, M, fa, ws.q64);
+        k_finish<<<M, 128, 0, sq>>>(src, ball, nranks, M, fa, ws.q64);
         IA_LAUNCH_CHECK("k_finish");
     }
     return IA_OK;
