@@ -6,15 +6,15 @@ namespace ia {
 
 // ---- database chunking (shared by ia_db_build and the screen) -------------------
 // A screen workgroup owns one chunk of CH rows: 4 waves x (CH/4) rows, 32-row tiles.
-// CH is chosen so a DB produces ~1024 chunks (>= 4 workgroups per CU per query group).
+// CH is chosen so a DB produces ~target_chunks(N) chunks (512 or 1024).
 constexpr int SCREEN_K = 4;            // candidates kept per (query, chunk)
-// ~chunks per database: IA_TARGET_CHUNKS (read once per process, default 1024; a
-// tuning knob for tools/screen_bench — the DB build and the screen must agree on it)
-int target_chunks();
+// ~chunks per database: IA_TARGET_CHUNKS (read once per process; default 512 for
+// 2^19 <= rows < 2^21, 1024 otherwise; a tuning knob for tools/screen_bench — the DB build and the screen must agree on it)
+int target_chunks(long nrows);
 
 // tiles per wave: a power of two in [1, 64] (so screen segments divide it)
 static inline int db_chunk_rows(long nrows) {
-    const long tc = target_chunks();
+    const long tc = target_chunks(nrows);
     const long want = (nrows + tc * 128 - 1) / (tc * 128);
     long tpw = 1;
     while (tpw < want && tpw < 64) tpw <<= 1;

@@ -11,14 +11,18 @@
 
 namespace ia {
 
-int target_chunks() {
+int target_chunks(long nrows) {
     static int tc = -1;
     if (tc < 0) {
         const char *e = getenv("IA_TARGET_CHUNKS");
-        tc = e ? atoi(e) : 1024;
-        if (tc < 64 || tc > 65536) tc = 1024;
+        tc = e ? atoi(e) : 0;
+        if (tc != 0 && (tc < 64 || tc > 65536)) tc = 0;
     }
-    return tc;
+    if (tc) return tc;
+    // default: 512 chunks (one per screen slot at 2 blocks per CU) for 2^19 <= rows < 2^21
+    // (a sharded c4 rank at 4-8 GPUs, the single-GPU level 4): measured 4-10 % faster than
+    // 1024 there (profiles/r01_screen_bench_shard_sizes.txt); 1024 otherwise
+    return (nrows >= (1L << 19) && nrows < (1L << 21)) ? 512 : 1024;
 }
 
 

@@ -871,7 +871,7 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
     // it off; 8 and 12 split evenly anyway)
     static const int bal_env = getenv("IA_SCREEN_BAL") ? atoi(getenv("IA_SCREEN_BAL")) : 1;
     if (((flags & 0x80000) || (bal_env && flags == 0)) && T >= 5 && T <= 11 && T != 8 &&
-        seg_rows >= 4 * STAGE_TILES * 32) {
+        seg_rows >= STAGE_TILES * 32) {   // segments of whole stages (tps >= 4)
         const long nb = ((nchunks + 7) / 8) * 8;
 #define IA_H16C_CASE(GG)                                                                        \
         if (T == GG) {                                                                          \

@@ -1,0 +1,57 @@
+"""Per-rank cost of the sharded c4 synthesis, simulated on one GPU (diagnostic).
+
+Runs the synthesis as rank `r` of G database shards (each level's rows
+`shard_rows(N, r, G)`), with a 1-rank RCCL communicator: the per-wave path is the
+sharded one (unfused exact stage, all-gather, k_finish), but the all-gather moves one
+shard's winners only, so the time excludes the real collective's xGMI latency.  The
+winners are this shard's, so B' differs from the real result: timing only.
+Per level wall time between torch.cuda.synchronize() calls, second repetition reported.
+
+Usage: python tools/shard_sim.py G [G ...]        (G = 1 runs the sharded path unsharded)
+"""
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import torch  # noqa: E402
+
+ip, cfg, ia, _ia = bench.ip, bench.cfg, bench.ia, bench._ia
+
+
+def one_rank_comm():
+    buf = ctypes.create_string_buffer(128)
+    _ia.check(_ia.lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
+    h = ctypes.c_void_p()
+    _ia.check(_ia.lib().ia_comm_init(buf.raw, 1, 0, ctypes.byref(h)), 'ia_comm_init')
+    return h
+
+
+def main():
+    gs = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8]
+    job = bench.Job(bench.CONFIGS['c4'], 0, 'cuda:0')
+    A_pyr = ip.gaussian_pyramid_dev(job.A, cfg.n_sm, job.levels)
+    Ap_pyr = ip.gaussian_pyramid_dev(job.Ap, cfg.n_sm, job.levels)
+    B_pyr = ip.gaussian_pyramid_dev(job.B, cfg.n_sm, job.levels)
+    comm = one_rank_comm()
+    for G in gs:
+        res = {}
+        for rep in range(2):
+            for level in range(1, job.max_levels):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, job.Bp, job.max_levels, job.k,
+                                  job.weights, comm=comm, rank=0, nranks=G, levels={level})
+                torch.cuda.synchronize()
+                res[level] = (time.perf_counter() - t0) * 1e3
+        tot = sum(res.values())
+        print('G=%d rank0 %.1f ms/step ' % (G, tot) +
+              ' '.join('L%d %.1f' % (l, t) for l, t in sorted(res.items())), flush=True)
+    _ia.lib().ia_comm_destroy(comm)
+
+
+if __name__ == '__main__':
+    main()
