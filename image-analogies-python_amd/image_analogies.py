@@ -9,7 +9,8 @@ exact matcher, or the LSH matcher with ``c.matcher = 'lsh'``) with the pyramids,
 
 ``synthesize_dev`` is the device-level entry used by bench.py and the parity tests:
 device pyramids in, per-level (s, im) index maps out, B' pyramid updated in place;
-with ``comm`` it shards every level's database over the ranks (RCCL all-gather per wave).
+with ``comm`` it shards the databases of the large levels over the ranks (RCCL all-gather
+per wave) and synthesises the small ones on every rank alone (``shard_level``).
 """
 import ctypes
 import os
@@ -35,6 +36,27 @@ def shard_rows(N, rank, nranks):
     """Contiguous row range of one rank: [N*r/G, N*(r+1)/G)."""
     r0 = N * rank // nranks
     return r0, N * (rank + 1) // nranks - r0
+
+
+def shard_min_rows():
+    """Smallest level database (rows) that is sharded over the ranks (IA_SHARD_MIN_ROWS,
+    default 2**19).  Below it every rank synthesises the level alone from its replicated
+    state with the fused single-GPU path: a sharded rank still pays the whole per-wave
+    fixed cost (query gather, exact stage, tail) plus one RCCL all-gather per wave, which
+    on c4's 64-256 px levels exceeds the screen time sharding saves."""
+    return int(os.environ.get('IA_SHARD_MIN_ROWS', 1 << 19))
+
+
+def shard_level(N, nranks):
+    """True when a level with an N-row database is sharded over nranks ranks.  A 1-rank
+    communicator always takes the exchange path (that is how the RCCL path is tested on
+    one GPU)."""
+    return nranks == 1 or N >= shard_min_rows()
+
+
+def level_rows(Ap_pyr_list, level):
+    """Rows of a level's database: n_A' x H x W of A' at that level (algorithms.py:63-67)."""
+    return sum(p[level].shape[0] * p[level].shape[1] for p in Ap_pyr_list)
 
 
 def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
@@ -84,18 +106,19 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     matcher) or LevelIndex.build_lsh arguments (approximate matcher).
     Returns {level: (s, im)} device tensors."""
     w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
-    row_range = None
-    if comm is not None:
-        row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
     out = {}
     t_start = time.time()
     for level in range(1, max_levels):
         if levels is not None and level not in levels:
             continue
+        lcomm, row_range = None, None
+        if comm is not None and shard_level(level_rows(Ap_pyr_list, level), nranks):
+            lcomm = comm
+            row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
         index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range, lsh)
         out[level] = synthesize_level_dev(level, max_levels, index, B_pyr[level - 1],
                                           B_pyr[level], Bp_pyr[level - 1], Bp_pyr[level], w,
-                                          k, comm, prof, eager)
+                                          k, lcomm, prof, eager)
         del index
         if os.environ.get('IA_VERBOSE'):
             torch.cuda.synchronize()

@@ -208,3 +208,18 @@ def test_branch_free_symmetric_index_equals_period_map():
     for n in range(1, 12):
         for i in range(-2, n + 2):
             assert symi2(i, n) == o.sym_index(i, n), (i, n)
+
+
+def test_shard_level_policy(monkeypatch):
+    """Levels below IA_SHARD_MIN_ROWS run replicated on every rank; a 1-rank communicator
+    always takes the exchange path; c4's level databases: only the 1 M and 4 M-row levels
+    are sharded by default."""
+    from image_analogies import level_rows, shard_level
+    monkeypatch.delenv('IA_SHARD_MIN_ROWS', raising=False)
+    c4 = [128 * 128, 256 * 256, 512 * 512, 1024 * 1024, 2048 * 2048]
+    assert [shard_level(n, 8) for n in c4] == [False, False, False, True, True]
+    assert all(shard_level(n, 1) for n in c4)
+    monkeypatch.setenv('IA_SHARD_MIN_ROWS', '0')
+    assert all(shard_level(n, 4) for n in c4)
+    pyr = [[np.zeros((2, 3)), np.zeros((4, 6))], [np.zeros((2, 3)), np.zeros((4, 6))]]
+    assert level_rows(pyr, 1) == 2 * 24
