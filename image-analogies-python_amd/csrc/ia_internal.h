@@ -32,10 +32,12 @@ template <typename T>
 static inline T *db16_of(T *db, long nrows) {
     return db + (size_t)db_rows_padded(nrows) * IA_DP * 4 / sizeof(T);
 }
-// segment-minimum matcher: one running minimum per (query, segment) of <= 512 rows
+// segment-minimum matcher: one running minimum per (query, segment) of <= seg_rows_max()
+// rows (IA_SEG_MAX, read once per process: 512 [default] or 256)
+int seg_rows_max();
 static inline int db_seg_rows(long nrows) {
-    const int rpw = db_chunk_rows(nrows) / 4;
-    return rpw < 512 ? rpw : 512;
+    const int rpw = db_chunk_rows(nrows) / 4, cap = seg_rows_max();
+    return rpw < cap ? rpw : cap;
 }
 static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_rows(nrows); }
 

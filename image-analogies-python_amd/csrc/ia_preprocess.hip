@@ -11,6 +11,16 @@
 
 namespace ia {
 
+int seg_rows_max() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("IA_SEG_MAX");
+        v = e ? atoi(e) : 512;
+        if (v != 256 && v != 512) v = 512;
+    }
+    return v;
+}
+
 int target_chunks(long nrows) {
     static int tc = -1;
     if (tc < 0) {
