@@ -68,27 +68,35 @@ __device__ __forceinline__ CohSel coh_pick(const DbSrc &src, int m, const Finish
     return r;
 }
 
-// The rest of the tail for the exact-match winner app (global row): the kappa test
-// (image_analogies.py:200-211) against the coherence candidate c, and the B' / s / im
-// update (:213-217).
+// Weighted distance of the exact-match winner app (algorithms.py:133-135) for the kappa
+// test: one gather round by lane 0, valid in every lane.  Runs beside coh_pick (another
+// wave), so the tail's critical path is max(exact winner + 1 round, coh_pick's 2 rounds).
+__device__ __forceinline__ long long app_clamp(long long app, const FinishArgs &f) {
+    return (app < 0 || app >= f.N_total) ? 0 : app;   // unreachable: every search has a winner
+}
+__device__ __forceinline__ double app_wdist(const DbSrc &src, long long app, const FinishArgs &f,
+                                            const double *qs, int lane) {
+    double d = 0.0;
+    if (lane == 0) d = row_wdist(src, app_clamp(app, f), qs, f.weights);
+    return __shfl(d, 0);
+}
+
+// The rest of the tail: the kappa test (image_analogies.py:200-211) of the coherence
+// candidate c against the exact-match winner app (weighted distance d_app, app_wdist), and
+// the B' / s / im update (:213-217).
 __device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, int m,
-                                             const FinishArgs &f, const CohSel &c,
-                                             const double *qs, int lane) {
+                                             const FinishArgs &f, const CohSel &c, double d_app,
+                                             int lane) {
     const int y = f.y_lo + m, x = f.t - 3 * y;
     const int W = f.W;
     const int Aw = src.A.w;
     const long hw = src.hw;
-    if (app < 0 || app >= f.N_total) app = 0;   // unreachable: every search has a winner
+    app = app_clamp(app, f);
     long img = app / hw;
     long rem = app - img * hw;
     int pr = (int)(rem / Aw), pc = (int)(rem - (long)(rem / Aw) * Aw);
-    if (c.valid) {
-        double d = 0.0;
-        if (lane == 0) d = row_wdist(src, app, qs, f.weights);
-        const double d_app = __shfl(d, 0);
-        if (c.dcoh <= d_app * f.kappa_factor) {
-            pr = c.wr; pc = c.wc; img = c.wim;
-        }
+    if (c.valid && c.dcoh <= d_app * f.kappa_factor) {
+        pr = c.wr; pc = c.wc; img = c.wim;
     }
     if (lane == 0) {
         const long q = (long)y * W + x;
@@ -99,13 +107,9 @@ __device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, in
     }
 }
 
-// The whole tail for query pixel m (one wave).  (Picking the coherence candidate ahead, on a
-// side stream beside the screen, measured 5 % slower on c4: the per-wave cross-stream
-// event waits cost more than the two gather rounds they hide.)
-__device__ __forceinline__ void finish_pixel(const DbSrc &src, long long app, int m,
-                                             const FinishArgs &f, const double *qs, int lane) {
-    const CohSel c = coh_pick(src, m, f, qs, lane);
-    finish_apply(src, app, m, f, c, qs, lane);
-}
+// The tail kernels run coh_pick on one wave and app_wdist + finish_apply on another.
+// (Picking the coherence candidate ahead, on a side stream beside the screen, measured 5 %
+// slower on c4: the per-wave cross-stream event waits cost more than the two gather rounds
+// they hide.)
 
 }  // namespace ia

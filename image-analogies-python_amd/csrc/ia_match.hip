@@ -876,6 +876,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
                                                  int probe) {
     __shared__ int slist[RESCORE_SEGCAP];
     __shared__ long long win;
+    __shared__ CohSel cs;
     __shared__ int scount;
     __shared__ float redf[4];
     __shared__ double redd[4];
@@ -1062,9 +1063,18 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
             atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
-    if (FIN) {
+    if (FIN) {   // wave 1 picks the coherence candidate while wave 0 weighs the winner
         __syncthreads();
-        if (tid < 64) finish_pixel(src, win, q, fa, qs, tid);
+        const int wv = tid >> 6, lane = tid & 63;
+        double d_app = 0.0;
+        if (wv == 1) {
+            const CohSel c = coh_pick(src, q, fa, qs, lane);
+            if (lane == 0) cs = c;
+        } else if (wv == 0) {
+            d_app = app_wdist(src, win, fa, qs, lane);
+        }
+        __syncthreads();
+        if (wv == 0) finish_apply(src, win, q, fa, cs, d_app, lane);
         IA_PROBE_MARK(6);
     }
 }
@@ -1277,8 +1287,9 @@ __global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restric
         if (m == 0 && lane == 0) *ctr = 0;   // every k_items block has read it
     }
     if (FIN) {
+        const double d_app = wv == 0 ? app_wdist(src, bi, fa, qs, lane) : 0.0;
         __syncthreads();
-        if (wv == 0) finish_apply(src, bi, m, fa, cs, qs, lane);
+        if (wv == 0) finish_apply(src, bi, m, fa, cs, d_app, lane);
     } else if (wv == 0 && lane == 0) {
         best[m] = Best{bd, bi};
     }

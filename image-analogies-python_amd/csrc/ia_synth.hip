@@ -48,8 +48,9 @@ __global__ __launch_bounds__(128) void k_finish(DbSrc src, const Best *__restric
             fin_best(ad, app, b.d, b.idx);
         }
     }
+    const double d_app = wv == 0 ? app_wdist(src, app, f, qs, lane) : 0.0;
     __syncthreads();
-    if (wv == 0) finish_apply(src, app, m, f, cs, qs, lane);
+    if (wv == 0) finish_apply(src, app, m, f, cs, d_app, lane);
 }
 
 // -------------------------------- workspace ----------------------------------------
