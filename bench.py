@@ -44,9 +44,11 @@ F16_MFMA_PEAK_TFLOPS = 4096 * 256 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 # HBM traffic of one finest-level screen launch, from rocprofv3 PMC (FETCH_SIZE x 2 on
 # gfx950 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench at M = 342 queries
-# against the 4,194,304-row c4 database (profiles/r01_screen_h16s_pmc_m342.txt)
-SCREEN_PMC = {'fetch_kb': 4.592e5, 'write_kb': 5.503e4, 'M': 342, 'rows': 4194304,
-              'source': 'profiles/r01_screen_h16s_pmc_m342_nt.txt'}
+# against the 4,194,304-row c4 database: the chain-balanced k_screen_h16c<11>
+# (profiles/r01_end_screen_pmc_m342.txt; WRITE_SIZE 88 MB vs 11 MB of segment minima: 4-B
+# writes strided by the segment count, each likely a partial-line write)
+SCREEN_PMC = {'fetch_kb': 4.593e5, 'write_kb': 8.57e4, 'M': 342, 'rows': 4194304,
+              'source': 'profiles/r01_end_screen_pmc_m342.txt'}
 
 CONFIGS = {
     'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),
@@ -287,7 +289,7 @@ def main():
     if split:
         # split-f16 screen: 3 f16 products (a_h q_h + a_h q_l + a_l q_h) of 2 flop per
         # feature per (query, row) pair on v_mfma_f32_32x32x16_f16
-        per_pair, peak, kname = 3 * 2 * 55, F16_MFMA_PEAK_TFLOPS, 'k_screen_h16s'
+        per_pair, peak, kname = 3 * 2 * 55, F16_MFMA_PEAK_TFLOPS, 'k_screen_h16c/h16s'
     else:
         per_pair, peak, kname = 2 * 55, FP32_MFMA_PEAK_TFLOPS, 'k_screen_seg'
     achieved = per_pair * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
