@@ -867,10 +867,11 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
         set_error("launch_screen16: bad span split");
         return IA_E_ARG;
     }
-    // chain-balanced form: the default for 5..7 and 9..11 query tiles (IA_SCREEN_BAL=0 turns
-    // it off; 8 and 12 split evenly anyway)
+    // chain-balanced form: the default for 3, 5..7 and 9..11 query tiles (IA_SCREEN_BAL=0
+    // turns it off; 4, 8 and 12 split evenly anyway; T = 3: 8-10 % faster than 4 x 1 tiles,
+    // profiles/r01_screen_bench_h16c_t3.txt)
     static const int bal_env = getenv("IA_SCREEN_BAL") ? atoi(getenv("IA_SCREEN_BAL")) : 1;
-    if (((flags & 0x80000) || (bal_env && flags == 0)) && T >= 5 && T <= 11 && T != 8 &&
+    if (((flags & 0x80000) || (bal_env && flags == 0)) && T >= 3 && T <= 11 && T != 4 && T != 8 &&
         seg_rows >= STAGE_TILES * 32) {   // segments of whole stages (tps >= 4)
         const long nb = ((nchunks + 7) / 8) * 8;
 #define IA_H16C_CASE(GG)                                                                        \
@@ -880,6 +881,7 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
             IA_LAUNCH_CHECK("k_screen_h16c");                                                   \
             return IA_OK;                                                                       \
         }
+        IA_H16C_CASE(3)
         IA_H16C_CASE(5)
         IA_H16C_CASE(6)
         IA_H16C_CASE(7)
