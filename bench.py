@@ -197,6 +197,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
     ap.add_argument('--jobs', type=int, default=4, help='c5: jobs per GPU per step')
+    ap.add_argument('--streams', type=int, default=4,
+                    help='c5: jobs run concurrently per GPU (one HIP stream + host thread each; '
+                         '4 = the HIP hardware queues per process)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--matcher', default='brute', choices=['brute', 'lsh'],
@@ -226,9 +229,34 @@ def main():
     else:
         jobs = [Job(conf, 0, dev, lsh)]
 
+    # c5: --streams S runs the GPU's jobs S at a time, each on its own HIP stream driven by
+    # its own host thread (ctypes drops the GIL inside ia_synth_level, so the threads enqueue
+    # their latency-bound waves concurrently); results are per job and stream-independent
+    nstreams = max(1, min(args.streams, len(jobs))) if args.config == 'c5' else 1
+    pool = streams = None
+    if nstreams > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(nstreams)
+        streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+
+    def run_jobs(fn):
+        if pool is None:
+            return [fn(jb) for jb in jobs]
+        main = torch.cuda.current_stream(dev)
+
+        def lane(i):
+            torch.cuda.set_device(dev)
+            st = streams[i]
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                return [fn(jb) for jb in jobs[i::nstreams]]
+        res = list(pool.map(lane, range(nstreams)))
+        for st in streams:
+            main.wait_stream(st)
+        return [r for part in res for r in part]
+
     def run_step(prof=None):
-        for jb in jobs:
-            jb.step(comm, rank, world, prof)
+        run_jobs(lambda jb: jb.step(comm, rank, world, prof))
 
     for _ in range(args.warmup):
         run_step()
@@ -256,6 +284,18 @@ def main():
     for l, (s, im) in out.items():
         chk += float(jobs[0].Bp[l].sum().item()) + float(s.double().sum().item())
     ct = torch.tensor([chk], dtype=torch.float64)
+    concurrent_ok = None
+    if pool is not None:   # every job's result: concurrent streams == one stream, in order
+
+        def job_sum(jb, out):
+            return sum(float(jb.Bp[l].sum().item()) + float(s_.double().sum().item())
+                       for l, (s_, _) in out.items())
+        outs = run_jobs(lambda jb: jb.step(comm, rank, world))
+        torch.cuda.synchronize()
+        order = [j for i in range(nstreams) for j in jobs[i::nstreams]]
+        conc = [job_sum(jb, o) for jb, o in zip(order, outs)]
+        seq = {id(jb): job_sum(jb, jb.step(comm, rank, world)) for jb in jobs}
+        concurrent_ok = all(c == seq[id(jb)] for c, jb in zip(conc, order))
     replicas_ok = True
     if world > 1 and args.config != 'c5':
         lo, hi = ct.clone(), ct.clone()
@@ -343,7 +383,7 @@ def main():
         'data': 'synthetic (gaussian-filtered noise; A\' = blur(A)); seeded',
         'config': {'workload': args.config + ': ' + conf['name'],
                    'A': list(conf['A']), 'B': list(conf['B']), 'kappa': conf['k'],
-                   'levels_cap': conf['levels'], 'jobs_per_gpu': len(jobs),
+                   'levels_cap': conf['levels'], 'jobs_per_gpu': len(jobs), 'streams_per_gpu': nstreams,
                    'pixels_per_step': pixels_per_step,
                    'parallelism': ('jobs%d' % world) if args.config == 'c5' else
                                   ('db-shard%d' % world if world > 1 else 'single')},
@@ -353,7 +393,9 @@ def main():
                     'candidate_segments': sum(p['candidate_segments'] for p in prof),
                     'full_scans': sum(p['full_scans'] for p in prof),
                     'queries': pixels_per_step * args.steps // (world if args.config == 'c5' else 1)},
-        'checks': {'replicas_identical': replicas_ok, 'checksum': chk},
+        'checks': {'replicas_identical': replicas_ok, 'checksum': chk,
+                   **({'concurrent_streams': nstreams, 'concurrent_identical': concurrent_ok}
+                      if concurrent_ok is not None else {})},
     }
     if lsh is not None:
         result['lsh_quality'] = jobs[0].lsh_quality()
