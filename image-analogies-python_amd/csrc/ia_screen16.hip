@@ -870,9 +870,10 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
     // chain-balanced form: the default for 1, 3, 5..7 and 9..11 query tiles (IA_SCREEN_BAL=0
     // turns it off; 4, 8 and 12 split evenly anyway; T = 3: 8-10 % faster than 4 x 1 tiles,
     // profiles/r01_screen_bench_h16c_t3.txt; T = 1: 15 % faster than the per-wave stream,
-    // 6.6 TB/s, T = 2: no gain — A/B only, profiles/r01_screen_bench_h16c_t12.txt)
+    // 6.6 TB/s; T = 2, 4, 8: no gain — A/B only, profiles/r01_screen_bench_h16c_t12.txt,
+    // _t48.txt)
     static const int bal_env = getenv("IA_SCREEN_BAL") ? atoi(getenv("IA_SCREEN_BAL")) : 1;
-    const bool bal_t = T <= 11 && T != 4 && T != 8 && (T != 2 || (flags & 0x80000));
+    const bool bal_t = T <= 11 && ((T != 2 && T != 4 && T != 8) || (flags & 0x80000));
     if (((flags & 0x80000) || (bal_env && flags == 0)) && bal_t &&
         seg_rows >= STAGE_TILES * 32) {   // segments of whole stages (tps >= 4)
         const long nb = ((nchunks + 7) / 8) * 8;
@@ -886,9 +887,11 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
         IA_H16C_CASE(1)
         IA_H16C_CASE(2)
         IA_H16C_CASE(3)
+        IA_H16C_CASE(4)
         IA_H16C_CASE(5)
         IA_H16C_CASE(6)
         IA_H16C_CASE(7)
+        IA_H16C_CASE(8)
         IA_H16C_CASE(9)
         IA_H16C_CASE(10)
         IA_H16C_CASE(11)
