@@ -4,11 +4,22 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/ia.h"
 
 namespace ia {
+
+// integer from the environment (tuning / A/B knobs).  Callers keep the value in a
+// function-local static (thread-safe initialisation) or a std::atomic when a diagnostic
+// entry can change it: libia is called from several host threads at once (bench.py c5).
+static inline int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 
 void set_error(const std::string &msg);
 int hip_fail(hipError_t e, const char *what);

@@ -496,12 +496,10 @@ __global__ __launch_bounds__(256, 2) void k_screen_pipe(const float *__restrict_
 // fastest on MI355X (tools/screen_bench, profiles/).  IA_SCREEN_VARIANT selects another
 // for A/B runs (bits 0-3 kind, 4-7 tile cap).
 int screen_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("IA_SCREEN_VARIANT");
-        v = e ? atoi(e) : 0;
-        if (v < 0 || (v & 15) > 3) v = 0;
-    }
+    static const int v = [] {
+        const int x = env_int("IA_SCREEN_VARIANT", 0);
+        return (x < 0 || (x & 15) > 3) ? 0 : x;
+    }();
     return v;
 }
 
@@ -1295,22 +1293,13 @@ __global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restric
     }
 }
 
-static int g_rescore_mode = -2;
-static int rescore_mode() {
-    int &v = g_rescore_mode;
-    if (v == -2) {
-        const char *e = getenv("IA_RESCORE");   // 0: per-query k_rescore, 1: work list
-        v = e ? atoi(e) : -1;                   // default: see launch_match
-    }
-    return v;
-}
+// 0: per-query k_rescore, 1: work list, -1: default (see launch_match); settable through
+// ia_diag_set_rescore_mode
+static std::atomic<int> g_rescore_mode{env_int("IA_RESCORE", -1)};
+static int rescore_mode() { return g_rescore_mode.load(std::memory_order_relaxed); }
 
 int fuse_finish() {
-    static int f = -1;
-    if (f < 0) {
-        const char *e = getenv("IA_FUSE_FINISH");
-        f = e ? atoi(e) : 2;
-    }
+    static const int f = env_int("IA_FUSE_FINISH", 2);
     return f;
 }
 
@@ -1357,17 +1346,13 @@ int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float
     return IA_E_ARG;
 }
 
-static int g_match_alg = -1;
-int match_alg() {
-    int &a = g_match_alg;
-    if (a < 0) {
-        // 0 = per-lane top-K, 1 = segment minima (f32 MFMA), 2 = segment minima (split f16)
-        const char *e = getenv("IA_MATCH_ALG");
-        a = e ? atoi(e) : 2;
-        if (a < 0 || a > 2) a = 2;
-    }
-    return a;
-}
+// 0 = per-lane top-K, 1 = segment minima (f32 MFMA), 2 = segment minima (split f16);
+// settable through ia_diag_set_match_alg
+static std::atomic<int> g_match_alg{[] {
+    const int a = env_int("IA_MATCH_ALG", 2);
+    return (a < 0 || a > 2) ? 2 : a;
+}()};
+int match_alg() { return g_match_alg.load(std::memory_order_relaxed); }
 
 // segment matcher scratch: [list counter | segment minima | items | item winners | per-query
 // records]; the counter sits at a fixed offset (it carries over between calls, emptied by
@@ -1447,7 +1432,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
         IA_LAUNCH_CHECK("k_gather");
         return IA_OK;
     }
-    static const int probe = getenv("IA_PRUNE_PROBE") ? atoi(getenv("IA_PRUNE_PROBE")) : 0;
+    static const int probe = env_int("IA_PRUNE_PROBE", 0);
 #define IA_RESCORE(F, SP)                                                                      \
     k_rescore<F, SP><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows), \
                                         segmin, db, qp, q64, nq, amax, best, stats, fa, probe)
@@ -1610,13 +1595,13 @@ int ia_diag_query_rows16(const double *q64, int M, const double *center, const f
 
 int ia_diag_set_match_alg(int alg) {
     const int prev = match_alg();
-    if (alg >= 0 && alg <= 2) g_match_alg = alg;
+    if (alg >= 0 && alg <= 2) g_match_alg.store(alg);
     return prev;
 }
 
 int ia_diag_set_rescore_mode(int mode) {
     const int prev = rescore_mode();
-    if (mode >= -1 && mode <= 1) g_rescore_mode = mode;
+    if (mode >= -1 && mode <= 1) g_rescore_mode.store(mode);
     return prev;
 }
 

@@ -12,22 +12,18 @@
 namespace ia {
 
 int seg_rows_max() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("IA_SEG_MAX");
-        v = e ? atoi(e) : 512;
-        if (v != 256 && v != 512) v = 512;
-    }
+    static const int v = [] {
+        const int x = env_int("IA_SEG_MAX", 512);
+        return x == 256 ? 256 : 512;
+    }();
     return v;
 }
 
 int target_chunks(long nrows) {
-    static int tc = -1;
-    if (tc < 0) {
-        const char *e = getenv("IA_TARGET_CHUNKS");
-        tc = e ? atoi(e) : 0;
-        if (tc != 0 && (tc < 64 || tc > 65536)) tc = 0;
-    }
+    static const int tc = [] {
+        const int x = env_int("IA_TARGET_CHUNKS", 0);
+        return (x < 64 || x > 65536) ? 0 : x;
+    }();
     if (tc) return tc;
     // default: 512 chunks (one per screen slot at 2 blocks per CU) for 2^19 <= rows < 2^21
     // (a sharded c4 rank at 4-8 GPUs, the single-GPU level 4): measured 4-10 % faster than

@@ -822,11 +822,7 @@ __global__ __launch_bounds__(256, 2) void k_screen_h16c(const half8 *__restrict_
 }
 
 static int h16_shared() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("IA_H16S");   // 0: per-wave form
-        v = e ? atoi(e) : 1;
-    }
+    static const int v = env_int("IA_H16S", 1);   // 0: per-wave form
     return v;
 }
 
@@ -872,7 +868,7 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
     // profiles/r01_screen_bench_h16c_t3.txt; T = 1: 15 % faster than the per-wave stream,
     // 6.6 TB/s; T = 2, 4, 8: no gain — A/B only, profiles/r01_screen_bench_h16c_t12.txt,
     // _t48.txt)
-    static const int bal_env = getenv("IA_SCREEN_BAL") ? atoi(getenv("IA_SCREEN_BAL")) : 1;
+    static const int bal_env = env_int("IA_SCREEN_BAL", 1);
     const bool bal_t = T <= 11 && ((T != 2 && T != 4 && T != 8) || (flags & 0x80000));
     if (((flags & 0x80000) || (bal_env && flags == 0)) && bal_t &&
         seg_rows >= STAGE_TILES * 32) {   // segments of whole stages (tps >= 4)
@@ -940,7 +936,7 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
         const int mode = (flags & 0x10000) ? 3 : (pf ? 2 : (pipe ? 1 : 0));
         // bit 17 / IA_SCREEN_NT (default 1): the DB stream copied with non-temporal loads (it
         // is read once per launch and never fits the caches)
-        static const int nt_env = getenv("IA_SCREEN_NT") ? atoi(getenv("IA_SCREEN_NT")) : 1;
+        static const int nt_env = env_int("IA_SCREEN_NT", 1);
         const bool nt = (flags & 0x20000) || nt_env;
 #define IA_H16S_NT_CASE(NQ, WQ, MD)                                                             \
         if (nt && nq == NQ && wq == WQ && mode == MD) {                                         \

@@ -127,15 +127,9 @@ static thread_local GraphKeeper g_graphs;
 
 // measured (tools/level_times.py, profiles/r01_level_times_graph.txt): eager launches beat
 // a captured graph on every c4 level once instantiation is counted, so capture is opt-in
-static int g_graph_mode = -1;
-static int graph_mode() {
-    int &g = g_graph_mode;
-    if (g < 0) {
-        const char *e = getenv("IA_GRAPH");
-        g = e ? atoi(e) : 0;
-    }
-    return g;
-}
+// (settable through ia_diag_set_graph_mode)
+static std::atomic<int> g_graph_mode{env_int("IA_GRAPH", 0)};
+static int graph_mode() { return g_graph_mode.load(std::memory_order_relaxed); }
 
 static unsigned long long slots_max(const std::vector<unsigned long long> &s, int i) {
     unsigned long long m = 0;
@@ -154,7 +148,7 @@ extern "C" {
 
 int ia_diag_set_graph_mode(int mode) {
     const int prev = graph_mode();
-    if (mode >= 0 && mode <= 2) g_graph_mode = mode;
+    if (mode >= 0 && mode <= 2) g_graph_mode.store(mode);
     return prev;
 }
 
