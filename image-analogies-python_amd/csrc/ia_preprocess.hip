@@ -93,6 +93,11 @@ __global__ void k_axpb(const double *x, long n, int mode, double a, double m, do
 // pass result in LDS, then the horizontal pass writes the tile and block min/max.
 // ---------------------------------------------------------------------------------
 constexpr int BT_W = 64, BT_H = 16, BH = 3;
+// min/max of the smoothed image (warp's clip range) as order-preserving int64 keys, spread
+// over MM_SLOTS slots of one 128-B line each: k_blur's blocks hit 64 lines instead of two
+// addresses (the serialised atomics made k_blur 0.6 TB/s), k_resample reduces the slots
+constexpr int MM_SLOTS = 64, MM_STRIDE = 16;
+static_assert(MM_SLOTS == 64, "k_resample reduces the slots with one wave");
 constexpr int IN_W = BT_W + 2 * BH, IN_H = BT_H + 2 * BH;
 
 __global__ __launch_bounds__(256) void k_blur(const double *__restrict__ src, int H, int W,
@@ -147,8 +152,9 @@ __global__ __launch_bounds__(256) void k_blur(const double *__restrict__ src, in
             kmin = red[0][i] < kmin ? red[0][i] : kmin;
             kmax = red[1][i] > kmax ? red[1][i] : kmax;
         }
-        atomicMin(reinterpret_cast<long long *>(&minmax[0]), kmin);
-        atomicMax(reinterpret_cast<long long *>(&minmax[1]), kmax);
+        unsigned long long *sl = minmax + ((blockIdx.x + blockIdx.y * gridDim.x) % MM_SLOTS) * MM_STRIDE;
+        atomicMin(reinterpret_cast<long long *>(&sl[0]), kmin);
+        atomicMax(reinterpret_cast<long long *>(&sl[1]), kmax);
     }
 }
 
@@ -158,6 +164,18 @@ __global__ __launch_bounds__(256) void k_resample(const double *__restrict__ sm,
                                                   double *__restrict__ dst, int h, int w,
                                                   double sx, double tx, double sy, double ty,
                                                   const unsigned long long *minmax) {
+    __shared__ double clip[2];
+    if (threadIdx.x < 64) {   // MM_SLOTS == 64: one slot per lane of wave 0
+        long long kmin = (long long)minmax[threadIdx.x * MM_STRIDE];
+        long long kmax = (long long)minmax[threadIdx.x * MM_STRIDE + 1];
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+            kmin = a < kmin ? a : kmin;
+            kmax = b > kmax ? b : kmax;
+        }
+        if (threadIdx.x == 0) { clip[0] = dkey_inv(kmin); clip[1] = dkey_inv(kmax); }
+    }
+    __syncthreads();
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= w || y >= h) return;
@@ -173,15 +191,15 @@ __global__ __launch_bounds__(256) void k_resample(const double *__restrict__ sm,
     const double top = (1 - dc) * tl + dc * tr;
     const double bot = (1 - dc) * bl + dc * br;
     double v = (1 - dr) * top + dr * bot;
-    const double lo = dkey_inv((long long)minmax[0]), hi = dkey_inv((long long)minmax[1]);
+    const double lo = clip[0], hi = clip[1];
     v = v < lo ? lo : v;   // np.clip(out, min, max) (NaN-free inputs)
     v = v > hi ? hi : v;
     dst[(long)y * w + x] = v;
 }
 
-__global__ void k_init_minmax(unsigned long long *mm) {
-    mm[0] = 0x7fffffffffffffffULL;
-    mm[1] = 0x8000000000000000ULL;
+__global__ void k_init_minmax(unsigned long long *mm) {   // <<<1, MM_SLOTS>>>
+    mm[threadIdx.x * MM_STRIDE] = 0x7fffffffffffffffULL;
+    mm[threadIdx.x * MM_STRIDE + 1] = 0x8000000000000000ULL;
 }
 
 // deterministic two-pass mean: block partial sums (fixed order) then one block.
@@ -261,7 +279,7 @@ int ia_axpb_f64(const double *x, long n, int mode, double a, double m, double b,
 }
 
 size_t ia_pyr_workspace_bytes(int H, int W) {
-    return align_up((size_t)H * W * sizeof(double), 256) + 256;
+    return align_up((size_t)H * W * sizeof(double), 256) + MM_SLOTS * MM_STRIDE * 8;
 }
 
 int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w,
@@ -274,7 +292,7 @@ int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w
     unsigned long long *mm = reinterpret_cast<unsigned long long *>(
         reinterpret_cast<char *>(workspace) + align_up((size_t)H * W * sizeof(double), 256));
     hipStream_t st = S(stream);
-    k_init_minmax<<<1, 1, 0, st>>>(mm);
+    k_init_minmax<<<1, MM_SLOTS, 0, st>>>(mm);
     IA_LAUNCH_CHECK("k_init_minmax");
     dim3 g1(nblk(W, BT_W), nblk(H, BT_H));
     k_blur<<<g1, 256, 0, st>>>(src, H, W, taps[0], taps[1], taps[2], taps[3], sm, mm);
