@@ -275,3 +275,35 @@ def test_sharded_level_index_rows(gpu):
             dd = np.add.reduce((As - q) ** 2, axis=1)
             j = int(np.argmin(dd))
             assert win == (dd[j], j)
+
+
+def test_concurrent_jobs_on_streams_match_oracle(gpu):
+    """bench.py c5 drives libia from several host threads, one HIP stream each: jobs
+    synthesised concurrently that way give the oracle's result, job by job."""
+    from concurrent.futures import ThreadPoolExecutor
+    import image_analogies as ia
+    w = o.compute_weights(3, 5, 12, 1)
+    jobs = []
+    for j in range(3):
+        A, Aps, B = analogy_inputs(50 + j, (36, 44), (30, 41), n_ap=1)
+        A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=50 + j)
+        ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 0.5, w)
+        jobs.append((A_pyr, Ap_list, B_pyr, Bp_pyr, L, ref))
+    main = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream() for _ in jobs]
+
+    def run(i):
+        A_pyr, Ap_list, B_pyr, Bp_pyr, L, _ = jobs[i]
+        streams[i].wait_stream(main)
+        with torch.cuda.stream(streams[i]):
+            out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                                    [dev(p) for p in B_pyr], [dev(b) for b in Bp_pyr], L, 0.5, w)
+            res = {l: (s.cpu().numpy(), im.cpu().numpy()) for l, (s, im) in out.items()}
+        return res
+
+    with ThreadPoolExecutor(len(jobs)) as pool:
+        outs = list(pool.map(run, range(len(jobs))))
+    for (_, _, _, _, _, ref), out in zip(jobs, outs):
+        for l in ref:
+            assert np.array_equal(out[l][0], ref[l][1]), l
+            assert np.array_equal(out[l][1], ref[l][2]), l
