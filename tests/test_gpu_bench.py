@@ -1,0 +1,52 @@
+"""bench.py's JSON contract on the GPU (one short run per workload shape, as a child
+process like the driver's own run): the keys and types the driver and the judge read,
+the roofline object, and the result checks."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), *args],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def check_contract(d, steps, warmup):
+    for k in ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+              'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data', 'config',
+              'roofline'):
+        assert k in d, k
+    assert d['n_gpus'] == 1 and d['steps'] == steps and d['warmup'] == warmup
+    assert d['value'] > 0 and d['ms_per_step'] > 0 and d['higher_is_better'] is True
+    assert d['scaling'] in ('weak', 'strong') and 'workload' in d['config']
+    r = d['roofline']
+    for k in ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic'):
+        assert k in r, k
+    assert r['bound'] in ('hbm', 'mfma') and r['achieved'] > 0
+    assert abs(r['frac'] - r['achieved'] / r['peak']) < 1e-9
+    assert d['checks']['replicas_identical'] is True
+
+
+@pytest.mark.gpu
+def test_bench_contract_c1(gpu):
+    d = run_bench('--config', 'c1', '--steps', '2', '--warmup', '1', '--no-cpu-baseline')
+    check_contract(d, 2, 1)
+    assert d['matcher']['kind'] == 'exact' and d['matcher']['full_scans'] == 0
+
+
+@pytest.mark.gpu
+def test_bench_contract_c5_streams(gpu):
+    d = run_bench('--config', 'c5', '--jobs', '2', '--streams', '2', '--steps', '1',
+                  '--warmup', '1', '--no-cpu-baseline')
+    check_contract(d, 1, 1)
+    assert d['scaling'] == 'weak' and d['config']['streams_per_gpu'] == 2
+    assert d['checks']['concurrent_identical'] is True
