@@ -6,10 +6,9 @@ namespace ia {
 
 // ---- database chunking (shared by ia_db_build and the screen) -------------------
 // A screen workgroup owns one chunk of CH rows: 4 waves x (CH/4) rows, 32-row tiles.
-// CH is chosen so a DB produces ~target_chunks(N) chunks (512 or 1024).
+// CH is chosen so a DB produces ~target_chunks(N) chunks (512 by default).
 constexpr int SCREEN_K = 4;            // candidates kept per (query, chunk)
-// ~chunks per database: IA_TARGET_CHUNKS (read once per process; default 512 for
-// 2^19 <= rows < 2^21, 1024 otherwise; a tuning knob for tools/screen_bench — the DB build and the screen must agree on it)
+// ~chunks per database: IA_TARGET_CHUNKS (read once per process; default 512; a tuning knob for tools/screen_bench — the DB build and the screen must agree on it)
 int target_chunks(long nrows);
 
 // tiles per wave: a power of two in [1, 64] (so screen segments divide it)

@@ -25,10 +25,12 @@ int target_chunks(long nrows) {
         return (x < 64 || x > 65536) ? 0 : x;
     }();
     if (tc) return tc;
-    // default: 512 chunks (one per screen slot at 2 blocks per CU) for 2^19 <= rows < 2^21
-    // (a sharded c4 rank at 4-8 GPUs, the single-GPU level 4): measured 4-10 % faster than
-    // 1024 there (profiles/r01_screen_bench_shard_sizes.txt); 1024 otherwise
-    return (nrows >= (1L << 19) && nrows < (1L << 21)) ? 512 : 1024;
+    // default: 512 chunks (one per screen slot at 2 blocks per CU): measured 4-10 % faster
+    // than 1024 at 0.5-1 M rows (a sharded c4 rank, profiles/r01_screen_bench_shard_sizes.txt),
+    // c4 level 3 (262 K rows) 37.8 -> 34.0 ms, equal at 4.19 M rows
+    // (profiles/r01_chunks_ab_end.txt); below 128 K rows both give 128-row chunks
+    (void)nrows;
+    return 512;
 }
 
 
