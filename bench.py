@@ -45,9 +45,9 @@ HBM_PEAK_GBS = 8000.0
 # HBM traffic of one finest-level screen launch, from rocprofv3 PMC (FETCH_SIZE x 2 on
 # gfx950 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench at M = 342 queries
 # against the 4,194,304-row c4 database: the chain-balanced k_screen_h16c<11>
-# (profiles/r01_end_screen_pmc_m342.txt; WRITE_SIZE 88 MB vs 11 MB of segment minima: 4-B
+# (profiles/r01_end_screen_pmc_m342.txt; WRITE_SIZE 133 MB vs 11 MB of segment minima: 4-B
 # writes strided by the segment count, each likely a partial-line write)
-SCREEN_PMC = {'fetch_kb': 4.593e5, 'write_kb': 8.57e4, 'M': 342, 'rows': 4194304,
+SCREEN_PMC = {'fetch_kb': 4.593e5, 'write_kb': 1.298e5, 'M': 342, 'rows': 4194304,
               'source': 'profiles/r01_end_screen_pmc_m342.txt'}
 
 CONFIGS = {
