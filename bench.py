@@ -13,14 +13,19 @@ Workloads (BASELINE.json configs):
     c3  362x638, kappa 25, 5-level cap      c4  A = A' 2048x2048, B 1024x1024, 5-level cap
     c5  independent 512x512 jobs (multi_script batch), --jobs per GPU
 Default: c4 — the configuration the metric and its 1/2/4/8-GPU scaling are quoted on.
-With N > 1 (torch.distributed.run, one process per GPU) c4 shards every level's database
-rows over the ranks with one RCCL all-gather per wave (strong scaling); c5 spreads jobs
-(weak scaling, no collective).  rank 0 prints ONE JSON line.
+With N > 1 (one process per GPU) c4 shards the databases of its large levels over the
+ranks with one RCCL all-gather per wave (strong scaling); c5 spreads jobs (weak scaling,
+no collective).  `--gpus N` launched without torch.distributed.run's environment starts
+the N rank processes itself (torch.distributed.run as a child, before any GPU call in
+this process); every rank checks that the world size equals --gpus.  rank 0 prints ONE
+JSON line.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,17 +47,15 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 
 # x 2.4 GHz (MI355X_MICROARCH.md: ~2.5 PF dense)
 F16_MFMA_PEAK_TFLOPS = 4096 * 256 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
-# HBM traffic of one finest-level screen launch, from rocprofv3 PMC (FETCH_SIZE x 2 on
-# gfx950 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench at M = 342 queries
-# against the 4,194,304-row c4 database: the chain-balanced k_screen_h16c<11>
-# (profiles/r01_end_screen_pmc_m342.txt; WRITE_SIZE 133 MB vs 11 MB of segment minima: 4-B
-# writes strided by the segment count, each likely a partial-line write)
-SCREEN_PMC = {'fetch_kb': 4.593e5, 'write_kb': 1.298e5, 'M': 342, 'rows': 4194304,
-              'source': 'profiles/r01_end_screen_pmc_m342.txt'}
+# HBM traffic of one finest-level screen launch (k_screen16<11>, M = 342 queries against
+# the 4,194,304-row c4 database), from rocprofv3 PMC passes (FETCH_SIZE x 2 on gfx950 +
+# WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench; None until measured for the
+# current kernel (profiles/)
+SCREEN_PMC = None
 
 CONFIGS = {
     'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),
-    'c2': dict(A=(180, 117), B=(180, 117), k=5.0, levels=None, name='freud-crop 180x117 kappa=5, brute force'),
+    'c2': dict(A=(180, 117), B=(180, 117), k=5.0, levels=None, name='freud-crop 180x117 kappa=5'),
     'c3': dict(A=(362, 638), B=(362, 638), k=25.0, levels=5, name='texture transfer 362x638 kappa=25, 5-level'),
     'c4': dict(A=(2048, 2048), B=(1024, 1024), k=0.5, levels=5, name='A/A\' 2048x2048 x B 1024x1024, 5-level, DB sharded'),
     'c5': dict(A=(512, 512), B=(512, 512), k=0.5, levels=5, name='independent 512x512 analogies (multi_script batch)'),
@@ -94,11 +97,13 @@ class Job:
         self.Bp = [x.clone() for x in self.Bp_init]
         self.weights = torch.as_tensor(cfg.compute_weights(3, 5, 12, 1)).to(dev)
         self.pixels = sum(s[0] * s[1] for s in shapes[1:self.max_levels])
+        self.waves = sum(_ia.waves(*s) for s in shapes[1:self.max_levels])
 
-    def step(self, comm=None, rank=0, nranks=1, prof=None, eager=False):
+    def step(self, comm=None, rank=0, nranks=1, prof=False, eager=False):
         A_pyr = ip.gaussian_pyramid_dev(self.A, cfg.n_sm, self.levels)
         Ap_pyr = ip.gaussian_pyramid_dev(self.Ap, cfg.n_sm, self.levels)
         B_pyr = ip.gaussian_pyramid_dev(self.B, cfg.n_sm, self.levels)
+        self.Ap_pyr_last = Ap_pyr
         for dst, src in zip(self.Bp, self.Bp_init):
             dst.copy_(src)
         return ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, self.Bp, self.max_levels, self.k,
@@ -139,10 +144,21 @@ class Job:
         return sum(bl[l][0] * bl[l][1] * al[l][0] * al[l][1] for l in range(1, self.max_levels))
 
 
-def cpu_baseline(job, seconds=20.0):
-    """The C oracle (exact brute force, 1 core) on a bounded sample of the same workload:
-    the first pixels of the FINEST level in scanline order against its full database;
-    extrapolated to the whole job by (query, row) pair count."""
+def cpu_threads():
+    """Host threads of the all-cores CPU baseline: OMP_NUM_THREADS when set (the GPU box
+    sets it to the box's CPU share), else every CPU of this process's affinity mask."""
+    env = os.environ.get('OMP_NUM_THREADS')
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(job, seconds=10.0):
+    """The C oracle (scanline synthesis with the exact brute-force matcher)
+    timed on a bounded sample of the same workload: the first pixels of the FINEST level
+    in scanline order against its full database, extrapolated to the whole job by (query,
+    row) pair count.  Two legs in the same run: 1 thread, and all host threads (the 1-NN
+    scan split over rows, same result).  ~`seconds` of CPU work per leg."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import ia_oracle_c as oc
     A_pyr = [p.cpu().numpy() for p in ip.gaussian_pyramid_dev(job.A, cfg.n_sm, job.levels)]
@@ -153,26 +169,36 @@ def cpu_baseline(job, seconds=20.0):
     w = cfg.compute_weights(3, 5, 12, 1)
     N = A_pyr[level].size
     f = ia.kappa_factor(level, job.max_levels, job.k)
+    H, W = B_pyr[level].shape
     probe = oc.LevelJob(level, A_pyr, [Ap_pyr], B_pyr, Bp_pyr, w, f, max_pixels=2)
-    probe.build_db()
-    t0 = time.perf_counter()
-    probe.run()
-    per_px = max((time.perf_counter() - t0) / 2, 1e-6)
-    npx = int(max(2, min(B_pyr[level].size, seconds / per_px)))
-    job_s = oc.LevelJob(level, A_pyr, [Ap_pyr], B_pyr, Bp_pyr, w, f, max_pixels=npx)
-    job_s.db = probe.db
-    probe.db = None
-    t0 = time.perf_counter()
-    job_s.run()
-    dt = time.perf_counter() - t0
-    pairs_per_s = npx * N / dt
-    value = pairs_per_s * job.pixels / job.algorithmic_pairs()
-    return {'value': value, 'unit': "B' pixels/s", 'cores': 1, 'kind': 'port',
-            'sample': '%d B\' pixels (scanline) of the finest level (%dx%d) against its full '
-                      '%d-row database, %.1f s on 1 core of %d; extrapolated to the whole '
-                      'job by (query,row) pairs' % (npx, B_pyr[level].shape[0],
-                                                    B_pyr[level].shape[1], N, dt,
-                                                    os.cpu_count())}
+    db = probe.build_db()
+
+    def leg(threads):
+        got = oc.set_threads(threads)
+        probe.L.max_pixels = 2
+        t0 = time.perf_counter()
+        probe.run()
+        per_px = max((time.perf_counter() - t0) / 2, 1e-6)
+        npx = int(max(2, min(H * W, seconds / per_px)))
+        job_s = oc.LevelJob(level, A_pyr, [Ap_pyr], B_pyr, Bp_pyr, w, f, max_pixels=npx)
+        job_s.db = db
+        t0 = time.perf_counter()
+        try:
+            job_s.run()
+        finally:
+            job_s.db = None       # owned by probe
+        dt = time.perf_counter() - t0
+        value = npx * N / dt * job.pixels / job.algorithmic_pairs()
+        return {'value': value, 'unit': "B' pixels/s", 'cores': got, 'kind': 'port',
+                'sample': '%d B\' pixels (scanline) of the finest level (%dx%d) against its '
+                          'full %d-row database, %.1f s on %d thread(s) (host reports %d CPUs); '
+                          'extrapolated to the whole job by (query,row) pairs'
+                          % (npx, H, W, N, dt, got, os.cpu_count())}
+    one = leg(1)
+    allc = leg(cpu_threads())
+    oc.set_threads(1)
+    allc['single_core'] = one
+    return allc
 
 
 def hbm_kernels(dev, reps=20):
@@ -259,6 +285,28 @@ def init_comm(rank, world):
     return h
 
 
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(('127.0.0.1', 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) outside torch.distributed.run: start the N rank processes with it
+    as a child (this process has made no GPU call: torch.cuda.device_count() does not
+    initialise the device on this image) and exit with its status."""
+    if not args.dry_run:
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print('bench.py: --gpus %d but only %d GPU(s) visible' % (args.gpus, ndev),
+                  file=sys.stderr, flush=True)
+            sys.exit(2)
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -270,17 +318,44 @@ def main():
                     help='c5: jobs run concurrently per GPU (one HIP stream + host thread each; '
                          '4 = the HIP hardware queues per process)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--cpu-seconds', type=float, default=10.0,
+                    help='CPU work per leg of the CPU baseline (1 thread, all threads)')
     ap.add_argument('--matcher', default='brute', choices=['brute', 'lsh'],
                     help="lsh: the approximate E2LSH matcher (SURVEY §8(f)1, config c2)")
     ap.add_argument('--lsh', default='16,4,1.0', help='tables,hashes,width for --matcher lsh')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launcher check without a GPU: ranks meet over gloo, rank 0 prints '
+                         'the world it saw')
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        launch_ranks(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print('bench.py: world size %d != --gpus %d' % (world, args.gpus), file=sys.stderr,
+              flush=True)
+        sys.exit(2)
     if world > 1:
         dist.init_process_group('gloo')
+    if args.dry_run:
+        t = torch.tensor([float(rank)])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({'dry_run': True, 'n_gpus': world, 'gpus': args.gpus,
+                              'rank_sum': float(t.item()), 'config': args.config}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if torch.cuda.device_count() <= local:
+        print('bench.py: rank %d needs GPU %d, %d visible' % (rank, local,
+                                                            torch.cuda.device_count()),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     conf = CONFIGS[args.config]
@@ -324,23 +399,30 @@ def main():
             main.wait_stream(st)
         return [r for part in res for r in part]
 
-    def run_step(prof=None):
+    def run_step(prof=False):
         run_jobs(lambda jb: jb.step(comm, rank, world, prof))
 
+    # warm-up steps run profiled too; the event pool is created before the timed region
+    nev = 2 * args.steps * sum(jb.waves for jb in jobs)
+    _ia.prof_begin(nev)
     for _ in range(args.warmup):
-        run_step()
+        run_step(True)
+    _ia.prof_end()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    prof = []
+    # the timed steps: the product path, plus HIP events around every screen launch and the
+    # matcher statistics copied stream-ordered (no host synchronisation inside the region)
+    _ia.prof_begin()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run_step(prof)
+        run_step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    prof = _ia.prof_end()
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -350,8 +432,12 @@ def main():
     # identical replicas across ranks
     out = jobs[0].step(comm, rank, world)
     chk = 0.0
+    consistent = True
     for l, (s, im) in out.items():
         chk += float(jobs[0].Bp[l].sum().item()) + float(s.double().sum().item())
+        src = jobs[0].Ap_pyr_last[l]
+        consistent &= bool(torch.equal(jobs[0].Bp[l].flatten(),
+                                       src[s[:, 0].long(), s[:, 1].long()]))
     ct = torch.tensor([chk], dtype=torch.float64)
     concurrent_ok = None
     if pool is not None:   # every job's result: concurrent streams == one stream, in order
@@ -374,47 +460,37 @@ def main():
 
     pixels_per_step = sum(jb.pixels for jb in jobs) * (world if args.config == 'c5' else 1)
     value = pixels_per_step * args.steps / elapsed
-    # roofline of the screen: HIP events around every screen launch of the timed steps,
-    # except launches inside captured graphs (small levels, which events cannot time);
-    # when no launch was timed (every level captured, e.g. c1) one extra eager step
-    # after the timed region supplies the events.
-    rprof, rsource = prof, 'timed steps (eager levels)'
-    if sum(p['timed_screens'] for p in prof) == 0:
-        rprof, rsource = [], 'one extra eager step after the timed region (all levels graph-captured)'
-        for jb in jobs:
-            jb.step(comm, rank, world, rprof, eager=True)
-    screen_ms = sum(p['screen_ms'] for p in rprof)
-    screens = sum(p['timed_screens'] for p in rprof)
-    pairs = sum(p['timed_pairs'] for p in rprof)
-    rescored = sum(p['rows_rescored'] for p in prof)
-    # the dominant kernel: the screen at the finest level (most timed screen time)
+    # roofline of the dominant kernel: the screen launches of the level with the most
+    # screen time (the finest), HIP events on the library's stream around each launch
     by_level = {}
-    for p in rprof:
-        d = by_level.setdefault(p['level'], [0.0, 0, 0.0])
-        d[0] += p['screen_ms']; d[1] += p['timed_screens']; d[2] += p['timed_pairs']
+    for p in prof:
+        d = by_level.setdefault(p['level'], [0.0, 0, 0.0, p['rows']])
+        d[0] += p['screen_ms']; d[1] += p['timed_screens']; d[2] += p['pairs'] if p['timed_screens'] else 0.0
     dom = max(by_level, key=lambda l: by_level[l][0]) if by_level else None
-    d_ms, d_n, d_pairs = by_level[dom] if dom is not None else (0.0, 0, 0.0)
-    split = _ia.match_alg() == 2
-    if split:
-        # split-f16 screen: 3 f16 products (a_h q_h + a_h q_l + a_l q_h) of 2 flop per
-        # feature per (query, row) pair on v_mfma_f32_32x32x16_f16
-        per_pair, peak, kname = 3 * 2 * 55, F16_MFMA_PEAK_TFLOPS, 'k_screen_h16c/h16s'
-    else:
-        per_pair, peak, kname = 2 * 55, FP32_MFMA_PEAK_TFLOPS, 'k_screen_seg'
+    d_ms, d_n, d_pairs, d_rows = by_level[dom] if dom is not None else (0.0, 0, 0.0, 0)
+    screen_ms = sum(v[0] for v in by_level.values())
+    screens = sum(v[1] for v in by_level.values())
+    pairs = sum(v[2] for v in by_level.values())
+    # split-f16 screen: 3 f16 products (a_h q_h + a_h q_l + a_l q_h) of 2 flop per feature
+    # per (query, row) pair on v_mfma_f32_32x32x16_f16
+    per_pair = 3 * 2 * 55
     achieved = per_pair * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
     fp32eq = 2.0 * 55 * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
     traffic = None
-    if split and args.config == 'c4' and world == 1:
+    if SCREEN_PMC and args.config == 'c4' and world == 1:
         traffic = (SCREEN_PMC['fetch_kb'] * 2 + SCREEN_PMC['write_kb']) * 1024
-    roof = {'bound': 'mfma', 'kernel': kname, 'achieved': achieved, 'peak': peak,
-            'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': traffic,
-            'algorithmic': '%d flop per (query,row) pair; level %s: %.4g pairs over %d launches'
-                           % (per_pair, dom, d_pairs, d_n),
-            'screen_avg_us': d_ms * 1e3 / max(d_n, 1), 'source': rsource,
+    roof = {'bound': 'mfma', 'kernel': 'k_screen16', 'achieved': achieved,
+            'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / F16_MFMA_PEAK_TFLOPS,
+            'traffic': traffic,
+            'algorithmic': '%d f16 flop per (query,row) pair; level %s (%d DB rows): %.4g pairs '
+                           'over %d launches' % (per_pair, dom, d_rows, d_pairs, d_n),
+            'screen_avg_us': d_ms * 1e3 / max(d_n, 1),
+            'source': 'HIP events around every screen launch of the timed steps',
             'fp32_equivalent_tflops': fp32eq,
             'fp32_equivalent_frac_of_fp32_mfma_peak': fp32eq / FP32_MFMA_PEAK_TFLOPS,
             'all_levels': {'launches': screens, 'pairs': pairs,
                            'screen_avg_us': screen_ms * 1e3 / max(screens, 1),
+                           'screen_ms_per_step': screen_ms / args.steps,
                            'fp32_equivalent_tflops':
                                2.0 * 55 * pairs / (screen_ms * 1e-3) / 1e12 if screen_ms else 0.0}}
     if traffic is not None:
@@ -424,16 +500,15 @@ def main():
                                    SCREEN_PMC['rows'] * 224 / 1e6))
     if lsh is not None:
         # k_lsh_query is a gather: each examined row costs its 55 fp64 features (440 B)
-        # (rows counted over the same launches the events timed)
-        examined = sum(p['rows_rescored'] for p in rprof) if rprof is not prof else \
-            sum(p['rows_rescored'] for p in prof if p['timed_screens'])
+        examined = sum(p['rows_rescored'] for p in prof if p['timed_screens'])
         gbs = examined * 440.0 / (screen_ms * 1e-3) / 1e9 if screen_ms > 0 else 0.0
         roof = {'bound': 'hbm', 'kernel': 'k_lsh_query', 'achieved': gbs,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
                 'traffic': None,
                 'algorithmic': '440 B (55 fp64) per examined row; %d rows over %d launches'
                                % (examined, screens),
-                'screen_avg_us': screen_ms * 1e3 / max(screens, 1), 'source': rsource}
+                'screen_avg_us': screen_ms * 1e3 / max(screens, 1),
+                'source': 'HIP events around every LSH query launch of the timed steps'}
 
     result = {
         'metric': "B' pixels/sec (brute-force match, 5-level pyramid) + MFMA util @1/2/4/8 GPU"
@@ -447,10 +522,11 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak' if args.config == 'c5' else 'strong',
         'vs_baseline': None,
-        'dtype': ('f16x3 split (MFMA screen, f32 accumulate)' if split else
-                  'f32 (MFMA screen)') + ' + f64 (exact rescore, pyramids)',
+        'dtype': 'f16x3 split (MFMA screen, f32 accumulate) + f32 (re-screen) + f64 (exact '
+                 'rescore, pyramids)',
         'data': 'synthetic (gaussian-filtered noise; A\' = blur(A)); seeded',
-        'config': {'workload': args.config + ': ' + conf['name'],
+        'config': {'workload': args.config + ': ' + conf['name'] +
+                               (', LSH matcher' if lsh is not None else ', brute force'),
                    'A': list(conf['A']), 'B': list(conf['B']), 'kappa': conf['k'],
                    'levels_cap': conf['levels'], 'jobs_per_gpu': len(jobs), 'streams_per_gpu': nstreams,
                    'pixels_per_step': pixels_per_step,
@@ -458,11 +534,12 @@ def main():
                                   ('db-shard%d' % world if world > 1 else 'single')},
         'roofline': roof,
         'matcher': {'kind': 'lsh' if lsh is not None else 'exact',
-                    'rows_rescored_fp64': rescored,
+                    'rows_rescored_fp64': sum(p['rows_rescored'] for p in prof),
                     'candidate_segments': sum(p['candidate_segments'] for p in prof),
                     'full_scans': sum(p['full_scans'] for p in prof),
                     'queries': pixels_per_step * args.steps // (world if args.config == 'c5' else 1)},
-        'checks': {'replicas_identical': replicas_ok, 'checksum': chk,
+        'checks': {'replicas_identical': replicas_ok, 'bp_equals_ap_at_s': consistent,
+                   'checksum': chk,
                    **({'concurrent_streams': nstreams, 'concurrent_identical': concurrent_ok}
                       if concurrent_ok is not None else {})},
     }

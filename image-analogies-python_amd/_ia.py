@@ -51,11 +51,13 @@ class IaSynthArgs(ctypes.Structure):
                 ('B_ws', ctypes.c_int), ('H', ctypes.c_int), ('W', ctypes.c_int),
                 ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
                 ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
-                ('workspace', _dp), ('comm', _dp), ('prof', ctypes.POINTER(ctypes.c_double)),
-                ('lsh', ctypes.POINTER(IaLsh)), ('flags', ctypes.c_int)]
+                ('workspace', _dp), ('comm', _dp), ('lsh', ctypes.POINTER(IaLsh)),
+                ('flags', ctypes.c_int), ('tag', ctypes.c_int)]
 
 
 IA_SYNTH_EAGER = 1
+IA_SYNTH_PROF = 2
+IA_PROF_FIELDS = 8
 
 _SIGS = {
     'ia_last_error': (ctypes.c_char_p, []),
@@ -94,14 +96,16 @@ _SIGS = {
                                     ctypes.POINTER(ctypes.c_void_p)]),
     'ia_comm_destroy': (ctypes.c_int, [_dp]),
     'ia_comm_nranks': (ctypes.c_int, [_dp]),
+    'ia_prof_begin': (ctypes.c_int, []),
+    'ia_prof_prepare': (ctypes.c_int, [ctypes.c_long]),
+    'ia_prof_end': (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    'ia_release_thread_resources': (ctypes.c_int, []),
     # diagnostics (include/ia_diag.h)
-    'ia_diag_set_match_alg': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_graph_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
-    'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, ctypes.c_int,
-                                        _dp]),
+    'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
 }
 
 _lib = None
@@ -139,12 +143,6 @@ def lib():
     return _lib
 
 
-def match_alg(alg=-1):
-    """Select the exact matcher's screen for this process (0 per-lane top-K, 1 f32-MFMA
-    segment minima, 2 split-f16 segment minima [default]); returns the previous value."""
-    return lib().ia_diag_set_match_alg(int(alg))
-
-
 def rescore_mode(mode=-2):
     """Select the exact stage's form for this process (0 per-query workgroups, 1 work list,
     -1 default); returns the previous value."""
@@ -155,6 +153,44 @@ def graph_mode(mode=-1):
     """HIP-graph capture of the synthesis wave loop for this process (0 off [default],
     1 levels <= 2^18 rows, 2 all single-GPU levels); returns the previous value."""
     return lib().ia_diag_set_graph_mode(int(mode))
+
+
+PROF_KEYS = ('level', 'rows', 'pairs', 'screen_ms', 'timed_screens', 'rows_rescored',
+             'candidate_segments', 'full_scans')
+
+
+def prof_begin(nevents=0):
+    """Open a profile: every ia_synth_level call flagged IA_SYNTH_PROF from now on records
+    HIP events around its screen launches and its matcher statistics, without
+    synchronising (include/ia.h).  nevents: create that many events up front."""
+    if nevents:
+        check(lib().ia_prof_prepare(int(nevents)), 'ia_prof_prepare')
+    check(lib().ia_prof_begin(), 'ia_prof_begin')
+
+
+def waves(H, W):
+    """Skewed waves t = x + 3y of an H x W level: (W - 1) + 3 (H - 1) + 1."""
+    return (W - 1) + 3 * (H - 1) + 1
+
+
+def prof_end():
+    """Synchronise the device and read the open profile: one dict per profiled level call
+    (PROF_KEYS), in call order."""
+    n = lib().ia_prof_end(None, 0)
+    if n < 0:
+        check(n, 'ia_prof_end')
+    buf = (ctypes.c_double * (IA_PROF_FIELDS * max(n, 1)))()
+    n = lib().ia_prof_end(buf, n)
+    if n < 0:
+        check(n, 'ia_prof_end')
+    out = []
+    for r in range(n):
+        rec = dict(zip(PROF_KEYS, buf[r * IA_PROF_FIELDS:(r + 1) * IA_PROF_FIELDS]))
+        for k in ('level', 'rows', 'timed_screens', 'rows_rescored', 'candidate_segments',
+                  'full_scans'):
+            rec[k] = int(rec[k])
+        out.append(rec)
+    return out
 
 
 def check(rc, what):

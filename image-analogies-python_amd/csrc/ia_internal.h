@@ -4,46 +4,43 @@
 
 namespace ia {
 
-// ---- database chunking (shared by ia_db_build and the screen) -------------------
-// A screen workgroup owns one chunk of CH rows: 4 waves x (CH/4) rows, 32-row tiles.
-// CH is chosen so a DB produces ~target_chunks(N) chunks (512 by default).
-constexpr int SCREEN_K = 4;            // candidates kept per (query, chunk)
-// ~chunks per database: IA_TARGET_CHUNKS (read once per process; default 512; a tuning knob for tools/screen_bench — the DB build and the screen must agree on it)
-int target_chunks(long nrows);
+// ---- database chunking (shared by ia_db_build, the screen and the exact stage) ------
+// A screen workgroup owns one chunk of ch rows (32-row tiles, 4-tile stages).  ch is
+// chosen so a DB produces ~DB_TARGET_CHUNKS chunks (one per screen slot at 2 blocks per
+// CU: measured 4-10 % faster than 1024 at 0.5-1 M rows, equal at 4.19 M rows;
+// profiles/r01_screen_bench_shard_sizes.txt, r01_chunks_ab_end.txt).  The chunk count is
+// rounded up to a multiple of 4 (the exact stage reads the segment minima as float4).
+constexpr long DB_TARGET_CHUNKS = 512;
+constexpr int DB_CHUNK_MAX = 8192;     // 64 tiles
+constexpr int DB_SEG_MAX = 512;        // rows per segment (one minimum per query)
 
-// tiles per wave: a power of two in [1, 64] (so screen segments divide it)
 static inline int db_chunk_rows(long nrows) {
-    const long tc = target_chunks(nrows);
-    const long want = (nrows + tc * 128 - 1) / (tc * 128);
-    long tpw = 1;
-    while (tpw < want && tpw < 64) tpw <<= 1;
+    const long want = (nrows + DB_TARGET_CHUNKS * 128 - 1) / (DB_TARGET_CHUNKS * 128);
+    long tpw = 1;   // 128-row units, a power of two in [1, 64]
+    while (tpw < want && tpw < DB_CHUNK_MAX / 128) tpw <<= 1;
     return (int)(128 * tpw);
 }
 static inline long db_nchunks(long nrows) {
     const long ch = db_chunk_rows(nrows);
-    return (nrows + ch - 1) / ch;
+    return ((nrows + ch - 1) / ch + 3) / 4 * 4;
 }
 static inline long db_rows_padded(long nrows) { return db_nchunks(nrows) * db_chunk_rows(nrows); }
-// one DB buffer = the fp32 screening rows (npad x IA_DP floats, fragment-major) followed
-// by their split-f16 copy (npad x 112 halves, ia_split16.h): 2 x 224 B per padded row
+// one DB buffer = the fp32 screening rows (npad x IA_DP floats, fragment-major; the exact
+// stage's re-screen) followed by their split-f16 copy (npad x 112 halves, ia_split16.h;
+// the screen's operand): 2 x 224 B per padded row
 static inline size_t db_bytes(long nrows) { return (size_t)db_rows_padded(nrows) * IA_DP * 4 * 2; }
 template <typename T>
 static inline T *db16_of(T *db, long nrows) {
     return db + (size_t)db_rows_padded(nrows) * IA_DP * 4 / sizeof(T);
 }
-// segment-minimum matcher: one running minimum per (query, segment) of <= seg_rows_max()
-// rows (IA_SEG_MAX, read once per process: 512 [default] or 256)
-int seg_rows_max();
+// segment-minimum matcher: one running minimum per (query, segment) of min(ch, 512) rows
+// (a whole number of 4-tile stages; <= 16 segments per chunk)
 static inline int db_seg_rows(long nrows) {
-    const int rpw = db_chunk_rows(nrows) / 4, cap = seg_rows_max();
-    return rpw < cap ? rpw : cap;
+    const int ch = db_chunk_rows(nrows);
+    return ch < DB_SEG_MAX ? ch : DB_SEG_MAX;
 }
 static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_rows(nrows); }
 
-struct Cand {            // one screen candidate: fp32 screen value + local row
-    float e;
-    int idx;
-};
 struct Best {            // exact winner of a (query, shard): fp64 distance + global row
     double d;
     long long idx;
@@ -57,31 +54,12 @@ struct QSel {            // per-query record of k_select: re-screen threshold, i
     int base, count;
 };
 
-// query-group split of M queries (32-query tiles, NQ tiles per group)
-struct QSplit {
-    int nq, groups, rows_pad;
-};
-// T = ceil(M/32) query tiles in groups of nq <= maxnq tiles: fewest padded tiles, then
-// the largest nq (fewest re-reads of the database).
-static inline QSplit qsplit(int M, int maxnq) {
-    const int T = (M + 31) / 32;
-    QSplit s;
-    if (T <= maxnq) {
-        s.nq = T; s.groups = 1;
-    } else {
-        int bestnq = maxnq, bestpad = 1 << 30;
-        for (int nq = maxnq; nq >= 2; --nq) {
-            int pad = (T + nq - 1) / nq * nq;
-            if (pad < bestpad) { bestpad = pad; bestnq = nq; }
-        }
-        s.nq = bestnq; s.groups = (T + bestnq - 1) / bestnq;
-    }
-    s.rows_pad = s.nq * s.groups * 32;
-    return s;
+// query rows allocated for Mmax queries: the screen reads whole groups of query tiles
+// (T = ceil(M/32) tiles in ceil(T/11) equal groups, so at most groups - 1 padding tiles)
+static inline int qrows_alloc(int Mmax) {
+    const int T = (Mmax + 31) / 32;
+    return (T + (T + 10) / 11) * 32;
 }
-constexpr int MAX_NQ = 6;
-// query rows allocated for Mmax queries: the screens read up to 2 * MAX_NQ padding tiles
-static inline int qrows_alloc(int Mmax) { return ((Mmax + 31) / 32 + 2 * MAX_NQ) * 32; }
 
 // the level state one wave of the per-pixel tail updates (ia_finish.h)
 struct FinishArgs {
@@ -103,27 +81,19 @@ __device__ __forceinline__ unsigned long long *stats_slot(unsigned long long *s,
 }
 
 // ---- launchers ------------------------------------------------------------------
-// q16 (nullable): the split-f16 query rows (Q16_ROW half8 each, ia_split16.h)
+// query rows of wave t: q64 (fp64 features), qp (fp32 rows of the exact stage's
+// re-screen), nq = |q - c|^2 and q16 (the split-f16 screen operand, Q16_ROW half8 each)
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
                       const double *center, double *q64, float *qp, double *nq,
                       const float *amax, _Float16 *q16, hipStream_t st);
 int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
                       const float *amax, _Float16 *q16, hipStream_t st);
-// screen of M queries (qp) against nrows DB rows -> cand[M][nchunks][SCREEN_K]
-// variant 0: queries in VGPRs (<= 3 tiles/wave); 1: queries in LDS (<= 6 tiles/wave)
-int launch_screen(const float *db, long nrows, const float *qp, int M, Cand *cand,
-                  hipStream_t st);
-int launch_screen_v(const float *db, long nrows, const float *qp, int M, Cand *cand,
-                    int variant, hipStream_t st);
-// exact rescore of the screen's candidates -> best[M]; stats[0..2] += (#cand, #overflow
-// chunks, #full scans) when stats != nullptr
-int launch_merge(const DbSrc &src, long row0, long nrows, const Cand *cand, int M,
-                 const double *q64, const double *nq, const float *amax, Best *best,
-                 unsigned long long *stats, hipStream_t st);
-// the whole exact matcher (screen + exact stage) with the selected algorithm
-// (IA_MATCH_ALG: 1 segment minima [default], 0 per-lane top-K); scratch of
-// match_scratch_bytes(qrows_alloc(M), nrows).  stats (segment alg): rows rescored,
-// candidate segments, full scans.
+// the split-f16 segment screen (ia_screen16.hip) of M queries over db16_of(db) ->
+// segmin[M][db_nsegs(nrows)] (screen units); q16 holds qrows_alloc(M) rows
+int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
+                    hipStream_t st);
+// the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
+// stats (nullable): rows rescored, candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);
 // ev0 / ev1 (nullable) are recorded on st immediately before / after the screen launch.
 // fin (nullable, single shard only): the exact stage also runs the per-pixel tail of the
@@ -134,21 +104,6 @@ int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const
                  hipStream_t st,
                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                  const FinishArgs *fin = nullptr);
-int fuse_finish();    // IA_FUSE_FINISH: 0 off, 1 levels <= 2^20 rows, 2 on [default]
-int match_alg();      // IA_MATCH_ALG (default 2: segment minima, split-f16 screen)
-// q16 != nullptr: the split-f16 screen (k_screen_h16) over db16_of(db)
-int launch_screen_seg(const float *db, long nrows, const float *qp, int M, float *segmin,
-                      int maxnq, hipStream_t st, const _Float16 *q16 = nullptr);
-int screen_variant();
-// split-f16 segment screen (ia_screen16.hip) over db16_of(db): flags bits 0-3 cap on
-// query tiles per wave (0 = shape rule), bit 8 per-wave kernel (no LDS sharing), bit 9 no
-// pipelined epilogue, bit 10 fragment-prefetch form, bit 11 keep the epilogue at
-// NQ = 3, bit 12 spanning form (bits 13 / 15: its no-copy diagnostics), bit 14 uneven
-// query shares, bit 16 double-buffered fragment registers,
-// bit 17 non-temporal DB stream, bit 18 balanced query shares, bit 19
-// chain-balanced stages (9..11 query tiles)
-int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
-                    int flags, hipStream_t st);
 // approximate matcher (ia_lsh.hip): best[M] from the LSH buckets of each query
 int launch_lsh_match(const IaLsh *lsh, const DbSrc &src, long row0, long nrows, int M,
                      const double *q64, const double *center, Best *best,

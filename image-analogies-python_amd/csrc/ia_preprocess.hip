@@ -11,29 +11,6 @@
 
 namespace ia {
 
-int seg_rows_max() {
-    static const int v = [] {
-        const int x = env_int("IA_SEG_MAX", 512);
-        return x == 256 ? 256 : 512;
-    }();
-    return v;
-}
-
-int target_chunks(long nrows) {
-    static const int tc = [] {
-        const int x = env_int("IA_TARGET_CHUNKS", 0);
-        return (x < 64 || x > 65536) ? 0 : x;
-    }();
-    if (tc) return tc;
-    // default: 512 chunks (one per screen slot at 2 blocks per CU): measured 4-10 % faster
-    // than 1024 at 0.5-1 M rows (a sharded c4 rank, profiles/r01_screen_bench_shard_sizes.txt),
-    // c4 level 3 (262 K rows) 37.8 -> 34.0 ms, equal at 4.19 M rows
-    // (profiles/r01_chunks_ab_end.txt); below 128 K rows both give 128-row chunks
-    (void)nrows;
-    return 512;
-}
-
-
 thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 int hip_fail(hipError_t e, const char *what) {

@@ -9,16 +9,18 @@
 // t = x + 3y in increasing t, each wave fully in parallel, reads exactly the values the
 // scanline loop reads (DESIGN.md gives the case analysis; tests/test_oracle.py checks it
 // exhaustively for small H, W).  Per wave:
-//   k_query_wave  -> q64 / qp / nq       (ia_features.hip)
-//   k_screen_seg  -> segment minima     (ia_match.hip, MFMA)
-//   k_rescore     -> best (this shard)   (ia_match.hip, exact fp64)
-//   [RCCL all-gather of best over ranks when the DB is sharded]
+//   k_query_wave  -> q64 / qp / q16 / nq        (ia_features.hip)
+//   k_screen16    -> segment minima             (ia_screen16.hip, split-f16 MFMA)
+//   k_rescore or k_select/k_items/k_gather -> the exact winner (ia_match.hip, fp64);
+//                    on one GPU the same kernel runs the per-pixel tail (ia_finish.h)
+//   sharded DB: RCCL all-gather of the per-rank winners, then
 //   k_finish      -> coherence, kappa test, B'/s/im update (this file)
 #include "ia_finish.h"
 #include "ia_split16.h"
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -88,21 +90,8 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     return off;
 }
 
-struct EventPool {
-    std::vector<hipEvent_t> ev;
-    int get(size_t n) {
-        while (ev.size() < n) {
-            hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return -1;
-            ev.push_back(e);
-        }
-        return 0;
-    }
-};
-static thread_local EventPool g_events;
-
 // executable graphs stay alive until their launch has completed (destroyed lazily at the
-// next capture, after an event wait)
+// next capture, after an event wait; ia_release_thread_resources frees them)
 struct GraphKeeper {
     hipStream_t cap = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -125,17 +114,70 @@ struct GraphKeeper {
 };
 static thread_local GraphKeeper g_graphs;
 
+// ---- profiling (IA_SYNTH_PROF): HIP events around every screen launch and the matcher
+// statistics, collected WITHOUT synchronising: events come from a process-wide pool and
+// the statistics are copied stream-ordered into pinned host memory; ia_prof_end()
+// synchronises once and reads everything back.  So a profiled level runs the same
+// launches with no host round trip (bench.py profiles its timed steps this way).
+struct ProfRec {
+    int tag;
+    long nrows;
+    double pairs;
+    size_t ev0;
+    int nscreen, timed;
+    unsigned long long *hstats;
+};
+struct ProfCollector {
+    std::mutex mu;
+    bool active = false;
+    std::vector<hipEvent_t> ev;
+    size_t next = 0;
+    std::vector<ProfRec> recs;
+    std::vector<unsigned long long *> pinned;
+    size_t pinned_next = 0;
+};
+// never destroyed: the HIP runtime may be torn down before static destructors run
+static ProfCollector *const g_prof = new ProfCollector;
+
+static bool prof_active() {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    return g_prof->active;
+}
+
+// events [*ev0, *ev0 + nev) and one pinned statistics buffer for one level call
+static int prof_reserve(size_t nev, size_t *ev0, unsigned long long **hstats) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    while (g_prof->ev.size() < g_prof->next + nev) {
+        hipEvent_t e;
+        IA_HIP(hipEventCreate(&e));
+        g_prof->ev.push_back(e);
+    }
+    *ev0 = g_prof->next;
+    g_prof->next += nev;
+    if (g_prof->pinned_next == g_prof->pinned.size()) {
+        void *p = nullptr;
+        IA_HIP(hipHostMalloc(&p, STATS_BYTES, hipHostMallocDefault));
+        g_prof->pinned.push_back(reinterpret_cast<unsigned long long *>(p));
+    }
+    *hstats = g_prof->pinned[g_prof->pinned_next++];
+    return IA_OK;
+}
+
+static hipEvent_t prof_event(size_t i) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    return g_prof->ev[i];
+}
+
+static void prof_push(const ProfRec &r) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    g_prof->recs.push_back(r);
+}
+
 // measured (tools/level_times.py, profiles/r01_level_times_graph.txt): eager launches beat
 // a captured graph on every c4 level once instantiation is counted, so capture is opt-in
 // (settable through ia_diag_set_graph_mode)
 static std::atomic<int> g_graph_mode{env_int("IA_GRAPH", 0)};
 static int graph_mode() { return g_graph_mode.load(std::memory_order_relaxed); }
-
-static unsigned long long slots_max(const std::vector<unsigned long long> &s, int i) {
-    unsigned long long m = 0;
-    for (int sl = 0; sl < STATS_SLOTS; ++sl) m = s[sl * STATS_LINE + i] > m ? s[sl * STATS_LINE + i] : m;
-    return m;
-}
 
 int comm_allgather_best(void *comm, const Best *send, Best *recv, int M, hipStream_t st);
 int comm_nranks(void *comm);
@@ -150,6 +192,61 @@ int ia_diag_set_graph_mode(int mode) {
     const int prev = graph_mode();
     if (mode >= 0 && mode <= 2) g_graph_mode.store(mode);
     return prev;
+}
+
+int ia_release_thread_resources(void) {
+    IA_HIP(g_graphs.retire());
+    if (g_graphs.cap) { IA_HIP(hipStreamDestroy(g_graphs.cap)); g_graphs.cap = nullptr; }
+    if (g_graphs.done) { IA_HIP(hipEventDestroy(g_graphs.done)); g_graphs.done = nullptr; }
+    return IA_OK;
+}
+
+int ia_prof_begin(void) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    g_prof->active = true;
+    g_prof->next = 0;
+    g_prof->pinned_next = 0;
+    g_prof->recs.clear();
+    return IA_OK;
+}
+
+int ia_prof_prepare(long nevents) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    while ((long)g_prof->ev.size() < nevents) {
+        hipEvent_t e;
+        IA_HIP(hipEventCreate(&e));
+        g_prof->ev.push_back(e);
+    }
+    return IA_OK;
+}
+
+int ia_prof_end(double *out, int maxrec) {
+    IA_HIP(hipDeviceSynchronize());
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    g_prof->active = false;
+    const int n = (int)g_prof->recs.size();
+    for (int r = 0; r < n && r < maxrec && out; ++r) {
+        const ProfRec &p = g_prof->recs[r];
+        double ms = 0.0;
+        for (int i = 0; p.timed && i < p.nscreen; ++i) {
+            float e = 0.f;
+            IA_HIP(hipEventElapsedTime(&e, g_prof->ev[p.ev0 + 2 * i], g_prof->ev[p.ev0 + 2 * i + 1]));
+            ms += e;
+        }
+        unsigned long long st[STATS_LINE] = {};
+        for (int sl = 0; sl < STATS_SLOTS; ++sl)
+            for (int i = 0; i < STATS_LINE; ++i) st[i] += p.hstats[sl * STATS_LINE + i];
+        double *o = out + (size_t)r * IA_PROF_FIELDS;
+        o[0] = p.tag;
+        o[1] = (double)p.nrows;
+        o[2] = p.pairs;
+        o[3] = p.timed ? ms : 0.0;
+        o[4] = p.timed ? p.nscreen : 0;
+        o[5] = (double)st[0];
+        o[6] = (double)st[1];
+        o[7] = (double)st[2];
+    }
+    return n;
 }
 
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks) {
@@ -184,11 +281,19 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     const ImgPair B{a->B_sm, a->B_lg, a->B_hs, a->B_ws, H, W};
     const ImgPair Bp{a->Bp_sm, a->Bp_lg, a->B_hs, a->B_ws, H, W};
     const int nw = (W - 1) + 3 * (H - 1) + 1;
-    const bool prof = a->prof != nullptr;
-    if (prof && g_events.get(2 * (size_t)nw)) { set_error("hipEventCreate failed"); return IA_E_HIP; }
+    const bool prof = (a->flags & IA_SYNTH_PROF) && prof_active();
+    size_t ev0 = 0;
+    unsigned long long *hstats = nullptr;
+    if (prof) {
+        const int rc = prof_reserve(2 * (size_t)nw, &ev0, &hstats);
+        if (rc) return rc;
+    }
     double pairs = 0.0;
     int nscreen = 0;
     bool timed = prof;
+    // fused tail (one launch + one round trip less per wave): on a single shard the exact
+    // stage's last kernel (k_rescore, or k_gather of the work list) runs the per-pixel tail
+    const bool fused = !a->comm && !a->lsh;
     auto enqueue_waves = [&](hipStream_t sq) -> int {
     for (int t = 0; t < nw; ++t) {
         const int lo_num = t - (W - 1);
@@ -198,17 +303,12 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         if (M <= 0) continue;
         int rc;
         if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
-                                    match_alg() == 2 ? ws.q16 : nullptr, sq)))
+                                    ws.q16, sq)))
             return rc;
-        hipEvent_t e0 = timed ? g_events.ev[2 * nscreen] : nullptr;
-        hipEvent_t e1 = timed ? g_events.ev[2 * nscreen + 1] : nullptr;
+        hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
+        hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
         const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
                             a->im};
-        // fused tail (one launch + one round trip less per wave): the exact stage's last
-        // kernel (k_rescore, or k_gather of the work list) runs the per-pixel tail
-        const int fm = fuse_finish();
-        const bool fused = !a->comm && !a->lsh && match_alg() >= 1 &&
-                           (fm == 2 || (fm == 1 && a->nrows <= (1L << 20)));
         if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
             if (e0) IA_HIP(hipEventRecord(e0, sq));
             if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
@@ -234,10 +334,9 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     }
     return IA_OK;
     };
-    // Small levels are launch-bound (a few us of work per wave): capture the whole wave
-    // loop into one HIP graph and launch it once (IA_GRAPH: 0 off, 1 levels of <= 2^18
-    // rows [default], 2 always).  Sharded levels stay eager (RCCL calls per wave).
-    // Kernel events cannot be timed inside a graph: captured launches are not timed.
+    // HIP-graph capture of the whole wave loop (IA_GRAPH / ia_diag_set_graph_mode: 0 off
+    // [default], 1 levels of <= 2^18 rows, 2 every single-GPU level).  Sharded levels stay
+    // eager (RCCL calls per wave).  Launches inside a graph are not timed.
     const int gm = graph_mode();
     const bool use_graph = !a->comm && !(a->flags & IA_SYNTH_EAGER) &&
                            (gm == 2 || (gm == 1 && a->nrows <= (1L << 18)));
@@ -262,32 +361,9 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         IA_HIP(hipGraphLaunch(exec, st));
         IA_HIP(g_graphs.hold(exec, st));
     }
-    if (prof) {
-        IA_HIP(hipStreamSynchronize(st));
-        double ms = 0.0;
-        const int ntimed = timed ? nscreen : 0;
-        for (int i = 0; i < ntimed; ++i) {
-            float e = 0.f;
-            IA_HIP(hipEventElapsedTime(&e, g_events.ev[2 * i], g_events.ev[2 * i + 1]));
-            ms += e;
-        }
-        std::vector<unsigned long long> slots(STATS_SLOTS * STATS_LINE);
-        IA_HIP(hipMemcpy(slots.data(), ws.stats, STATS_BYTES, hipMemcpyDeviceToHost));
-        unsigned long long st_h[STATS_LINE] = {};
-        for (int sl = 0; sl < STATS_SLOTS; ++sl)
-            for (int i = 0; i < STATS_LINE; ++i) st_h[i] += slots[sl * STATS_LINE + i];
-        a->prof[0] = ms;
-        a->prof[1] = nscreen;
-        a->prof[2] = pairs;
-        a->prof[3] = (double)st_h[0];
-        a->prof[4] = (double)st_h[1];
-        a->prof[5] = (double)st_h[2];
-        a->prof[6] = ntimed;
-        a->prof[7] = timed ? pairs : 0.0;
-        if (getenv("IA_PRUNE_PROBE"))   // diagnostic: see k_rescore
-            fprintf(stderr, "prune-probe nrows %ld queries %.0f segs %llu rows %llu c4x2 %llu c4x4 %llu "
-                    "c8x2 %llu c4x2max %llu\n", a->nrows, pairs / (double)a->nrows, st_h[1], st_h[0],
-                    st_h[3], st_h[4], st_h[5], slots_max(slots, 6));
+    if (prof) {   // read back by ia_prof_end (no synchronisation here)
+        IA_HIP(hipMemcpyAsync(hstats, ws.stats, STATS_BYTES, hipMemcpyDeviceToHost, st));
+        prof_push(ProfRec{a->tag, a->nrows, pairs, ev0, nscreen, timed ? 1 : 0, hstats});
     }
     return IA_OK;
 }

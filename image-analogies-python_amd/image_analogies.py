@@ -60,10 +60,10 @@ def level_rows(Ap_pyr_list, level):
 
 
 def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
-                         comm=None, prof=None, eager=False):
+                         comm=None, prof=False, eager=False):
     """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32.
-    eager=True: never capture the level's wave loop into a HIP graph (every screen launch
-    is then timed when prof is given)."""
+    prof=True: record this level into the open profile (_ia.prof_begin / prof_end; no
+    synchronisation).  eager=True: never capture the level's wave loop into a HIP graph."""
     dev = B_lg.device
     H, W = B_lg.shape
     s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
@@ -84,23 +84,14 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
     a.workspace = _ia.ptr(ws).value
     a.comm = comm
     a.lsh = index.lsh_ptr()
-    a.flags = _ia.IA_SYNTH_EAGER if eager else 0
-    pbuf = None
-    if prof is not None:
-        pbuf = (ctypes.c_double * 8)()
-        a.prof = ctypes.cast(pbuf, ctypes.POINTER(ctypes.c_double))
+    a.flags = (_ia.IA_SYNTH_EAGER if eager else 0) | (_ia.IA_SYNTH_PROF if prof else 0)
+    a.tag = level
     _ia.check(_ia.lib().ia_synth_level(ctypes.byref(a), _ia.stream()), 'ia_synth_level')
-    if pbuf is not None:
-        prof.append({'level': level, 'screen_ms': pbuf[0], 'screens': int(pbuf[1]),
-                     'pairs': pbuf[2], 'rows_rescored': int(pbuf[3]),
-                     'candidate_segments': int(pbuf[4]), 'full_scans': int(pbuf[5]),
-                     'timed_screens': int(pbuf[6]), 'timed_pairs': pbuf[7],
-                     'rows': index.nrows, 'pixels': H * W})
     return s, im
 
 
 def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
-                   comm=None, rank=0, nranks=1, prof=None, levels=None, lsh=None, eager=False):
+                   comm=None, rank=0, nranks=1, prof=False, levels=None, lsh=None, eager=False):
     """Synthesise levels 1..max_levels-1 (image_analogies.py:119-220) from device
     pyramids.  Bp_pyr (list of device tensors) is updated in place.  lsh: None (exact
     matcher) or LevelIndex.build_lsh arguments (approximate matcher).

@@ -11,8 +11,9 @@
  *   - return 0 on success, <0 on error (IA_E_*); ia_last_error() gives the message
  *     (thread-local).  The Python host layer raises on any non-zero return.
  *   - numerics: fp64 everywhere the reference computes in fp64, in the reference's
- *     operation order (numpy pairwise-8 sums, no FMA contraction); the matcher screens in
- *     fp32 MFMA and rescores candidates in fp64, so indices are exact.
+ *     operation order (numpy pairwise-8 sums, no FMA contraction); the matcher screens with
+ *     split-f16 MFMA (a filter with a proven error bound), re-screens the candidates in
+ *     fp32 and rescores them in fp64, so indices and distances are exact.
  */
 #ifndef IA_H
 #define IA_H
@@ -77,17 +78,19 @@ int ia_mean_f64(const double *x, long n, double *out, void *workspace, void *str
 int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, int h, int w,
                           int full, double *out, void *stream);
 
-/* ---- a10: algorithms.py:50-70 create_index — fp32 screening database for rows
- * [row0, row0 + nrows) of As[level] (= A full | A'_i half).  Each row holds IA_DP floats:
- * element k = 2s + h of (a - center, k < 55; |a - center|^2 at k = 55) at position
- * p = h*28 + s.  Storage is fragment-major for the 32x32x2 MFMA: float4 number
- * (tile*7 + v)*64 + lane holds row tile*32 + (lane & 31), positions (lane >> 5)*28 + 4v
- * .. +3.  Rows are padded to ia_db_rows_padded(nrows) with sentinel rows.
- * amax (device, 1 float) receives max_row |a - center| (atomic max; zero it first). */
+/* ---- a10: algorithms.py:50-70 create_index — the screening database for rows
+ * [row0, row0 + nrows) of As[level] (= A full | A'_i half), in two parts of one buffer:
+ *   fp32 rows (the exact stage's re-screen): IA_DP floats per row, element k = 2s + h of
+ *     (a - center, k < 55; |a - center|^2 at k = 55) at position p = h*28 + s, stored
+ *     fragment-major by 32-row tiles: float4 number (tile*7 + v)*64 + lane holds row
+ *     tile*32 + (lane & 31), positions (lane >> 5)*28 + 4v .. +3;
+ *   their split-f16 copy (the MFMA screen's operand): per 32-row tile, 7
+ *     contiguous 1 KiB register groups (224 B per row).
+ * Rows are padded to ia_db_rows_padded(nrows) (whole chunks of ia_db_chunk_rows, a multiple
+ * of 4 chunks); padding rows repeat the last real row in the split copy.  amax (device, 1
+ * float) receives max_row |a - center| (atomic max; zero it first). */
 long ia_db_rows_padded(long nrows);
-/* bytes of the db buffer ia_db_build fills: the fp32 rows above (ia_db_rows_padded x
- * IA_DP floats) followed by their split-f16 copy for the default screen (the same size
- * again). */
+/* bytes of the db buffer ia_db_build fills: 2 x 224 B per padded row */
 size_t ia_db_bytes(long nrows);
 int ia_db_chunk_rows(long nrows);
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
@@ -115,8 +118,8 @@ int ia_lsh_build(const float *db, long nrows, const IaLsh *lsh, void *stream);
 int ia_lsh_bits(long nrows);
 
 /* ---- a11: algorithms.py:73-75 best_approximate_match, batched: exact 1-NN of M
- * fp64 queries (M x 55, row stride IA_DP) over the DB rows built above (fp32 MFMA screen
- * + fp64 rescore from the src pyramids).  Outputs idx (global row, int64) and the fp64
+ * fp64 queries (M x 55, row stride IA_DP) over the DB rows built above (split-f16 MFMA
+ * screen, fp32 re-screen of the candidate segments, fp64 rescore from the src pyramids).  Outputs idx (global row, int64) and the fp64
  * distance (pairwise-8 sum of squares, the oracle's value).  lsh (nullable): use the
  * approximate LSH matcher over the same rows instead. */
 typedef struct {
@@ -163,22 +166,36 @@ typedef struct {
     int32_t *s, *im;
     void *workspace;
     void *comm;
-    /* optional profiling: when non-NULL the call synchronises at the end and writes 8
-     * doubles {sum screen-kernel ms over the timed launches, #screen launches, sum
-     * query-pixels x rows (pairs), #rows rescored, #candidate segments, #full scans,
-     * #timed launches, pairs of the timed launches}.  Launches inside a captured graph
-     * (see flags) are not timed. */
-    double *prof;
     const IaLsh *lsh;   /* NULL: exact matcher; else LSH tables of this shard's rows */
     /* IA_SYNTH_EAGER: never capture the wave loop into a HIP graph.  Capture is off by
      * default (a graph's instantiation costs more than it saves on every c4 level); the
      * environment variable IA_GRAPH=1 captures levels of <= 2^18 rows on one GPU, =2 every
-     * single-GPU level. */
+     * single-GPU level.
+     * IA_SYNTH_PROF: while a profile is open (ia_prof_begin), record HIP events around every
+     * screen launch and the matcher statistics under `tag` (no synchronisation; read back
+     * by ia_prof_end).  Launches inside a captured graph are not timed. */
     int flags;
+    int tag;
 } IaSynthArgs;
 #define IA_SYNTH_EAGER 1
+#define IA_SYNTH_PROF 2
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);
+
+/* profiling of ia_synth_level calls flagged IA_SYNTH_PROF (process-wide, thread-safe):
+ * ia_prof_begin opens a profile (the caller has synchronised); ia_prof_end synchronises the
+ * device and writes IA_PROF_FIELDS doubles per recorded level call, in call order:
+ * {tag, DB rows, (query, row) pairs, screen ms over the timed launches, #timed screen
+ * launches, #rows rescored in fp64, #candidate segments, #full scans}; returns the number
+ * of records (<0: error). */
+#define IA_PROF_FIELDS 8
+int ia_prof_begin(void);
+/* create the event pool up front (2 events per wave of every profiled level call of the
+ * profile), so that no event is created inside a timed region */
+int ia_prof_prepare(long nevents);
+int ia_prof_end(double *out, int maxrec);
+/* destroy the calling host thread's graph-capture stream and last executable graph */
+int ia_release_thread_resources(void);
 
 /* ---- multi-GPU: RCCL communicator over xGMI, one process per GPU. */
 int ia_comm_unique_id(uint8_t out[128]);

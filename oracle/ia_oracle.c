@@ -15,9 +15,13 @@
  *                 d = s*s, s = sqrt(pairwise8(((a-q)*w)^2)); coh iff d_coh <= d_app*f
  *   update        image_analogies.py:214-220
  * pairwise8 is numpy's pairwise_sum (8 accumulators for n <= 128, recursive halves
- * above).  Build: see oracle/Makefile (-O2 -ffp-contract=off: no FMA contraction).
+ * above).  Build: see oracle/Makefile (-O3 -ffp-contract=off: no FMA contraction; OpenMP
+ * splits the 1-NN scan over rows, combined in row order).
  */
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -106,18 +110,84 @@ double *ia_oracle_build_db(const IaOracleLevel *L) {
 
 void ia_oracle_free(void *p) { free(p); }
 
-/* exact 1-NN over db (N x 55): first minimum of pairwise8((a-q)^2) */
-long ia_oracle_nn(const double *db, long N, const double *q, double *dmin_out) {
-    double t[D], best = INFINITY;
+/* pairwise8((a - q)^2) for n = 55, written out: the same operations in the same order as
+ * pairwise8 above (8 accumulators over k < 48, tree combine, k = 48..54 sequential), in a
+ * form the compiler vectorises across the 8 accumulators (no reassociation: the sums are
+ * element-wise vector adds). */
+static inline double dist55(const double *a, const double *q) {
+    double r[8];
+    for (int j = 0; j < 8; j++) { double x = a[j] - q[j]; r[j] = x * x; }
+    for (int i = 8; i < 48; i += 8)
+        for (int j = 0; j < 8; j++) { double x = a[i + j] - q[i + j]; r[j] += x * x; }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int i = 48; i < D; i++) { double x = a[i] - q[i]; res += x * x; }
+    return res;
+}
+
+/* threads of the 1-NN scan (0 = OpenMP's default, i.e. OMP_NUM_THREADS) */
+static int g_threads = 1;
+void ia_oracle_set_threads(int n) { g_threads = n; }
+int ia_oracle_threads(void) {
+#ifdef _OPENMP
+    return g_threads > 0 ? g_threads : omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* first minimum over rows [lo, hi) */
+static long nn_range(const double *db, long lo, long hi, const double *q, double *best_out) {
+    double best = INFINITY;
     long bi = -1;
-    for (long i = 0; i < N; i++) {
-        const double *a = db + i * D;
-        for (int j = 0; j < D; j++) { double x = a[j] - q[j]; t[j] = x * x; }
-        double d = pairwise8(t, D);
+    for (long i = lo; i < hi; i++) {
+        double d = dist55(db + i * D, q);
         if (d < best) { best = d; bi = i; }
     }
+    *best_out = best;
+    return bi;
+}
+
+/* exact 1-NN over db (N x 55): first minimum of pairwise8((a-q)^2).  With several
+ * threads the rows are cut into contiguous blocks, each block's first minimum is taken,
+ * and the blocks are combined in row order keeping the first strict minimum: the same
+ * row as the serial scan, for any thread count. */
+long ia_oracle_nn(const double *db, long N, const double *q, double *dmin_out) {
+    int T = ia_oracle_threads();
+    if (T > 64) T = 64;
+    if (T <= 1 || N < 4096) {
+        double best;
+        long bi = nn_range(db, 0, N, q, &best);
+        if (dmin_out) *dmin_out = best;
+        return bi;
+    }
+    double bd[64];
+    long bix[64];
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+#endif
+    for (int t = 0; t < T; t++)
+        bix[t] = nn_range(db, N * t / T, N * (t + 1) / T, q, &bd[t]);
+    double best = INFINITY;
+    long bi = -1;
+    for (int t = 0; t < T; t++)
+        if (bix[t] >= 0 && bd[t] < best) { best = bd[t]; bi = bix[t]; }
     if (dmin_out) *dmin_out = best;
     return bi;
+}
+
+/* M queries (M x 55) at once: idx[m], dmin[m] (the bench's all-cores baseline and the
+ * large-database fixtures parallelise over queries) */
+void ia_oracle_nn_batch(const double *db, long N, const double *Q, long M, long *idx,
+                        double *dmin) {
+    int T = ia_oracle_threads();
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(T > 0 ? T : 1) schedule(dynamic, 1)
+#endif
+    for (long m = 0; m < M; m++) {
+        double d;
+        idx[m] = nn_range(db, 0, N, Q + m * D, &d);
+        dmin[m] = d;
+    }
 }
 
 static double wdist(const double *a, const double *q, const double *w) {

@@ -44,7 +44,31 @@ def lib():
         _lib.ia_oracle_free.argtypes = [ctypes.c_void_p]
         _lib.ia_oracle_nn.restype = ctypes.c_long
         _lib.ia_oracle_nn.argtypes = [_dp, ctypes.c_long, _dp, _dp]
+        _lib.ia_oracle_set_threads.argtypes = [ctypes.c_int]
+        _lib.ia_oracle_threads.restype = ctypes.c_int
+        _lib.ia_oracle_nn_batch.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_long,
+                                            ctypes.POINTER(ctypes.c_long), _dp]
     return _lib
+
+
+def set_threads(n):
+    """Threads of the oracle's 1-NN scan (1 = serial; 0 = OMP_NUM_THREADS).  Any count
+    gives the serial scan's result (row blocks combined in row order).  Returns the count
+    in effect."""
+    lib().ia_oracle_set_threads(int(n))
+    return lib().ia_oracle_threads()
+
+
+def nn_batch(db_ptr, N, Q):
+    """Exact 1-NN (first minimum of the pairwise-8 squared distance) of the rows of Q
+    (M x 55) over an oracle database (ia_oracle_build_db) -> (idx int64, dist fp64)."""
+    Q = np.ascontiguousarray(Q, dtype=np.float64)
+    M = Q.shape[0]
+    idx = np.empty(M, np.int64)
+    d = np.empty(M, np.float64)
+    lib().ia_oracle_nn_batch(db_ptr, N, _d(Q), M, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_long)),
+                             _d(d))
+    return idx, d
 
 
 def _d(a):

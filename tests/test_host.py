@@ -223,3 +223,53 @@ def test_shard_level_policy(monkeypatch):
     assert all(shard_level(n, 4) for n in c4)
     pyr = [[np.zeros((2, 3)), np.zeros((4, 6))], [np.zeros((2, 3)), np.zeros((4, 6))]]
     assert level_rows(pyr, 1) == 2 * 24
+
+
+def test_bench_launcher_starts_the_requested_ranks():
+    """`bench.py --gpus 2` without torch.distributed.run's environment starts 2 rank
+    processes itself (torch.distributed.run as a child); every rank checks its world size
+    against --gpus.  --dry-run: the ranks meet over gloo without touching a GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
+    out = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2',
+                          '--dry-run'], capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(line) == 1, out.stdout
+    rec = json.loads(line[0])
+    assert rec['n_gpus'] == 2 and rec['rank_sum'] == 1.0
+    # a world that does not match --gpus is refused
+    env2 = dict(env, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+    bad = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2',
+                          '--dry-run'], capture_output=True, text=True, env=env2, timeout=300)
+    assert bad.returncode != 0 and 'world size 1 != --gpus 2' in bad.stderr
+
+
+def test_threaded_oracle_scan_equals_serial():
+    """The oracle's 1-NN scan split over threads (row blocks combined in row order) gives
+    the serial scan's rows and distances, ties included."""
+    import ia_oracle_c as oc
+    rs = np.random.RandomState(3)
+    A, Aps, B = analogy_inputs(61, (70, 90), (40, 52), n_ap=2, flat=True)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=61)
+    job = oc.LevelJob(L - 1, A_pyr, Ap_list, B_pyr, Bp_pyr, o.compute_weights(3, 5, 12, 1), 1.5)
+    db = job.build_db()
+    N = 2 * A_pyr[L - 1].size
+    As = np.ctypeslib.as_array(db, shape=(N * 55,)).reshape(N, 55)
+    Q = np.vstack([As[rs.randint(0, N, 40)], As[rs.randint(0, N, 40)] + 1e-9, rs.rand(20, 55)])
+    try:
+        oc.set_threads(1)
+        i1, d1 = oc.nn_batch(db, N, Q)
+        serial = [oc.lib().ia_oracle_nn(db, N, oc._d(np.ascontiguousarray(q)), None) for q in Q]
+        oc.set_threads(5)
+        i5, d5 = oc.nn_batch(db, N, Q)
+        par = [oc.lib().ia_oracle_nn(db, N, oc._d(np.ascontiguousarray(q)), None) for q in Q]
+    finally:
+        oc.set_threads(1)
+    ref = [int(np.argmin(np.add.reduce((As - q) ** 2, axis=1))) for q in Q]
+    assert list(i1) == ref == serial == par and list(i5) == ref
+    assert np.array_equal(d1, d5)

@@ -25,7 +25,7 @@ for M in 342 256; do
     for P in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
         i=$((i+1))
         timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d "$OUT/pmc_m${M}_p$i" -o pmc -- \
-            "$R/tools/screen_bench" --M $M --variants 0x007 --reps 2 --rounds 1 > "$OUT/pmc_m${M}_p$i.txt" 2>&1
+            "$R/tools/screen_bench" --M $M --reps 2 --rounds 1 > "$OUT/pmc_m${M}_p$i.txt" 2>&1
     done
     python3 "$R/tools/pmc_summary.py" "$OUT"/pmc_m${M}_p*/pmc_counter_collection.csv > "$OUT/pmc_m$M.txt"
     echo "pmc M=$M done"

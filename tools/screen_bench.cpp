@@ -1,12 +1,11 @@
-// screen_bench — standalone A/B timing of the matcher's MFMA screen (no Python / torch),
-// also the process rocprofv3 --pmc runs against (tools/README in DESIGN.md).
+// screen_bench — standalone timing of the matcher's split-f16 MFMA screen (no Python /
+// torch), also the process rocprofv3 --pmc runs against.
 //
-//   screen_bench [--A 2048] [--M 32,64,128,256,342] [--variants 0,1] [--reps 5]
+//   screen_bench [--A 2048] [--M 32,64,128,256,342] [--reps 5] [--rounds 5]
 //
 // Builds the c4 finest-level database (A = A' smooth noise, 2048x2048 -> 4,194,304 rows)
 // with libia's own kernels, makes M queries from perturbed database pixels and times
-// ia_diag_screen per variant with HIP events.  Prints TFLOP/s of 2*55*M*N algorithmic
-// flops, and checks that every variant returns identical candidates.
+// ia_diag_screen16 with HIP events.  Prints f16 TFLOP/s of 330*M*N algorithmic flops.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,9 +19,6 @@
 
 #include "../include/ia.h"
 #include "../include/ia_diag.h"
-#ifdef IA_PROBE
-extern "C" int ia_probe_set(unsigned long long *buf);
-#endif
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -73,11 +69,10 @@ static inline int symi(int i, int n) {
 
 int main(int argc, char **argv) {
     int S = 2048, reps = 3, rounds = 5;
-    std::vector<int> Ms = {32, 64, 128, 256, 342}, vars = {0, 1};
+    std::vector<int> Ms = {32, 64, 128, 256, 342};
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--A")) S = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--M")) Ms = parse_list(argv[i + 1]);
-        else if (!strcmp(argv[i], "--variants")) vars = parse_list(argv[i + 1]);
         else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--rounds")) rounds = atoi(argv[i + 1]);
     }
@@ -142,101 +137,31 @@ int main(int argc, char **argv) {
     void *q16;
     CK(hipMalloc(&q16, (size_t)256 * qrows)); CK(hipMemset(q16, 0, (size_t)256 * qrows));
     CI(ia_diag_query_rows16(dq, Mmax, dc, amax, qp, q16, dnq, st));
-    // variant 7 (bits 4-7 cap, bit 8 uniform): the split-f16 screen
-    auto screen = [&](int M, void *out, int v) {
-        if ((v & 15) == 7)
-            CI(ia_diag_screen16(db, N, q16, M, reinterpret_cast<float *>(out), ((v >> 4) & 15) | (v & 0xfff00), st));
-        else
-            CI(ia_diag_screen(db, N, qp, M, out, v, st));
-    };
-#ifdef IA_PROBE
-    {   // rescore_probe: phase timestamps of the exact stage (k_rescore) for M queries
-        unsigned long long *probe;
-        const int NS = 64 * 4 * 16;
-        CK(hipMalloc(&probe, NS * 8));
-        const int M = Ms.back();
-        void *mw; CK(hipMalloc(&mw, ia_match_workspace_bytes(M, N)));
-        int64_t *idx; double *dist;
-        CK(hipMalloc(&idx, 8 * M)); CK(hipMalloc(&dist, 8 * M));
-        IaMatchArgs a{};
-        a.src = src; a.db = db; a.row0 = 0; a.nrows = N; a.center = dc; a.amax = amax;
-        a.q64 = dq; a.M = M; a.idx = idx; a.dist = dist; a.workspace = mw; a.lsh = nullptr;
-        for (int rep = 0; rep < reps + 1; ++rep) {
-            CK(hipMemset(probe, 0, NS * 8));
-            CI(ia_probe_set(probe));
-            CI(ia_match_batch(&a, st));
-            CK(hipStreamSynchronize(st));
-            CI(ia_probe_set(nullptr));
-            std::vector<unsigned long long> h(NS);
-            CK(hipMemcpy(h.data(), probe, h.size() * 8, hipMemcpyDeviceToHost));
-            if (rep == 0) continue;   // warm-up
-            const int nb = M < 64 ? M : 64;
-            unsigned long long t0 = ~0ULL;
-            for (int b = 0; b < nb; ++b) if (h[b * 64]) t0 = std::min(t0, h[b * 64]);
-            printf("M=%d rep %d: wall_clock64 @100 MHz; us after the block's wave-0 mark 0; "
-                   "mean / max over %d blocks\n", M, rep, nb);
-            for (int i = 1; i < 16; ++i) {
-                printf("  mark %2d:", i);
-                bool any = false;
-                for (int w = 0; w < 4; ++w) {
-                    double sum = 0, mx = 0; int n = 0;
-                    for (int b = 0; b < nb; ++b) {
-                        const unsigned long long x = h[(b * 4 + w) * 16 + i], s0 = h[b * 64];
-                        if (!x || !s0) continue;
-                        const double d = ((double)x - (double)s0) / 100.0;
-                        sum += d; mx = std::max(mx, d); ++n;
-                    }
-                    if (n) { printf("  w%d %6.2f/%6.2f", w, sum / n, mx); any = true; }
-                    else printf("  w%d      -/     -", w);
-                }
-                printf("%s\n", any ? "" : "  (unused)");
-            }
-            double sk = 0;
-            for (int b = 0; b < nb; ++b) sk = std::max(sk, (h[b * 64] - t0) / 100.0);
-            printf("  block start skew: %.2f us\n", sk);
-        }
-        return 0;
-    }
-#endif
-    const size_t cb = ia_diag_cand_bytes(Mmax, N);
-    char *cand, *cand_ref;
-    CK(hipMalloc(&cand, cb)); CK(hipMalloc(&cand_ref, cb));
-    std::vector<char> h1(cb), h2(cb);
+    const long npad = ia_db_rows_padded(N);
+    const int ch = ia_db_chunk_rows(N);
+    const long nseg = npad / (ch < 512 ? ch : 512);
+    float *segmin;
+    CK(hipMalloc(&segmin, sizeof(float) * (size_t)qrows * nseg));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    printf("N=%ld rows, DB %.1f MB; %d interleaved rounds x %d reps per variant\n", N,
-           N * IA_DP * 4 / 1e6, rounds, reps);
+    printf("N=%ld rows, split-f16 DB %.1f MB; %d rounds x %d reps\n", N, npad * 224 / 1e6, rounds, reps);
     for (int M : Ms) {
-        std::vector<std::vector<float>> t(vars.size());
-        for (size_t vi = 0; vi < vars.size(); ++vi)       // warm-up + result check
-            screen(M, vi == 0 ? cand_ref : cand, vars[vi]);
-        for (int rd = 0; rd < rounds; ++rd)
-            for (size_t vi = 0; vi < vars.size(); ++vi) {
-                char *out = vi == 0 ? cand_ref : cand;
-                CK(hipEventRecord(e0, st));
-                for (int r = 0; r < reps; ++r) screen(M, out, vars[vi]);
-                CK(hipEventRecord(e1, st));
-                CK(hipEventSynchronize(e1));
-                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-                t[vi].push_back(ms / reps);
-            }
-        for (size_t vi = 0; vi < vars.size(); ++vi) {
-            std::vector<float> v = t[vi];
-            std::sort(v.begin(), v.end());
-            const float med = v[v.size() / 2], mn = v[0];
-            const double tf = 2.0 * 55 * M * (double)N / (med * 1e-3) / 1e12;
-            long diff = 0;
-            if (vi > 0 && (vars[vi] & 15) == (vars[0] & 15)) {
-                screen(M, cand_ref, vars[0]);
-                screen(M, cand, vars[vi]);
-                CK(hipStreamSynchronize(st));
-                CK(hipMemcpy(h1.data(), cand_ref, cb, hipMemcpyDeviceToHost));
-                CK(hipMemcpy(h2.data(), cand, cb, hipMemcpyDeviceToHost));
-                const size_t used = (size_t)M * cb / ia_diag_qp_rows(Mmax);
-                for (size_t i = 0; i < used && i < cb; ++i) diff += h1[i] != h2[i];
-            }
-            printf("variant 0x%03x M %4d  median %9.1f us  min %9.1f us  %6.1f TFLOP/s  %5.1f%% of 157.3  out-diff %ld\n",
-                   vars[vi], M, med * 1e3, mn * 1e3, tf, 100 * tf / 157.3, diff);
+        CI(ia_diag_screen16(db, N, q16, M, segmin, st));   // warm-up
+        std::vector<float> t;
+        for (int rd = 0; rd < rounds; ++rd) {
+            CK(hipEventRecord(e0, st));
+            for (int r = 0; r < reps; ++r) CI(ia_diag_screen16(db, N, q16, M, segmin, st));
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            t.push_back(ms / reps);
         }
+        std::sort(t.begin(), t.end());
+        const float med = t[t.size() / 2], mn = t[0];
+        // 330 f16 flop per (query, row) pair (3 split products x 55 features x 2)
+        const double tf = 330.0 * M * (double)N / (med * 1e-3) / 1e12;
+        const double peak = 4096.0 * 256 * 2.4e9 / 1e12;
+        printf("screen M %4d  median %9.1f us  min %9.1f us  %7.1f TFLOP/s f16  %5.1f%% of %.0f\n",
+               M, med * 1e3, mn * 1e3, tf, 100 * tf / peak, peak);
         fflush(stdout);
     }
     return 0;
