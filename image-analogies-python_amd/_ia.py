@@ -52,7 +52,8 @@ class IaSynthArgs(ctypes.Structure):
                 ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
                 ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
                 ('workspace', _dp), ('comm', _dp), ('lsh', ctypes.POINTER(IaLsh)),
-                ('flags', ctypes.c_int), ('tag', ctypes.c_int)]
+                ('flags', ctypes.c_int), ('tag', ctypes.c_int), ('dbg_px', _dp),
+                ('dbg_dist', _dp)]
 
 
 IA_SYNTH_EAGER = 1

@@ -10,6 +10,7 @@ namespace ia {
 struct CohSel {
     long long wix;       // winning candidate's DB row
     int wr, wc, wim;     // its pixel and A' image
+    int rr, rc;          // r*: the B' pixel whose source it continues
     int valid;           // 0: no candidate (first pixel of the level, or none in range)
     double dcoh;         // its weighted distance to the query
 };
@@ -25,7 +26,7 @@ __device__ __forceinline__ void fin_best(double &bd, long long &bi, double d, lo
 // Result valid in every lane.
 __device__ __forceinline__ CohSel coh_pick(const DbSrc &src, int m, const FinishArgs &f,
                                            const double *qs, int lane) {
-    CohSel r{0, 0, 0, 0, 0, 0.0};
+    CohSel r{0, 0, 0, 0, 0, 0, 0, 0.0};
     const int y = f.y_lo + m, x = f.t - 3 * y;
     if (y == 0 && x == 0) return r;
     const int W = f.W;
@@ -61,6 +62,8 @@ __device__ __forceinline__ CohSel coh_pick(const DbSrc &src, int m, const Finish
     r.wr = __shfl(cr, win);
     r.wc = __shfl(cc, win);
     r.wim = __shfl(cim, win);
+    r.rr = y - 2 + win / 5;
+    r.rc = x - 2 + win % 5;
     r.valid = 1;
     double d = 0.0;
     if (lane == 1) d = row_wdist(src, r.wix, qs, f.weights);
@@ -83,7 +86,9 @@ __device__ __forceinline__ double app_wdist(const DbSrc &src, long long app, con
 
 // The rest of the tail: the kappa test (image_analogies.py:200-211) of the coherence
 // candidate c against the exact-match winner app (weighted distance d_app, app_wdist), and
-// the B' / s / im update (:213-217).
+// the B' / s / im update (:213-217).  With the debug outputs (image_analogies.py:141-159,
+// 222-240): per pixel {p_app row, col, p_coh row, col, r* row, col, has coherence} and
+// {d_app, d_coh} (zeros where there is no coherence candidate, as the reference).
 __device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, int m,
                                              const FinishArgs &f, const CohSel &c, double d_app,
                                              int lane) {
@@ -100,6 +105,18 @@ __device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, in
     }
     if (lane == 0) {
         const long q = (long)y * W + x;
+        if (f.dbg_px) {
+            int32_t *o = f.dbg_px + 7 * q;
+            o[0] = (int32_t)(rem / Aw);
+            o[1] = (int32_t)(rem - (long)(rem / Aw) * Aw);
+            o[2] = c.valid ? c.wr : 0;
+            o[3] = c.valid ? c.wc : 0;
+            o[4] = c.valid ? c.rr : 0;
+            o[5] = c.valid ? c.rc : 0;
+            o[6] = c.valid;
+            f.dbg_dist[2 * q] = c.valid ? d_app : 0.0;
+            f.dbg_dist[2 * q + 1] = c.valid ? c.dcoh : 0.0;
+        }
         f.Bp_lg[q] = src.Ap.lg[img * hw + (long)pr * Aw + pc];
         f.s[2 * q] = pr;
         f.s[2 * q + 1] = pc;

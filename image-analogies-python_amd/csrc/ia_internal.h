@@ -69,6 +69,8 @@ struct FinishArgs {
     double kappa_factor;
     double *Bp_lg;
     int32_t *s, *im;
+    int32_t *dbg_px;     // nullable: 7 int32 per pixel (ia.h IaSynthArgs)
+    double *dbg_dist;    // nullable: 2 doubles per pixel
 };
 
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS

@@ -265,6 +265,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     IA_ARG(a->B_hs == (a->H + 1) / 2 && a->B_ws == (a->W + 1) / 2, "ia_synth_level: B level shapes");
     IA_ARG(a->src.A_hs == (a->src.Ah + 1) / 2 && a->src.A_ws == (a->src.Aw + 1) / 2,
            "ia_synth_level: A level shapes");
+    IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level: debug outputs come in pairs");
     const int nranks = a->comm ? comm_nranks(a->comm) : 1;
     IA_ARG(nranks >= 1, "ia_synth_level: bad communicator");
     hipStream_t st = S(stream);
@@ -308,7 +309,7 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
         hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
         const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
-                            a->im};
+                            a->im, a->dbg_px, a->dbg_dist};
         if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
             if (e0) IA_HIP(hipEventRecord(e0, sq));
             if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,

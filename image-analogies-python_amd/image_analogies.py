@@ -60,14 +60,20 @@ def level_rows(Ap_pyr_list, level):
 
 
 def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
-                         comm=None, prof=False, eager=False):
-    """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32.
-    prof=True: record this level into the open profile (_ia.prof_begin / prof_end; no
-    synchronisation).  eager=True: never capture the level's wave loop into a HIP graph."""
+                         comm=None, prof=False, eager=False, debug=False):
+    """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32,
+    plus with debug=True the per-pixel debug record (dbg_px (H*W, 7) int32, dbg_dist
+    (H*W, 2) fp64; include/ia.h).  prof=True: record this level into the open profile
+    (_ia.prof_begin / prof_end; no synchronisation).  eager=True: never capture the
+    level's wave loop into a HIP graph."""
     dev = B_lg.device
     H, W = B_lg.shape
     s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
     im = torch.empty(H * W, dtype=torch.int32, device=dev)
+    dbg_px = dbg_dist = None
+    if debug:
+        dbg_px = torch.zeros((H * W, 7), dtype=torch.int32, device=dev)
+        dbg_dist = torch.zeros((H * W, 2), dtype=torch.float64, device=dev)
     nranks = _ia.lib().ia_comm_nranks(comm) if comm else 1
     ws = _ia.workspace(_ia.lib().ia_synth_workspace_bytes(H, W, index.nrows, nranks))
     a = _ia.IaSynthArgs()
@@ -86,7 +92,10 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
     a.lsh = index.lsh_ptr()
     a.flags = (_ia.IA_SYNTH_EAGER if eager else 0) | (_ia.IA_SYNTH_PROF if prof else 0)
     a.tag = level
+    a.dbg_px, a.dbg_dist = _ia.ptr(dbg_px).value, _ia.ptr(dbg_dist).value
     _ia.check(_ia.lib().ia_synth_level(ctypes.byref(a), _ia.stream()), 'ia_synth_level')
+    if debug:
+        return s, im, (dbg_px, dbg_dist)
     return s, im
 
 
@@ -212,10 +221,63 @@ def color_output(level, Bp_lvl, s, im, color_pyr_list, c):
     return vals.cpu().numpy()
 
 
-def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False):
+def debug_record(s, im, dbg, shape):
+    """The reference's per-level debug structures (image_analogies.py:141-159, 222-247)
+    from a level's device debug record: the lists sa, sc, rstars, s, im (its pickle) and
+    the maps p_src (colour code), app_dist, coh_dist, img_src."""
+    H, W = shape
+    s = s.cpu().numpy()
+    im = im.cpu().numpy()
+    px = dbg[0].cpu().numpy()
+    dd = dbg[1].cpu().numpy()
+    sa = [(int(r), int(c)) for r, c in px[:, 0:2]]
+    sc = [(int(r), int(c)) for r, c in px[:, 2:4]]
+    rstars = [(int(r), int(c)) for r, c in px[:, 4:6]]
+    has = px[:, 6].astype(bool)
+    app_color, coh_color, err_color = np.array([1, 0, 0]), np.array([1, 1, 0]), np.array([0, 0, 0])
+    p_src = np.empty((H * W, 3))
+    is_coh = np.all(s == px[:, 2:4], axis=1)            # np.allclose(p, p_coh)
+    is_app = np.all(s == px[:, 0:2], axis=1)
+    p_src[has & is_coh] = coh_color
+    p_src[has & ~is_coh & is_app] = app_color
+    p_src[~has] = err_color
+    if np.any(has & ~is_coh & ~is_app):
+        raise RuntimeError('debug record: a pixel took neither p_app nor p_coh')
+    with np.errstate(invalid='ignore', divide='ignore'):
+        img_src = (im.astype(np.float64) / np.max(im)).reshape(H, W)
+    return {'sa': sa, 'sc': sc, 'rstars': rstars,
+            's': [(int(r), int(c)) for r, c in s], 'im': [int(i) for i in im],
+            'p_src': p_src.reshape(H, W, 3), 'app_dist': dd[:, 0].reshape(H, W),
+            'coh_dist': dd[:, 1].reshape(H, W), 'img_src': img_src}
+
+
+def save_debug(out_path, level, rec, Bp_level):
+    """image_analogies.py:242-253: the per-level maps as borderless .eps images and the
+    [sa, sc, rstars, s, im] lists (pickle, as the reference; also .npz arrays)."""
+    import pickle
+    import matplotlib.pyplot as plt
+    paths = ['%d_psrc.eps' % level, '%d_appdist.eps' % level, '%d_cohdist.eps' % level,
+             '%d_output.eps' % level, '%d_imgsrc.eps' % level]
+    maps = [rec['p_src'], rec['app_dist'], rec['coh_dist'], Bp_level, rec['img_src']]
+    for path, var in zip(paths, maps):
+        fig = plt.imshow(var, interpolation='nearest', cmap='gray')
+        ip.savefig_noborder(out_path + path, fig)
+        plt.close()
+    with open(out_path + '%d_srcs.pickle' % level, 'wb') as f:
+        pickle.dump([rec['sa'], rec['sc'], rec['rstars'], rec['s'], rec['im']], f)
+    np.savez(out_path + '%d_srcs.npz' % level, sa=np.array(rec['sa'], np.int32),
+             sc=np.array(rec['sc'], np.int32), rstars=np.array(rec['rstars'], np.int32),
+             s=np.array(rec['s'], np.int32), im=np.array(rec['im'], np.int32),
+             app_dist=rec['app_dist'], coh_dist=rec['coh_dist'])
+
+
+def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False,
+                         outputs=None):
     """Full run (image_analogies.py:97-268): setup, per-level synthesis on device, colour
-    output images.  debug=True also saves each level's index maps as
-    ``%d_s.npy`` / ``%d_im.npy`` (the s / im lists of the reference's debug pickle)."""
+    output images.  debug=True also writes the reference's debug structures per level
+    (save_debug).  outputs (dict, optional) receives per level {'color': the RGB image
+    before plt.imsave, 's', 'im', and with debug 'debug': debug_record(...)}.  Returns the
+    B' pyramid (numpy)."""
     import matplotlib.pyplot as plt
     begin_time = start_time = time.time()
     if not os.path.exists(out_path):
@@ -237,12 +299,18 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
         print('Computing level %d of %d' % (level, c.max_levels - 1))
         index = algorithms.level_index(A_pyr, Ap_pyr_list, level,
                                        lsh=algorithms.lsh_params(c))
-        s, im = synthesize_level_dev(level, c.max_levels, index, B_pyr[level - 1], B_pyr[level],
-                                     Bp_pyr[level - 1], Bp_pyr[level], weights, c.k)
+        res = synthesize_level_dev(level, c.max_levels, index, B_pyr[level - 1], B_pyr[level],
+                                   Bp_pyr[level - 1], Bp_pyr[level], weights, c.k, debug=debug)
+        s, im = res[0], res[1]
         color_im_out = color_output(level, Bp_pyr[level], s, im, color_pyr_list, c)
+        rec = None
         if debug:
-            np.save(out_path + '%d_s.npy' % level, s.cpu().numpy())
-            np.save(out_path + '%d_im.npy' % level, im.cpu().numpy())
+            rec = debug_record(s, im, res[2], Bp_pyr[level].shape[:2])
+            save_debug(out_path, level, rec, Bp_pyr[level].cpu().numpy())
+        if outputs is not None:
+            outputs[level] = {'color': color_im_out, 's': s.cpu().numpy(), 'im': im.cpu().numpy()}
+            if rec is not None:
+                outputs[level]['debug'] = rec
         plt.imsave(out_path + 'level_%d_color.jpg' % level, color_im_out)
         plt.imsave(out_path + out_path.split('/')[-2] + '.jpg', color_im_out)
         print('Level %d time: %f' % (level, time.time() - start_time))

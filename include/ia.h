@@ -176,6 +176,11 @@ typedef struct {
      * by ia_prof_end).  Launches inside a captured graph are not timed. */
     int flags;
     int tag;
+    /* optional debug outputs (image_analogies.py:141-159, 222-253; both or neither):
+     * dbg_px: H*W x 7 int32 {p_app row, col, p_coh row, col, r* row, col, has coherence
+     * candidate}; dbg_dist: H*W x 2 fp64 {d_app, d_coh} (zeros without a candidate) */
+    int32_t *dbg_px;
+    double *dbg_dist;
 } IaSynthArgs;
 #define IA_SYNTH_EAGER 1
 #define IA_SYNTH_PROF 2

@@ -419,18 +419,23 @@ def kappa_factor(level, max_levels, k):
 # ----------------------------------------------------------------------------------
 
 def synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, As_level,
-                     weights, k, matcher=None):
+                     weights, k, matcher=None, debug=None):
     """image_analogies.py:130-220 for ONE level, scanline order, luminance only.
     Updates Bp_pyr[level] in place; returns (s, im) as int arrays (H*W, 2), (H*W,).
     matcher: q -> row (default: the exact best_approximate_match; an LshIndex's match
-    for the LSH variant)."""
+    for the LSH variant).  debug (dict, optional) receives the reference's debug lists
+    and maps (image_analogies.py:141-159, 222-240): sa, sc, rstars, app_dist, coh_dist."""
     imh, imw = Bp_pyr[level].shape[:2]
     A_h, A_w = Ap_pyr_list[0][level].shape[:2]
     Bfeat = level_features(B_pyr[level - 1], B_pyr[level], True)
     factor = kappa_factor(level, max_levels, k)
     s, im = [], []
+    if debug is not None:
+        sa, sc, rstars = [], [], []
+        app_dist, coh_dist = np.zeros((imh, imw)), np.zeros((imh, imw))
     for row in range(imh):
         for col in range(imw):
+            p_coh = r_star = None
             q = np.hstack([Bfeat[row * imw + col],
                            extract_pixel_feature(Bp_pyr[level - 1], Bp_pyr[level],
                                                  (row, col), False)])
@@ -440,8 +445,8 @@ def synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, As_le
             if len(s) < 1:
                 p, i = p_app, i_app
             else:
-                p_coh, i_coh, _ = best_coherence_match(As_level, (A_h, A_w), q, s, im,
-                                                       (row, col), imw)
+                p_coh, i_coh, r_star = best_coherence_match(As_level, (A_h, A_w), q, s, im,
+                                                            (row, col), imw)
                 if p_coh == (-1, -1):
                     p, i = p_app, i_app
                 else:
@@ -455,6 +460,18 @@ def synthesize_level(level, max_levels, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, As_le
             Bp_pyr[level][row, col] = Ap_pyr_list[i][level][p[0], p[1]]
             s.append((int(p[0]), int(p[1])))
             im.append(int(i))
+            if debug is not None:
+                sa.append((int(p_app[0]), int(p_app[1])))
+                if len(s) > 1 and tuple(p_coh) != (-1, -1):
+                    sc.append((int(p_coh[0]), int(p_coh[1])))
+                    rstars.append((int(r_star[0]), int(r_star[1])))
+                    app_dist[row, col] = d_app
+                    coh_dist[row, col] = d_coh
+                else:
+                    sc.append((0, 0))
+                    rstars.append((0, 0))
+    if debug is not None:
+        debug.update(sa=sa, sc=sc, rstars=rstars, app_dist=app_dist, coh_dist=coh_dist)
     return np.array(s, dtype=np.int32).reshape(-1, 2), np.array(im, dtype=np.int32)
 
 

@@ -138,3 +138,19 @@ def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels
         Bp_pyr[level] = job.Bp_lg.reshape(Bp_pyr[level].shape)
         out[level] = (Bp_pyr[level].copy(), job.s.copy(), job.im.copy())
     return out
+
+
+class LevelDB:
+    """The oracle's As[level] (algorithms.py:50-70: [A full | A'_i half] rows, fp64) built
+    by the C oracle; ``rows`` is a numpy view (N x 55) valid while this object lives."""
+
+    def __init__(self, level, A_pyr, Ap_pyr_list):
+        dummy = [np.zeros((2, 2))] * (level + 1)
+        self._job = LevelJob(level, A_pyr, Ap_pyr_list, dummy, dummy, np.zeros(55), 1.0)
+        self.ptr = self._job.build_db()
+        self.N = self._job.Ap_lg.size
+        self.rows = np.ctypeslib.as_array(self.ptr, shape=(self.N * 55,)).reshape(self.N, 55)
+
+    def nn(self, Q):
+        """Exact 1-NN rows and distances of Q (M x 55)."""
+        return nn_batch(self.ptr, self.N, Q)

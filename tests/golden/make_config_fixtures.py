@@ -1,0 +1,86 @@
+"""Golden fixtures of the BASELINE configs, computed HERE (CPU) by the C oracle
+(oracle/ia_oracle.c: the reference's scanline loop, image_analogies.py:130-220, with the
+exact brute-force matcher, algorithms.py:73-75 restated):
+
+  c3_oracle.npz   config c3 at full size (362x638 A = A' blur, B, kappa 25, 5-level cap,
+                  bench.py's seeded synthetic inputs): per synthesized level the index
+                  maps s, im and the SHA-256 of B' (float64 bytes, C order).
+  c4_queries.npz  config c4's finest level (A = A' 2048x2048, 4,194,304 database rows):
+                  fp64 queries captured from a GPU synthesis (tools/capture_c4_queries.py,
+                  committed as c4_queries_in.npz) plus synthetic near-ties, with the
+                  oracle's exact 1-NN row and distance over the full database.
+
+Usage:  python tests/golden/make_config_fixtures.py c3|c4 [threads]
+The inputs are rebuilt from bench.py's workload definitions, so the GPU tests regenerate
+them identically on the box.
+"""
+import hashlib
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+sys.path.insert(0, ROOT)
+
+import ia_oracle as o      # noqa: E402
+import ia_oracle_c as oc   # noqa: E402
+
+
+def workload(name):
+    """(A, [A'], B, kappa, levels cap, B' init seed) of a bench.py config, job seed 0."""
+    import bench
+    conf = bench.CONFIGS[name]
+    A, Ap, B = bench.make_inputs(conf, 0)
+    return A, [Ap], B, conf['k'], conf['levels'], 2
+
+
+def bp_hash(x):
+    return hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest()
+
+
+def make_c3():
+    A, Aps, B, k, cap, seed = workload('c3')
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, cap=cap, seed=seed)
+    w = o.compute_weights(3, 5, 12, 1)
+    t0 = time.time()
+    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w)
+    print('c3 oracle: %d levels in %.1f s' % (len(out), time.time() - t0))
+    rec = {'max_levels': np.int32(L)}
+    for l, (bp, s, im) in out.items():
+        rec['s%d' % l] = s.astype(np.int16)
+        rec['im%d' % l] = im.astype(np.uint8)
+        rec['bp_sha%d' % l] = np.array(bp_hash(bp))
+        rec['bp_sum%d' % l] = np.float64(bp.sum())
+    np.savez_compressed(os.path.join(HERE, 'c3_oracle.npz'), **rec)
+
+
+def make_c4():
+    A, Aps, B, k, cap, seed = workload('c4')
+    A_pyr = o.compute_gaussian_pyramid(A, 3, cap)
+    Ap_pyr = o.compute_gaussian_pyramid(Aps[0], 3, cap)
+    level = len(A_pyr) - 1
+    cap_in = np.load(os.path.join(HERE, 'c4_queries_in.npz'))
+    Q = cap_in['q']
+    rs = np.random.RandomState(44)
+    db = oc.LevelDB(level, A_pyr, [Ap_pyr])
+    As = db.rows
+    N = db.N
+    # near ties: exact database rows, and rows nudged by 1 ulp-scale noise
+    rows = rs.randint(0, N, 32)
+    Qt = np.vstack([As[rows], As[rows[:32]] + rs.randn(32, 55) * 1e-12])
+    Qall = np.vstack([Q, Qt])
+    t0 = time.time()
+    idx, d = db.nn(Qall)
+    print('c4 oracle: %d queries over %d rows in %.1f s' % (len(Qall), N, time.time() - t0))
+    np.savez_compressed(os.path.join(HERE, 'c4_queries.npz'), q=Qall, idx=idx, dist=d,
+                        pixels=cap_in['pixels'], n_captured=np.int32(len(Q)))
+
+
+if __name__ == '__main__':
+    if len(sys.argv) > 2:
+        oc.set_threads(int(sys.argv[2]))
+    {'c3': make_c3, 'c4': make_c4}[sys.argv[1]]()

@@ -1,0 +1,154 @@
+"""Parity at the BASELINE configs' own sizes (bench.py's workload definitions, seeded):
+
+  c3  362x638, kappa 25, 5-level cap: every level's s / im / B' bit-exact against the C
+      oracle's full scanline run (tests/golden/c3_oracle.npz, make_config_fixtures.py c3)
+  c4  A = A' 2048x2048 x B 1024x1024: (1) the matcher over the 4,194,304-row finest
+      database against the oracle's exact 1-NN of 500+ queries captured from a GPU
+      synthesis plus near-ties (tests/golden/c4_queries.npz); (2) the whole synthesis,
+      spot-checked: at hundreds of border / interior pixels of the two largest levels the
+      reference's decision is re-derived from the run's own state with the oracle
+      (tests/spotcheck.py) and must equal what the GPU wrote; B' == A'[im][s] everywhere
+  c2  180x117, kappa 5, LSH matcher: every level bit-exact against the oracle's scanline
+      loop driven by the same LSH tables (oracle LshIndex)
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import ia_oracle as o
+import ia_oracle_c as oc
+import spotcheck
+from conftest import ROOT, golden
+
+pytestmark = pytest.mark.gpu
+
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _bench():
+    import bench
+    return bench
+
+
+def _job(name, **kw):
+    bench = _bench()
+    return bench.Job(bench.CONFIGS[name], 0, torch.device('cuda', 0), **kw)
+
+
+def _pyr(job, img):
+    import config as cfg
+    import img_preprocess as ip
+    return ip.gaussian_pyramid_dev(img, cfg.n_sm, job.levels)
+
+
+def _threads():
+    env = os.environ.get('OMP_NUM_THREADS', '')
+    return max(1, min(16, int(env) if env.isdigit() else (os.cpu_count() or 1)))
+
+
+def test_c3_full_size_bit_exact_vs_oracle(gpu):
+    g = golden('c3_oracle.npz')
+    job = _job('c3')
+    out = job.step()
+    torch.cuda.synchronize()
+    assert job.max_levels == int(g['max_levels'])
+    assert sorted(out) == list(range(1, job.max_levels))
+    for l, (s, im) in out.items():
+        assert np.array_equal(s.cpu().numpy(), g['s%d' % l].astype(np.int32)), l
+        assert np.array_equal(im.cpu().numpy(), g['im%d' % l].astype(np.int32)), l
+        bp = job.Bp[l].cpu().numpy()
+        assert hashlib.sha256(np.ascontiguousarray(bp).tobytes()).hexdigest() == str(g['bp_sha%d' % l]), l
+
+
+def test_c4_matcher_vs_oracle_fixture(gpu):
+    """The exact matcher over c4's full finest database (4,194,304 rows) against the
+    oracle's brute force, bit-exact in row and distance."""
+    import algorithms
+    g = golden('c4_queries.npz')
+    job = _job('c4')
+    level = job.max_levels - 1
+    A_pyr, Ap_pyr = _pyr(job, job.A), _pyr(job, job.Ap)
+    index = algorithms.level_index(A_pyr, [Ap_pyr], level)
+    assert index.N == 4194304
+    gi, gd = index.match(g['q'])
+    gi, gd = gi.cpu().numpy(), gd.cpu().numpy()
+    bad = np.nonzero((gi != g['idx']) | (gd != g['dist']))[0]
+    assert len(bad) == 0, (len(bad), bad[:10])
+
+
+def _spot_check(job, out, level, n_rand, seed):
+    import config as cfg
+    A_pyr = [p.cpu().numpy() for p in _pyr(job, job.A)]
+    Ap_pyr = [p.cpu().numpy() for p in _pyr(job, job.Ap)]
+    B_pyr = [p.cpu().numpy() for p in _pyr(job, job.B)]
+    Bp = [p.cpu().numpy() for p in job.Bp]
+    init = job.Bp_init[level].cpu().numpy()
+    s = out[level][0].cpu().numpy()
+    im = out[level][1].cpu().numpy()
+    H, W = B_pyr[level].shape
+    px = spotcheck.sample_pixels(H, W, np.random.RandomState(seed), n_rand)
+    Q = spotcheck.queries(B_pyr, Bp, init, level, px)
+    db = oc.LevelDB(level, A_pyr, [Ap_pyr])
+    try:
+        oc.set_threads(_threads())
+        app, _ = db.nn(Q)
+    finally:
+        oc.set_threads(1)
+    w = cfg.compute_weights(3, 5, 12, 1)
+    f = 1 + (2.0 ** (level - job.max_levels)) * job.k
+    A_shape = A_pyr[level].shape
+    wrong = []
+    for (y, x), q, a in zip(px, Q, app):
+        exp = spotcheck.decide(db.rows, A_shape, q, a, s, im, y, x, W, w, f)
+        got = (int(s[y * W + x, 0]), int(s[y * W + x, 1]), int(im[y * W + x]))
+        if exp != got:
+            wrong.append(((y, x), exp, got))
+    return len(px), wrong
+
+
+def test_c4_full_synthesis_spot_check(gpu):
+    job = _job('c4')
+    out = job.step()
+    torch.cuda.synchronize()
+    Ap_pyr = _pyr(job, job.Ap)
+    for l, (s, im) in out.items():     # B' == A'[im][s] at every pixel of every level
+        src = Ap_pyr[l]
+        assert torch.equal(job.Bp[l].flatten(), src[s[:, 0].long(), s[:, 1].long()]), l
+        assert int(im.max().item()) == 0 and int(im.min().item()) == 0
+    for level, n_rand, seed in ((job.max_levels - 1, 240, 7), (job.max_levels - 2, 120, 8)):
+        n, wrong = _spot_check(job, out, level, n_rand, seed)
+        assert not wrong, (level, n, wrong[:5])
+
+
+def test_c2_lsh_full_size_vs_oracle(gpu):
+    """c2 (180x117, kappa 5) with c.matcher = 'lsh' (bench.py --matcher lsh defaults):
+    every level's s / im / B' equal the oracle's scanline loop driven by the same tables."""
+    import algorithms
+    import image_analogies as ia
+    lsh = dict(tables=16, hashes=4, width=1.0, seed=0)
+    job = _job('c2', lsh=lsh)
+    A_d, Ap_d, B_d = _pyr(job, job.A), _pyr(job, job.Ap), _pyr(job, job.B)
+    A_pyr = [p.cpu().numpy() for p in A_d]
+    Ap_list = [[p.cpu().numpy() for p in Ap_d]]
+    B_pyr = [p.cpu().numpy() for p in B_d]
+    Bp_d = [x.clone() for x in job.Bp_init]
+    Bp_ref = [x.cpu().numpy() for x in job.Bp_init]
+    w = o.compute_weights(3, 5, 12, 1)
+    As = o.create_index(A_pyr, Ap_list, job.max_levels)
+    for level in range(1, job.max_levels):
+        index = algorithms.level_index(A_d, [Ap_d], level, lsh=lsh)
+        s, im = ia.synthesize_level_dev(level, job.max_levels, index, B_d[level - 1], B_d[level],
+                                        Bp_d[level - 1], Bp_d[level], job.weights, job.k)
+        h = index.lsh
+        table = o.LshIndex(As[level], index.center.cpu().numpy(), index.lsh_proj_host, h.L, h.k,
+                           np.float32(h.w))
+        rs_, rim = o.synthesize_level(level, job.max_levels, A_pyr, Ap_list, B_pyr, Bp_ref,
+                                      As[level], w, job.k, matcher=lambda q: table.match(q)[0][0])
+        assert np.array_equal(s.cpu().numpy(), rs_), level
+        assert np.array_equal(im.cpu().numpy(), rim), level
+        assert np.array_equal(Bp_d[level].cpu().numpy(), Bp_ref[level]), level

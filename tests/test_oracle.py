@@ -235,3 +235,25 @@ def test_lsh_recall_on_perturbed_rows():
     exact = np.array([np.add.reduce((As - q) ** 2, axis=1).min() for q in Q])
     assert np.all(dist >= exact)
     assert np.mean(dist == exact) > 0.9
+
+
+def test_c3_fixture_reproduces_coarse_levels():
+    """tests/golden/c3_oracle.npz (make_config_fixtures.py c3) re-derived here for its
+    three coarsest synthesized levels from bench.py's c3 inputs."""
+    import hashlib
+    import sys
+    import ia_oracle_c as oc
+    from conftest import ROOT
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    g = golden('c3_oracle.npz')
+    conf = bench.CONFIGS['c3']
+    A, Ap, B = bench.make_inputs(conf, 0)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, [Ap], B, cap=conf['levels'], seed=2)
+    assert L == int(g['max_levels'])
+    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, conf['k'],
+                        o.compute_weights(3, 5, 12, 1), levels=[1, 2, 3])
+    for l, (bp, s, im) in out.items():
+        assert np.array_equal(s, g['s%d' % l]) and np.array_equal(im, g['im%d' % l])
+        assert hashlib.sha256(bp.tobytes()).hexdigest() == str(g['bp_sha%d' % l])
