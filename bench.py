@@ -208,9 +208,9 @@ def hbm_kernels(dev, reps=20):
       yiq        ia_rgb_to_yiq, 2048x2048 uint8 RGB -> YIQ + Y fp64: 3 + 32 B/px
       pyr_reduce ia_pyr_reduce_f64 (k_blur + k_resample), 2048^2 -> 1024^2 fp64:
                  8 B per input + 8 B per output pixel
-      db_build   ia_db_build (k_db_build + k_db_split), the c4 finest level, 4,194,304
-                 rows: 448 B written per row (fp32 rows + split-f16 copy) + the fp64
-                 pyramids read once (8 B x (2 fine + 2 coarse) pixels per row)
+      db_build   ia_db_build (k_db_norms + k_db_build), the c4 finest level, 4,194,304
+                 rows: 224 B written per row (split-f16 rows) + the fp64 pyramids read
+                 once (A, A' fine: 8 B per row each; coarse: 8 B per 4 rows each)
     """
     import algorithms
     st = torch.cuda.current_stream(dev)
@@ -265,8 +265,8 @@ def hbm_kernels(dev, reps=20):
     def build():
         _ia.check(lib.ia_db_build(ctypes.byref(ix.src), 0, ix.nrows, _ia.ptr(ix.center),
                                   _ia.ptr(ix.db), _ia.ptr(ix.amax), _ia.stream()), 'ia_db_build')
-    put('db_build', timed(build), N * 448 + 8 * 2 * (N + 1024 * 1024),
-        'ia_db_build (k_db_build + k_db_split), 4,194,304 rows')
+    put('db_build', timed(build), N * 224 + 8 * 2 * (N + 1024 * 1024),
+        'ia_db_build (k_db_norms + k_db_build), 4,194,304 rows')
     return out
 
 

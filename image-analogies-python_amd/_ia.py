@@ -90,7 +90,8 @@ _SIGS = {
                                                    ctypes.c_int]),
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
-    'ia_lsh_build': (ctypes.c_int, [_dp, ctypes.c_long, ctypes.POINTER(IaLsh), _dp]),
+    'ia_lsh_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp,
+                                    ctypes.POINTER(IaLsh), _dp]),
     'ia_lsh_bits': (ctypes.c_int, [ctypes.c_long]),
     'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'ia_comm_init': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,

@@ -2,7 +2,7 @@
 (reference algorithms.py:1-135), computed by libia.so.
 
     compute_feature_array   ia_level_features_f64 (a9)
-    create_index            per level: resident fp64 source pyramids + the fp32 MFMA
+    create_index            per level: resident fp64 source pyramids + the split-f16
                             screening database (ia_db_build, a10); returns
                             (index handles, params, As, As_size) like the reference
     best_approximate_match  ia_match_batch on one query (a11) — EXACT 1-NN, where the
@@ -72,9 +72,9 @@ class LevelIndex:
     """Device-resident As[level] for rows [row0, row0 + nrows) (a shard when sharded).
 
     Holds the fp64 A / A' pyramid levels (the exact rescore gathers features straight
-    from them) and the fp32 screening database built by ia_db_build.  Centre = the means
+    from them) and the split-f16 screening database built by ia_db_build.  Centre = the means
     of A (34 A dims) and of the A' images (21 A' dims): any centre is exact for the
-    distances; centring only tightens the fp32 screen's error bound.
+    distances; centring only tightens the screen's error bound.
     """
 
     def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg, row0=0, nrows=None):
@@ -92,9 +92,8 @@ class LevelIndex:
         mAp = _ia.mean_dev(self.Ap_lg)
         self.center = torch.empty(55, dtype=torch.float64, device=dev)
         _ia.check(lib.ia_center_fill(_ia.ptr(self.center), mA, mAp, st), 'ia_center_fill')
-        nbytes = lib.ia_db_bytes(self.nrows)      # fp32 rows + their split-f16 copy
-        self.db = torch.empty((nbytes // (4 * _ia.IA_DP), _ia.IA_DP), dtype=torch.float32,
-                              device=dev)
+        nbytes = lib.ia_db_bytes(self.nrows)      # split-f16 rows, 224 B each
+        self.db = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
         _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
                                   _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),
@@ -119,7 +118,8 @@ class LevelIndex:
         h = _ia.IaLsh()
         h.mem, h.proj, h.L, h.k, h.w = (_ia.ptr(self.lsh_mem).value, _ia.ptr(self.lsh_proj).value,
                                         L, k, w)
-        _ia.check(lib.ia_lsh_build(_ia.ptr(self.db), self.nrows, ctypes.byref(h), _ia.stream()),
+        _ia.check(lib.ia_lsh_build(ctypes.byref(self.src), self.row0, self.nrows,
+                                   _ia.ptr(self.center), ctypes.byref(h), _ia.stream()),
                   'ia_lsh_build')
         self.lsh = h
         return self

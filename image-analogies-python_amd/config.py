@@ -8,7 +8,7 @@ longer accepts as indices).  Fields added by this build (SURV
 
     levels   cap on pyramid halvings (skimage ``max_layer``); None = reference rule
     seed     seed of the B' random initialisation (the reference draws unseeded)
-    matcher  'brute': exact 1-NN (fp32 MFMA screen + fp64 rescore), the default;
+    matcher  'brute': exact 1-NN (split-f16 MFMA screen + fp64 rescore), the default;
              'lsh': approximate E2LSH matcher with
              lsh_tables x lsh_hashes projections, bucket width lsh_width (in units of
              the rows' RMS per-dimension spread) and projection seed lsh_seed

@@ -1,11 +1,12 @@
 // ia_features.hip — neighbourhood feature construction.
 //   * compute_feature_array (algorithms.py:11-47) for the API,
-//   * the fp32 screening database (algorithms.py:50-70 As[level], centred, MFMA
-//     operand order, squared norm folded in as element 55),
-//   * per-wave query rows (image_analogies.py:166-168: B full | B' half) in fp64 for the
-//     exact rescore and in fp32 MFMA order for the screen.
-// Feature values are pure gathers (exact); centring and fp32 rounding only feed the
-// screen, whose error bound is accounted for in ia_match.hip.
+//   * the screening database (algorithms.py:50-70 As[level]): centred rows with the
+//     squared norm folded in as element 55, split into f16 pairs in the MFMA operand
+//     order (ia_split16.h), 224 B per row,
+//   * per-wave query rows (image_analogies.py:166-168: B full | B' half): fp64 for the
+//     exact rescore, fp32 for the re-screen, split-f16 for the screen.
+// Feature values are pure gathers (exact); centring, rounding and splitting only feed the
+// screen and re-screen, whose error bounds are accounted for in ia_match.hip.
 #include "ia_common.h"
 #include "ia_internal.h"
 #include "ia_split16.h"
@@ -25,102 +26,91 @@ __global__ void k_level_features(ImgPair p, int full, double *out) {
     }
 }
 
-// MFMA operand order of element k = 2s + h: position h*28 + s (see ia_match.hip).
+// MFMA operand order of element k = 2s + h: position h*28 + s (the fp32 query rows qp).
 __device__ __forceinline__ int perm56(int k) { return (k & 1) * 28 + (k >> 1); }
 
-// One thread per database row: 55 gathers, centre, fp32, permute; 224 B per row written
-// through LDS so that the block's stores are contiguous 16-B vectors.
-__global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nrows, long npad,
-                                                  const double *__restrict__ center,
-                                                  float *__restrict__ db, float *amax) {
-    __shared__ float tile[256 * IA_DP];
+// Centred row of DB row ix: my[k] = fl32(a_k - c_k) (k < 55), my[55] = fl32(|a - c|^2)
+// (fp64 sum in feature order); returns |a - c| in fp32.
+__device__ __forceinline__ float db_row(const DbSrc &src, long ix, const double *__restrict__ center,
+                                        float *my) {
+    ImgPair ap; int r, c;
+    src.locate(ix, ap, r, c);
+    double n2 = 0.0;
+    emit_feature(src.A, ap, r, c, [&](int k, double v) {
+        const double d = v - center[k];
+        n2 += d * d;
+        my[k] = (float)d;
+    });
+    my[55] = (float)n2;
+    return (float)sqrt(n2);
+}
+
+// Pass 1: amax = max over rows of |a - c| (the split scale and the error bounds need it
+// before any row is split).  One thread per row, a block max, one atomic per block.
+__global__ __launch_bounds__(256) void k_db_norms(DbSrc src, long row0, long nrows,
+                                                  const double *__restrict__ center, float *amax) {
     __shared__ float redmax[4];
-    const long lr = (long)blockIdx.x * 256 + threadIdx.x;  // local row
-    float *my = tile + threadIdx.x * IA_DP;
+    const long lr = (long)blockIdx.x * 256 + threadIdx.x;
     float nrm = 0.f;
     if (lr < nrows) {
-        ImgPair ap; int r, c;
-        src.locate(row0 + lr, ap, r, c);
-        double n2 = 0.0;
-        emit_feature(src.A, ap, r, c, [&](int k, double v) {
-            const double d = v - center[k];
-            n2 += d * d;
-            my[perm56(k)] = (float)d;
-        });
-        my[perm56(55)] = (float)n2;
-        nrm = (float)sqrt(n2);
-    } else if (lr < npad) {
-        for (int k = 0; k < 55; ++k) my[perm56(k)] = 0.f;
-        my[perm56(55)] = 1e30f;  // sentinel row: screen value 1e30, never a candidate
+        float my[IA_DP];
+        nrm = db_row(src, row0 + lr, center, my);
     }
     for (int o = 32; o > 0; o >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, o));
     if ((threadIdx.x & 63) == 0) redmax[threadIdx.x >> 6] = nrm;
     __syncthreads();
     if (threadIdx.x == 0) {
-        float m = fmaxf(fmaxf(redmax[0], redmax[1]), fmaxf(redmax[2], redmax[3]));
+        const float m = fmaxf(fmaxf(redmax[0], redmax[1]), fmaxf(redmax[2], redmax[3]));
         atomicMax(reinterpret_cast<unsigned int *>(amax), __float_as_uint(m));
-    }
-    // fragment-major copy-out (the screen's operand order, ia_match.hip load_tile):
-    // float4 (tile T, v, lane l) = row T*32 + (l & 31), positions (l >> 5)*28 + 4v..4v+3.
-    // The block's 256 rows are 8 whole tiles, written as one contiguous 57 KB range.
-    const long base = (long)blockIdx.x * 256;
-    const long rows_here = npad - base < 256 ? npad - base : 256;   // multiple of 32
-    const long nvec = rows_here * IA_DP / 4;
-    float4 *dst = reinterpret_cast<float4 *>(db + base * IA_DP);
-    for (long i = threadIdx.x; i < nvec; i += 256) {
-        const int T = (int)(i / (7 * 64)), rem = (int)(i - (long)T * 7 * 64);
-        const int v = rem >> 6, l = rem & 63;
-        const float *s = tile + (T * 32 + (l & 31)) * IA_DP + (l >> 5) * 28 + 4 * v;
-        dst[i] = make_float4(s[0], s[1], s[2], s[3]);
     }
 }
 
-// Split-f16 copy of the fp32 DB (ia_split16.h): one wave per 32-row tile, the tile
-// un-permuted through LDS, then lane (j, h) emits its 7 half8 register groups; output
-// half8 (tile, g, lane) at (tile * 7 + g) * 64 + lane, so each of the screen's 7 loads
-// per tile is one contiguous 1 KiB wave access.  Padding rows (>= nrows) repeat row
-// nrows - 1: their screen values are those of a real row, so the segment minima need no
-// masking (the exact stage never rescores a row >= nrows).  Runs after k_db_build on the
-// same stream (needs the final amax).
-__global__ __launch_bounds__(256) void k_db_split(const float *__restrict__ db, long nrows,
+// Pass 2: the split-f16 rows (ia_split16.h), written once.  One thread per row computes
+// its 56 centred fp32 values into LDS (256 rows = 8 tiles per block); then lane (j, h) of
+// each wave emits its 7 register groups of two tiles: half8 (tile, g, lane) at
+// (tile * 7 + g) * 64 + lane, so each of the screen's 7 loads per tile is one contiguous
+// 1 KiB wave access.  Padding rows (>= nrows) repeat row nrows - 1: their screen values
+// are those of a real row, so the segment minima need no masking (the exact stage never
+// rescores a row >= nrows).
+__global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nrows, long npad,
+                                                  const double *__restrict__ center,
                                                   const float *__restrict__ amax,
                                                   half8 *__restrict__ db16) {
     constexpr int LD = IA_DP + 1;
-    __shared__ float t[4][32 * LD];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int j = lane & 31, h = lane >> 5;
-    const long T = (long)blockIdx.x * 4 + wv;
-    const long rr = T * 32 + j < nrows ? T * 32 + j : nrows - 1;   // source row
-    const float4 *src = reinterpret_cast<const float4 *>(db) + (rr >> 5) * (7 * 64) + h * 32 +
-                        (rr & 31);
-    float *tr = t[wv] + j * LD;
+    __shared__ float tile[256 * LD];
+    const long base = (long)blockIdx.x * 256;
+    const long lr = base + threadIdx.x;
+    if (lr < npad) {
+        float my[IA_DP];
+        db_row(src, row0 + (lr < nrows ? lr : nrows - 1), center, my);
 #pragma unroll
-    for (int v = 0; v < 7; ++v) {   // positions h*28 + 4v + c = element 2(4v + c) + h
-        const float4 x = src[v * 64];
-        tr[2 * (4 * v + 0) + h] = x.x;
-        tr[2 * (4 * v + 1) + h] = x.y;
-        tr[2 * (4 * v + 2) + h] = x.z;
-        tr[2 * (4 * v + 3) + h] = x.w;
+        for (int k = 0; k < IA_DP; ++k) tile[threadIdx.x * LD + k] = my[k];
     }
     __syncthreads();
     const Split16Db s = split16_db_scale(amax[0]);
-    auto val = [&](int k) { return k < 55 ? ldexpf(tr[k], s.ea) : ldexpf(tr[55], s.ea - s.R); };
-    half8 *out = db16 + T * (DB16_GROUPS * 64) + lane;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j = lane & 31, h = lane >> 5;
+    for (int tt = wv; tt < 8; tt += 4) {
+        const long T = (base >> 5) + tt;
+        if (T * 32 >= npad) break;
+        const float *tr = tile + (tt * 32 + j) * LD;
+        half8 *out = db16 + T * (DB16_GROUPS * 64) + lane;
 #pragma unroll
-    for (int g = 0; g < DB16_GROUPS; ++g) {
-        // (h, g) -> 8 features k0..k0+7, hi or lo part (ia_split16.h table)
-        int k0;
-        bool hi;
-        if (h == 0) { hi = g < 4; k0 = hi ? 8 * g : 8 * (g - 4); }
-        else { hi = g < 3; k0 = hi ? 32 + 8 * g : (g == 3 ? 24 : 32 + 8 * (g - 4)); }
-        half8 o;
+        for (int g = 0; g < DB16_GROUPS; ++g) {
+            int k0;
+            bool hi;
+            split16_db_group(h, g, k0, hi);
+            half8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            _Float16 xh, xl;
-            split16f(val(k0 + e), xh, xl);
-            o[e] = hi ? xh : xl;
+            for (int e = 0; e < 8; ++e) {
+                const int k = k0 + e;
+                const float v = k < 55 ? ldexpf(tr[k], s.ea) : ldexpf(tr[55], s.ea - s.R);
+                _Float16 xh, xl;
+                split16f(v, xh, xl);
+                o[e] = hi ? xh : xl;
+            }
+            out[g * 64] = o;
         }
-        out[g * 64] = o;
     }
 }
 
@@ -228,16 +218,16 @@ long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
 size_t ia_db_bytes(long nrows) { return db_bytes(nrows); }
 
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
-                float *db, float *amax, void *stream) {
+                void *db, float *amax, void *stream) {
     IA_ARG(src && center && db && amax && nrows > 0 && row0 >= 0, "ia_db_build: bad args");
     IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build: rows out of range");
     const long npad = db_rows_padded(nrows);
     DbSrc d = make_dbsrc(*src);
-    k_db_build<<<(unsigned)((npad + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, npad,
-                                                                     center, db, amax);
+    k_db_norms<<<(unsigned)((nrows + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, center, amax);
+    IA_LAUNCH_CHECK("k_db_norms");
+    k_db_build<<<(unsigned)((npad + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, npad, center,
+                                                                     amax, reinterpret_cast<half8 *>(db));
     IA_LAUNCH_CHECK("k_db_build");
-    k_db_split<<<(unsigned)(npad / 128), 256, 0, S(stream)>>>(db, nrows, amax, reinterpret_cast<half8 *>(db16_of(db, nrows)));
-    IA_LAUNCH_CHECK("k_db_split");
     return IA_OK;
 }
 

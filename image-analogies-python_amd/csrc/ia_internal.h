@@ -25,14 +25,9 @@ static inline long db_nchunks(long nrows) {
     return ((nrows + ch - 1) / ch + 3) / 4 * 4;
 }
 static inline long db_rows_padded(long nrows) { return db_nchunks(nrows) * db_chunk_rows(nrows); }
-// one DB buffer = the fp32 screening rows (npad x IA_DP floats, fragment-major; the exact
-// stage's re-screen) followed by their split-f16 copy (npad x 112 halves, ia_split16.h;
-// the screen's operand): 2 x 224 B per padded row
-static inline size_t db_bytes(long nrows) { return (size_t)db_rows_padded(nrows) * IA_DP * 4 * 2; }
-template <typename T>
-static inline T *db16_of(T *db, long nrows) {
-    return db + (size_t)db_rows_padded(nrows) * IA_DP * 4 / sizeof(T);
-}
+// the DB buffer: npad split-f16 rows (112 halves = 224 B each, ia_split16.h), the screen's
+// MFMA operand and the exact stage's re-screen input
+static inline size_t db_bytes(long nrows) { return (size_t)db_rows_padded(nrows) * 224; }
 // segment-minimum matcher: one running minimum per (query, segment) of min(ch, 512) rows
 // (a whole number of 4-tile stages; <= 16 segments per chunk)
 static inline int db_seg_rows(long nrows) {
@@ -47,7 +42,8 @@ struct Best {            // exact winner of a (query, shard): fp64 distance + gl
 };
 struct WItem {           // one (query, candidate segment) of the work-list exact stage
     int q, seg;
-    double trow;         // the query's fp32 re-screen threshold
+    float twoR;          // the re-screen's norm-slot factor 2^R
+    double trow;         // the query's fp32 re-screen threshold (units of sa)
 };
 struct QSel {            // per-query record of k_select: re-screen threshold, items
     double trow;
@@ -90,9 +86,9 @@ int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int 
                       const float *amax, _Float16 *q16, hipStream_t st);
 int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
                       const float *amax, _Float16 *q16, hipStream_t st);
-// the split-f16 segment screen (ia_screen16.hip) of M queries over db16_of(db) ->
+// the split-f16 segment screen (ia_screen16.hip) of M queries over the DB ->
 // segmin[M][db_nsegs(nrows)] (screen units); q16 holds qrows_alloc(M) rows
-int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
+int launch_screen16(const void *db, long nrows, const _Float16 *q16, int M, float *segmin,
                     hipStream_t st);
 // the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
 // stats (nullable): rows rescored, candidate segments, full scans.
@@ -100,7 +96,7 @@ size_t match_scratch_bytes(int qrows, long nrows);
 // ev0 / ev1 (nullable) are recorded on st immediately before / after the screen launch.
 // fin (nullable, single shard only): the exact stage also runs the per-pixel tail of the
 // wave (coherence, kappa, B'/s/im update) in the same kernel.
-int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp,
+int launch_match(const DbSrc &src, long row0, long nrows, const void *db, const float *qp,
                  const _Float16 *q16, int M, const double *q64, const double *nq,
                  const float *amax, void *scratch, Best *best, unsigned long long *stats,
                  hipStream_t st,

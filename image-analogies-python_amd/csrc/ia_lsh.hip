@@ -8,6 +8,7 @@
 // per table and masked to B = lsh_bits(nrows) bits (2^B >= 2 nrows buckets).  Build: one
 // pass over the fp32 DB computes L keys per row, one hipCUB radix sort of (key, row)
 // pairs per table, and a bucket directory start[t][0..2^B] (counting-sort offsets).
+// The rows' centred fp32 values are gathered from the pyramids like the DB build's.
 // Query (one wave per query): L keys, two directory loads per table, and the exact fp64
 // distance (the oracle's pairwise-8 value) of up to LSH_CAP rows per bucket, spread over
 // the wave's lanes; the lexicographic (distance, row) minimum is returned.
@@ -32,9 +33,11 @@ __device__ __forceinline__ unsigned int lsh_mix(int h, int i) {
     return (unsigned int)h * (0x9E3779B1u + 2u * (unsigned int)i) + 0x7F4A7C15u * (unsigned int)i;
 }
 
-// keys_in[t][r] for rows r of the fragment-major DB (centred values, element 55 skipped)
-__global__ __launch_bounds__(256) void k_lsh_keys(const float *__restrict__ db, long nrows,
-                                                  long npad, const float *__restrict__ proj,
+// keys_in[t][r] for the local rows r of [row0, row0 + nrows): the centred fp32 values
+// fl32(a_k - c_k) gathered from the pyramids (the rows the exact matcher screens)
+__global__ __launch_bounds__(256) void k_lsh_keys(DbSrc src, long row0, long nrows, long npad,
+                                                  const double *__restrict__ center,
+                                                  const float *__restrict__ proj,
                                                   int L, int k, float w, int bits,
                                                   unsigned int *__restrict__ keys,
                                                   int *__restrict__ rows) {
@@ -44,17 +47,11 @@ __global__ __launch_bounds__(256) void k_lsh_keys(const float *__restrict__ db, 
     const long r = (long)blockIdx.x * 256 + threadIdx.x;
     if (r >= npad) return;
     float a[IA_DP];
-    const float4 *t4 = reinterpret_cast<const float4 *>(db) + (r >> 5) * (32 * IA_DP / 4) + (r & 31);
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int v = 0; v < 7; ++v) {
-            const float4 x = t4[v * 64 + hh * 32];
-            a[2 * (4 * v + 0) + hh] = x.x;
-            a[2 * (4 * v + 1) + hh] = x.y;
-            a[2 * (4 * v + 2) + hh] = x.z;
-            a[2 * (4 * v + 3) + hh] = x.w;
-        }
+    {
+        ImgPair ap; int rr, cc;
+        src.locate(row0 + (r < nrows ? r : nrows - 1), ap, rr, cc);
+        emit_feature(src.A, ap, rr, cc, [&](int kk, double v) { a[kk] = (float)(v - center[kk]); });
+    }
     for (int t = 0; t < L; ++t) {
         unsigned int key = 0;
         for (int i = 0; i < k; ++i) {
@@ -218,8 +215,10 @@ size_t ia_lsh_bytes(long nrows, int L) {
 
 int ia_lsh_bits(long nrows) { return nrows > 0 ? lsh_bits(nrows) : 0; }
 
-int ia_lsh_build(const float *db, long nrows, const IaLsh *lsh, void *stream) {
-    IA_ARG(db && lsh && lsh->mem && lsh->proj && nrows > 0, "ia_lsh_build: bad args");
+int ia_lsh_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                 const IaLsh *lsh, void *stream) {
+    IA_ARG(src && center && lsh && lsh->mem && lsh->proj && nrows > 0 && row0 >= 0,
+           "ia_lsh_build: bad args");
     IA_ARG(lsh->L >= 1 && lsh->k >= 1 && lsh->L * lsh->k <= LSH_MAXH && lsh->w > 0.f,
            "ia_lsh_build: need 1 <= L*k <= 64 and w > 0");
     IA_ARG(nrows < (1L << 31), "ia_lsh_build: too many rows");
@@ -237,8 +236,8 @@ int ia_lsh_build(const float *db, long nrows, const IaLsh *lsh, void *stream) {
     size_t tb = sort_temp_bytes(npad, bits);
     IA_ARG(tb > 0, "ia_lsh_build: radix-sort size query failed");
     const unsigned nb = (unsigned)((npad + 255) / 256);
-    k_lsh_keys<<<nb, 256, 0, st>>>(db, nrows, npad, lsh->proj, lsh->L, lsh->k, lsh->w, bits,
-                                   keys_in, rows_in);
+    k_lsh_keys<<<nb, 256, 0, st>>>(make_dbsrc(*src), row0, nrows, npad, center, lsh->proj,
+                                   lsh->L, lsh->k, lsh->w, bits, keys_in, rows_in);
     IA_LAUNCH_CHECK("k_lsh_keys");
     for (int t = 0; t < lsh->L; ++t) {
         IA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_in + (long)t * npad,

@@ -8,7 +8,8 @@
 //     screening centre), in units of sa * sq; no per-row state, branch free;
 //  2. the exact stage (this file): e* = the minimum over all segments; every segment whose
 //     minimum is within Tseg = e* + 2 eps16 is re-screened row by row in fp32 (VALU, from
-//     the fp32 DB rows), and every row within Trow = e* + eps16 + eps_q is rescored in fp64
+//     the same split-f16 rows, x = x_h + x_l exactly in fp32), and every row within
+//     Trow = e* + eps16 + eps_q is rescored in fp64
 //     in the oracle's exact operation order (numpy pairwise-8, no FMA contraction),
 //     gathering its 55 features from the fp64 pyramids; ties break to the lowest row
 //     (np.argmin).  eps16 / eps_q bound the screen / re-screen error for ANY summation
@@ -26,17 +27,20 @@
 
 namespace ia {
 
-constexpr int TILE_VEC = 32 * IA_DP / 4;   // float4s per 32-row tile of the fp32 DB
+constexpr int TILE_H8 = DB16_GROUPS * 64;  // half8 per 32-row tile of the split-f16 DB
 
 __device__ __forceinline__ void best_update(double &bd, long long &bi, double d, long long i) {
     if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
 }
 
 // Thresholds of the exact stage from the minimum segment minimum emin (screen units):
-// Tseg for segment minima (screen units), Trow for the fp32 VALU re-screen (unscaled).
-// e* = emin / (sa sq) exactly; Tseg = e* + 2 eps16, Trow = e* + eps16 + eps_q (+ a 1e-12
-// relative allowance for the fp64 rounding of d and of the centring); force_full when the
-// query's norm slot nears the f16 floor (|q'| > 2^24 Amax).
+// Tseg for segment minima (screen units), Trow for the fp32 VALU re-screen (in units of
+// sa, the re-screen's scale).  e* = emin / (sa sq) exactly; Tseg = e* + 2 eps16,
+// Trow = e* + eps16 + eps_q (+ a 1e-12 relative allowance for the fp64 rounding of d and
+// of the centring); force_full when the query's norm slot nears the f16 floor
+// (|q'| > 2^24 Amax).  eps_q = 70 u (2 A|q'| + A^2) bounds the re-screen (§4): fp32
+// conversions 2u on the 2A|q'| term and u on A^2, the split residual |x - x_h - x_l| <=
+// 4u|x|, a 56-term fp32 chain in any order <= 56u (1 + O(u)): 62u + O(u^2) in all.
 __device__ __forceinline__ void rescore_thresholds(float emin, float amax0, double nqq,
                                                    double &Tseg, double &Trow, bool &force_full) {
     constexpr double U32 = 5.9604644775390625e-08;
@@ -49,32 +53,38 @@ __device__ __forceinline__ void rescore_thresholds(float emin, float amax0, doub
     const double eps16 = U32 * (300.0 * A * sqrt(nqq) + 50.0 * A * A);
     const double slack = 1e-12 * (fabs(em) + nqq + A * A);
     Tseg = ldexp(em + 2.0 * eps16 + slack, e2);
-    Trow = em + eps16 + eps + slack;
+    Trow = ldexp(em + eps16 + eps + slack, sc.ea);
     force_full = eq + sc.R < -10;
 }
 
-// fp32 re-screen value of DB row r (fragment-major fp32 DB, row r = tile*32 + (r & 31)):
-// the same 56-term dot product [a', |a'|^2] . [-2 q', 1] as the screen, any order (§4)
-__device__ __forceinline__ float rescreen_row(const float *__restrict__ db, long r,
-                                              const float *qf) {
-    const float4 *t4 = reinterpret_cast<const float4 *>(db) + (r >> 5) * TILE_VEC + (r & 31);
-    float4 x[14];
+// The 14 register groups of DB row r (split-f16, ia_split16.h): g0 = lane half 0, g1 = 1
+__device__ __forceinline__ void load_row16(const half8 *__restrict__ db16, long r,
+                                           half8 (&g0)[DB16_GROUPS], half8 (&g1)[DB16_GROUPS]) {
+    const half8 *t = db16 + (r >> 5) * TILE_H8 + (r & 31);
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int v = 0; v < 7; ++v) x[hh * 7 + v] = t4[v * 64 + hh * 32];
+    for (int g = 0; g < DB16_GROUPS; ++g) {
+        g0[g] = t[g * 64];
+        g1[g] = t[g * 64 + 32];
+    }
+}
+
+// fp32 re-screen value of a row from its split record, in units of sa: the same 56-term
+// dot product [a', |a'|^2] . [-2 q', 1] as the screen (qf: the fp32 query row, MFMA
+// operand order perm56), each value reassembled exactly as x_h + x_l in fp32; the norm
+// slot carries sa 2^-R |a'|^2, so its query factor is 2^R.  Any summation order (§4).
+__device__ __forceinline__ float rescreen16(const half8 (&g0)[DB16_GROUPS],
+                                            const half8 (&g1)[DB16_GROUPS], const float *qf,
+                                            float twoR) {
     float acc = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int v = 0; v < 7; ++v) {
-            const float4 xv = x[hh * 7 + v];
-            const float *qv = qf + hh * 28 + 4 * v;
-            acc = fmaf(xv.x, qv[0], acc);
-            acc = fmaf(xv.y, qv[1], acc);
-            acc = fmaf(xv.z, qv[2], acc);
-            acc = fmaf(xv.w, qv[3], acc);
-        }
+    for (int k = 0; k < IA_DP; ++k) {
+        _Float16 hi, lo;
+        if (k < 24) { hi = g0[k >> 3][k & 7]; lo = g0[4 + (k >> 3)][k & 7]; }
+        else if (k < 32) { hi = g0[3][k & 7]; lo = g1[3][k & 7]; }
+        else { hi = g1[(k - 32) >> 3][k & 7]; lo = g1[4 + ((k - 32) >> 3)][k & 7]; }
+        const float x = (float)hi + (float)lo;
+        acc = fmaf(x, k < 55 ? qf[(k & 1) * 28 + (k >> 1)] : twoR, acc);
+    }
     return acc;
 }
 
@@ -141,7 +151,7 @@ __device__ __forceinline__ void segmin_select(const float4 *sq4, long n4, const 
 template <bool FIN>
 __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrows, long nseg,
                                                  int seg_rows, const float *__restrict__ segmin,
-                                                 const float *__restrict__ db,
+                                                 const half8 *__restrict__ db,
                                                  const float *__restrict__ qp,
                                                  const double *__restrict__ q64,
                                                  const double *__restrict__ nq,
@@ -176,6 +186,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     double Tseg, Trow;
     bool force_full;
     rescore_thresholds(emin, amax[0], nqq, Tseg, Trow, force_full);
+    const float twoR = ldexpf(1.f, split16_db_scale(amax[0]).R);
     segmin_select(sq4, n4, v, Tseg, slist, &scount);
     __syncthreads();
     const int ns = scount;
@@ -199,7 +210,9 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
             const long seg = k < nrs ? (full ? k / seg_rows : slist[k / seg_rows]) : 0;
             lr[u] = k < nrs ? seg * seg_rows + k % seg_rows : nrows;
             // out-of-range rows read row 0 and are discarded below
-            e[u] = rescreen_row(db, lr[u] < nrows ? lr[u] : 0, qf);
+            half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
+            load_row16(db, lr[u] < nrows ? lr[u] : 0, g0, g1);
+            e[u] = rescreen16(g0, g1, qf, twoR);
         }
 #pragma unroll
         for (int u = 0; u < RESCORE_RPT; ++u) {
@@ -297,13 +310,14 @@ __global__ __launch_bounds__(256) void k_select(long nseg, const float *__restri
     }
     __syncthreads();
     const int base = sbase;
-    for (int i = tid; i < cnt; i += 256) items[base + i] = WItem{q, full ? i : slist[i], Trow};
+    const float twoR = ldexpf(1.f, split16_db_scale(amax[0]).R);
+    for (int i = tid; i < cnt; i += 256) items[base + i] = WItem{q, full ? i : slist[i], twoR, Trow};
 }
 
 __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows, int seg_rows,
                                                const WItem *__restrict__ items,
                                                const int *__restrict__ ctr,
-                                               const float *__restrict__ db,
+                                               const half8 *__restrict__ db,
                                                const float *__restrict__ qp,
                                                const double *__restrict__ q64,
                                                Best *__restrict__ ibest,
@@ -320,18 +334,13 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
         const WItem w = items[it];
         // this thread's rows of the segment, issued before the query is staged so that the
         // two round trips overlap
-        float4 x[RESCORE_RPT][14];
+        half8 x0[RESCORE_RPT][DB16_GROUPS], x1[RESCORE_RPT][DB16_GROUPS];
         long lr[RESCORE_RPT];
 #pragma unroll
         for (int u = 0; u < RESCORE_RPT; ++u) {
             const int k = u * 256 + tid;
             lr[u] = k < seg_rows ? (long)w.seg * seg_rows + k : nrows;
-            const long r = lr[u] < nrows ? lr[u] : 0;
-            const float4 *t4 = reinterpret_cast<const float4 *>(db) + (r >> 5) * TILE_VEC + (r & 31);
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-                for (int v = 0; v < 7; ++v) x[u][hh * 7 + v] = t4[v * 64 + hh * 32];
+            load_row16(db, lr[u] < nrows ? lr[u] : 0, x0[u], x1[u]);
         }
         __syncthreads();                       // the previous item's LDS reads are done
         if (tid < IA_DP) {
@@ -344,18 +353,7 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
         // (a single round of feature gathers, however the passing rows fall over lanes)
 #pragma unroll
         for (int u = 0; u < RESCORE_RPT; ++u) {
-            float acc = 0.f;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-                for (int v = 0; v < 7; ++v) {
-                    const float4 xv = x[u][hh * 7 + v];
-                    const float *qv = qf + hh * 28 + 4 * v;
-                    acc = fmaf(xv.x, qv[0], acc);
-                    acc = fmaf(xv.y, qv[1], acc);
-                    acc = fmaf(xv.z, qv[2], acc);
-                    acc = fmaf(xv.w, qv[3], acc);
-                }
+            const float acc = rescreen16(x0[u], x1[u], qf, w.twoR);
             if (lr[u] < nrows && (double)acc <= w.trow) plist[atomicAdd(&pcount, 1)] = u * 256 + tid;
         }
         __syncthreads();
@@ -457,12 +455,13 @@ size_t match_scratch_bytes(int qrows, long nrows) {
            align_up(n * sizeof(Best), 256) + align_up((size_t)qrows * sizeof(QSel), 256);
 }
 
-int launch_match(const DbSrc &src, long row0, long nrows, const float *db, const float *qp,
+int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const float *qp,
                  const _Float16 *q16, int M, const double *q64, const double *nq,
                  const float *amax, void *scratch, Best *best, unsigned long long *stats,
                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, const FinishArgs *fin) {
     int rc;
     IA_ARG(q16, "launch_match: no split-f16 query rows");
+    const half8 *db = reinterpret_cast<const half8 *>(dbv);
     const SegWs ws = seg_ws(scratch, M, nrows);
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
     if ((rc = launch_screen16(db, nrows, q16, M, ws.segmin, st))) return rc;
@@ -643,7 +642,7 @@ int ia_diag_set_rescore_mode(int mode) {
     return prev;
 }
 
-int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
+int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *segmin,
                      void *stream) {
     IA_ARG(db && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16: bad args");
     return launch_screen16(db, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin,

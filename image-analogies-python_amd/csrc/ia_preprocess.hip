@@ -176,6 +176,168 @@ __global__ __launch_bounds__(256) void k_resample(const double *__restrict__ sm,
     dst[(long)y * w + x] = v;
 }
 
+// ---------------------------------------------------------------------------------
+// Fused pyramid_reduce: one output tile of PT_H x PT_W per block.  The block works out
+// which blurred rows / cols its bilinear samples read (mirror-mapped floor / ceil of
+// s * dst + t) plus the blurred pixels it OWNS for the clip range (the blurred rows
+// [floor(r(y0)), floor(r(y0 + PT_H))) and likewise cols: the owned sets partition the
+// image), blurs that region from an LDS-staged input tile (symmetric halo of 3, the
+// k_blur operation order), resamples it (the k_resample order) and writes the UNCLIPPED
+// value; the min / max of its owned blurred pixels go to the slots.  k_pyr_clip then
+// clips to [min, max] of the whole blurred image (warp's clip), writing only the rare
+// values outside it.  No fp64 intermediate image in HBM: input read once (+ halo from
+// L2), output written once and read once.
+// ---------------------------------------------------------------------------------
+constexpr int PT_H = 16, PT_W = 32;                  // output tile
+constexpr int PR_H = 2 * PT_H + 8, PR_W = 2 * PT_W + 8;   // max blurred region (rows, cols)
+
+__device__ __forceinline__ int floor_i(double v) { return (int)floor(v); }
+__device__ __forceinline__ int ceil_i(double v) { return (int)ceil(v); }
+
+__global__ __launch_bounds__(256) void k_pyr_reduce(const double *__restrict__ src, int H, int W,
+                                                    double *__restrict__ dst, int h, int w,
+                                                    double sx, double tx, double sy, double ty,
+                                                    double w0, double w1, double w2, double w3,
+                                                    unsigned long long *minmax) {
+    __shared__ double tin[(PR_H + 6) * (PR_W + 6)];     // input region + halo, then blurred
+    __shared__ double tv[PR_H * (PR_W + 6)];            // vertical pass
+    __shared__ int ext[8];
+    __shared__ long long red[2][4];
+    const int tid = threadIdx.x;
+    const int y0 = blockIdx.y * PT_H, x0 = blockIdx.x * PT_W;
+    const int y1 = min(y0 + PT_H, h), x1 = min(x0 + PT_W, w);
+    if (tid < 8) ext[tid] = (tid & 1) ? -0x40000000 : 0x40000000;
+    __syncthreads();
+    // blurred region [R0, R1] x [C0, C1]: every mirrored sample row / col + the owned set
+    if (tid < PT_H && y0 + tid < y1) {
+        const double r = (double)(y0 + tid) * sy + ty;
+        const int a = (int)mirrori(floor_i(r), H), b = (int)mirrori(ceil_i(r), H);
+        atomicMin(&ext[0], min(a, b));
+        atomicMax(&ext[1], max(a, b));
+    } else if (tid >= 64 && tid < 64 + PT_W && x0 + tid - 64 < x1) {
+        const double c = (double)(x0 + tid - 64) * sx + tx;
+        const int a = (int)mirrori(floor_i(c), W), b = (int)mirrori(ceil_i(c), W);
+        atomicMin(&ext[2], min(a, b));
+        atomicMax(&ext[3], max(a, b));
+    } else if (tid == 128) {
+        const int o0 = blockIdx.y == 0 ? 0 : max(0, min(H, floor_i((double)y0 * sy + ty)));
+        const int o1 = y1 == h ? H : max(0, min(H, floor_i((double)y1 * sy + ty)));
+        ext[4] = o0; ext[5] = o1;
+    } else if (tid == 192) {
+        const int o0 = blockIdx.x == 0 ? 0 : max(0, min(W, floor_i((double)x0 * sx + tx)));
+        const int o1 = x1 == w ? W : max(0, min(W, floor_i((double)x1 * sx + tx)));
+        ext[6] = o0; ext[7] = o1;
+    }
+    __syncthreads();
+    const int oR0 = ext[4], oR1 = ext[5], oC0 = ext[6], oC1 = ext[7];
+    const int R0 = oR1 > oR0 ? min(ext[0], oR0) : ext[0];
+    const int R1 = oR1 > oR0 ? max(ext[1], oR1 - 1) : ext[1];
+    const int C0 = oC1 > oC0 ? min(ext[2], oC0) : ext[2];
+    const int C1 = oC1 > oC0 ? max(ext[3], oC1 - 1) : ext[3];
+    const int RH = R1 - R0 + 1, RW = C1 - C0 + 1;   // <= PR_H, PR_W (checked by the host)
+    const int IW = RW + 6;
+    // 2-D loops (64 columns x 4 rows per pass, no index division); the halo reflects once
+    // on each side for images of >= 3 rows / cols (symi otherwise)
+    const int tx0 = tid & 63, ty0 = tid >> 6;
+    const bool big = H >= 3 && W >= 3;
+    for (int ty_ = ty0; ty_ < RH + 6; ty_ += 4) {
+        const int gy = big ? symi2(R0 - 3 + ty_, H) : symi(R0 - 3 + ty_, H);
+        const double *row = src + (long)gy * W;
+        for (int tx_ = tx0; tx_ < IW; tx_ += 64)
+            tin[ty_ * IW + tx_] = row[big ? symi2(C0 - 3 + tx_, W) : symi(C0 - 3 + tx_, W)];
+    }
+    __syncthreads();
+    for (int ty_ = ty0; ty_ < RH; ty_ += 4)
+        for (int tx_ = tx0; tx_ < IW; tx_ += 64) {
+            const double *c = tin + (ty_ + 3) * IW + tx_;
+            double acc = c[0] * w0;
+            acc = acc + (c[-3 * IW] + c[3 * IW]) * w3;
+            acc = acc + (c[-2 * IW] + c[2 * IW]) * w2;
+            acc = acc + (c[-IW] + c[IW]) * w1;
+            tv[ty_ * IW + tx_] = acc;
+        }
+    __syncthreads();
+    long long kmin = 0x7fffffffffffffffLL, kmax = (long long)0x8000000000000000ULL;
+    for (int ty_ = ty0; ty_ < RH; ty_ += 4)        // blurred region (into tin), owned min/max
+        for (int tx_ = tx0; tx_ < RW; tx_ += 64) {
+            const double *c = tv + ty_ * IW + tx_ + 3;
+            double acc = c[0] * w0;
+            acc = acc + (c[-3] + c[3]) * w3;
+            acc = acc + (c[-2] + c[2]) * w2;
+            acc = acc + (c[-1] + c[1]) * w1;
+            tin[ty_ * RW + tx_] = acc;
+            const int gy = R0 + ty_, gx = C0 + tx_;
+            if (gy >= oR0 && gy < oR1 && gx >= oC0 && gx < oC1) {
+                const long long k = dkey(acc);
+                kmin = k < kmin ? k : kmin;
+                kmax = k > kmax ? k : kmax;
+            }
+        }
+    __syncthreads();
+    {   // bilinear samples of the blurred region (k_resample's operation order), unclipped
+        const int ox = x0 + (tid & 31), oy0 = y0 + (tid >> 5);
+        if (ox < x1) {
+            const double c = (double)ox * sx + tx;
+            const double fc = floor(c);
+            const long minc = (long)fc, maxc = (long)ceil(c);
+            const double dc = c - (double)minc;
+            const int c0 = (int)mirrori(minc, W) - C0, c1 = (int)mirrori(maxc, W) - C0;
+            for (int oy = oy0; oy < y1; oy += 8) {
+                const double r = (double)oy * sy + ty;
+                const double fr = floor(r);
+                const long minr = (long)fr, maxr = (long)ceil(r);
+                const double dr = r - (double)minr;
+                const int r0 = (int)mirrori(minr, H) - R0, r1 = (int)mirrori(maxr, H) - R0;
+                const double tl = tin[r0 * RW + c0], tr = tin[r0 * RW + c1];
+                const double bl = tin[r1 * RW + c0], br = tin[r1 * RW + c1];
+                const double top = (1 - dc) * tl + dc * tr;
+                const double bot = (1 - dc) * bl + dc * br;
+                dst[(long)oy * w + ox] = (1 - dr) * top + dr * bot;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+        kmin = a < kmin ? a : kmin;
+        kmax = b > kmax ? b : kmax;
+    }
+    if ((tid & 63) == 0) { red[0][tid >> 6] = kmin; red[1][tid >> 6] = kmax; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int i = 1; i < 4; ++i) {
+            kmin = red[0][i] < kmin ? red[0][i] : kmin;
+            kmax = red[1][i] > kmax ? red[1][i] : kmax;
+        }
+        unsigned long long *sl = minmax + ((blockIdx.x + blockIdx.y * gridDim.x) % MM_SLOTS) * MM_STRIDE;
+        atomicMin(reinterpret_cast<long long *>(&sl[0]), kmin);
+        atomicMax(reinterpret_cast<long long *>(&sl[1]), kmax);
+    }
+}
+
+// warp's clip of the resampled level to [min, max] of the blurred image (np.clip; only
+// values outside the range, which bilinear weights can produce by rounding, are written)
+__global__ __launch_bounds__(256) void k_pyr_clip(double *__restrict__ dst, long n,
+                                                  const unsigned long long *minmax) {
+    __shared__ double clip[2];
+    if (threadIdx.x < 64) {
+        long long kmin = (long long)minmax[threadIdx.x * MM_STRIDE];
+        long long kmax = (long long)minmax[threadIdx.x * MM_STRIDE + 1];
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+            kmin = a < kmin ? a : kmin;
+            kmax = b > kmax ? b : kmax;
+        }
+        if (threadIdx.x == 0) { clip[0] = dkey_inv(kmin); clip[1] = dkey_inv(kmax); }
+    }
+    __syncthreads();
+    const double lo = clip[0], hi = clip[1];
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const double v = dst[i];
+        if (v < lo) dst[i] = lo;
+        else if (v > hi) dst[i] = hi;
+    }
+}
+
 __global__ void k_init_minmax(unsigned long long *mm) {   // <<<1, MM_SLOTS>>>
     mm[threadIdx.x * MM_STRIDE] = 0x7fffffffffffffffULL;
     mm[threadIdx.x * MM_STRIDE + 1] = 0x8000000000000000ULL;
@@ -273,6 +435,22 @@ int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w
     hipStream_t st = S(stream);
     k_init_minmax<<<1, MM_SLOTS, 0, st>>>(mm);
     IA_LAUNCH_CHECK("k_init_minmax");
+    // fused form when every output tile's sample rows / cols fit the LDS region (skimage's
+    // coefficients of a halving: s <= 2 up to rounding (its fit gives 2.0000000000000004),
+    // 0 <= t < 1; the region has 8 spare rows / cols; anything else takes the two-kernel path)
+    const bool fused = coef[0] > 0 && coef[0] <= 2.01 && coef[2] > 0 && coef[2] <= 2.01 &&
+                       coef[1] >= 0 && coef[1] < 1.0 && coef[3] >= 0 && coef[3] < 1.0 &&
+                       H >= 2 && W >= 2;
+    if (fused) {
+        dim3 g(nblk(w, PT_W), nblk(h, PT_H));
+        k_pyr_reduce<<<g, 256, 0, st>>>(src, H, W, dst, h, w, coef[0], coef[1], coef[2], coef[3],
+                                        taps[0], taps[1], taps[2], taps[3], mm);
+        IA_LAUNCH_CHECK("k_pyr_reduce");
+        const long n = (long)h * w;
+        k_pyr_clip<<<(unsigned)std::min<long>(nblk(n, 256), 1024), 256, 0, st>>>(dst, n, mm);
+        IA_LAUNCH_CHECK("k_pyr_clip");
+        return IA_OK;
+    }
     dim3 g1(nblk(W, BT_W), nblk(H, BT_H));
     k_blur<<<g1, 256, 0, st>>>(src, H, W, taps[0], taps[1], taps[2], taps[3], sm, mm);
     IA_LAUNCH_CHECK("k_blur");

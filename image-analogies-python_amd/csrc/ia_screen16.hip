@@ -21,7 +21,7 @@
 // [M][nseg], the exact stage's layout): full 64-B runs instead of one 4-B store per
 // (query, segment) strided by nseg.
 //
-// Padding rows of the DB's last chunks repeat its last real row (k_db_split), so the
+// Padding rows of the DB's last chunks repeat its last real row (k_db_build), so the
 // minima need no masking.  Built with -fno-honor-nans (the min-reductions need no NaN
 // canonicalisation: inputs are finite by construction) and -amdgpu-mfma-vgpr-form (MFMA
 // results in VGPRs: the reductions read them without v_accvgpr_read copies).
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
 // query tiles per launch group: T tiles in ceil(T / 11) equal groups
 static inline int screen_groups(int T) { return (T + MAX_G - 1) / MAX_G; }
 
-int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, float *segmin,
+int launch_screen16(const void *db, long nrows, const _Float16 *q16, int M, float *segmin,
                     hipStream_t st) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
@@ -200,7 +200,7 @@ int launch_screen16(const float *db, long nrows, const _Float16 *q16, int M, flo
     IA_ARG(M > 0 && ch % (STAGE_TILES * 32) == 0 && seg_rows % (STAGE_TILES * 32) == 0 &&
                ch / seg_rows <= SPC_MAX,
            "launch_screen16: bad chunking");
-    const half8 *db16 = reinterpret_cast<const half8 *>(db16_of(db, nrows));
+    const half8 *db16 = reinterpret_cast<const half8 *>(db);
     const half8 *q = reinterpret_cast<const half8 *>(q16);
     const int T = (M + 31) / 32;
     const int groups = screen_groups(T);

@@ -76,6 +76,12 @@ __device__ __forceinline__ void split16d(double x, _Float16 &h, _Float16 &l) {
     l = (_Float16)(float)(x - (double)h);  // x - h exact in f64
 }
 
+// DB register group g (0..6) of lane half h: features k0..k0+7, hi or lo part (table above)
+__host__ __device__ __forceinline__ void split16_db_group(int h, int g, int &k0, bool &hi) {
+    if (h == 0) { hi = g < 4; k0 = hi ? 8 * g : 8 * (g - 4); }
+    else { hi = g < 3; k0 = hi ? 32 + 8 * g : (g == 3 ? 24 : 32 + 8 * (g - 4)); }
+}
+
 // query slots of feature k (0..55), as h * 8 + group: the hi value goes to one or two
 // slots (hi1 = -1: none), the lo value to one; element = k & 7.
 __device__ __forceinline__ void split16_q_slots(int k, int &lo, int &hi0, int &hi1) {

@@ -140,8 +140,12 @@ def _read(fname):
 def setup_dev(A_orig, Ap_orig_list, B_orig, c):
     """Numeric part of img_setup on device, from already-decoded images.
     Returns device (A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list) and sets c.*."""
-    dev = _ia.require_device()
     assert len(A_orig.shape) == len(B_orig.shape)
+    if not c.convert and np.ndim(A_orig) == 3:
+        raise NotImplementedError('3-channel matching (convert=False on colour images, 165-dim '
+                                  'features) is not supported by this build yet; use '
+                                  'convert=True (YIQ luminance) or greyscale inputs')
+    dev = _ia.require_device()
     for Ap in Ap_orig_list:
         assert A_orig.shape == Ap.shape
     # scale to [0, 1]; the A' scale comes from the first row of the LAST A'
@@ -159,9 +163,6 @@ def setup_dev(A_orig, Ap_orig_list, B_orig, c):
         A = ip.scale_dev(up(A_orig), scales[0])
         B = ip.scale_dev(up(B_orig), scales[1])
         Ap_list = [ip.scale_dev(up(x), scales[2]) for x in Ap_orig_list]
-    if A.dim() != 2:
-        raise NotImplementedError('3-channel matching (convert=False on colour images) is not '
-                                  'supported by this build; use convert=True (YIQ luminance)')
     if c.remap_lum:
         A, Ap_list = ip.remap_luminance_dev(A, Ap_list, B)
     levels = getattr(c, 'levels', None)

@@ -79,22 +79,19 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
                           int full, double *out, void *stream);
 
 /* ---- a10: algorithms.py:50-70 create_index — the screening database for rows
- * [row0, row0 + nrows) of As[level] (= A full | A'_i half), in two parts of one buffer:
- *   fp32 rows (the exact stage's re-screen): IA_DP floats per row, element k = 2s + h of
- *     (a - center, k < 55; |a - center|^2 at k = 55) at position p = h*28 + s, stored
- *     fragment-major by 32-row tiles: float4 number (tile*7 + v)*64 + lane holds row
- *     tile*32 + (lane & 31), positions (lane >> 5)*28 + 4v .. +3;
- *   their split-f16 copy (the MFMA screen's operand): per 32-row tile, 7
- *     contiguous 1 KiB register groups (224 B per row).
- * Rows are padded to ia_db_rows_padded(nrows) (whole chunks of ia_db_chunk_rows, a multiple
- * of 4 chunks); padding rows repeat the last real row in the split copy.  amax (device, 1
- * float) receives max_row |a - center| (atomic max; zero it first). */
+ * [row0, row0 + nrows) of As[level] (= A full | A'_i half): each row (a - center, k < 55;
+ * |a - center|^2 at k = 55) scaled by powers of two and split into f16 pairs x = x_h + x_l
+ * (DESIGN.md §4b), stored per 32-row tile as 7 contiguous 1 KiB register groups (224 B per
+ * row): the MFMA screen's operand, and the exact stage's fp32 re-screen input (x_h + x_l
+ * is exact in fp32).  Rows are padded to ia_db_rows_padded(nrows) (whole chunks of
+ * ia_db_chunk_rows, a multiple of 4 chunks) by repeating the last real row.  amax (device,
+ * 1 float) receives max_row |a - center| (atomic max; zero it first). */
 long ia_db_rows_padded(long nrows);
-/* bytes of the db buffer ia_db_build fills: 2 x 224 B per padded row */
+/* bytes of the db buffer ia_db_build fills: 224 B per padded row */
 size_t ia_db_bytes(long nrows);
 int ia_db_chunk_rows(long nrows);
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
-                float *db, float *amax, void *stream);
+                void *db, float *amax, void *stream);
 /* per-dimension screening centre: k < 34 -> mA, k >= 34 -> mAp (host scalars). */
 int ia_center_fill(double *center, double mA, double mAp, void *stream);
 
@@ -102,8 +99,8 @@ int ia_center_fill(double *center, double mA, double mAp, void *stream);
  * output/freud-crop-filt-lsh.jpg variant; no reference code exists for it).  E2LSH over
  * the centred DB rows: L tables of k hashes h = floor((p . a' + b) / w); proj is
  * L*k rows of IA_DP floats on device (p in elements 0..54, b in element 55).
- * mem: ia_lsh_bytes(nrows, L) bytes of device memory, filled by ia_lsh_build from the
- * ia_db_build output.  A query returns the exact-distance (fp64) best of up to 32 rows
+ * mem: ia_lsh_bytes(nrows, L) bytes of device memory, filled by ia_lsh_build from rows
+ * [row0, row0 + nrows) of the level (fp32 of a - center, gathered from the pyramids).  A query returns the exact-distance (fp64) best of up to 32 rows
  * per table bucket it falls in (lexicographic (distance, row) minimum; an empty bucket
  * contributes the 4 entries around its position in the sorted table). */
 typedef struct {
@@ -113,7 +110,8 @@ typedef struct {
     float w;
 } IaLsh;
 size_t ia_lsh_bytes(long nrows, int L);
-int ia_lsh_build(const float *db, long nrows, const IaLsh *lsh, void *stream);
+int ia_lsh_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                 const IaLsh *lsh, void *stream);
 /* bucket keys are masked to ia_lsh_bits(nrows) = ceil(log2(nrows)) + 1 bits (<= 30). */
 int ia_lsh_bits(long nrows);
 
@@ -124,7 +122,7 @@ int ia_lsh_bits(long nrows);
  * approximate LSH matcher over the same rows instead. */
 typedef struct {
     IaSrcLevel src;
-    const float *db;           /* ia_db_build output                       */
+    const void *db;            /* ia_db_build output                       */
     long row0, nrows;          /* this shard's global row range            */
     const double *center;      /* 55 (device)                              */
     const float *amax;         /* device scalar from ia_db_build           */
@@ -158,7 +156,7 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
  * per-rank (dist, idx) winners with one RCCL all-gather. */
 typedef struct {
     IaSrcLevel src;
-    const float *db; long row0, nrows, N_total;
+    const void *db; long row0, nrows, N_total;
     const double *center; const float *amax;
     const double *B_sm, *B_lg; int B_hs, B_ws, H, W;
     const double *Bp_sm; double *Bp_lg;

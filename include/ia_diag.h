@@ -20,7 +20,7 @@ int ia_diag_query_rows16(const double *q64, int M, const double *center, const f
                          float *qp, void *q16, double *nq, void *stream);
 /* one split-f16 screen launch (the exact matcher's stage 1) -> segment
  * minima segmin[M][nseg] (screen units; nseg = ia_db_rows_padded / segment rows) */
-int ia_diag_screen16(const float *db, long nrows, const void *q16, int M, float *segmin,
+int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *segmin,
                      void *stream);
 /* exact stage form for this process: 0 one workgroup per query (k_rescore), 1 the work list
  * (k_select / k_items / k_gather), -1 the default (work list above 2^20 rows); other values

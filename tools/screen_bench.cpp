@@ -107,7 +107,7 @@ int main(int argc, char **argv) {
     CI(ia_center_fill(dc, means[0], means[1], st));
     IaSrcLevel src{dAs, dA, dAps, dAp, hs, ws, H, W, 1};
     const long N = (long)H * W;
-    float *db, *amax;
+    void *db; float *amax;
     CK(hipMalloc(&db, ia_db_bytes(N)));
     CK(hipMalloc(&amax, sizeof(float))); CK(hipMemset(amax, 0, sizeof(float)));
     CI(ia_db_build(&src, 0, N, dc, db, amax, st));
