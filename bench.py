@@ -47,11 +47,19 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 
 # x 2.4 GHz (MI355X_MICROARCH.md: ~2.5 PF dense)
 F16_MFMA_PEAK_TFLOPS = 4096 * 256 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
-# HBM traffic of one finest-level screen launch (k_screen16<11>, M = 342 queries against
-# the 4,194,304-row c4 database), from rocprofv3 PMC passes (FETCH_SIZE x 2 on gfx950 +
-# WRITE_SIZE, MI355X_MICROARCH.md §HBM) of tools/screen_bench; None until measured for the
-# current kernel (profiles/)
-SCREEN_PMC = None
+# HBM traffic of one launch of the dominant screen instance (k_screen16<11>, the c4 finest
+# level's plateau waves: 321-342 queries x 4,194,304 rows), from rocprofv3 PMC passes of
+# bench.py itself (tools/pmc_bench.sh: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
+# MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process)
+SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r02_screen_traffic_bench_pmc.json')
+
+
+def screen_pmc():
+    if not os.path.exists(SCREEN_PMC_FILE):
+        return None
+    d = json.load(open(SCREEN_PMC_FILE))
+    return {'bytes': d['traffic_bytes'], 'kernel': d['kernel'], 'dispatches': d['dispatches'],
+            'source': os.path.relpath(SCREEN_PMC_FILE, ROOT)}
 
 CONFIGS = {
     'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),
@@ -130,6 +138,17 @@ class Job:
                 'mean_dist_exact': float(ed.mean().item()),
                 'mean_dist_ratio': float(ld.mean().item() / max(ed.mean().item(), 1e-300)),
                 'params': dict(self.lsh)}
+
+    def sharded_levels(self, nranks):
+        """Levels whose database is sharded over nranks ranks (image_analogies.shard_level)."""
+        def shapes(img):
+            n = ip.num_layers(img.shape[0], img.shape[1], cfg.n_sm, self.levels)
+            out = [tuple(img.shape)]
+            for _ in range(n):
+                out.append(((out[-1][0] + 1) // 2, (out[-1][1] + 1) // 2))
+            return out[::-1]
+        al = shapes(self.A)
+        return sum(ia.shard_level(al[l][0] * al[l][1], nranks) for l in range(1, self.max_levels))
 
     def algorithmic_pairs(self):
         """sum over synthesized levels of q_l * N_l (the matcher's (query, row) pairs);
@@ -362,7 +381,10 @@ def main():
 
     comm = None
     if world > 1 and args.config != 'c5':
-        comm = init_comm(rank, world)
+        # one RCCL communicator per sharded level: the levels run pipelined, each exchange
+        # stream-ordered on its own level's stream
+        nshard = Job(conf, 0, dev).sharded_levels(world)
+        comm = [init_comm(rank, world) for _ in range(max(nshard, 1))]
 
     lsh = None
     if args.matcher == 'lsh':
@@ -460,47 +482,60 @@ def main():
 
     pixels_per_step = sum(jb.pixels for jb in jobs) * (world if args.config == 'c5' else 1)
     value = pixels_per_step * args.steps / elapsed
-    # roofline of the dominant kernel: the screen launches of the level with the most
-    # screen time (the finest), HIP events on the library's stream around each launch
-    by_level = {}
+    # roofline of the dominant kernel: the screen instance k_screen16<G> (G = query tiles
+    # per block) with the most time over the timed steps, from the HIP events on its
+    # stream around each of its launches; also the whole finest level and all levels
+    per_pair = 3 * 2 * 55      # split-f16: 3 f16 products x 2 flop x 55 features per pair
+    inst = {}
+    lv = {}
     for p in prof:
-        d = by_level.setdefault(p['level'], [0.0, 0, 0.0, p['rows']])
-        d[0] += p['screen_ms']; d[1] += p['timed_screens']; d[2] += p['pairs'] if p['timed_screens'] else 0.0
-    dom = max(by_level, key=lambda l: by_level[l][0]) if by_level else None
-    d_ms, d_n, d_pairs, d_rows = by_level[dom] if dom is not None else (0.0, 0, 0.0, 0)
-    screen_ms = sum(v[0] for v in by_level.values())
-    screens = sum(v[1] for v in by_level.values())
-    pairs = sum(v[2] for v in by_level.values())
-    # split-f16 screen: 3 f16 products (a_h q_h + a_h q_l + a_l q_h) of 2 flop per feature
-    # per (query, row) pair on v_mfma_f32_32x32x16_f16
-    per_pair = 3 * 2 * 55
-    achieved = per_pair * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
-    fp32eq = 2.0 * 55 * d_pairs / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
-    traffic = None
-    if SCREEN_PMC and args.config == 'c4' and world == 1:
-        traffic = (SCREEN_PMC['fetch_kb'] * 2 + SCREEN_PMC['write_kb']) * 1024
-    roof = {'bound': 'mfma', 'kernel': 'k_screen16', 'achieved': achieved,
-            'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / F16_MFMA_PEAK_TFLOPS,
-            'traffic': traffic,
-            'algorithmic': '%d f16 flop per (query,row) pair; level %s (%d DB rows): %.4g pairs '
-                           'over %d launches' % (per_pair, dom, d_rows, d_pairs, d_n),
-            'screen_avg_us': d_ms * 1e3 / max(d_n, 1),
-            'source': 'HIP events around every screen launch of the timed steps',
+        for ms, M in zip(p['launch_ms'], p['launch_M']):
+            T = (int(M) + 31) // 32
+            g = (T + 10) // 11
+            G = (T + g - 1) // g
+            d = inst.setdefault(G, [0.0, 0, 0.0, 0])
+            d[0] += ms; d[1] += 1; d[2] += float(M) * p['rows']; d[3] += int(M)
+            e = lv.setdefault(p['level'], [0.0, 0, 0.0, p['rows']])
+            e[0] += ms; e[1] += 1; e[2] += float(M) * p['rows']
+    domG = max(inst, key=lambda G: inst[G][0]) if inst else None
+    i_ms, i_n, i_pairs, i_q = inst[domG] if domG is not None else (0.0, 0, 0.0, 0)
+    achieved = per_pair * i_pairs / (i_ms * 1e-3) / 1e12 if i_ms > 0 else 0.0
+    fp32eq = 2.0 * 55 * i_pairs / (i_ms * 1e-3) / 1e12 if i_ms > 0 else 0.0
+    fin = max(lv) if lv else None
+    f_ms, f_n, f_pairs, f_rows = lv[fin] if fin is not None else (0.0, 0, 0.0, 0)
+    screen_ms = sum(v[0] for v in lv.values())
+    screens = sum(v[1] for v in lv.values())
+    pairs = sum(v[2] for v in lv.values())
+    traffic, pmc = None, screen_pmc()
+    if pmc and args.config == 'c4' and world == 1 and domG == 11 and lsh is None:
+        traffic = pmc['bytes']
+    roof = {'bound': 'mfma', 'kernel': 'k_screen16<%s>' % domG, 'achieved': achieved,
+            'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': achieved / F16_MFMA_PEAK_TFLOPS, 'traffic': traffic,
+            'algorithmic': '%d f16 flop per (query,row) pair; %d launches, %.4g pairs (mean M '
+                           '%.1f queries)' % (per_pair, i_n, i_pairs, i_q / max(i_n, 1)),
+            'screen_avg_us': i_ms * 1e3 / max(i_n, 1),
+            'source': 'HIP events around every launch of this kernel in the timed steps',
             'fp32_equivalent_tflops': fp32eq,
             'fp32_equivalent_frac_of_fp32_mfma_peak': fp32eq / FP32_MFMA_PEAK_TFLOPS,
+            'finest_level': {'level': fin, 'rows': f_rows, 'launches': f_n,
+                             'screen_avg_us': f_ms * 1e3 / max(f_n, 1),
+                             'frac': (per_pair * f_pairs / (f_ms * 1e-3) / 1e12 /
+                                      F16_MFMA_PEAK_TFLOPS) if f_ms else 0.0},
             'all_levels': {'launches': screens, 'pairs': pairs,
                            'screen_avg_us': screen_ms * 1e3 / max(screens, 1),
                            'screen_ms_per_step': screen_ms / args.steps,
                            'fp32_equivalent_tflops':
                                2.0 * 55 * pairs / (screen_ms * 1e-3) / 1e12 if screen_ms else 0.0}}
     if traffic is not None:
-        roof['traffic_note'] = ('HBM bytes of one M=%d finest-level launch (PMC FETCH_SIZE x 2 + '
-                                'WRITE_SIZE, %s); algorithmic: %.0f MB split-f16 DB read once'
-                                % (SCREEN_PMC['M'], SCREEN_PMC['source'],
-                                   SCREEN_PMC['rows'] * 224 / 1e6))
+        roof['traffic_note'] = ('HBM bytes per launch (mean of %d dispatches), PMC FETCH_SIZE x 2 '
+                                '+ WRITE_SIZE of bench.py under rocprofv3 (%s); algorithmic: the '
+                                '939.5 MB split-f16 DB read once + 11 MB of segment minima'
+                                % (pmc['dispatches'], pmc['source']))
     if lsh is not None:
         # k_lsh_query is a gather: each examined row costs its 55 fp64 features (440 B)
         examined = sum(p['rows_rescored'] for p in prof if p['timed_screens'])
+        screen_ms = sum(float(p['launch_ms'].sum()) for p in prof)
         gbs = examined * 440.0 / (screen_ms * 1e-3) / 1e9 if screen_ms > 0 else 0.0
         roof = {'bound': 'hbm', 'kernel': 'k_lsh_query', 'achieved': gbs,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': gbs / HBM_PEAK_GBS,
@@ -550,7 +585,8 @@ def main():
     if rank == 0 and world == 1 and args.config == 'c4':
         result['hbm_kernels'] = hbm_kernels(dev)
     if comm is not None:
-        _ia.lib().ia_comm_destroy(comm)
+        for cm in comm:
+            _ia.lib().ia_comm_destroy(cm)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

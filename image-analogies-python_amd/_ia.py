@@ -89,6 +89,7 @@ _SIGS = {
     'ia_synth_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long,
                                                    ctypes.c_int]),
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_synth_levels': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
     'ia_lsh_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp,
                                     ctypes.POINTER(IaLsh), _dp]),
@@ -101,6 +102,8 @@ _SIGS = {
     'ia_prof_begin': (ctypes.c_int, []),
     'ia_prof_prepare': (ctypes.c_int, [ctypes.c_long]),
     'ia_prof_end': (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    'ia_prof_launches': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                        ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     'ia_release_thread_resources': (ctypes.c_int, []),
     # diagnostics (include/ia_diag.h)
     'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
@@ -191,6 +194,14 @@ def prof_end():
         for k in ('level', 'rows', 'timed_screens', 'rows_rescored', 'candidate_segments',
                   'full_scans'):
             rec[k] = int(rec[k])
+        nl = rec['timed_screens']
+        ms = (ctypes.c_float * max(nl, 1))()
+        Ms = (ctypes.c_int * max(nl, 1))()
+        got = lib().ia_prof_launches(r, ms, Ms, nl)
+        if got < 0:
+            check(got, 'ia_prof_launches')
+        rec['launch_ms'] = np.array(ms[:got], dtype=np.float64)
+        rec['launch_M'] = np.array(Ms[:got], dtype=np.int64)
         out.append(rec)
     return out
 

@@ -20,6 +20,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <mutex>
 #include <vector>
 
@@ -126,6 +127,7 @@ struct ProfRec {
     size_t ev0;
     int nscreen, timed;
     unsigned long long *hstats;
+    std::vector<int> M;      // queries of each screen launch, in launch order
 };
 struct ProfCollector {
     std::mutex mu;
@@ -182,6 +184,164 @@ static int graph_mode() { return g_graph_mode.load(std::memory_order_relaxed); }
 int comm_allgather_best(void *comm, const Best *send, Best *recv, int M, hipStream_t st);
 int comm_nranks(void *comm);
 
+static int check_args(const IaSynthArgs *a) {
+    IA_ARG(a && a->db && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
+               a->weights && a->s && a->im && a->workspace,
+           "ia_synth_level: null argument");
+    IA_ARG(a->H > 0 && a->W > 0 && a->nrows > 0 && a->row0 >= 0 &&
+               a->row0 + a->nrows <= a->N_total,
+           "ia_synth_level: bad sizes");
+    IA_ARG(a->N_total == (long)a->src.nAp * a->src.Ah * a->src.Aw, "ia_synth_level: N_total mismatch");
+    IA_ARG(a->B_hs == (a->H + 1) / 2 && a->B_ws == (a->W + 1) / 2, "ia_synth_level: B level shapes");
+    IA_ARG(a->src.A_hs == (a->src.Ah + 1) / 2 && a->src.A_ws == (a->src.Aw + 1) / 2,
+           "ia_synth_level: A level shapes");
+    IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level: debug outputs come in pairs");
+    IA_ARG(comm_nranks(a->comm) >= 1, "ia_synth_level: bad communicator");
+    return IA_OK;
+}
+
+// One level's synthesis state: init() on its stream, then wave(t) for t = 0..nw-1 in order
+// (each enqueues that wave's launches), then done().
+struct LevelRun {
+    const IaSynthArgs *a = nullptr;
+    SynthWs ws{};
+    DbSrc src{};
+    ImgPair B{}, Bp{};
+    int H = 0, W = 0, nw = 0, nranks = 1;
+    bool prof = false, timed = false, fused = false;
+    size_t ev0 = 0;
+    unsigned long long *hstats = nullptr;
+    double pairs = 0.0;
+    int nscreen = 0;
+    std::vector<int> Ms;
+
+    int init(const IaSynthArgs *args, hipStream_t st) {
+        a = args;
+        int rc = check_args(a);
+        if (rc) return rc;
+        nranks = a->comm ? comm_nranks(a->comm) : 1;
+        H = a->H; W = a->W;
+        nw = (W - 1) + 3 * (H - 1) + 1;
+        carve(&ws, reinterpret_cast<char *>(a->workspace), H, W, a->nrows, nranks);
+        const int Mmax = wave_max_queries(H, W);
+        IA_HIP(hipMemsetAsync(ws.qp, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
+        IA_HIP(hipMemsetAsync(ws.q16, 0, (size_t)qrows_alloc(Mmax) * Q16_ROW * 16, st));
+        IA_HIP(hipMemsetAsync(ws.stats, 0, STATS_BYTES, st));
+        IA_HIP(hipMemsetAsync(ws.scratch, 0, 256, st));   // the exact stage's empty work list
+        src = make_dbsrc(a->src);
+        B = ImgPair{a->B_sm, a->B_lg, a->B_hs, a->B_ws, H, W};
+        Bp = ImgPair{a->Bp_sm, a->Bp_lg, a->B_hs, a->B_ws, H, W};
+        prof = (a->flags & IA_SYNTH_PROF) && prof_active();
+        timed = prof;
+        if (prof && (rc = prof_reserve(2 * (size_t)nw, &ev0, &hstats))) return rc;
+        // fused tail (one launch + one round trip less per wave): on a single shard the exact
+        // stage's last kernel (k_rescore, or k_gather of the work list) runs the pixel tail
+        fused = !a->comm && !a->lsh;
+        return IA_OK;
+    }
+
+    // wave t: pixels y in [y_lo, y_hi], x = t - 3y
+    static void wave_rows(int H, int W, int t, int &y_lo, int &M) {
+        const int lo_num = t - (W - 1);
+        y_lo = lo_num > 0 ? (lo_num + 2) / 3 : 0;
+        const int y_hi = t / 3 < H - 1 ? t / 3 : H - 1;
+        M = y_hi - y_lo + 1;
+    }
+
+    int wave(int t, hipStream_t sq) {
+        int y_lo, M;
+        wave_rows(H, W, t, y_lo, M);
+        if (M <= 0) return IA_OK;
+        int rc;
+        if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
+                                    ws.q16, sq)))
+            return rc;
+        hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
+        hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
+        const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
+                            a->im, a->dbg_px, a->dbg_dist};
+        if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
+            if (e0) IA_HIP(hipEventRecord(e0, sq));
+            if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
+                                       ws.best_local, prof ? ws.stats : nullptr, sq)))
+                return rc;
+            if (e1) IA_HIP(hipEventRecord(e1, sq));
+        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, ws.q16, M, ws.q64, ws.nq,
+                                      a->amax, ws.scratch, ws.best_local,
+                                      prof ? ws.stats : nullptr, sq, e0, e1,
+                                      fused ? &fa : nullptr))) {
+            return rc;
+        }
+        ++nscreen;
+        pairs += (double)M * (double)a->nrows;
+        if (prof) Ms.push_back(M);
+        // diagnostic (IA_SYNC_EVERY=n): wait for the stream every n waves, bounding the
+        // dispatches in flight (rocprofv3 --pmc runs of the whole bench crash otherwise)
+        static const int sync_every = env_int("IA_SYNC_EVERY", 0);
+        if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
+        if (fused) return IA_OK;   // the exact stage already ran the per-pixel tail
+        const Best *ball = ws.best_local;
+        if (a->comm) {   // also with one rank: the same RCCL path, exercised by the tests
+            if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, sq))) return rc;
+            ball = ws.best_all;
+        }
+        k_finish<<<M, 128, 0, sq>>>(src, ball, nranks, M, fa, ws.q64);
+        IA_LAUNCH_CHECK("k_finish");
+        return IA_OK;
+    }
+
+    int done(hipStream_t st) {
+        if (prof) {   // read back by ia_prof_end (no synchronisation here)
+            IA_HIP(hipMemcpyAsync(hstats, ws.stats, STATS_BYTES, hipMemcpyDeviceToHost, st));
+            prof_push(ProfRec{a->tag, a->nrows, pairs, ev0, nscreen, timed ? 1 : 0, hstats,
+                              std::move(Ms)});
+        }
+        return IA_OK;
+    }
+};
+
+// ---- pipelined levels (ia_synth_levels) ---------------------------------------------
+// Level l's wave t reads the coarse level l-1 only through the 3x3 coarse windows of its
+// pixels: coarse pixels up to (y/2 + 1, x/2 + 1), i.e. coarse waves <= need(t) =
+// max over the wave's pixels of min(x/2 + 1, W'-1) + 3 min(y/2 + 1, H'-1) (the mirror at
+// the coarse level's far edges stays inside that box).  So level l may start as soon as
+// level l-1 has finished need(0) and run concurrently behind it on its own stream: the
+// step's critical path becomes ~ the finest level's waves instead of the sum of all
+// levels' waves.  Levels wait on events recorded every PIPE_BLOCK waves of the level below.
+constexpr int PIPE_BLOCK = 4;
+constexpr int PIPE_AHEAD = 64;   // waves a coarse level is enqueued ahead of its need
+
+static int coarse_need(const IaSynthArgs *a, int t) {
+    int y_lo, M;
+    LevelRun::wave_rows(a->H, a->W, t, y_lo, M);
+    const int Hc = a->B_hs, Wc = a->B_ws;
+    int need = 0;
+    for (int y = y_lo; y < y_lo + M; ++y) {
+        const int x = t - 3 * y;
+        const int cy = y / 2 + 1 < Hc - 1 ? y / 2 + 1 : Hc - 1;
+        const int cx = x / 2 + 1 < Wc - 1 ? x / 2 + 1 : Wc - 1;
+        need = cx + 3 * cy > need ? cx + 3 * cy : need;
+    }
+    return need;
+}
+
+struct PipeRes {   // per host thread: the level streams and events of ia_synth_levels
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;
+    size_t next_event = 0;
+    hipError_t event(hipEvent_t *e) {
+        if (next_event == events.size()) {
+            hipEvent_t x;
+            hipError_t r = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+            if (r != hipSuccess) return r;
+            events.push_back(x);
+        }
+        *e = events[next_event++];
+        return hipSuccess;
+    }
+};
+static thread_local PipeRes g_pipe;
+
 }  // namespace ia
 
 using namespace ia;
@@ -196,6 +356,12 @@ int ia_diag_set_graph_mode(int mode) {
 
 int ia_release_thread_resources(void) {
     IA_HIP(g_graphs.retire());
+    IA_HIP(hipDeviceSynchronize());
+    for (hipStream_t s : g_pipe.streams) IA_HIP(hipStreamDestroy(s));
+    for (hipEvent_t e : g_pipe.events) IA_HIP(hipEventDestroy(e));
+    g_pipe.streams.clear();
+    g_pipe.events.clear();
+    g_pipe.next_event = 0;
     if (g_graphs.cap) { IA_HIP(hipStreamDestroy(g_graphs.cap)); g_graphs.cap = nullptr; }
     if (g_graphs.done) { IA_HIP(hipEventDestroy(g_graphs.done)); g_graphs.done = nullptr; }
     return IA_OK;
@@ -218,6 +384,18 @@ int ia_prof_prepare(long nevents) {
         g_prof->ev.push_back(e);
     }
     return IA_OK;
+}
+
+int ia_prof_launches(int rec, float *ms, int *M, int max) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    IA_ARG(rec >= 0 && rec < (int)g_prof->recs.size(), "ia_prof_launches: no such record");
+    const ProfRec &p = g_prof->recs[rec];
+    const int n = p.timed ? p.nscreen : 0;
+    for (int i = 0; i < n && i < max; ++i) {
+        if (ms) IA_HIP(hipEventElapsedTime(&ms[i], g_prof->ev[p.ev0 + 2 * i], g_prof->ev[p.ev0 + 2 * i + 1]));
+        if (M) M[i] = p.M[i];
+    }
+    return n;
 }
 
 int ia_prof_end(double *out, int maxrec) {
@@ -255,86 +433,10 @@ size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks) {
 }
 
 int ia_synth_level(const IaSynthArgs *a, void *stream) {
-    IA_ARG(a && a->db && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
-               a->weights && a->s && a->im && a->workspace,
-           "ia_synth_level: null argument");
-    IA_ARG(a->H > 0 && a->W > 0 && a->nrows > 0 && a->row0 >= 0 &&
-               a->row0 + a->nrows <= a->N_total,
-           "ia_synth_level: bad sizes");
-    IA_ARG(a->N_total == (long)a->src.nAp * a->src.Ah * a->src.Aw, "ia_synth_level: N_total mismatch");
-    IA_ARG(a->B_hs == (a->H + 1) / 2 && a->B_ws == (a->W + 1) / 2, "ia_synth_level: B level shapes");
-    IA_ARG(a->src.A_hs == (a->src.Ah + 1) / 2 && a->src.A_ws == (a->src.Aw + 1) / 2,
-           "ia_synth_level: A level shapes");
-    IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level: debug outputs come in pairs");
-    const int nranks = a->comm ? comm_nranks(a->comm) : 1;
-    IA_ARG(nranks >= 1, "ia_synth_level: bad communicator");
     hipStream_t st = S(stream);
-    const int H = a->H, W = a->W;
-    SynthWs ws;
-    carve(&ws, reinterpret_cast<char *>(a->workspace), H, W, a->nrows, nranks);
-    const int Mmax = wave_max_queries(H, W);
-    IA_HIP(hipMemsetAsync(ws.qp, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
-    IA_HIP(hipMemsetAsync(ws.q16, 0, (size_t)qrows_alloc(Mmax) * Q16_ROW * 16, st));
-    IA_HIP(hipMemsetAsync(ws.stats, 0, STATS_BYTES, st));
-    IA_HIP(hipMemsetAsync(ws.scratch, 0, 256, st));   // the exact stage's empty work list
-
-    const DbSrc src = make_dbsrc(a->src);
-    const ImgPair B{a->B_sm, a->B_lg, a->B_hs, a->B_ws, H, W};
-    const ImgPair Bp{a->Bp_sm, a->Bp_lg, a->B_hs, a->B_ws, H, W};
-    const int nw = (W - 1) + 3 * (H - 1) + 1;
-    const bool prof = (a->flags & IA_SYNTH_PROF) && prof_active();
-    size_t ev0 = 0;
-    unsigned long long *hstats = nullptr;
-    if (prof) {
-        const int rc = prof_reserve(2 * (size_t)nw, &ev0, &hstats);
-        if (rc) return rc;
-    }
-    double pairs = 0.0;
-    int nscreen = 0;
-    bool timed = prof;
-    // fused tail (one launch + one round trip less per wave): on a single shard the exact
-    // stage's last kernel (k_rescore, or k_gather of the work list) runs the per-pixel tail
-    const bool fused = !a->comm && !a->lsh;
-    auto enqueue_waves = [&](hipStream_t sq) -> int {
-    for (int t = 0; t < nw; ++t) {
-        const int lo_num = t - (W - 1);
-        const int y_lo = lo_num > 0 ? (lo_num + 2) / 3 : 0;
-        const int y_hi = t / 3 < H - 1 ? t / 3 : H - 1;
-        const int M = y_hi - y_lo + 1;
-        if (M <= 0) continue;
-        int rc;
-        if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
-                                    ws.q16, sq)))
-            return rc;
-        hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
-        hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
-        const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
-                            a->im, a->dbg_px, a->dbg_dist};
-        if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
-            if (e0) IA_HIP(hipEventRecord(e0, sq));
-            if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
-                                       ws.best_local, prof ? ws.stats : nullptr, sq)))
-                return rc;
-            if (e1) IA_HIP(hipEventRecord(e1, sq));
-        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, ws.q16, M, ws.q64, ws.nq,
-                                      a->amax, ws.scratch, ws.best_local,
-                                      prof ? ws.stats : nullptr, sq, e0, e1,
-                                      fused ? &fa : nullptr))) {
-            return rc;
-        }
-        ++nscreen;
-        pairs += (double)M * (double)a->nrows;
-        if (fused) continue;   // the exact stage already ran the per-pixel tail
-        const Best *ball = ws.best_local;
-        if (a->comm) {   // also with one rank: the same RCCL path, exercised by the tests
-            if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, sq))) return rc;
-            ball = ws.best_all;
-        }
-        k_finish<<<M, 128, 0, sq>>>(src, ball, nranks, M, fa, ws.q64);
-        IA_LAUNCH_CHECK("k_finish");
-    }
-    return IA_OK;
-    };
+    LevelRun run;
+    int rc = run.init(a, st);
+    if (rc) return rc;
     // HIP-graph capture of the whole wave loop (IA_GRAPH / ia_diag_set_graph_mode: 0 off
     // [default], 1 levels of <= 2^18 rows, 2 every single-GPU level).  Sharded levels stay
     // eager (RCCL calls per wave).  Launches inside a graph are not timed.
@@ -342,15 +444,15 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
     const bool use_graph = !a->comm && !(a->flags & IA_SYNTH_EAGER) &&
                            (gm == 2 || (gm == 1 && a->nrows <= (1L << 18)));
     if (!use_graph) {
-        int rc = enqueue_waves(st);
-        if (rc) return rc;
+        for (int t = 0; t < run.nw; ++t)
+            if ((rc = run.wave(t, st))) return rc;
     } else {
         // capture on a private stream (the legacy default stream cannot capture)
-        timed = false;
+        run.timed = false;
         IA_HIP(g_graphs.retire());
         if (!g_graphs.cap) IA_HIP(hipStreamCreateWithFlags(&g_graphs.cap, hipStreamNonBlocking));
         IA_HIP(hipStreamBeginCapture(g_graphs.cap, hipStreamCaptureModeThreadLocal));
-        const int rc = enqueue_waves(g_graphs.cap);
+        for (int t = 0; t < run.nw && !rc; ++t) rc = run.wave(t, g_graphs.cap);
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(g_graphs.cap, &graph);
         if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
@@ -362,9 +464,96 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         IA_HIP(hipGraphLaunch(exec, st));
         IA_HIP(g_graphs.hold(exec, st));
     }
-    if (prof) {   // read back by ia_prof_end (no synchronisation here)
-        IA_HIP(hipMemcpyAsync(hstats, ws.stats, STATS_BYTES, hipMemcpyDeviceToHost, st));
-        prof_push(ProfRec{a->tag, a->nrows, pairs, ev0, nscreen, timed ? 1 : 0, hstats});
+    return run.done(st);
+}
+
+int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
+    IA_ARG(levels && n >= 1 && n <= 64, "ia_synth_levels: bad level count");
+    for (int j = 1; j < n; ++j)
+        IA_ARG(levels[j].Bp_sm == levels[j - 1].Bp_lg && levels[j].B_hs == levels[j - 1].H &&
+                   levels[j].B_ws == levels[j - 1].W,
+               "ia_synth_levels: levels must be consecutive (level j's coarse B' = level j-1's B')");
+    hipStream_t st = S(stream);
+    // one stream per level; coarser levels at high priority (IA_PIPE_PRIO, default 1) so
+    // that they run ahead of the finest level instead of time-sharing with it.  Measured
+    // (c4, one box, tools/ab_pipeline.sh): one level at a time 1706-1713 ms/step; pipelined
+    // with the coarse levels enqueued whole first at high priority 1641-1643 ms (the finest
+    // level's plateau screens undisturbed: k_screen16<11> 400 vs 396 us); enqueued just
+    // ahead of their need 1619-1621 ms but the plateau screens contended (414 us)
+    static const int prio_on = env_int("IA_PIPE_PRIO", 1);
+    while ((int)g_pipe.streams.size() < n) {
+        const int j = (int)g_pipe.streams.size();
+        int lo = 0, hi = 0;
+        IA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        hipStream_t s;
+        if (prio_on && j < n - 1)
+            IA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+        else
+            IA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        (void)lo;
+        g_pipe.streams.push_back(s);
+    }
+    g_pipe.next_event = 0;
+    hipEvent_t start;
+    IA_HIP(g_pipe.event(&start));
+    IA_HIP(hipEventRecord(start, st));
+    std::vector<LevelRun> run(n);
+    std::vector<std::vector<hipEvent_t>> blk(n);   // blk[j][b]: level j done through block b
+    std::vector<int> next(n, 0), waited(n, -1), need_max(n, 0);
+    for (int j = 0; j < n; ++j) {
+        hipStream_t sj = g_pipe.streams[j];
+        IA_HIP(hipStreamWaitEvent(sj, start, 0));
+        int rc = run[j].init(&levels[j], sj);
+        if (rc) return rc;
+        blk[j].assign((run[j].nw + PIPE_BLOCK - 1) / PIPE_BLOCK, nullptr);
+    }
+    // enqueue level j through wave `target` (and the coarse waves it needs, first)
+    std::function<int(int, int)> advance = [&](int j, int target) -> int {
+        hipStream_t sj = g_pipe.streams[j];
+        if (target > run[j].nw - 1) target = run[j].nw - 1;
+        while (next[j] <= target) {
+            const int t = next[j];
+            if (j > 0) {
+                int w = coarse_need(&levels[j], t);
+                need_max[j] = w > need_max[j] ? w : need_max[j];
+                w = need_max[j];
+                if (w > waited[j]) {
+                    const int b = w / PIPE_BLOCK;
+                    int rc = advance(j - 1, b * PIPE_BLOCK + PIPE_BLOCK - 1 + PIPE_AHEAD);
+                    if (rc) return rc;
+                    IA_HIP(hipStreamWaitEvent(sj, blk[j - 1][b], 0));
+                    waited[j] = b * PIPE_BLOCK + PIPE_BLOCK - 1;
+                }
+            }
+            int rc = run[j].wave(t, sj);
+            if (rc) return rc;
+            if ((t + 1) % PIPE_BLOCK == 0 || t == run[j].nw - 1) {
+                hipEvent_t e;
+                IA_HIP(g_pipe.event(&e));
+                IA_HIP(hipEventRecord(e, sj));
+                blk[j][t / PIPE_BLOCK] = e;
+            }
+            ++next[j];
+        }
+        return IA_OK;
+    };
+    // enqueue order (IA_PIPE_ORDER): 1 [default] every level whole, coarse to fine (the
+    // coarse levels' commands are all in flight before the finest level's); 0 the finest
+    // level first, coarse waves just ahead of their need
+    static const int order = env_int("IA_PIPE_ORDER", 1);
+    for (int i = 0; i < n; ++i) {
+        const int j = order ? i : n - 1 - i;
+        int rc = advance(j, run[j].nw - 1);
+        if (rc) return rc;
+    }
+    for (int j = 0; j < n; ++j) {
+        hipStream_t sj = g_pipe.streams[j];
+        int rc = run[j].done(sj);
+        if (rc) return rc;
+        hipEvent_t e;
+        IA_HIP(g_pipe.event(&e));
+        IA_HIP(hipEventRecord(e, sj));
+        IA_HIP(hipStreamWaitEvent(st, e, 0));
     }
     return IA_OK;
 }

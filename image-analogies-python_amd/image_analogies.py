@@ -59,6 +59,49 @@ def level_rows(Ap_pyr_list, level):
     return sum(p[level].shape[0] * p[level].shape[1] for p in Ap_pyr_list)
 
 
+class _LevelCall:
+    """Arguments (IaSynthArgs) and outputs of one level's device synthesis; keeps every
+    buffer the call reads alive until the caller drops it."""
+
+    def __init__(self, level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
+                 comm=None, prof=False, eager=False, debug=False):
+        dev = B_lg.device
+        H, W = B_lg.shape
+        self.index = index
+        self.s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
+        self.im = torch.empty(H * W, dtype=torch.int32, device=dev)
+        self.dbg = None
+        if debug:
+            self.dbg = (torch.zeros((H * W, 7), dtype=torch.int32, device=dev),
+                        torch.zeros((H * W, 2), dtype=torch.float64, device=dev))
+        nranks = _ia.lib().ia_comm_nranks(comm) if comm else 1
+        self.ws = _ia.workspace(_ia.lib().ia_synth_workspace_bytes(H, W, index.nrows, nranks))
+        a = _ia.IaSynthArgs()
+        a.src = index.src
+        a.db, a.row0, a.nrows, a.N_total = _ia.ptr(index.db).value, index.row0, index.nrows, index.N
+        a.center, a.amax = _ia.ptr(index.center).value, _ia.ptr(index.amax).value
+        a.B_sm, a.B_lg = _ia.ptr(B_sm).value, _ia.ptr(B_lg).value
+        a.B_hs, a.B_ws = B_sm.shape
+        a.H, a.W = H, W
+        a.Bp_sm, a.Bp_lg = _ia.ptr(Bp_sm).value, _ia.ptr(Bp_lg).value
+        a.weights = _ia.ptr(weights).value
+        a.kappa_factor = kappa_factor(level, max_levels, k)
+        a.s, a.im = _ia.ptr(self.s).value, _ia.ptr(self.im).value
+        a.workspace = _ia.ptr(self.ws).value
+        a.comm = comm
+        a.lsh = index.lsh_ptr()
+        a.flags = (_ia.IA_SYNTH_EAGER if eager else 0) | (_ia.IA_SYNTH_PROF if prof else 0)
+        a.tag = level
+        if debug:
+            a.dbg_px, a.dbg_dist = _ia.ptr(self.dbg[0]).value, _ia.ptr(self.dbg[1]).value
+        self.args = a
+
+    def result(self):
+        if self.dbg is not None:
+            return self.s, self.im, self.dbg
+        return self.s, self.im
+
+
 def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k,
                          comm=None, prof=False, eager=False, debug=False):
     """One level on device: Bp_lg updated in place; returns (s (H*W, 2), im (H*W,)) int32,
@@ -66,64 +109,77 @@ def synthesize_level_dev(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, wei
     (H*W, 2) fp64; include/ia.h).  prof=True: record this level into the open profile
     (_ia.prof_begin / prof_end; no synchronisation).  eager=True: never capture the
     level's wave loop into a HIP graph."""
-    dev = B_lg.device
-    H, W = B_lg.shape
-    s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
-    im = torch.empty(H * W, dtype=torch.int32, device=dev)
-    dbg_px = dbg_dist = None
-    if debug:
-        dbg_px = torch.zeros((H * W, 7), dtype=torch.int32, device=dev)
-        dbg_dist = torch.zeros((H * W, 2), dtype=torch.float64, device=dev)
-    nranks = _ia.lib().ia_comm_nranks(comm) if comm else 1
-    ws = _ia.workspace(_ia.lib().ia_synth_workspace_bytes(H, W, index.nrows, nranks))
-    a = _ia.IaSynthArgs()
-    a.src = index.src
-    a.db, a.row0, a.nrows, a.N_total = _ia.ptr(index.db).value, index.row0, index.nrows, index.N
-    a.center, a.amax = _ia.ptr(index.center).value, _ia.ptr(index.amax).value
-    a.B_sm, a.B_lg = _ia.ptr(B_sm).value, _ia.ptr(B_lg).value
-    a.B_hs, a.B_ws = B_sm.shape
-    a.H, a.W = H, W
-    a.Bp_sm, a.Bp_lg = _ia.ptr(Bp_sm).value, _ia.ptr(Bp_lg).value
-    a.weights = _ia.ptr(weights).value
-    a.kappa_factor = kappa_factor(level, max_levels, k)
-    a.s, a.im = _ia.ptr(s).value, _ia.ptr(im).value
-    a.workspace = _ia.ptr(ws).value
-    a.comm = comm
-    a.lsh = index.lsh_ptr()
-    a.flags = (_ia.IA_SYNTH_EAGER if eager else 0) | (_ia.IA_SYNTH_PROF if prof else 0)
-    a.tag = level
-    a.dbg_px, a.dbg_dist = _ia.ptr(dbg_px).value, _ia.ptr(dbg_dist).value
-    _ia.check(_ia.lib().ia_synth_level(ctypes.byref(a), _ia.stream()), 'ia_synth_level')
-    if debug:
-        return s, im, (dbg_px, dbg_dist)
-    return s, im
+    call = _LevelCall(level, max_levels, index, B_sm, B_lg, Bp_sm, Bp_lg, weights, k, comm,
+                      prof, eager, debug)
+    _ia.check(_ia.lib().ia_synth_level(ctypes.byref(call.args), _ia.stream()), 'ia_synth_level')
+    return call.result()
+
+
+def synthesize_levels_dev(calls):
+    """Consecutive levels (a list of _LevelCall, coarse to fine) synthesised together by
+    ia_synth_levels: each level on its own stream, running behind the level below as far
+    as its coarse windows allow (include/ia.h).  Same results as one level at a time."""
+    arr = (_ia.IaSynthArgs * len(calls))(*[c.args for c in calls])
+    _ia.check(_ia.lib().ia_synth_levels(arr, len(calls), _ia.stream()), 'ia_synth_levels')
+    return [c.result() for c in calls]
+
+
+def pipeline_default():
+    """Levels run pipelined by default (IA_PIPELINE=0: one level at a time)."""
+    return os.environ.get('IA_PIPELINE', '1') != '0'
 
 
 def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
-                   comm=None, rank=0, nranks=1, prof=False, levels=None, lsh=None, eager=False):
+                   comm=None, rank=0, nranks=1, prof=False, levels=None, lsh=None, eager=False,
+                   pipeline=None, debug=False):
     """Synthesise levels 1..max_levels-1 (image_analogies.py:119-220) from device
     pyramids.  Bp_pyr (list of device tensors) is updated in place.  lsh: None (exact
-    matcher) or LevelIndex.build_lsh arguments (approximate matcher).
-    Returns {level: (s, im)} device tensors."""
+    matcher) or LevelIndex.build_lsh arguments (approximate matcher).  comm: one
+    communicator, or a list (one per sharded level, needed when sharded levels run
+    pipelined).  pipeline: run the levels concurrently (ia_synth_levels; default
+    pipeline_default()), else one after the other.
+    Returns {level: (s, im[, debug])} device tensors."""
     w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
+    if pipeline is None:
+        pipeline = pipeline_default() and not eager
+    todo = [l for l in range(1, max_levels) if levels is None or l in levels]
+    comms = list(comm) if isinstance(comm, (list, tuple)) else None
+    sharded = [l for l in todo
+               if comm is not None and shard_level(level_rows(Ap_pyr_list, l), nranks)]
+    if pipeline and comms is None and len(sharded) > 1:
+        pipeline = False      # one communicator cannot serve concurrent levels
     out = {}
     t_start = time.time()
-    for level in range(1, max_levels):
-        if levels is not None and level not in levels:
-            continue
+    calls = []
+    for level in todo:
         lcomm, row_range = None, None
-        if comm is not None and shard_level(level_rows(Ap_pyr_list, level), nranks):
-            lcomm = comm
+        if level in sharded:
+            lcomm = comms[sharded.index(level) % len(comms)] if comms else comm
             row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
         index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range, lsh)
-        out[level] = synthesize_level_dev(level, max_levels, index, B_pyr[level - 1],
-                                          B_pyr[level], Bp_pyr[level - 1], Bp_pyr[level], w,
-                                          k, lcomm, prof, eager)
-        del index
+        call = _LevelCall(level, max_levels, index, B_pyr[level - 1], B_pyr[level],
+                          Bp_pyr[level - 1], Bp_pyr[level], w, k, lcomm, prof, eager, debug)
+        if pipeline:
+            calls.append((level, call))
+            continue
+        _ia.check(_ia.lib().ia_synth_level(ctypes.byref(call.args), _ia.stream()),
+                  'ia_synth_level')
+        out[level] = call.result()
+        del index, call
         if os.environ.get('IA_VERBOSE'):
             torch.cuda.synchronize()
             print('[ia] level %d/%d done %.3f s' % (level, max_levels - 1, time.time() - t_start),
                   file=sys.stderr, flush=True)
+    # runs of consecutive levels go to ia_synth_levels together
+    i = 0
+    while i < len(calls):
+        j = i + 1
+        while j < len(calls) and calls[j][0] == calls[j - 1][0] + 1:
+            j += 1
+        res = synthesize_levels_dev([c for _, c in calls[i:j]])
+        for (level, _), r in zip(calls[i:j], res):
+            out[level] = r
+        i = j
     return out
 
 
@@ -295,18 +351,19 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
     torch.cuda.synchronize()
     print('Environment Setup: %f' % (time.time() - start_time))
     weights = _ia.to_dev(c.weights)
+    # all levels on device, pipelined (ia_synth_levels); then each level's outputs
+    start_time = time.time()
+    print('Computing levels 1 to %d' % (c.max_levels - 1))
+    res = synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c.max_levels, c.k, weights,
+                         lsh=algorithms.lsh_params(c), debug=debug)
+    torch.cuda.synchronize()
+    print('Synthesis time: %f' % (time.time() - start_time))
     for level in range(1, c.max_levels):
-        start_time = time.time()
-        print('Computing level %d of %d' % (level, c.max_levels - 1))
-        index = algorithms.level_index(A_pyr, Ap_pyr_list, level,
-                                       lsh=algorithms.lsh_params(c))
-        res = synthesize_level_dev(level, c.max_levels, index, B_pyr[level - 1], B_pyr[level],
-                                   Bp_pyr[level - 1], Bp_pyr[level], weights, c.k, debug=debug)
-        s, im = res[0], res[1]
+        s, im = res[level][0], res[level][1]
         color_im_out = color_output(level, Bp_pyr[level], s, im, color_pyr_list, c)
         rec = None
         if debug:
-            rec = debug_record(s, im, res[2], Bp_pyr[level].shape[:2])
+            rec = debug_record(s, im, res[level][2], Bp_pyr[level].shape[:2])
             save_debug(out_path, level, rec, Bp_pyr[level].cpu().numpy())
         if outputs is not None:
             outputs[level] = {'color': color_im_out, 's': s.cpu().numpy(), 'im': im.cpu().numpy()}
@@ -314,6 +371,5 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
                 outputs[level]['debug'] = rec
         plt.imsave(out_path + 'level_%d_color.jpg' % level, color_im_out)
         plt.imsave(out_path + out_path.split('/')[-2] + '.jpg', color_im_out)
-        print('Level %d time: %f' % (level, time.time() - start_time))
     print('Total time: %f' % (time.time() - begin_time))
     return [p.cpu().numpy() for p in Bp_pyr]

@@ -184,6 +184,12 @@ typedef struct {
 #define IA_SYNTH_PROF 2
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);
+/* n consecutive levels (coarse to fine: levels[j].Bp_sm == levels[j-1].Bp_lg) at once, with
+ * the same results as n ia_synth_level calls in order: each level runs on its own stream
+ * and wave t of level j waits only for the waves of level j-1 its 3x3 coarse windows read
+ * (coarse pixel (y/2 + 1, x/2 + 1) and before), so the levels overlap and the critical
+ * path is about the finest level's waves.  Sharded levels need one communicator each. */
+int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream);
 
 /* profiling of ia_synth_level calls flagged IA_SYNTH_PROF (process-wide, thread-safe):
  * ia_prof_begin opens a profile (the caller has synchronised); ia_prof_end synchronises the
@@ -197,6 +203,9 @@ int ia_prof_begin(void);
  * profile), so that no event is created inside a timed region */
 int ia_prof_prepare(long nevents);
 int ia_prof_end(double *out, int maxrec);
+/* after ia_prof_end: record rec's screen launches one by one (ms from the HIP events, M
+ * the launch's query count); returns the number of timed launches */
+int ia_prof_launches(int rec, float *ms, int *M, int max);
 /* destroy the calling host thread's graph-capture stream and last executable graph */
 int ia_release_thread_resources(void);
 

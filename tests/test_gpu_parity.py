@@ -244,8 +244,64 @@ def test_synthesis_through_rccl_exchange(gpu):
         for l in ref:
             assert np.array_equal(out[l][0].cpu().numpy(), ref[l][1]), l
             assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
+            assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l
     finally:
         _ia.check(_ia.lib().ia_comm_destroy(comm), 'ia_comm_destroy')
+
+
+def test_pipelined_sharded_levels_through_rccl(gpu):
+    """Every level sharded (1-rank communicators, one per level) AND pipelined
+    (ia_synth_levels: each level's RCCL exchange on its own stream): the oracle's B', s, im."""
+    import ctypes
+    import _ia
+    import image_analogies as ia
+    comms = []
+    try:
+        A, Aps, B = analogy_inputs(32, (44, 50), (37, 45), n_ap=2)
+        A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=32)
+        for _ in range(1, L):
+            buf = ctypes.create_string_buffer(128)
+            _ia.check(_ia.lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
+            cm = ctypes.c_void_p()
+            _ia.check(_ia.lib().ia_comm_init(buf.raw, 1, 0, ctypes.byref(cm)), 'ia_comm_init')
+            comms.append(cm)
+        w = o.compute_weights(3, 5, 12, 1)
+        ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 0.7, w)
+        Bp_dev = [dev(b) for b in Bp_pyr]
+        out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                                [dev(p) for p in B_pyr], Bp_dev, L, 0.7, w, comm=comms, rank=0,
+                                nranks=1, pipeline=True)
+        for l in ref:
+            assert np.array_equal(out[l][0].cpu().numpy(), ref[l][1]), l
+            assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
+            assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l
+    finally:
+        torch.cuda.synchronize()
+        for cm in comms:
+            _ia.check(_ia.lib().ia_comm_destroy(cm), 'ia_comm_destroy')
+
+
+@pytest.mark.parametrize('seed', [51, 52])
+def test_pipelined_levels_equal_sequential(gpu, seed):
+    """ia_synth_levels (levels overlapped, each on its own stream) gives bitwise the same
+    B', s, im as one level at a time, and both equal the oracle."""
+    import image_analogies as ia
+    A, Aps, B = analogy_inputs(seed, (70, 83), (66, 90), n_ap=2, flat=(seed == 52))
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=seed)
+    w = o.compute_weights(3, 5, 12, 1)
+    ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 1.0, w)
+    outs = []
+    for pipe in (False, True):
+        Bp_dev = [dev(b) for b in Bp_pyr]
+        out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                                [dev(p) for p in B_pyr], Bp_dev, L, 1.0, w, pipeline=pipe)
+        outs.append({l: (out[l][0].cpu().numpy(), out[l][1].cpu().numpy(),
+                         Bp_dev[l].cpu().numpy()) for l in out})
+    for l in ref:
+        for o_ in outs:
+            assert np.array_equal(o_[l][0], ref[l][1]), l
+            assert np.array_equal(o_[l][1], ref[l][2]), l
+            assert np.array_equal(o_[l][2], ref[l][0]), l
 
 
 def test_sharded_level_index_rows(gpu):

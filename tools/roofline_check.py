@@ -14,6 +14,18 @@ import sys
 
 def main(trace, bench=None):
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r['Start_Timestamp']))
+    # the dominant screen instance (k_screen16<G> with the most total time)
+    tot = {}
+    for r in rows:
+        n = r['Kernel_Name']
+        if 'k_screen16' in n:
+            d = tot.setdefault(n, [0, 0])
+            d[0] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+            d[1] += 1
+    if tot:
+        dom = max(tot, key=lambda n: tot[n][0])
+        print('dominant kernel %s: %d dispatches, mean duration %.1f us'
+              % (dom, tot[dom][1], tot[dom][0] / tot[dom][1] / 1e3))
     levels, cur = [], None
     for r in rows:
         name = r['Kernel_Name']
@@ -29,8 +41,8 @@ def main(trace, bench=None):
                                      sum(fin) / len(fin) / 1e3))
     if bench:
         b = json.loads(open(bench).read().strip().splitlines()[-1])
-        print('bench.py roofline.screen_avg_us (HIP events): %.1f us'
-              % b['roofline']['screen_avg_us'])
+        print('bench.py roofline (%s) screen_avg_us (HIP events): %.1f us'
+              % (b['roofline']['kernel'], b['roofline']['screen_avg_us']))
 
 
 if __name__ == '__main__':
