@@ -56,6 +56,10 @@ class IaSynthArgs(ctypes.Structure):
                 ('dbg_dist', _dp)]
 
 
+class IaShardDb(ctypes.Structure):
+    _fields_ = [('db', _dp), ('row0', ctypes.c_long), ('nrows', ctypes.c_long), ('amax', _dp)]
+
+
 IA_SYNTH_EAGER = 1
 IA_SYNTH_PROF = 2
 IA_PROF_FIELDS = 8
@@ -111,6 +115,8 @@ _SIGS = {
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
+    'ia_diag_synth_level_shards': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs),
+                                                  ctypes.POINTER(IaShardDb), ctypes.c_int, _dp]),
 }
 
 _lib = None

@@ -1,10 +1,11 @@
 // ia_comm.hip — multi-GPU exchange for the sharded A-database.
 // One process per GPU; the DB rows of a level are split contiguously over ranks.  Each
-// wave every rank produces the exact (fp64 distance, global row) winner of its shard
-// for each query; one RCCL all-gather over xGMI (M x 16 B per rank, latency-bound)
-// gives every rank all shards' winners, and k_finish reduces them with the same
-// lexicographic (distance, lowest row) rule as np.argmin.  Coherence / kappa / update
-// then run identically on every rank from replicated state: no further collective.
+// wave every rank produces, per query, the exact (fp64 distance, global row) winner of its
+// shard and that row's weighted distance (ShardRec); one RCCL all-gather over xGMI (M x
+// 32 B per rank, latency-bound) gives every rank all shards' records, and k_finish reduces
+// them with the same lexicographic (distance, lowest row) rule as np.argmin.  Coherence /
+// kappa / update then run identically on every rank from replicated state: no further
+// collective.
 #include "ia_internal.h"
 
 #include <rccl/rccl.h>
@@ -25,10 +26,10 @@ static int nccl_fail(ncclResult_t r, const char *what) {
 
 int comm_nranks(void *comm) { return comm ? reinterpret_cast<Comm *>(comm)->nranks : 1; }
 
-int comm_allgather_best(void *comm, const Best *send, Best *recv, int M, hipStream_t st) {
+int comm_allgather(void *comm, const void *send, void *recv, size_t bytes, hipStream_t st) {
     Comm *c = reinterpret_cast<Comm *>(comm);
-    static_assert(sizeof(Best) == 16, "Best must be 16 bytes");
-    ncclResult_t r = ncclAllGather(send, recv, (size_t)M * 2, ncclUint64, c->c, st);
+    IA_ARG(bytes % 8 == 0, "comm_allgather: whole 8-byte words");
+    ncclResult_t r = ncclAllGather(send, recv, bytes / 8, ncclUint64, c->c, st);
     if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
     return IA_OK;
 }

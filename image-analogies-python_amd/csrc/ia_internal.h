@@ -40,6 +40,12 @@ struct Best {            // exact winner of a (query, shard): fp64 distance + gl
     double d;
     long long idx;
 };
+struct ShardRec {        // what a rank contributes per query to the cross-rank exchange
+    double d;            // its shard's exact winner: distance, global row,
+    long long idx;
+    double wd;           // and that row's weighted (kappa) distance to the query
+    double pad;
+};
 struct WItem {           // one (query, candidate segment) of the work-list exact stage
     int q, seg;
     float twoR;          // the re-screen's norm-slot factor 2^R
@@ -67,6 +73,10 @@ struct FinishArgs {
     int32_t *s, *im;
     int32_t *dbg_px;     // nullable: 7 int32 per pixel (ia.h IaSynthArgs)
     double *dbg_dist;    // nullable: 2 doubles per pixel
+    // sharded DB (nullable otherwise): the exact stage writes each query's ShardRec and
+    // its coherence pick (CohSel, ia_finish.h) here instead of finishing the pixel
+    ShardRec *shard_out;
+    void *coh_out;
 };
 
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS

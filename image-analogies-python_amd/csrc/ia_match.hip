@@ -96,24 +96,26 @@ static_assert(DB_SEG_MAX <= RESCORE_RPT * 256, "one re-screen step per segment")
 
 // e* of query q over its nseg segment minima (float4 reads, nseg a multiple of 4); the
 // first RESCORE_REG float4s per thread stay in v[] for the selection pass
+// (threads >= 256 of a block take no part but meet the barrier)
 __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, float4 (&v)[RESCORE_REG],
                                              float *redf) {
     const int tid = threadIdx.x;
+    const long lim = tid < 256 ? n4 : 0;
 #pragma unroll
     for (int j = 0; j < RESCORE_REG; ++j) {
         const long i = tid + (long)j * 256;
-        v[j] = i < n4 ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+        v[j] = i < lim ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
     }
     float emin = FLT_MAX;
 #pragma unroll
     for (int j = 0; j < RESCORE_REG; ++j)
         emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
-    for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
+    for (long i = tid + (long)RESCORE_REG * 256; i < lim; i += 256) {
         const float4 x = sq4[i];
         emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
     }
     for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
-    if ((tid & 63) == 0) redf[tid >> 6] = emin;
+    if ((tid & 63) == 0 && tid < 256) redf[tid >> 6] = emin;
     __syncthreads();
     return fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
 }
@@ -122,6 +124,7 @@ __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, float4 
 __device__ __forceinline__ void segmin_select(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
                                               double Tseg, int *slist, int *scount) {
     const int tid = threadIdx.x;
+    if (tid >= 256) return;
     auto push = [&](float e, long s) {
         if ((double)e <= Tseg) {
             const int pos = atomicAdd(scount, 1);
@@ -145,21 +148,52 @@ __device__ __forceinline__ void segmin_select(const float4 *sq4, long n4, const 
     }
 }
 
-// Exact stage, one 256-thread workgroup per query.  FIN: single shard — waves 0/1 then run
-// the per-pixel tail of the synthesis step (ia_finish.h) on the winner, saving a launch and
-// a round trip per wave.
-template <bool FIN>
-__global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrows, long nseg,
-                                                 int seg_rows, const float *__restrict__ segmin,
-                                                 const half8 *__restrict__ db,
-                                                 const float *__restrict__ qp,
-                                                 const double *__restrict__ q64,
-                                                 const double *__restrict__ nq,
-                                                 const float *__restrict__ amax,
-                                                 Best *__restrict__ best,
-                                                 unsigned long long *stats, FinishArgs fa) {
+// The end of the exact stage for query q once its winner win (distance bd) is known, by
+// the block's waves 0 and 1 (all threads call it; every wave reaches the barriers).
+// MODE 0: best[q] only (written by the caller); 1 (one shard): wave 1 picks the coherence
+// candidate while wave 0 weighs the winner, then wave 0 finishes the pixel (ia_finish.h),
+// saving a launch and a round trip per wave; 2 (sharded DB): the same two picks, written
+// out (ShardRec, CohSel) for k_finish after the cross-rank exchange.
+// have_cs: the coherence pick is already in *cs (k_rescore's fifth wave): only the weight.
+template <int MODE>
+__device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long win, double bd,
+                                           const FinishArgs &fa, const double *qs, CohSel *cs,
+                                           bool have_cs = false) {
+    if (MODE == 0) return;
+    __syncthreads();
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double d_app = 0.0;
+    if (wv == 1 && !have_cs) {
+        const CohSel c = coh_pick(src, q, fa, qs, lane);
+        if (lane == 0) *cs = c;
+    } else if (wv == 0) {
+        d_app = app_wdist(src, win, fa, qs, lane);
+    }
+    if (MODE == 1) {
+        if (!have_cs) __syncthreads();
+        if (wv == 0) finish_apply(src, win, q, fa, *cs, d_app, lane);
+    } else {
+        if (!have_cs) __syncthreads();
+        if (wv == 0 && lane == 0) {
+            fa.shard_out[q] = ShardRec{bd, win, d_app, 0.0};
+            reinterpret_cast<CohSel *>(fa.coh_out)[q] = *cs;
+        }
+    }
+}
+
+// Exact stage, one workgroup per query: waves 0-3 screen and rescore; with the pixel tail
+// (MODE 1, 2: exact_tail) a fifth wave picks the coherence candidate meanwhile (it needs
+// only s / im of earlier waves), so the tail after the winner is one gather round.
+template <int MODE>
+__global__ __launch_bounds__(MODE == 0 ? 256 : 320) void k_rescore(
+        DbSrc src, long row0, long nrows, long nseg, int seg_rows,
+        const float *__restrict__ segmin, const half8 *__restrict__ db,
+        const float *__restrict__ qp, const double *__restrict__ q64,
+        const double *__restrict__ nq, const float *__restrict__ amax, Best *__restrict__ best,
+        unsigned long long *stats, FinishArgs fa) {
     __shared__ int slist[RESCORE_SEGCAP];
     __shared__ long long win;
+    __shared__ double wind;
     __shared__ CohSel cs;
     __shared__ int scount;
     __shared__ float redf[4];
@@ -173,6 +207,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
 
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
+    const bool ex = tid < 256;               // the exact stage's waves
     if (tid < IA_DP) {
         qs[tid] = q64[(long)q * IA_DP + tid];
         qf[tid] = qp[(long)q * IA_DP + tid];
@@ -200,7 +235,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
     // loads issued together (seg_rows <= 512 = RESCORE_RPT * 256: one step per segment);
     // rows within Trow go to a list rescored one per thread after the loop (one round of
     // feature gathers); a list overflow is rescored in place
-    const long nrs = nscan * seg_rows;
+    const long nrs = ex ? nscan * seg_rows : 0;
     for (long base = 0; base < nrs; base += RESCORE_RPT * 256) {
         float e[RESCORE_RPT];
         long lr[RESCORE_RPT];
@@ -224,8 +259,12 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
             }
         }
     }
+    if (MODE != 0 && !ex) {                  // the fifth wave: coherence pick
+        const CohSel c = coh_pick(src, q, fa, qs, tid & 63);
+        if ((tid & 63) == 0) cs = c;
+    }
     __syncthreads();
-    {
+    if (ex) {
         const int nl = rcount < RESCORE_ROWCAP ? rcount : RESCORE_ROWCAP;
         for (int i = tid; i < nl; i += 256)
             best_update(bd, bi, row_dist2(src, row0 + rlist[i], qs), row0 + rlist[i]);
@@ -236,12 +275,13 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
         best_update(bd, bi, od, oi);
     }
     if (mine) atomicAdd(&nresc, mine);
-    if ((tid & 63) == 0) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
+    if ((tid & 63) == 0 && ex) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < 4; ++w) best_update(bd, bi, redd[w], redi[w]);
         best[q] = Best{bd, bi};
         win = bi;
+        wind = bd;
         if (stats) {
             unsigned long long *sl = stats_slot(stats, q);
             atomicAdd(&sl[0], (unsigned long long)nresc);
@@ -249,19 +289,7 @@ __global__ __launch_bounds__(256) void k_rescore(DbSrc src, long row0, long nrow
             atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
-    if (FIN) {   // wave 1 picks the coherence candidate while wave 0 weighs the winner
-        __syncthreads();
-        const int wv = tid >> 6, lane = tid & 63;
-        double d_app = 0.0;
-        if (wv == 1) {
-            const CohSel c = coh_pick(src, q, fa, qs, lane);
-            if (lane == 0) cs = c;
-        } else if (wv == 0) {
-            d_app = app_wdist(src, win, fa, qs, lane);
-        }
-        __syncthreads();
-        if (wv == 0) finish_apply(src, win, q, fa, cs, d_app, lane);
-    }
+    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, true);
 }
 
 // ---------------------------------------------------------------------------------
@@ -379,25 +407,20 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
     }
 }
 
-// FIN: two waves — wave 1 picks the coherence candidate (two gather rounds that need only
-// s / im of earlier waves) while wave 0 reduces the items; then wave 0 finishes the pixel
-template <bool FIN>
+// one wave per query reduces its items (lexicographic (distance, row) minimum); MODE as
+// exact_tail (1, 2: a second wave picks the coherence candidate meanwhile)
+template <int MODE>
 __global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restrict__ sel,
                                                 const Best *__restrict__ ibest, int *ctr,
                                                 Best *__restrict__ best, FinishArgs fa,
                                                 const double *__restrict__ q64) {
     __shared__ double qs[IA_DP];
     __shared__ CohSel cs;
+    __shared__ long long win;
+    __shared__ double wind;
     const int m = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (FIN) {
-        if (threadIdx.x < IA_DP) qs[threadIdx.x] = q64[(long)m * IA_DP + threadIdx.x];
-        __syncthreads();
-        if (wv == 1) {
-            const CohSel c = coh_pick(src, m, fa, qs, lane);
-            if (lane == 0) cs = c;
-        }
-    }
+    if (MODE != 0 && threadIdx.x < IA_DP) qs[threadIdx.x] = q64[(long)m * IA_DP + threadIdx.x];
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
     if (wv == 0) {
@@ -412,13 +435,15 @@ __global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restric
             best_update(bd, bi, od, oi);
         }
         if (m == 0 && lane == 0) *ctr = 0;   // every k_items block has read it
+        if (lane == 0) {
+            if (MODE == 0) best[m] = Best{bd, bi};
+            win = bi;
+            wind = bd;
+        }
     }
-    if (FIN) {
-        const double d_app = wv == 0 ? app_wdist(src, bi, fa, qs, lane) : 0.0;
+    if (MODE != 0) {
         __syncthreads();
-        if (wv == 0) finish_apply(src, bi, m, fa, cs, d_app, lane);
-    } else if (wv == 0 && lane == 0) {
-        best[m] = Best{bd, bi};
+        exact_tail<MODE>(src, m, win, wind, fa, qs, &cs);
     }
 }
 
@@ -471,6 +496,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     // default: the work list for levels above 2^20 rows (where k_rescore's per-query
     // serialisation costs most); k_rescore below, with or without the fused tail (a
     // sharded rank's 0.5 M-row shard: 13.9 vs 19.9 us per wave, profiles/r01_shard_sim_g8.txt)
+    const int mode = !fin ? 0 : (fin->shard_out ? 2 : 1);
     if (rm == 1 || (rm < 0 && nrows > (1L << 20))) {
         const long nseg = db_nsegs(nrows);
         k_select<<<M, 256, 0, st>>>(nseg, ws.segmin, nq, amax, ws.ctr, ws.items, ws.sel, stats);
@@ -479,19 +505,23 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         k_items<<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr, db, qp,
                                       q64, ws.ibest, stats);
         IA_LAUNCH_CHECK("k_items");
-        if (fin)
-            k_gather<true><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+        if (mode == 2)
+            k_gather<2><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+        else if (mode == 1)
+            k_gather<1><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
         else
-            k_gather<false><<<M, 64, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+            k_gather<0><<<M, 64, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
         IA_LAUNCH_CHECK("k_gather");
         return IA_OK;
     }
-    if (fin)
-        k_rescore<true><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows),
-                                           ws.segmin, db, qp, q64, nq, amax, best, stats, fa);
-    else
-        k_rescore<false><<<M, 256, 0, st>>>(src, row0, nrows, db_nsegs(nrows), db_seg_rows(nrows),
-                                            ws.segmin, db, qp, q64, nq, amax, best, stats, fa);
+#define IA_RESCORE_CASE(MD)                                                                      \
+    k_rescore<MD><<<M, MD == 0 ? 256 : 320, 0, st>>>(src, row0, nrows, db_nsegs(nrows),          \
+                                                     db_seg_rows(nrows), ws.segmin, db, qp, q64, \
+                                                     nq, amax, best, stats, fa)
+    if (mode == 2) IA_RESCORE_CASE(2);
+    else if (mode == 1) IA_RESCORE_CASE(1);
+    else IA_RESCORE_CASE(0);
+#undef IA_RESCORE_CASE
     IA_LAUNCH_CHECK("k_rescore");
     return IA_OK;
 }

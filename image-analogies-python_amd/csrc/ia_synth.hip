@@ -17,6 +17,7 @@
 //   k_finish      -> coherence, kappa test, B'/s/im update (this file)
 #include "ia_finish.h"
 #include "ia_split16.h"
+#include "../../include/ia_diag.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -28,12 +29,36 @@
 
 namespace ia {
 
-// two waves per query pixel: wave 1 picks the coherence candidate while wave 0 takes the
-// lexicographic (dist, row) minimum over the shards' exact winners; then wave 0 runs the
-// rest of the shared per-pixel tail (ia_finish.h)
-__global__ __launch_bounds__(128) void k_finish(DbSrc src, const Best *__restrict__ best_all,
-                                                int nranks, int M, FinishArgs f,
-                                                const double *__restrict__ q64) {
+// Sharded DB, after the cross-rank exchange: one wave per query pixel takes the
+// lexicographic (distance, row) minimum over the ranks' ShardRec (lane g = rank g), whose
+// weighted distance the owning rank already computed, and finishes the pixel with the
+// coherence pick its own exact stage stored (every rank holds the same replicated state,
+// so the picks agree; ia_finish.h).  No feature gathers here.
+__global__ __launch_bounds__(64) void k_finish(DbSrc src, const ShardRec *__restrict__ rec_all,
+                                               const CohSel *__restrict__ coh, int nranks, int M,
+                                               FinishArgs f) {
+    const int m = blockIdx.x;
+    const int lane = threadIdx.x;
+    double d = INFINITY, wd = 0.0;
+    long long idx = 0x7fffffffffffffffLL;
+    for (int g = lane; g < nranks; g += 64) {
+        const ShardRec r = rec_all[(long)g * M + m];
+        if (r.d < d || (r.d == d && r.idx < idx)) { d = r.d; idx = r.idx; wd = r.wd; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(d, o), owd = __shfl_xor(wd, o);
+        const long long oi = __shfl_xor(idx, o);
+        if (od < d || (od == d && oi < idx)) { d = od; idx = oi; wd = owd; }
+    }
+    finish_apply(src, idx, m, f, coh[m], wd, lane);
+}
+
+// Sharded DB, the other tail form (IA_SHARD_TAIL=0): the exact stage writes only its
+// shard's (distance, row); after the exchange wave 1 picks the coherence candidate while
+// wave 0 reduces the ranks' winners and weighs the global one, then finishes the pixel
+__global__ __launch_bounds__(128) void k_finish_gather(DbSrc src, const Best *__restrict__ best_all,
+                                                       int nranks, int M, FinishArgs f,
+                                                       const double *__restrict__ q64) {
     __shared__ double qs[IA_DP];
     __shared__ CohSel cs;
     const int m = blockIdx.x;
@@ -56,6 +81,26 @@ __global__ __launch_bounds__(128) void k_finish(DbSrc src, const Best *__restric
     if (wv == 0) finish_apply(src, app, m, f, cs, d_app, lane);
 }
 
+// LSH matcher (one shard): wave 1 picks the coherence candidate while wave 0 weighs the
+// LSH winner, then wave 0 finishes the pixel (ia_finish.h)
+__global__ __launch_bounds__(128) void k_lsh_tail(DbSrc src, const Best *__restrict__ best, int M,
+                                                  FinishArgs f, const double *__restrict__ q64) {
+    __shared__ double qs[IA_DP];
+    __shared__ CohSel cs;
+    const int m = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x < IA_DP) qs[threadIdx.x] = q64[(long)m * IA_DP + threadIdx.x];
+    __syncthreads();
+    const long long app = best[m].idx;
+    if (wv == 1) {
+        const CohSel c = coh_pick(src, m, f, qs, lane);
+        if (lane == 0) cs = c;
+    }
+    const double d_app = wv == 0 ? app_wdist(src, app, f, qs, lane) : 0.0;
+    __syncthreads();
+    if (wv == 0) finish_apply(src, app, m, f, cs, d_app, lane);
+}
+
 // -------------------------------- workspace ----------------------------------------
 struct SynthWs {
     double *q64;
@@ -64,7 +109,9 @@ struct SynthWs {
     double *nq;
     void *scratch;           // screen output (candidates or segment minima)
     Best *best_local;
-    Best *best_all;
+    ShardRec *rec_local;     // sharded DB: this rank's records, then all ranks'
+    ShardRec *rec_all;
+    CohSel *coh;
     unsigned long long *stats;
 };
 
@@ -85,7 +132,9 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     w.nq = (double *)take((size_t)qr * sizeof(double));
     w.scratch = take(match_scratch_bytes(qr, nrows));
     w.best_local = (Best *)take((size_t)Mmax * sizeof(Best));
-    w.best_all = (Best *)take((size_t)Mmax * nranks * sizeof(Best));
+    w.rec_local = (ShardRec *)take((size_t)Mmax * sizeof(ShardRec));
+    w.rec_all = (ShardRec *)take((size_t)Mmax * nranks * sizeof(ShardRec));
+    w.coh = (CohSel *)take((size_t)Mmax * sizeof(CohSel));
     w.stats = (unsigned long long *)take(STATS_BYTES);
     if (ws) *ws = w;
     return off;
@@ -181,8 +230,18 @@ static void prof_push(const ProfRec &r) {
 static std::atomic<int> g_graph_mode{env_int("IA_GRAPH", 0)};
 static int graph_mode() { return g_graph_mode.load(std::memory_order_relaxed); }
 
-int comm_allgather_best(void *comm, const Best *send, Best *recv, int M, hipStream_t st);
+int comm_allgather(void *comm, const void *send, void *recv, size_t bytes, hipStream_t st);
 int comm_nranks(void *comm);
+
+// sharded tail form (IA_SHARD_TAIL): 0 [default] the exchange carries (distance, row) and
+// k_finish_gather does the coherence pick and the weighting after it; 1 the exact stage
+// prepares the tail (ShardRec, CohSel) and k_finish only reduces.  Measured on the
+// simulated G = 8 rank (tools/ab_shard.sh, one box): finest level 335 vs 361 ms, pipelined
+// step 415 vs 450 ms, so 0
+static int shard_tail() {
+    static const int v = env_int("IA_SHARD_TAIL", 0);
+    return v;
+}
 
 static int check_args(const IaSynthArgs *a) {
     IA_ARG(a && a->db && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
@@ -197,6 +256,7 @@ static int check_args(const IaSynthArgs *a) {
            "ia_synth_level: A level shapes");
     IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level: debug outputs come in pairs");
     IA_ARG(comm_nranks(a->comm) >= 1, "ia_synth_level: bad communicator");
+    IA_ARG(!(a->lsh && a->comm), "ia_synth_level: the LSH matcher runs unsharded (comm must be NULL)");
     return IA_OK;
 }
 
@@ -204,6 +264,8 @@ static int check_args(const IaSynthArgs *a) {
 // (each enqueues that wave's launches), then done().
 struct LevelRun {
     const IaSynthArgs *a = nullptr;
+    const IaShardDb *sim = nullptr;   // diagnostic: nsim DB shards in this process
+    int nsim = 0;
     SynthWs ws{};
     DbSrc src{};
     ImgPair B{}, Bp{};
@@ -219,10 +281,12 @@ struct LevelRun {
         a = args;
         int rc = check_args(a);
         if (rc) return rc;
-        nranks = a->comm ? comm_nranks(a->comm) : 1;
+        nranks = a->comm ? comm_nranks(a->comm) : (sim ? nsim : 1);
         H = a->H; W = a->W;
         nw = (W - 1) + 3 * (H - 1) + 1;
-        carve(&ws, reinterpret_cast<char *>(a->workspace), H, W, a->nrows, nranks);
+        long rows_ws = a->nrows;
+        for (int r = 0; r < nsim; ++r) rows_ws = sim[r].nrows > rows_ws ? sim[r].nrows : rows_ws;
+        carve(&ws, reinterpret_cast<char *>(a->workspace), H, W, rows_ws, nranks);
         const int Mmax = wave_max_queries(H, W);
         IA_HIP(hipMemsetAsync(ws.qp, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
         IA_HIP(hipMemsetAsync(ws.q16, 0, (size_t)qrows_alloc(Mmax) * Q16_ROW * 16, st));
@@ -235,8 +299,10 @@ struct LevelRun {
         timed = prof;
         if (prof && (rc = prof_reserve(2 * (size_t)nw, &ev0, &hstats))) return rc;
         // fused tail (one launch + one round trip less per wave): on a single shard the exact
-        // stage's last kernel (k_rescore, or k_gather of the work list) runs the pixel tail
-        fused = !a->comm && !a->lsh;
+        // stage's last kernel (k_rescore, or k_gather of the work list) runs the pixel tail;
+        // on a sharded DB it prepares the tail (coherence pick, the winner's weighted
+        // distance) before the exchange
+        fused = !a->comm && !a->lsh && !sim;
         return IA_OK;
     }
 
@@ -253,13 +319,16 @@ struct LevelRun {
         wave_rows(H, W, t, y_lo, M);
         if (M <= 0) return IA_OK;
         int rc;
+        if (sim) return sim_wave(t, y_lo, M, sq);
         if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
                                     ws.q16, sq)))
             return rc;
         hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
         hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
         const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
-                            a->im, a->dbg_px, a->dbg_dist};
+                            a->im, a->dbg_px, a->dbg_dist,
+                            a->comm && shard_tail() ? ws.rec_local : nullptr,
+                            a->comm && shard_tail() ? ws.coh : nullptr};
         if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
             if (e0) IA_HIP(hipEventRecord(e0, sq));
             if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
@@ -269,7 +338,7 @@ struct LevelRun {
         } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, ws.q16, M, ws.q64, ws.nq,
                                       a->amax, ws.scratch, ws.best_local,
                                       prof ? ws.stats : nullptr, sq, e0, e1,
-                                      fused ? &fa : nullptr))) {
+                                      (fused || (a->comm && shard_tail())) ? &fa : nullptr))) {
             return rc;
         }
         ++nscreen;
@@ -280,12 +349,48 @@ struct LevelRun {
         static const int sync_every = env_int("IA_SYNC_EVERY", 0);
         if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
         if (fused) return IA_OK;   // the exact stage already ran the per-pixel tail
-        const Best *ball = ws.best_local;
-        if (a->comm) {   // also with one rank: the same RCCL path, exercised by the tests
-            if ((rc = comm_allgather_best(a->comm, ws.best_local, ws.best_all, M, sq))) return rc;
-            ball = ws.best_all;
+        if (a->lsh) {   // one shard, LSH winners: the tail in k_lsh_finish form
+            k_lsh_tail<<<M, 128, 0, sq>>>(src, ws.best_local, M, fa, ws.q64);
+            IA_LAUNCH_CHECK("k_lsh_tail");
+            return IA_OK;
         }
-        k_finish<<<M, 128, 0, sq>>>(src, ball, nranks, M, fa, ws.q64);
+        // sharded DB: the exact stage left this rank's records and coherence picks; the
+        // exchange (also with one rank: the same RCCL path, exercised by the tests), then
+        // the finish
+        if (!shard_tail()) {
+            Best *all = reinterpret_cast<Best *>(ws.rec_all);
+            if ((rc = comm_allgather(a->comm, ws.best_local, all, (size_t)M * sizeof(Best), sq)))
+                return rc;
+            k_finish_gather<<<M, 128, 0, sq>>>(src, all, nranks, M, fa, ws.q64);
+            IA_LAUNCH_CHECK("k_finish_gather");
+            return IA_OK;
+        }
+        if ((rc = comm_allgather(a->comm, ws.rec_local, ws.rec_all, (size_t)M * sizeof(ShardRec), sq)))
+            return rc;
+        k_finish<<<M, 64, 0, sq>>>(src, ws.rec_all, ws.coh, nranks, M, fa);
+        IA_LAUNCH_CHECK("k_finish");
+        return IA_OK;
+    }
+
+    // diagnostic: the sharded path with every shard's exact stage run here, one after the
+    // other, each writing its records straight into the all-ranks array; then k_finish
+    int sim_wave(int t, int y_lo, int M, hipStream_t sq) {
+        int rc;
+        for (int r = 0; r < nsim; ++r) {
+            if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq,
+                                        sim[r].amax, ws.q16, sq)))
+                return rc;
+            const FinishArgs fr{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg,
+                                a->s, a->im, a->dbg_px, a->dbg_dist, ws.rec_all + (long)r * M,
+                                ws.coh};
+            if ((rc = launch_match(src, sim[r].row0, sim[r].nrows, sim[r].db, ws.qp, ws.q16, M,
+                                   ws.q64, ws.nq, sim[r].amax, ws.scratch, ws.best_local, nullptr,
+                                   sq, nullptr, nullptr, &fr)))
+                return rc;
+        }
+        const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
+                            a->im, a->dbg_px, a->dbg_dist, nullptr, nullptr};
+        k_finish<<<M, 64, 0, sq>>>(src, ws.rec_all, ws.coh, nsim, M, fa);
         IA_LAUNCH_CHECK("k_finish");
         return IA_OK;
     }
@@ -464,6 +569,27 @@ int ia_synth_level(const IaSynthArgs *a, void *stream) {
         IA_HIP(hipGraphLaunch(exec, st));
         IA_HIP(g_graphs.hold(exec, st));
     }
+    return run.done(st);
+}
+
+int ia_diag_synth_level_shards(const IaSynthArgs *a, const IaShardDb *shards, int n,
+                               void *stream) {
+    IA_ARG(a && shards && n >= 1 && !a->comm && !a->lsh, "ia_diag_synth_level_shards: bad args");
+    long total = 0;
+    for (int r = 0; r < n; ++r) {
+        IA_ARG(shards[r].db && shards[r].amax && shards[r].row0 == total && shards[r].nrows > 0,
+               "ia_diag_synth_level_shards: shards must tile the rows in order");
+        total += shards[r].nrows;
+    }
+    IA_ARG(total == a->N_total, "ia_diag_synth_level_shards: shards must cover the DB");
+    hipStream_t st = S(stream);
+    LevelRun run;
+    run.sim = shards;
+    run.nsim = n;
+    int rc = run.init(a, st);
+    if (rc) return rc;
+    for (int t = 0; t < run.nw; ++t)
+        if ((rc = run.wave(t, st))) return rc;
     return run.done(st);
 }
 

@@ -144,8 +144,9 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         pipeline = pipeline_default() and not eager
     todo = [l for l in range(1, max_levels) if levels is None or l in levels]
     comms = list(comm) if isinstance(comm, (list, tuple)) else None
-    sharded = [l for l in todo
-               if comm is not None and shard_level(level_rows(Ap_pyr_list, l), nranks)]
+    sharded = [l for l in todo            # (the LSH matcher runs unsharded, replicated)
+               if comm is not None and lsh is None and
+               shard_level(level_rows(Ap_pyr_list, l), nranks)]
     if pipeline and comms is None and len(sharded) > 1:
         pipeline = False      # one communicator cannot serve concurrent levels
     out = {}

@@ -152,8 +152,8 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
  * im: H*W int32 A' image number.  weights: 55 fp64 (config.py:68-79);
  * kappa_factor = 1 + 2**(level - max_levels) * k.
  * comm: NULL (single GPU) or an ia_comm_init() communicator — the DB rows are then
- * sharded (row0/nrows of this rank, N_total overall) and each wave exchanges the
- * per-rank (dist, idx) winners with one RCCL all-gather. */
+ * sharded (row0/nrows of this rank, N_total overall) and each wave exchanges the per-rank
+ * (dist, idx, weighted dist) winners with one RCCL all-gather (exact matcher only). */
 typedef struct {
     IaSrcLevel src;
     const void *db; long row0, nrows, N_total;

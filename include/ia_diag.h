@@ -7,6 +7,8 @@
 
 #include <stddef.h>
 
+#include "ia.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -30,6 +32,19 @@ int ia_diag_set_rescore_mode(int mode);
  * 0 off, 1 levels of <= 2^18 rows, 2 every single-GPU level; other values leave it;
  * returns the previous value */
 int ia_diag_set_graph_mode(int mode);
+
+/* the sharded synthesis path in ONE process: level a (a->comm = NULL, a->db unused) with
+ * its database split into n shards {db, row0, nrows, amax} (each ia_db_build'ed from its
+ * row range, in row order, covering all N_total rows); per wave every shard's exact stage
+ * runs here in turn and k_finish reduces their records as after the cross-rank exchange.
+ * The product's multi-rank reduction on one GPU, for tests. */
+typedef struct {
+    const void *db;
+    long row0, nrows;
+    const float *amax;
+} IaShardDb;
+int ia_diag_synth_level_shards(const IaSynthArgs *a, const IaShardDb *shards, int n,
+                               void *stream);
 
 #ifdef __cplusplus
 }

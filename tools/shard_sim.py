@@ -5,7 +5,9 @@ Runs the synthesis as rank `r` of G database shards (each level's rows
 sharded one (unfused exact stage, all-gather, k_finish), but the all-gather moves one
 shard's winners only, so the time excludes the real collective's xGMI latency.  The
 winners are this shard's, so B' differs from the real result: timing only.
-Per level wall time between torch.cuda.synchronize() calls, second repetition reported.
+Per level wall time between torch.cuda.synchronize() calls (levels one at a time), and the
+whole step with the levels pipelined (ia_synth_levels, one communicator per sharded
+level); second repetition reported.
 
 Usage: python tools/shard_sim.py G [G ...]        (G = 1 runs the sharded path unsharded)
 """
@@ -36,7 +38,7 @@ def main():
     A_pyr = ip.gaussian_pyramid_dev(job.A, cfg.n_sm, job.levels)
     Ap_pyr = ip.gaussian_pyramid_dev(job.Ap, cfg.n_sm, job.levels)
     B_pyr = ip.gaussian_pyramid_dev(job.B, cfg.n_sm, job.levels)
-    comm = one_rank_comm()
+    comms = [one_rank_comm() for _ in range(job.max_levels)]
     for G in gs:
         res = {}
         for rep in range(2):
@@ -44,13 +46,24 @@ def main():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, job.Bp, job.max_levels, job.k,
-                                  job.weights, comm=comm, rank=0, nranks=G, levels={level})
+                                  job.weights, comm=comms[0], rank=0, nranks=G, levels={level},
+                                  pipeline=False)
                 torch.cuda.synchronize()
                 res[level] = (time.perf_counter() - t0) * 1e3
         tot = sum(res.values())
-        print('G=%d rank0 %.1f ms/step ' % (G, tot) +
-              ' '.join('L%d %.1f' % (l, t) for l, t in sorted(res.items())), flush=True)
-    _ia.lib().ia_comm_destroy(comm)
+        pipe = []
+        for rep in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, job.Bp, job.max_levels, job.k, job.weights,
+                              comm=comms, rank=0, nranks=G, pipeline=True)
+            torch.cuda.synchronize()
+            pipe.append((time.perf_counter() - t0) * 1e3)
+        print('G=%d rank0 %.1f ms/step (levels one at a time: ' % (G, tot) +
+              ' '.join('L%d %.1f' % (l, t) for l, t in sorted(res.items())) +
+              '); pipelined %.1f ms/step' % min(pipe[1:]), flush=True)
+    for cm in comms:
+        _ia.lib().ia_comm_destroy(cm)
 
 
 if __name__ == '__main__':
