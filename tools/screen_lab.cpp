@@ -1,0 +1,491 @@
+// screen_lab — A/B variants of the split-f16 screen body (tools build only; the product
+// kernel is csrc/ia_screen16.hip).  Each variant is k_screen16's structure with one part
+// removed or changed, timed on the c4 finest-level database at M queries:
+//   0  the product body (copy)           1  no DB loads after the first stage (stale LDS)
+//   2  no loads, no stage barriers        3  running minimum of one accumulator value only
+//   4  one MFMA per chain instead of 11   5  segment minima kept in registers, no LDS atomics
+//   6  loads re-read the chunk's first two stages (L2-resident: the issue cost without HBM)
+//   7  plain loads (cache policy 0)          8  sc1 loads          9  sc0 loads
+//  10  the next stage's 7 loads interleaved with the first tile's MFMAs (one per MFMA)
+//  14, 15, 16  persistent 512 / 256 / 1024 blocks pulling 2048-row chunks from a queue
+//  11, 12, 13  variants 0, 1, 6 with s_memtime / s_memrealtime stamps around each block's
+//      loop (wave 0): prints the median in-kernel clock and the MFMA share of its cycles
+// Prints per-variant median time and whether its minima equal the library screen's
+// (variants 0 and 5 must; the others are timing probes).
+//
+//   screen_lab [--M 342] [--reps 5] [--rounds 5] [--V 0,1,2,3,4,5]
+#include "screen_setup.h"
+
+#include <float.h>
+#include <type_traits>
+
+#include "../image-analogies-python_amd/csrc/ia_internal.h"
+#include "../image-analogies-python_amd/csrc/ia_split16.h"
+
+using namespace ia;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int TILE_H8 = DB16_GROUPS * 64;
+constexpr int STAGE_TILES = 4;
+constexpr int STAGE_H8 = STAGE_TILES * TILE_H8;
+constexpr int SPC_MAX = 16;
+
+__host__ __device__ constexpr int bal_t0(int G, int W) { return (G * W) / 4; }
+__host__ __device__ constexpr int bal_ns(int G, int W) { return (G * W + G - 1) / 4 - (G * W) / 4 + 1; }
+__host__ __device__ constexpr bool bal_on(int G, int W, int k, int u) {
+    return 4 * (bal_t0(G, W) + k) + u >= G * W && 4 * (bal_t0(G, W) + k) + u < G * W + G;
+}
+template <int K, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (K < N) {
+        f(std::integral_constant<int, K>{});
+        static_for<K + 1, N>(f);
+    }
+}
+__device__ __forceinline__ int fkey(float x) {
+    const int b = __float_as_int(x);
+    return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float fkey_inv(int b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
+
+// stamped variants run the body of their base variant
+__host__ __device__ constexpr int base_v(int V) { return V == 11 ? 0 : (V == 12 ? 1 : (V == 13 ? 6 : V)); }
+
+template <int G, int W, int V0>
+__device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
+                                           long ctile0, int nstage, int tps,
+                                           const half8 *__restrict__ q16) {
+    constexpr int V = base_v(V0);
+    constexpr int T0 = bal_t0(G, W), NS = bal_ns(G, W);
+    constexpr int NM = V == 4 ? 1 : MFMA16;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    half8 bq[NS][Q16_GROUPS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const half8 *p = q16 + (long)((T0 + k) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m) bq[k][m] = p[m];
+    }
+    constexpr int POL = V == 7 ? 0 : (V == 8 ? 16 : (V == 9 ? 1 : 2));
+    auto piece = [&](int s, int buf, int k) {
+        const long st = V == 6 ? (s & 1) : s;
+        const half8 *src = db16 + (ctile0 + st * STAGE_TILES) * TILE_H8 + tid;
+        __builtin_amdgcn_global_load_lds((const void *)(src + k * 256),
+                                         (void *)(sbuf + buf * STAGE_H8 + k * 256 + W * 64),
+                                         16, 0, POL);
+    };
+    auto issue = [&](int s, int buf) {
+#pragma unroll
+        for (int k = 0; k < DB16_GROUPS; ++k) piece(s, buf, k);
+    };
+    auto stage_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    float mn[NS];
+    float segm[V == 5 ? SPC_MAX : 1][NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    const floatx16 zero = {};
+    issue(0, 0);
+    if (V == 1 || V == 2) issue(1, 1);
+    stage_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (V != 1 && V != 2 && V != 10 && s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        const half8 *sb = sbuf + (s & 1) * STAGE_H8;
+        static_for<0, STAGE_TILES>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            half8 a[DB16_GROUPS];
+            const half8 *p = sb + u * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+            floatx16 acc[NS];
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u))
+                    acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[k][0], zero, 0, 0, 0);
+            });
+#pragma unroll
+            for (int m = 1; m < NM; ++m) {
+                static_for<0, NS>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (bal_on(G, W, k, u))
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[k][mfma_b(m)],
+                                                                         acc[k], 0, 0, 0);
+                });
+                if constexpr (V == 10 && u == 0) {
+                    if (m <= DB16_GROUPS && s + 1 < nstage) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        piece(s + 1, (s + 1) & 1, m - 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            }
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u)) {
+                    const floatx16 &x = acc[k];
+                    if constexpr (V == 3) {
+                        mn[k] = fminf(mn[k], x[0]);
+                    } else {
+                        const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+                        const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+                        const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+                        const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+                        mn[k] = fminf(fminf(mn[k], u0), u1);
+                    }
+                }
+            });
+        });
+        const int done = (s + 1) * STAGE_TILES;
+        if (done % tps == 0) {
+            if constexpr (V == 5) {
+                const int sg = done / tps - 1;
+#pragma unroll
+                for (int q = 0; q < SPC_MAX; ++q)
+                    if (q == sg) {
+#pragma unroll
+                        for (int k = 0; k < NS; ++k) segm[q][k] = fminf(mn[k], __shfl_xor(mn[k], 32));
+                    }
+#pragma unroll
+                for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+            } else {
+                int *sm = smin + (done / tps - 1) * (G * 32);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
+                    if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
+                    mn[k] = FLT_MAX;
+                }
+            }
+        }
+        if (V != 2) stage_barrier();
+    }
+    if constexpr (V == 5) {
+        const int spc = nstage * STAGE_TILES / tps;
+#pragma unroll
+        for (int q = 0; q < SPC_MAX; ++q)
+            if (q < spc) {
+                int *sm = smin + q * (G * 32);
+#pragma unroll
+                for (int k = 0; k < NS; ++k)
+                    if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(segm[q][k]));
+            }
+    }
+}
+
+template <int G, int V>
+__global__ __launch_bounds__(256, 2) void k_lab(const half8 *__restrict__ db16, int nchunks, int ch,
+                                                int seg_rows, const half8 *__restrict__ q16, int M,
+                                                int groups, float *__restrict__ segmin, long nseg,
+                                                unsigned long long *stamps) {
+    __shared__ half8 sbuf[2 * STAGE_H8];
+    __shared__ int smin[SPC_MAX * G * 32];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+    const int spc = ch / seg_rows;
+    for (int i = threadIdx.x; i < spc * G * 32; i += 256) smin[i] = 0x7fffffff;
+    const int tpc = ch >> 5;
+    const long ctile0 = (long)chunk * tpc;
+    const int nstage = tpc / STAGE_TILES;
+    const int tps = seg_rows >> 5;
+    const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    unsigned long long t0 = 0, r0 = 0;
+    if (V >= 11) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+    if (wv == 0) chain_body<G, 0, V>(db16, sbuf, smin, ctile0, nstage, tps, qg);
+    else if (wv == 1) chain_body<G, 1, V>(db16, sbuf, smin, ctile0, nstage, tps, qg);
+    else if (wv == 2) chain_body<G, 2, V>(db16, sbuf, smin, ctile0, nstage, tps, qg);
+    else chain_body<G, 3, V>(db16, sbuf, smin, ctile0, nstage, tps, qg);
+    __syncthreads();
+    if (V >= 11 && threadIdx.x == 0) {   // vector stores of the stamps (diagnostic buffer only)
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        stamps[4 * blockIdx.x] = t1 - t0;
+        stamps[4 * blockIdx.x + 1] = r1 - r0;
+        stamps[4 * blockIdx.x + 2] = r0;
+        stamps[4 * blockIdx.x + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) |
+                                     (unsigned)__builtin_amdgcn_s_getreg(63492);
+    }
+    const long seg0 = (long)chunk * spc;
+    const int q0 = group * G * 32;
+    for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
+        const int ql = i / spc, s = i - ql * spc;
+        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + s] = fkey_inv(smin[s * (G * 32) + ql]);
+    }
+}
+
+template <int V>
+static void launch_lab(const ScreenSetup &su, int M, float *out, unsigned long long *stamps) {
+    const int ch = ia_db_chunk_rows(su.N);
+    const long nchunks = su.npad / ch;
+    const int seg_rows = ch < 512 ? ch : 512;
+    const int T = (M + 31) / 32;
+    const int groups = (T + 10) / 11;
+    const int G = (T + groups - 1) / groups;
+    const long nb = ((nchunks + 7) / 8) * 8 * groups;
+    const half8 *db = reinterpret_cast<const half8 *>(su.db);
+    const half8 *q = reinterpret_cast<const half8 *>(su.q16);
+    switch (G) {
+#define LAB_CASE(GG) \
+        case GG: k_lab<GG, V><<<(unsigned)nb, 256, 0, su.st>>>(db, (int)nchunks, ch, seg_rows, q, M, groups, out, su.nseg, stamps); break;
+        LAB_CASE(8) LAB_CASE(9) LAB_CASE(10) LAB_CASE(11)
+#undef LAB_CASE
+        default: fprintf(stderr, "lab: G=%d not instantiated\n", G); exit(1);
+    }
+    CK(hipGetLastError());
+}
+
+
+// ---- variant 14: persistent blocks pulling QCH-row chunks from a queue ----------------
+constexpr int QCH = 2048, QSPC = QCH / 512, QSTAGES = QCH / 32 / STAGE_TILES;
+
+template <int G, int W>
+__device__ __forceinline__ void q_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
+                                       int *sticket, int nq, const half8 *__restrict__ q16,
+                                       float *__restrict__ segmin, long nseg, int M, int *ctr) {
+    constexpr int T0 = bal_t0(G, W), NS = bal_ns(G, W);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    half8 bq[NS][Q16_GROUPS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const half8 *p = q16 + (long)((T0 + k) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m) bq[k][m] = p[m];
+    }
+    auto issue = [&](int c, int s, int buf) {
+        const half8 *src = db16 + ((long)c * (QCH / 32) + (long)s * STAGE_TILES) * TILE_H8 + tid;
+#pragma unroll
+        for (int k = 0; k < DB16_GROUPS; ++k)
+            __builtin_amdgcn_global_load_lds((const void *)(src + k * 256),
+                                             (void *)(sbuf + buf * STAGE_H8 + k * 256 + W * 64),
+                                             16, 0, 2);
+    };
+    auto stage_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    const floatx16 zero = {};
+    int cur = blockIdx.x;
+    if (cur >= nq) return;   // uniform; such a block never touches the queue
+    issue(cur, 0, 0);
+    if (tid == 0) *sticket = (int)gridDim.x + atomicAdd(ctr, 1);
+    stage_barrier();
+    int buf = 0;
+    int nxt = *sticket;
+    while (cur < nq) {
+        float mn[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+        for (int s = 0; s < QSTAGES; ++s) {
+            if (s + 1 < QSTAGES) issue(cur, s + 1, buf ^ 1);
+            else if (nxt < nq) issue(nxt, 0, buf ^ 1);
+            const half8 *sb = sbuf + buf * STAGE_H8;
+            static_for<0, STAGE_TILES>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                half8 a[DB16_GROUPS];
+                const half8 *p = sb + u * TILE_H8 + lane;
+#pragma unroll
+                for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+                floatx16 acc[NS];
+                static_for<0, NS>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (bal_on(G, W, k, u))
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[k][0], zero, 0, 0, 0);
+                });
+#pragma unroll
+                for (int m = 1; m < MFMA16; ++m)
+                    static_for<0, NS>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        if constexpr (bal_on(G, W, k, u))
+                            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[k][mfma_b(m)],
+                                                                             acc[k], 0, 0, 0);
+                    });
+                static_for<0, NS>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (bal_on(G, W, k, u)) {
+                        const floatx16 &x = acc[k];
+                        const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+                        const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+                        const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+                        const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+                        mn[k] = fminf(fminf(mn[k], u0), u1);
+                    }
+                });
+            });
+            if ((s + 1) % (512 / 32 / STAGE_TILES) == 0) {
+                int *sm = smin + ((s + 1) / (512 / 32 / STAGE_TILES) - 1) * (G * 32);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
+                    if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
+                    mn[k] = FLT_MAX;
+                }
+            }
+            if (s == 0 && tid == 0 && nxt < nq) *sticket = (int)gridDim.x + atomicAdd(ctr, 1);
+            stage_barrier();
+            buf ^= 1;
+        }
+        // the chunk's minima, QSPC consecutive segments per query; reset for the next chunk
+        for (int i = tid; i < G * 32 * QSPC; i += 256) {
+            const int ql = i / QSPC, sg = i - ql * QSPC;
+            if (ql < M) segmin[(long)ql * nseg + (long)cur * QSPC + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
+            smin[sg * (G * 32) + ql] = 0x7fffffff;
+        }
+        // the ticket thread 0 took in stage 0 (visible since that stage's barrier); its next
+        // write comes after the barrier below
+        const int nn = *sticket;
+        cur = nxt;
+        nxt = nn;
+        __syncthreads();
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(256, 2) void k_lab_q(const half8 *__restrict__ db16, int nq,
+                                                  const half8 *__restrict__ q16, int M,
+                                                  float *__restrict__ segmin, long nseg, int *ctr) {
+    __shared__ half8 sbuf[2 * STAGE_H8];
+    __shared__ int smin[QSPC * G * 32];
+    __shared__ int sticket;
+    for (int i = threadIdx.x; i < QSPC * G * 32; i += 256) smin[i] = 0x7fffffff;
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) q_body<G, 0>(db16, sbuf, smin, &sticket, nq, q16, segmin, nseg, M, ctr);
+    else if (wv == 1) q_body<G, 1>(db16, sbuf, smin, &sticket, nq, q16, segmin, nseg, M, ctr);
+    else if (wv == 2) q_body<G, 2>(db16, sbuf, smin, &sticket, nq, q16, segmin, nseg, M, ctr);
+    else q_body<G, 3>(db16, sbuf, smin, &sticket, nq, q16, segmin, nseg, M, ctr);
+    // the last block out resets the queue for the next launch
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(ctr + 1, 1) == (int)gridDim.x - 1) {
+            atomicExch(ctr, 0);
+            atomicExch(ctr + 1, 0);
+        }
+    }
+}
+
+static int *g_ctr;
+static void launch_q(const ScreenSetup &su, int M, float *out, int nblocks) {
+    const int nq = (int)(su.npad / QCH);
+    const int T = (M + 31) / 32;
+    const half8 *db = reinterpret_cast<const half8 *>(su.db);
+    const half8 *q = reinterpret_cast<const half8 *>(su.q16);
+    switch (T) {
+        case 11: k_lab_q<11><<<nblocks, 256, 0, su.st>>>(db, nq, q, M, out, su.nseg, g_ctr); break;
+        case 8: k_lab_q<8><<<nblocks, 256, 0, su.st>>>(db, nq, q, M, out, su.nseg, g_ctr); break;
+        default: fprintf(stderr, "lab q: T=%d not instantiated\n", T); exit(1);
+    }
+    CK(hipGetLastError());
+}
+
+static unsigned long long *g_stamps;
+static void run(int V, const ScreenSetup &su, int M, float *out) {
+    switch (V) {
+        case 0: launch_lab<0>(su, M, out, g_stamps); break;
+        case 1: launch_lab<1>(su, M, out, g_stamps); break;
+        case 2: launch_lab<2>(su, M, out, g_stamps); break;
+        case 3: launch_lab<3>(su, M, out, g_stamps); break;
+        case 4: launch_lab<4>(su, M, out, g_stamps); break;
+        case 5: launch_lab<5>(su, M, out, g_stamps); break;
+        case 6: launch_lab<6>(su, M, out, g_stamps); break;
+        case 7: launch_lab<7>(su, M, out, g_stamps); break;
+        case 8: launch_lab<8>(su, M, out, g_stamps); break;
+        case 9: launch_lab<9>(su, M, out, g_stamps); break;
+        case 10: launch_lab<10>(su, M, out, g_stamps); break;
+        case 11: launch_lab<11>(su, M, out, g_stamps); break;
+        case 12: launch_lab<12>(su, M, out, g_stamps); break;
+        case 13: launch_lab<13>(su, M, out, g_stamps); break;
+        case 14: launch_q(su, M, out, 512); break;
+        case 15: launch_q(su, M, out, 256); break;
+        case 16: launch_q(su, M, out, 1024); break;
+        default: fprintf(stderr, "bad variant %d\n", V); exit(1);
+    }
+}
+
+int main(int argc, char **argv) {
+    int reps = 5, rounds = 5;
+    std::vector<int> Ms = {342}, Vs = {0, 14, 15, 16, 0, 14};
+    for (int i = 1; i + 1 < argc; i += 2) {
+        if (!strcmp(argv[i], "--M")) Ms = parse_list(argv[i + 1]);
+        else if (!strcmp(argv[i], "--V")) Vs = parse_list(argv[i + 1]);
+        else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--rounds")) rounds = atoi(argv[i + 1]);
+    }
+    int Mmax = 0; for (int m : Ms) Mmax = std::max(Mmax, m);
+    const ScreenSetup su = make_setup(2048, Mmax);
+    float *lab;
+    CK(hipMalloc(&lab, sizeof(float) * (size_t)su.qrows * su.nseg));
+    const long nblk_max = 1 << 16;
+    CK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4 * nblk_max));
+    CK(hipMalloc(&g_ctr, 2 * sizeof(int)));
+    CK(hipMemset(g_ctr, 0, 2 * sizeof(int)));
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int M : Ms) {
+        CI(ia_diag_screen16(su.db, su.N, su.q16, M, su.segmin, su.st));
+        std::vector<float> ref((size_t)M * su.nseg), got(ref.size());
+        CK(hipMemcpy(ref.data(), su.segmin, sizeof(float) * ref.size(), hipMemcpyDeviceToHost));
+        for (int V : Vs) {
+            run(V, su, M, lab);
+            CK(hipMemcpy(got.data(), lab, sizeof(float) * got.size(), hipMemcpyDeviceToHost));
+            const bool same = !memcmp(ref.data(), got.data(), sizeof(float) * ref.size());
+            std::vector<float> t;
+            for (int rd = 0; rd < rounds; ++rd) {
+                CK(hipEventRecord(e0, su.st));
+                for (int r = 0; r < reps; ++r) run(V, su, M, lab);
+                CK(hipEventRecord(e1, su.st));
+                CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                t.push_back(ms / reps);
+            }
+            std::sort(t.begin(), t.end());
+            const double tf = 330.0 * M * (double)su.N / (t[t.size() / 2] * 1e-3) / 1e12;
+            printf("M %4d V%d  median %8.1f us  min %8.1f us  %7.1f TF/s f16 (%4.1f%%)  minima %s", M, V,
+                   t[t.size() / 2] * 1e3, t[0] * 1e3, tf, 100 * tf / 2516.6, same ? "equal" : "differ");
+            if (V >= 11 && V <= 13) {   // stamps of the last launch: clock and MFMA share per block
+                const int T = (M + 31) / 32;
+                const int G = (T + ((T + 10) / 11) - 1) / ((T + 10) / 11);
+                const long nb = su.npad / ia_db_chunk_rows(su.N);
+                std::vector<unsigned long long> h(4 * nb);
+                CK(hipMemcpy(h.data(), g_stamps, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+                std::vector<double> ghz, share;
+                const double mfma_cyc = (double)(ia_db_chunk_rows(su.N) / 32) * G * MFMA16 * 32 / 4 * 2;
+                for (long b = 0; b < nb; ++b) {
+                    ghz.push_back((double)h[4 * b] / (double)h[4 * b + 1] * 0.1);
+                    share.push_back(mfma_cyc / (double)h[4 * b]);
+                }
+                // residency: blocks per CU, start spread, overlap of co-resident blocks
+                unsigned long long rmin = ~0ull, rmax = 0, emin = ~0ull, emax = 0;
+                std::vector<std::pair<unsigned long long, long>> cu;
+                for (long b = 0; b < nb; ++b) {
+                    const unsigned long long hw = h[4 * b + 3];
+                    const unsigned xcc = (unsigned)(hw >> 32) & 0xf, id = (unsigned)hw;
+                    const unsigned cu_id = (id >> 8) & 0xf, sh = (id >> 12) & 1, se = (id >> 13) & 0x7;
+                    cu.push_back({((unsigned long long)xcc << 16) | (se << 8) | (sh << 4) | cu_id, b});
+                    rmin = std::min(rmin, h[4 * b + 2]); rmax = std::max(rmax, h[4 * b + 2]);
+                    emin = std::min(emin, h[4 * b + 2] + h[4 * b + 1]);
+                    emax = std::max(emax, h[4 * b + 2] + h[4 * b + 1]);
+                }
+                std::sort(cu.begin(), cu.end());
+                int ncu = 0, maxper = 0;
+                for (size_t i = 0; i < cu.size();) {
+                    size_t k = i; while (k < cu.size() && cu[k].first == cu[i].first) ++k;
+                    ++ncu; maxper = std::max(maxper, (int)(k - i)); i = k;
+                }
+                printf("  [CUs %d, max blocks/CU %d, starts spread %.1f us, ends %.1f..%.1f us]", ncu, maxper,
+                       (rmax - rmin) / 100.0, (emin - rmin) / 100.0, (emax - rmin) / 100.0);
+                std::sort(ghz.begin(), ghz.end()); std::sort(share.begin(), share.end());
+                printf("  clock %.2f GHz  MFMA share %.1f%% (2 blocks/CU)", ghz[ghz.size() / 2], 100 * share[share.size() / 2]);
+            }
+            printf("\n");
+            fflush(stdout);
+        }
+    }
+    return 0;
+}
