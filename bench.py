@@ -225,9 +225,9 @@ def hbm_kernels(dev, reps=20):
     timed with HIP events on the stream it launches on, median of `reps`, against
     algorithmic bytes (every input element read once, every output written once):
       yiq        ia_rgb_to_yiq, 2048x2048 uint8 RGB -> YIQ + Y fp64: 3 + 32 B/px
-      pyr_reduce ia_pyr_reduce_f64 (k_blur + k_resample), 2048^2 -> 1024^2 fp64:
-                 8 B per input + 8 B per output pixel
-      db_build   ia_db_build (k_db_norms + k_db_build), the c4 finest level, 4,194,304
+      pyr_reduce ia_pyr_reduce_f64 (k_init_minmax + fused k_pyr_reduce + k_pyr_clip),
+                 2048^2 -> 1024^2 fp64: 8 B per input + 8 B per output pixel
+      db_build   ia_db_build (LDS-tiled k_db_norms_t + k_db_build_t), the c4 finest level, 4,194,304
                  rows: 224 B written per row (split-f16 rows) + the fp64 pyramids read
                  once (A, A' fine: 8 B per row each; coarse: 8 B per 4 rows each)
     """
@@ -276,7 +276,7 @@ def hbm_kernels(dev, reps=20):
         _ia.check(lib.ia_pyr_reduce_f64(_ia.ptr(img), H, W, _ia.ptr(sm), 1024, 1024, coef, taps,
                                         _ia.ptr(ws), _ia.stream()), 'ia_pyr_reduce_f64')
     put('pyr_reduce', timed(reduce), 8 * (H * W + 1024 * 1024),
-        'ia_pyr_reduce_f64 (k_blur + k_resample) 2048^2 -> 1024^2')
+        'ia_pyr_reduce_f64 (k_init_minmax + fused k_pyr_reduce + k_pyr_clip) 2048^2 -> 1024^2')
     Ap_lg, Ap_sm = img[None].clone(), sm[None].clone()
     N = H * W
     ix = algorithms.LevelIndex(sm, img, Ap_sm, Ap_lg)
@@ -285,7 +285,7 @@ def hbm_kernels(dev, reps=20):
         _ia.check(lib.ia_db_build(ctypes.byref(ix.src), 0, ix.nrows, _ia.ptr(ix.center),
                                   _ia.ptr(ix.db), _ia.ptr(ix.amax), _ia.stream()), 'ia_db_build')
     put('db_build', timed(build), N * 224 + 8 * 2 * (N + 1024 * 1024),
-        'ia_db_build (k_db_norms + k_db_build), 4,194,304 rows')
+        'ia_db_build (LDS-tiled k_db_norms_t + k_db_build_t), 4,194,304 rows')
     return out
 
 

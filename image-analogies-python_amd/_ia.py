@@ -112,6 +112,7 @@ _SIGS = {
     # diagnostics (include/ia_diag.h)
     'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_graph_mode': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
@@ -164,6 +165,12 @@ def graph_mode(mode=-1):
     """HIP-graph capture of the synthesis wave loop for this process (0 off [default],
     1 levels <= 2^18 rows, 2 all single-GPU levels); returns the previous value."""
     return lib().ia_diag_set_graph_mode(int(mode))
+
+
+def db_build_form(tiled=-1):
+    """ia_db_build's kernels for this process (1 LDS-tiled where width and row0 are
+    multiples of 32 [default], 0 per-row gathers); returns the previous value."""
+    return lib().ia_diag_set_db_build_form(int(tiled))
 
 
 PROF_KEYS = ('level', 'rows', 'pairs', 'screen_ms', 'timed_screens', 'rows_rescored',

@@ -30,8 +30,8 @@ __global__ void k_level_features(ImgPair p, int full, double *out) {
 __device__ __forceinline__ int perm56(int k) { return (k & 1) * 28 + (k >> 1); }
 
 // Centred row of DB row ix: my[k] = fl32(a_k - c_k) (k < 55), my[55] = fl32(|a - c|^2)
-// (fp64 sum in feature order); returns |a - c| in fp32.
-__device__ __forceinline__ float db_row(const DbSrc &src, long ix, const double *__restrict__ center,
+// (fp64 sum in feature order).
+__device__ __forceinline__ void db_row(const DbSrc &src, long ix, const double *__restrict__ center,
                                         float *my) {
     ImgPair ap; int r, c;
     src.locate(ix, ap, r, c);
@@ -42,29 +42,247 @@ __device__ __forceinline__ float db_row(const DbSrc &src, long ix, const double 
         my[k] = (float)d;
     });
     my[55] = (float)n2;
-    return (float)sqrt(n2);
 }
 
-// Pass 1: amax = max over rows of |a - c| (the split scale and the error bounds need it
-// before any row is split).  One thread per row, a block max, one atomic per block.
-__global__ __launch_bounds__(256) void k_db_norms(DbSrc src, long row0, long nrows,
-                                                  const double *__restrict__ center, float *amax) {
-    __shared__ float redmax[4];
-    const long lr = (long)blockIdx.x * 256 + threadIdx.x;
-    float nrm = 0.f;
-    if (lr < nrows) {
-        float my[IA_DP];
-        nrm = db_row(src, row0 + lr, center, my);
+// ---- pass 1: the split scale's A >= max_row |a - c| (ia_split16.h) ---------
+// Every feature k reads one of four images (k < 9 coarse A, < 34 fine A, < 43 coarse A',
+// else fine A'), so |a - c|^2 <= sum_k max((hi_k - c_k)^2, (lo_k - c_k)^2) with [lo_k, hi_k]
+// the value range of feature k's image.  The bound needs one streaming min / max pass over
+// the level's images (no feature gathers) and holds for every row, shard and padding row;
+// it is within a few tens of percent of the row maximum on image data (c4: 3.7 vs 2.87),
+// which only widens the exact stage's thresholds by that factor.  Per-block partials go to
+// the head of the db buffer (overwritten by pass 2).
+constexpr int DBB_BLOCKS = 1024;   // partials: 64 KiB < the smallest db buffer (512 rows)
+
+// Blocks are dealt to the four images in proportion to their sizes (image g gets blocks
+// [first[g], first[g + 1])); each thread keeps 8 x 16 B loads in flight per step (a loop of
+// single loads is latency-bound).
+struct DbSpans {
+    const double *x[4];
+    long n[4];
+    int first[5];
+};
+
+__global__ __launch_bounds__(256) void k_db_range(DbSpans sp, double *__restrict__ part) {
+    __shared__ double red[4][2];
+    int g = 0;
+    while (g < 3 && (int)blockIdx.x >= sp.first[g + 1]) ++g;
+    const int nb = sp.first[g + 1] - sp.first[g], lb = blockIdx.x - sp.first[g];
+    const double *x = sp.x[g];
+    const long n = sp.n[g];
+    double lo = INFINITY, hi = -INFINITY;
+    const long stride = (long)nb * 256;
+    const double2 *x2 = reinterpret_cast<const double2 *>(x);
+    const long n2 = reinterpret_cast<uintptr_t>(x) % 16 == 0 ? n / 2 : 0;
+    long i = (long)lb * 256 + threadIdx.x;
+    for (; i + 7 * stride < n2; i += 8 * stride) {
+        double2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = x2[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            lo = fmin(lo, fmin(v[k].x, v[k].y));
+            hi = fmax(hi, fmax(v[k].x, v[k].y));
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, o));
-    if ((threadIdx.x & 63) == 0) redmax[threadIdx.x >> 6] = nrm;
+    for (; i < n2; i += stride) {
+        const double2 v = x2[i];
+        lo = fmin(lo, fmin(v.x, v.y));
+        hi = fmax(hi, fmax(v.x, v.y));
+    }
+    for (long j = 2 * n2 + (long)lb * 256 + threadIdx.x; j < n; j += stride) {
+        lo = fmin(lo, x[j]);
+        hi = fmax(hi, x[j]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o));
+        hi = fmax(hi, __shfl_xor(hi, o));
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[wv][0] = lo; red[wv][1] = hi; }
+    __syncthreads();
+    if (threadIdx.x < 8) {   // this block's partial: its image's range, +-inf for the others
+        const int i8 = threadIdx.x, gi = i8 >> 1;
+        double v = (i8 & 1) ? -INFINITY : INFINITY;
+        if (gi == g)
+            for (int w = 0; w < 4; ++w) v = (i8 & 1) ? fmax(v, red[w][1]) : fmin(v, red[w][0]);
+        part[(long)blockIdx.x * 8 + i8] = v;
+    }
+}
+
+// one block of DBB_BLOCKS threads, one partial each: reduce, then amax = max(amax, fl32
+// rounded up of sqrt(bound))
+__global__ __launch_bounds__(1024) void k_db_bound(const double *__restrict__ part, int nb,
+                                                   const double *__restrict__ center, float *amax) {
+    __shared__ double red[16][8];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        v[i] = (int)threadIdx.x < nb ? part[(long)threadIdx.x * 8 + i] : ((i & 1) ? -INFINITY : INFINITY);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        for (int o = 32; o > 0; o >>= 1)
+            v[i] = (i & 1) ? fmax(v[i], __shfl_xor(v[i], o)) : fmin(v[i], __shfl_xor(v[i], o));
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[wv][i] = v[i];
+    __syncthreads();
+    __shared__ double fin[8], term[64];
+    if (threadIdx.x < 8) {
+        const int i = threadIdx.x;
+        double x = red[0][i];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) x = (i & 1) ? fmax(x, red[w][i]) : fmin(x, red[w][i]);
+        fin[i] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 55) {   // feature k's term: the larger squared deviation of its image's range
+        const int k = threadIdx.x;
+        const int g = k < 9 ? 0 : (k < 34 ? 1 : (k < 43 ? 2 : 3));
+        const double dl = fin[2 * g] - center[k], dh = fin[2 * g + 1] - center[k];
+        term[k] = fmax(dl * dl, dh * dh);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float m = fmaxf(fmaxf(redmax[0], redmax[1]), fmaxf(redmax[2], redmax[3]));
-        atomicMax(reinterpret_cast<unsigned int *>(amax), __float_as_uint(m));
+        double b2 = 0.0;
+        for (int k = 0; k < 55; ++k) b2 += term[k];
+        const double a = sqrt(b2 * (1.0 + 1e-12));
+        float f = (float)a;
+        if ((double)f < a) f = nextafterf(f, INFINITY);
+        amax[0] = fmaxf(amax[0], f);
     }
 }
 
+// ---- tiled form (A width % 32 == 0, row0 % 32 == 0: every 32-row DB tile is 32 pixels of
+// one scanline).  A block takes 8 tiles; each tile's feature windows (fine rows y-2..y+2 of
+// A and y-2..y of A', coarse rows y/2-1..y/2+1 of both, 36 / 18 columns, symmetric index map
+// applied on load) are staged in LDS by the tile's 32 threads (row pointers and reflected
+// columns computed once, ~20 loads per thread), then every thread computes its row from LDS
+// with constant offsets: no per-feature index arithmetic.  A
+// tile past the last real row stages the last real tile instead, and its lanes take row
+// nrows - 1 (the padding rule below).
+constexpr int DBT_TILES = 8;                       // tiles per block (256 rows)
+constexpr int WF = 36, WC = 18;                    // fine / coarse window columns
+constexpr int WIN_FA = 0, WIN_FP = 5 * WF, WIN_CA = 8 * WF, WIN_CP = 8 * WF + 3 * WC;
+constexpr int WIN = 8 * WF + 6 * WC;               // doubles per tile window (396)
+
+struct DbWinCtx {
+    int e;        // this thread's row within its staged tile (0..31)
+    const double *w;
+};
+
+// stage the windows of tile group grp (tiles grp * 8 ..); returns this thread's window and row.
+// Threads 32u .. 32u + 31 stage tile u: lane c loads columns c and c + 32 of its 8 fine rows
+// and column c of its 6 coarse rows (row pointers and the reflected columns computed once).
+__device__ __forceinline__ DbWinCtx db_stage(const DbSrc &src, long row0, long nrows, long grp,
+                                             double *win) {
+    const long tiles0 = grp * DBT_TILES;
+    const long tlast = (nrows - 1) >> 5;
+    const int tid = threadIdx.x;
+    const int u = tid >> 5, c = tid & 31;
+    const long te = min(tiles0 + u, tlast);
+    const ImgPair &A = src.A;
+    int img = 0, y = 0, x0 = 0;
+    if (c == 0) {   // the tile's origin (64-bit divisions once per tile), broadcast below
+        const long g = row0 + te * 32;
+        const long im = g / src.hw;
+        const long rem = g - im * src.hw;
+        img = (int)im;
+        y = (int)(rem / A.w);
+        x0 = (int)(rem - (long)y * A.w);
+    }
+    img = __shfl(img, tid & 32);
+    y = __shfl(y, tid & 32);
+    x0 = __shfl(x0, tid & 32);
+    const double *Apl = src.Ap.lg + (long)img * src.hw, *Aps = src.Ap.sm + (long)img * src.hws;
+    // every load first (one basic block: they all issue before the first LDS store), with
+    // clamped columns where the lane has nothing to stage; then the stores
+    const int fc0 = symi2(x0 - 2 + c, A.w);
+    const int fc1 = symi2(x0 - 2 + min(c + 32, WF - 1), A.w);
+    const int cc = symi2((x0 >> 1) - 1 + min(c, WC - 1), A.ws);
+    double vf[8][2], vc[6];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const double *row = (r < 5 ? A.lg : Apl) + (long)symi2(y - 2 + (r < 5 ? r : r - 5), A.h) * A.w;
+        vf[r][0] = row[fc0];
+        vf[r][1] = row[fc1];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const long ro = (long)symi2((y >> 1) - 1 + r, A.hs) * A.ws + cc;
+        vc[r] = A.sm[ro];
+        vc[3 + r] = Aps[ro];
+    }
+    double *w = win + u * WIN;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        w[r * WF + c] = vf[r][0];   // WIN_FA rows 0..4 then WIN_FP rows 5..7 (contiguous)
+        if (c + 32 < WF) w[r * WF + c + 32] = vf[r][1];
+    }
+    if (c < WC) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) w[WIN_CA + r * WC + c] = vc[r];   // WIN_CA then WIN_CP
+    }
+    __syncthreads();
+    const long lr = (tiles0 + u) * 32 + c;
+    const long er = lr < nrows ? lr : nrows - 1;
+    return DbWinCtx{(int)(er - te * 32), w};
+}
+
+// the row's 55 features in emit_feature order from the staged window
+template <typename F>
+__device__ __forceinline__ void db_win_features(const DbWinCtx &c, F &&f) {
+    const double *w = c.w;
+    const int e = c.e, es = e >> 1;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) f(t, w[WIN_CA + (t / 3) * WC + es + t % 3]);
+#pragma unroll
+    for (int t = 0; t < 25; ++t) f(9 + t, w[WIN_FA + (t / 5) * WF + e + t % 5]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) f(34 + t, w[WIN_CP + (t / 3) * WC + es + t % 3]);
+#pragma unroll
+    for (int t = 0; t < 12; ++t) f(43 + t, w[WIN_FP + (t / 5) * WF + e + t % 5]);
+}
+
+// Pass 2 (tiled): each thread splits its own row and writes its 14 half8 groups straight to
+// the MFMA operand layout ((tile, g) blocks of 64 half8, lane = h * 32 + j): for each (g, h)
+// the 32 rows of a tile write one contiguous 512 B run.
+__global__ __launch_bounds__(256) void k_db_build_t(DbSrc src, long row0, long nrows,
+                                                    const double *__restrict__ center,
+                                                    const float *__restrict__ amax,
+                                                    half8 *__restrict__ db16) {
+    __shared__ double win[DBT_TILES * WIN];
+    const DbWinCtx c = db_stage(src, row0, nrows, blockIdx.x, win);
+    float my[IA_DP];
+    double n2 = 0.0;
+    db_win_features(c, [&](int k, double v) {
+        const double d = v - center[k];
+        n2 += d * d;
+        my[k] = (float)d;
+    });
+    my[55] = (float)n2;
+    const Split16Db s = split16_db_scale(amax[0]);
+    _Float16 xh[IA_DP], xl[IA_DP];
+#pragma unroll
+    for (int k = 0; k < IA_DP; ++k)
+        split16f(k < 55 ? ldexpf(my[k], s.ea) : ldexpf(my[55], s.ea - s.R), xh[k], xl[k]);
+    const long T = (long)blockIdx.x * DBT_TILES + (threadIdx.x >> 5);
+    half8 *out = db16 + T * (DB16_GROUPS * 64) + (threadIdx.x & 31);
+#pragma unroll
+    for (int g = 0; g < DB16_GROUPS; ++g)      // consecutive stores: adjacent 512 B halves
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int k0;
+            bool hi;
+            split16_db_group(h, g, k0, hi);
+            half8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = hi ? xh[k0 + e] : xl[k0 + e];
+            __builtin_nontemporal_store(o, out + g * 64 + h * 32);   // read back by the screen only
+        }
+}
+
+// ---- general form (any width / row offset): one thread gathers its row per feature ----
 // Pass 2: the split-f16 rows (ia_split16.h), written once.  One thread per row computes
 // its 56 centred fp32 values into LDS (256 rows = 8 tiles per block); then lane (j, h) of
 // each wave emits its 7 register groups of two tiles: half8 (tile, g, lane) at
@@ -217,14 +435,43 @@ int ia_db_chunk_rows(long nrows) { return db_chunk_rows(nrows); }
 long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
 size_t ia_db_bytes(long nrows) { return db_bytes(nrows); }
 
+static int g_db_tiled = 1;   // ia_diag_set_db_build_form
+int ia_diag_set_db_build_form(int tiled) {
+    const int prev = g_db_tiled;
+    if (tiled == 0 || tiled == 1) g_db_tiled = tiled;
+    return prev;
+}
+
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 void *db, float *amax, void *stream) {
     IA_ARG(src && center && db && amax && nrows > 0 && row0 >= 0, "ia_db_build: bad args");
     IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build: rows out of range");
     const long npad = db_rows_padded(nrows);
     DbSrc d = make_dbsrc(*src);
-    k_db_norms<<<(unsigned)((nrows + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, center, amax);
-    IA_LAUNCH_CHECK("k_db_norms");
+    double *part = reinterpret_cast<double *>(db);   // DBB_BLOCKS x 8 doubles, < db_bytes
+    {   // blocks per image in proportion to its size, at least one each
+        DbSpans sp;
+        sp.x[0] = src->A_sm; sp.n[0] = d.hws;
+        sp.x[1] = src->A_lg; sp.n[1] = d.hw;
+        sp.x[2] = src->Ap_sm; sp.n[2] = (long)src->nAp * d.hws;
+        sp.x[3] = src->Ap_lg; sp.n[3] = (long)src->nAp * d.hw;
+        const long tot = sp.n[0] + sp.n[1] + sp.n[2] + sp.n[3];
+        sp.first[0] = 0;
+        for (int g = 0; g < 4; ++g) {
+            const long want = std::max<long>(1, (long)((double)(DBB_BLOCKS - 4) * sp.n[g] / tot));
+            sp.first[g + 1] = sp.first[g] + (int)want;
+        }
+        k_db_range<<<sp.first[4], 256, 0, S(stream)>>>(sp, part);
+        IA_LAUNCH_CHECK("k_db_range");
+        k_db_bound<<<1, DBB_BLOCKS, 0, S(stream)>>>(part, sp.first[4], center, amax);
+    }
+    IA_LAUNCH_CHECK("k_db_bound");
+    if (g_db_tiled && src->Aw % 32 == 0 && row0 % 32 == 0) {   // tiled form (npad is a multiple of 256)
+        k_db_build_t<<<(unsigned)(npad / 256), 256, 0, S(stream)>>>(d, row0, nrows, center, amax,
+                                                                    reinterpret_cast<half8 *>(db));
+        IA_LAUNCH_CHECK("k_db_build_t");
+        return IA_OK;
+    }
     k_db_build<<<(unsigned)((npad + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, npad, center,
                                                                      amax, reinterpret_cast<half8 *>(db));
     IA_LAUNCH_CHECK("k_db_build");

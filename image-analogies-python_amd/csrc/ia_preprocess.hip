@@ -199,10 +199,12 @@ __global__ __launch_bounds__(256) void k_pyr_reduce(const double *__restrict__ s
                                                     double sx, double tx, double sy, double ty,
                                                     double w0, double w1, double w2, double w3,
                                                     unsigned long long *minmax) {
-    __shared__ double tin[(PR_H + 6) * (PR_W + 6)];     // input region + halo, then blurred
-    __shared__ double tv[PR_H * (PR_W + 6)];            // vertical pass
+    // one LDS region (28.7 KiB: up to 5 blocks per CU): the input tile, then the vertical
+    // pass, then the blurred region; each pass holds its results in registers across the
+    // barrier that frees the region for them
+    __shared__ double buf[(PR_H + 6) * (PR_W + 6)];
     __shared__ int ext[8];
-    __shared__ long long red[2][4];
+    __shared__ long long red[4][4];
     const int tid = threadIdx.x;
     const int y0 = blockIdx.y * PT_H, x0 = blockIdx.x * PT_W;
     const int y1 = min(y0 + PT_H, h), x1 = min(x0 + PT_W, w);
@@ -236,44 +238,90 @@ __global__ __launch_bounds__(256) void k_pyr_reduce(const double *__restrict__ s
     const int C1 = oC1 > oC0 ? max(ext[3], oC1 - 1) : ext[3];
     const int RH = R1 - R0 + 1, RW = C1 - C0 + 1;   // <= PR_H, PR_W (checked by the host)
     const int IW = RW + 6;
-    // 2-D loops (64 columns x 4 rows per pass, no index division); the halo reflects once
-    // on each side for images of >= 3 rows / cols (symi otherwise)
+    // 2-D loops: 64 columns x 4 rows per step (tx0 + 64 cx, ty0 + 4 ry); the halo reflects
+    // once on each side for images of >= 3 rows / cols (symi otherwise)
     const int tx0 = tid & 63, ty0 = tid >> 6;
+    constexpr int NRY = (PR_H + 6 + 3) / 4, NCX = (PR_W + 6 + 63) / 64;
     const bool big = H >= 3 && W >= 3;
-    for (int ty_ = ty0; ty_ < RH + 6; ty_ += 4) {
-        const int gy = big ? symi2(R0 - 3 + ty_, H) : symi(R0 - 3 + ty_, H);
-        const double *row = src + (long)gy * W;
-        for (int tx_ = tx0; tx_ < IW; tx_ += 64)
-            tin[ty_ * IW + tx_] = row[big ? symi2(C0 - 3 + tx_, W) : symi(C0 - 3 + tx_, W)];
+    double v[NRY][NCX];
+    {   // every load first (clamped slots re-read a valid element), then the LDS stores: the
+        // loads issue back to back instead of one memory round trip per loop iteration
+        int gx[NCX];
+#pragma unroll
+        for (int cx = 0; cx < NCX; ++cx) {
+            const int tx_ = min(tx0 + 64 * cx, IW - 1);
+            gx[cx] = big ? symi2(C0 - 3 + tx_, W) : symi(C0 - 3 + tx_, W);
+        }
+#pragma unroll
+        for (int ry = 0; ry < NRY; ++ry) {
+            const int ty_ = min(ty0 + 4 * ry, RH + 5);
+            const double *row = src + (long)(big ? symi2(R0 - 3 + ty_, H) : symi(R0 - 3 + ty_, H)) * W;
+#pragma unroll
+            for (int cx = 0; cx < NCX; ++cx) v[ry][cx] = row[gx[cx]];
+        }
+#pragma unroll
+        for (int ry = 0; ry < NRY; ++ry)
+#pragma unroll
+            for (int cx = 0; cx < NCX; ++cx) {
+                const int ty_ = ty0 + 4 * ry, tx_ = tx0 + 64 * cx;
+                if (ty_ < RH + 6 && tx_ < IW) buf[ty_ * IW + tx_] = v[ry][cx];
+            }
     }
     __syncthreads();
-    for (int ty_ = ty0; ty_ < RH; ty_ += 4)
-        for (int tx_ = tx0; tx_ < IW; tx_ += 64) {
-            const double *c = tin + (ty_ + 3) * IW + tx_;
-            double acc = c[0] * w0;
-            acc = acc + (c[-3 * IW] + c[3 * IW]) * w3;
-            acc = acc + (c[-2 * IW] + c[2 * IW]) * w2;
-            acc = acc + (c[-IW] + c[IW]) * w1;
-            tv[ty_ * IW + tx_] = acc;
-        }
-    __syncthreads();
-    long long kmin = 0x7fffffffffffffffLL, kmax = (long long)0x8000000000000000ULL;
-    for (int ty_ = ty0; ty_ < RH; ty_ += 4)        // blurred region (into tin), owned min/max
-        for (int tx_ = tx0; tx_ < RW; tx_ += 64) {
-            const double *c = tv + ty_ * IW + tx_ + 3;
-            double acc = c[0] * w0;
-            acc = acc + (c[-3] + c[3]) * w3;
-            acc = acc + (c[-2] + c[2]) * w2;
-            acc = acc + (c[-1] + c[1]) * w1;
-            tin[ty_ * RW + tx_] = acc;
-            const int gy = R0 + ty_, gx = C0 + tx_;
-            if (gy >= oR0 && gy < oR1 && gx >= oC0 && gx < oC1) {
-                const long long k = dkey(acc);
-                kmin = k < kmin ? k : kmin;
-                kmax = k > kmax ? k : kmax;
+#pragma unroll
+    for (int ry = 0; ry < NRY; ++ry)          // vertical pass (k_blur's order)
+#pragma unroll
+        for (int cx = 0; cx < NCX; ++cx) {
+            const int ty_ = ty0 + 4 * ry, tx_ = tx0 + 64 * cx;
+            if (ty_ < RH && tx_ < IW) {
+                const double *c = buf + (ty_ + 3) * IW + tx_;
+                double acc = c[0] * w0;
+                acc = acc + (c[-3 * IW] + c[3 * IW]) * w3;
+                acc = acc + (c[-2 * IW] + c[2 * IW]) * w2;
+                acc = acc + (c[-IW] + c[IW]) * w1;
+                v[ry][cx] = acc;
             }
         }
     __syncthreads();
+#pragma unroll
+    for (int ry = 0; ry < NRY; ++ry)
+#pragma unroll
+        for (int cx = 0; cx < NCX; ++cx) {
+            const int ty_ = ty0 + 4 * ry, tx_ = tx0 + 64 * cx;
+            if (ty_ < RH && tx_ < IW) buf[ty_ * IW + tx_] = v[ry][cx];
+        }
+    __syncthreads();
+    long long kmin = 0x7fffffffffffffffLL, kmax = (long long)0x8000000000000000ULL;
+#pragma unroll
+    for (int ry = 0; ry < NRY; ++ry)          // horizontal pass, owned min / max
+#pragma unroll
+        for (int cx = 0; cx < NCX; ++cx) {
+            const int ty_ = ty0 + 4 * ry, tx_ = tx0 + 64 * cx;
+            if (ty_ < RH && tx_ < RW) {
+                const double *c = buf + ty_ * IW + tx_ + 3;
+                double acc = c[0] * w0;
+                acc = acc + (c[-3] + c[3]) * w3;
+                acc = acc + (c[-2] + c[2]) * w2;
+                acc = acc + (c[-1] + c[1]) * w1;
+                v[ry][cx] = acc;
+                const int gy = R0 + ty_, gx = C0 + tx_;
+                if (gy >= oR0 && gy < oR1 && gx >= oC0 && gx < oC1) {
+                    const long long k = dkey(acc);
+                    kmin = k < kmin ? k : kmin;
+                    kmax = k > kmax ? k : kmax;
+                }
+            }
+        }
+    __syncthreads();
+#pragma unroll
+    for (int ry = 0; ry < NRY; ++ry)
+#pragma unroll
+        for (int cx = 0; cx < NCX; ++cx) {
+            const int ty_ = ty0 + 4 * ry, tx_ = tx0 + 64 * cx;
+            if (ty_ < RH && tx_ < RW) buf[ty_ * RW + tx_] = v[ry][cx];
+        }
+    __syncthreads();
+    long long omin = 0x7fffffffffffffffLL, omax = (long long)0x8000000000000000ULL;
     {   // bilinear samples of the blurred region (k_resample's operation order), unclipped
         const int ox = x0 + (tid & 31), oy0 = y0 + (tid >> 5);
         if (ox < x1) {
@@ -288,48 +336,74 @@ __global__ __launch_bounds__(256) void k_pyr_reduce(const double *__restrict__ s
                 const long minr = (long)fr, maxr = (long)ceil(r);
                 const double dr = r - (double)minr;
                 const int r0 = (int)mirrori(minr, H) - R0, r1 = (int)mirrori(maxr, H) - R0;
-                const double tl = tin[r0 * RW + c0], tr = tin[r0 * RW + c1];
-                const double bl = tin[r1 * RW + c0], br = tin[r1 * RW + c1];
+                const double tl = buf[r0 * RW + c0], tr = buf[r0 * RW + c1];
+                const double bl = buf[r1 * RW + c0], br = buf[r1 * RW + c1];
                 const double top = (1 - dc) * tl + dc * tr;
                 const double bot = (1 - dc) * bl + dc * br;
-                dst[(long)oy * w + ox] = (1 - dr) * top + dr * bot;
+                const double val = (1 - dr) * top + dr * bot;
+                dst[(long)oy * w + ox] = val;
+                const long long k = dkey(val);
+                omin = k < omin ? k : omin;
+                omax = k > omax ? k : omax;
             }
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
-        const long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+        long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
         kmin = a < kmin ? a : kmin;
         kmax = b > kmax ? b : kmax;
+        a = __shfl_xor(omin, o), b = __shfl_xor(omax, o);
+        omin = a < omin ? a : omin;
+        omax = b > omax ? b : omax;
     }
-    if ((tid & 63) == 0) { red[0][tid >> 6] = kmin; red[1][tid >> 6] = kmax; }
+    if ((tid & 63) == 0) {
+        red[0][tid >> 6] = kmin; red[1][tid >> 6] = kmax;
+        red[2][tid >> 6] = omin; red[3][tid >> 6] = omax;
+    }
     __syncthreads();
     if (tid == 0) {
         for (int i = 1; i < 4; ++i) {
             kmin = red[0][i] < kmin ? red[0][i] : kmin;
             kmax = red[1][i] > kmax ? red[1][i] : kmax;
+            omin = red[2][i] < omin ? red[2][i] : omin;
+            omax = red[3][i] > omax ? red[3][i] : omax;
         }
         unsigned long long *sl = minmax + ((blockIdx.x + blockIdx.y * gridDim.x) % MM_SLOTS) * MM_STRIDE;
         atomicMin(reinterpret_cast<long long *>(&sl[0]), kmin);
         atomicMax(reinterpret_cast<long long *>(&sl[1]), kmax);
+        atomicMin(reinterpret_cast<long long *>(&sl[2]), omin);
+        atomicMax(reinterpret_cast<long long *>(&sl[3]), omax);
     }
 }
 
 // warp's clip of the resampled level to [min, max] of the blurred image (np.clip; only
-// values outside the range, which bilinear weights can produce by rounding, are written)
+// values outside the range, which bilinear weights can produce by rounding, are written).
+// k_pyr_reduce also recorded the min / max of its outputs: when they lie inside the range
+// (the usual case) every block returns without reading the level.
 __global__ __launch_bounds__(256) void k_pyr_clip(double *__restrict__ dst, long n,
                                                   const unsigned long long *minmax) {
     __shared__ double clip[2];
+    __shared__ int skip;
     if (threadIdx.x < 64) {
         long long kmin = (long long)minmax[threadIdx.x * MM_STRIDE];
         long long kmax = (long long)minmax[threadIdx.x * MM_STRIDE + 1];
+        long long omin = (long long)minmax[threadIdx.x * MM_STRIDE + 2];
+        long long omax = (long long)minmax[threadIdx.x * MM_STRIDE + 3];
         for (int o = 32; o > 0; o >>= 1) {
-            const long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+            long long a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
             kmin = a < kmin ? a : kmin;
             kmax = b > kmax ? b : kmax;
+            a = __shfl_xor(omin, o), b = __shfl_xor(omax, o);
+            omin = a < omin ? a : omin;
+            omax = b > omax ? b : omax;
         }
-        if (threadIdx.x == 0) { clip[0] = dkey_inv(kmin); clip[1] = dkey_inv(kmax); }
+        if (threadIdx.x == 0) {
+            clip[0] = dkey_inv(kmin); clip[1] = dkey_inv(kmax);
+            skip = omin >= kmin && omax <= kmax;
+        }
     }
     __syncthreads();
+    if (skip) return;
     const double lo = clip[0], hi = clip[1];
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
         const double v = dst[i];
@@ -339,8 +413,10 @@ __global__ __launch_bounds__(256) void k_pyr_clip(double *__restrict__ dst, long
 }
 
 __global__ void k_init_minmax(unsigned long long *mm) {   // <<<1, MM_SLOTS>>>
-    mm[threadIdx.x * MM_STRIDE] = 0x7fffffffffffffffULL;
+    mm[threadIdx.x * MM_STRIDE] = 0x7fffffffffffffffULL;       // blurred min / max
     mm[threadIdx.x * MM_STRIDE + 1] = 0x8000000000000000ULL;
+    mm[threadIdx.x * MM_STRIDE + 2] = 0x7fffffffffffffffULL;   // output min / max (fused form)
+    mm[threadIdx.x * MM_STRIDE + 3] = 0x8000000000000000ULL;
 }
 
 // deterministic two-pass mean: block partial sums (fixed order) then one block.

@@ -85,7 +85,8 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
  * row): the MFMA screen's operand, and the exact stage's fp32 re-screen input (x_h + x_l
  * is exact in fp32).  Rows are padded to ia_db_rows_padded(nrows) (whole chunks of
  * ia_db_chunk_rows, a multiple of 4 chunks) by repeating the last real row.  amax (device,
- * 1 float) receives max_row |a - center| (atomic max; zero it first). */
+ * 1 float) receives A >= max_row |a - center|, bounded from the value ranges of the level's
+ * four images (max with its prior value: zero it first). */
 long ia_db_rows_padded(long nrows);
 /* bytes of the db buffer ia_db_build fills: 224 B per padded row */
 size_t ia_db_bytes(long nrows);

@@ -28,6 +28,10 @@ int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *
  * (k_select / k_items / k_gather), -1 the default (work list above 2^20 rows); other values
  * leave it; returns the previous value */
 int ia_diag_set_rescore_mode(int mode);
+/* ia_db_build form for this process: 1 [default] the LDS-tiled kernels where the level's
+ * width and row0 are multiples of 32, 0 always the per-row gather kernels (same bytes);
+ * other values leave it; returns the previous value */
+int ia_diag_set_db_build_form(int tiled);
 /* HIP-graph capture of ia_synth_level's wave loop for this process (overrides IA_GRAPH):
  * 0 off, 1 levels of <= 2^18 rows, 2 every single-GPU level; other values leave it;
  * returns the previous value */

@@ -137,6 +137,35 @@ def test_split16_screen_every_query_split(gpu):
     assert worst < 1.0
 
 
+@pytest.mark.parametrize('shape,n_ap,shards', [((64, 96), 2, 1), ((70, 128), 1, 3),
+                                               ((33, 32), 3, 2), ((256, 512), 1, 1)])
+def test_db_build_tiled_equals_per_row(gpu, shape, n_ap, shards):
+    """ia_db_build's LDS-tiled kernels (width and row0 multiples of 32) write the same
+    bytes and amax as the per-row gather kernels, for whole levels and for shards whose
+    row ranges end mid-tile (padding rows repeat the last real row)."""
+    import _ia
+    import algorithms
+    A, Aps, _ = analogy_inputs(47, shape, (8, 8), n_ap=n_ap)
+    A_pyr = [dev(p) for p in o.compute_gaussian_pyramid(A, 3, cap=2)]
+    Ap_pyr = [[dev(p) for p in o.compute_gaussian_pyramid(x, 3, cap=2)] for x in Aps]
+    L = len(A_pyr) - 1
+    N = n_ap * shape[0] * shape[1]
+    # shard boundaries on multiples of 32 with a ragged last shard
+    cuts = [0] + [((N * r // shards) // 32) * 32 for r in range(1, shards)] + [N]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        got = []
+        for form in (1, 0):
+            prev = _ia.db_build_form(form)
+            try:
+                idx = algorithms.level_index(A_pyr, Ap_pyr, L, lambda l, n: (r0, r1 - r0))
+                torch.cuda.synchronize()
+                got.append((idx.db.cpu().numpy().copy(), float(idx.amax.item())))
+            finally:
+                _ia.db_build_form(prev)
+        assert got[0][1] == got[1][1], (r0, r1)
+        assert np.array_equal(got[0][0], got[1][0]), (r0, r1)
+
+
 @pytest.mark.parametrize('scale', [1.0, 1e3, 1e-3])
 def test_match_exact(gpu, scale):
     A, Aps, _ = analogy_inputs(42, (70, 101), (8, 8), n_ap=2, flat=(scale == 1.0))
