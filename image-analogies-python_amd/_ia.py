@@ -41,7 +41,7 @@ class IaMatchArgs(ctypes.Structure):
     _fields_ = [('src', IaSrcLevel), ('db', _dp), ('row0', ctypes.c_long),
                 ('nrows', ctypes.c_long), ('center', _dp), ('amax', _dp), ('q64', _dp),
                 ('M', ctypes.c_int), ('idx', _dp), ('dist', _dp), ('workspace', _dp),
-                ('lsh', ctypes.POINTER(IaLsh))]
+                ('lsh', ctypes.POINTER(IaLsh)), ('dbi', _dp)]
 
 
 class IaSynthArgs(ctypes.Structure):
@@ -53,11 +53,12 @@ class IaSynthArgs(ctypes.Structure):
                 ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
                 ('workspace', _dp), ('comm', _dp), ('lsh', ctypes.POINTER(IaLsh)),
                 ('flags', ctypes.c_int), ('tag', ctypes.c_int), ('dbg_px', _dp),
-                ('dbg_dist', _dp)]
+                ('dbg_dist', _dp), ('dbi', _dp)]
 
 
 class IaShardDb(ctypes.Structure):
-    _fields_ = [('db', _dp), ('row0', ctypes.c_long), ('nrows', ctypes.c_long), ('amax', _dp)]
+    _fields_ = [('db', _dp), ('row0', ctypes.c_long), ('nrows', ctypes.c_long), ('amax', _dp),
+                ('dbi', _dp)]
 
 
 IA_SYNTH_EAGER = 1
@@ -85,6 +86,10 @@ _SIGS = {
     'ia_db_chunk_rows': (ctypes.c_int, [ctypes.c_long]),
     'ia_db_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
                                    _dp, _dp, _dp, _dp]),
+    'ia_db_image_bytes': (ctypes.c_size_t, [ctypes.POINTER(IaSrcLevel), ctypes.c_long,
+                                            ctypes.c_long]),
+    'ia_db_build_image': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
+                                         _dp, _dp, _dp, _dp, _dp]),
     'ia_center_fill': (ctypes.c_int, [_dp, ctypes.c_double, ctypes.c_double, _dp]),
     'ia_match_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_long]),
     'ia_match_batch': (ctypes.c_int, [ctypes.POINTER(IaMatchArgs), _dp]),
@@ -116,6 +121,8 @@ _SIGS = {
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
+    'ia_diag_screen16_image': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long,
+                                              ctypes.c_long, _dp, _dp, ctypes.c_int, _dp, _dp]),
     'ia_diag_synth_level_shards': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs),
                                                   ctypes.POINTER(IaShardDb), ctypes.c_int, _dp]),
 }
@@ -165,6 +172,12 @@ def graph_mode(mode=-1):
     """HIP-graph capture of the synthesis wave loop for this process (0 off [default],
     1 levels <= 2^18 rows, 2 all single-GPU levels); returns the previous value."""
     return lib().ia_diag_set_graph_mode(int(mode))
+
+
+def db_image_enabled():
+    """The screen streams the DB's image form where it applies (IA_DB_IMAGE, default 1;
+    0: always the 224-B rows).  Both give the same results bit for bit."""
+    return os.environ.get('IA_DB_IMAGE', '1') != '0'
 
 
 def db_build_form(tiled=-1):

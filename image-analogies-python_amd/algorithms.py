@@ -98,7 +98,19 @@ class LevelIndex:
         _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
                                   _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),
                                   st), 'ia_db_build')
+        # the image form the screen streams where it applies
+        ibytes = lib.ia_db_image_bytes(ctypes.byref(self.src), self.row0, self.nrows)
+        self.dbi = None
+        if ibytes and _ia.db_image_enabled():
+            self.dbi = torch.empty(ibytes, dtype=torch.uint8, device=dev)
+            _ia.check(lib.ia_db_build_image(ctypes.byref(self.src), self.row0, self.nrows,
+                                            _ia.ptr(self.center), _ia.ptr(self.db),
+                                            _ia.ptr(self.amax), _ia.ptr(self.dbi), st),
+                      'ia_db_build_image')
         self.lsh = None
+
+    def dbi_ptr(self):
+        return _ia.ptr(self.dbi).value if self.dbi is not None else None
 
     def build_lsh(self, tables=16, hashes=4, width=1.0, seed=0):
         """Switch this index to the approximate LSH matcher (c.matcher = 'lsh', SURVEY
@@ -146,6 +158,7 @@ class LevelIndex:
         a.center, a.amax, a.q64, a.M = (_ia.ptr(self.center).value, _ia.ptr(self.amax).value,
                                         _ia.ptr(q).value, M)
         a.idx, a.dist, a.workspace = _ia.ptr(idx).value, _ia.ptr(dist).value, _ia.ptr(ws).value
+        a.dbi = self.dbi_ptr()
         if not exact and self.lsh is not None:
             a.lsh = self.lsh_ptr()
         _ia.check(_ia.lib().ia_match_batch(ctypes.byref(a), _ia.stream()), 'ia_match_batch')

@@ -332,6 +332,36 @@ __global__ __launch_bounds__(256) void k_db_build(DbSrc src, long row0, long nro
     }
 }
 
+// ---- the image form of the DB (ia_db_build_image, ia_internal.h ImgDb) -----------------
+// one thread per padded pixel: the split pair of sa * fl32(v - c) for the reflected pixel v
+// (the same value k_db_build_t writes for every feature that reads this pixel)
+__global__ __launch_bounds__(256) void k_img_pad(const double *__restrict__ img, int h, int w,
+                                                 int wp, long n, const double *__restrict__ center,
+                                                 int ck, const float *__restrict__ amax,
+                                                 uint32_t *__restrict__ out) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int r = (int)(i / wp), q = (int)(i - (long)r * wp);
+    const double v = img[(long)symi(r - IMG_PY, h) * w + symi(q - IMG_PX, w)];
+    const Split16Db s = split16_db_scale(amax[0]);
+    _Float16 xh, xl;
+    split16f(ldexpf((float)(v - center[ck]), s.ea), xh, xl);
+    out[i] = (uint32_t)__builtin_bit_cast(uint16_t, xh) | ((uint32_t)__builtin_bit_cast(uint16_t, xl) << 16);
+}
+
+// the rows' norm-slot pairs, read back from the row form (feature 55: hi in lane half 1's
+// group 2, lo in its group 6, element 7; ia_split16.h)
+__global__ __launch_bounds__(256) void k_img_norm(const half8 *__restrict__ db16, long nrows,
+                                                  uint32_t *__restrict__ norm) {
+    const long r = (long)blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrows) return;
+    const long T = r >> 5;
+    const int j = (int)(r & 31);
+    const _Float16 xh = db16[(T * DB16_GROUPS + 2) * 64 + 32 + j][7];
+    const _Float16 xl = db16[(T * DB16_GROUPS + 6) * 64 + 32 + j][7];
+    norm[r] = (uint32_t)__builtin_bit_cast(uint16_t, xh) | ((uint32_t)__builtin_bit_cast(uint16_t, xl) << 16);
+}
+
 __global__ void k_center_fill(double *c, double mA, double mAp) {
     const int k = threadIdx.x;
     if (k < IA_D) c[k] = k < 34 ? mA : mAp;
@@ -475,6 +505,41 @@ int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *cent
     k_db_build<<<(unsigned)((npad + 255) / 256), 256, 0, S(stream)>>>(d, row0, nrows, npad, center,
                                                                      amax, reinterpret_cast<half8 *>(db));
     IA_LAUNCH_CHECK("k_db_build");
+    return IA_OK;
+}
+
+size_t ia_db_image_bytes(const IaSrcLevel *src, long row0, long nrows) {
+    if (!src || nrows <= 0 || row0 < 0) return 0;
+    ImgDb v;
+    size_t b = 0;
+    return img_db_layout(src->Ah, src->Aw, src->A_hs, src->A_ws, src->nAp, row0, nrows, nullptr, v,
+                         &b) ? b : 0;
+}
+
+int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                      const void *db, const float *amax, void *dbi, void *stream) {
+    IA_ARG(src && center && db && amax && dbi && nrows > 0 && row0 >= 0, "ia_db_build_image: bad args");
+    IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build_image: rows out of range");
+    ImgDb v;
+    IA_ARG(img_db_layout(src->Ah, src->Aw, src->A_hs, src->A_ws, src->nAp, row0, nrows, dbi, v, nullptr),
+           "ia_db_build_image: the image form needs width and row0 multiples of 128 and whole chunks");
+    hipStream_t st = S(stream);
+    auto pad = [&](const double *img, int h, int w, int wp, long n, int ck, const uint32_t *out) {
+        k_img_pad<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(img, h, w, wp, n, center, ck, amax,
+                                                              const_cast<uint32_t *>(out));
+    };
+    pad(src->A_lg, src->Ah, src->Aw, v.Wp, v.fsz, 0, v.fa);
+    pad(src->A_sm, src->A_hs, src->A_ws, v.Wcp, v.csz, 0, v.ca);
+    for (int i = 0; i < src->nAp; ++i) {
+        const uint32_t *f = v.ap + (long)i * v.apstride;
+        pad(src->Ap_lg + (long)i * src->Ah * src->Aw, src->Ah, src->Aw, v.Wp, v.fsz, 34, f);
+        pad(src->Ap_sm + (long)i * src->A_hs * src->A_ws, src->A_hs, src->A_ws, v.Wcp, v.csz, 34,
+            f + v.apc);
+    }
+    IA_LAUNCH_CHECK("k_img_pad");
+    k_img_norm<<<(unsigned)((nrows + 255) / 256), 256, 0, st>>>(reinterpret_cast<const half8 *>(db), nrows,
+                                                               const_cast<uint32_t *>(v.norm));
+    IA_LAUNCH_CHECK("k_img_norm");
     return IA_OK;
 }
 

@@ -36,6 +36,49 @@ static inline int db_seg_rows(long nrows) {
 }
 static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_rows(nrows); }
 
+// ---- the image form of a level's DB (ia_db_build_image) ---------------
+// A row's 55 features are pixels of its neighbourhood, so the screen can stage 128-row
+// stages (128 pixels of one scanline) from the images instead of from 224-B rows: every
+// pixel's split-f16 pair (hi | lo << 16) stored once, the images padded by reflection
+// (IMG_PX columns, IMG_PY rows on each side) so every window row is one contiguous run.
+// Buffer: [A fine][A coarse][norm slots of the rows][for each A' image: fine, coarse], each
+// section 256-B aligned.  Applies when the level width and row0 are multiples of 128 and
+// the rows fill whole chunks (no padding rows): see img_db_applies.
+constexpr int IMG_PX = 4, IMG_PY = 2;
+struct ImgDb {
+    const uint32_t *fa, *ca, *norm, *ap;   // ap: A' image 0's fine section
+    int W, Wp, Wcp;                         // width, padded fine / coarse widths
+    long fsz, csz, apstride, apc;           // padded image sizes (u32), A' image stride,
+                                            // offset of an A' image's coarse section
+    long hw, row0;                          // rows per image, global row of local row 0
+};
+static inline bool img_db_applies(int W, long row0, long nrows) {
+    return W % 128 == 0 && row0 % 128 == 0 && db_rows_padded(nrows) == nrows;
+}
+static inline size_t img_align(size_t b) { return (b + 255) / 256 * 256; }
+// the image-form buffer of rows [row0, row0 + nrows) of a level with fine images H x W and
+// coarse images hs x ws: its bytes (nAp A' images) and, with dbi, the section pointers.
+// False when the image form does not apply.
+static inline bool img_db_layout(int H, int W, int hs, int ws, int nAp, long row0, long nrows,
+                                 const void *dbi, ImgDb &v, size_t *bytes) {
+    if (!img_db_applies(W, row0, nrows)) return false;
+    v.W = W; v.Wp = W + 2 * IMG_PX; v.Wcp = ws + 2 * IMG_PX;
+    v.fsz = (long)(H + 2 * IMG_PY) * v.Wp;
+    v.csz = (long)(hs + 2 * IMG_PY) * v.Wcp;
+    v.hw = (long)H * W;
+    v.row0 = row0;
+    const size_t fb = img_align(v.fsz * 4), cb = img_align(v.csz * 4), nb = img_align(nrows * 4);
+    v.apstride = (long)((fb + cb) / 4);
+    v.apc = (long)(fb / 4);
+    if (bytes) *bytes = fb + cb + nb + (size_t)nAp * (fb + cb);
+    const char *p = reinterpret_cast<const char *>(dbi);
+    v.fa = reinterpret_cast<const uint32_t *>(p);
+    v.ca = reinterpret_cast<const uint32_t *>(p + fb);
+    v.norm = reinterpret_cast<const uint32_t *>(p + fb + cb);
+    v.ap = reinterpret_cast<const uint32_t *>(p + fb + cb + nb);
+    return true;
+}
+
 struct Best {            // exact winner of a (query, shard): fp64 distance + global row
     double d;
     long long idx;
@@ -98,16 +141,19 @@ int launch_query_rows(const double *qin, int M, const double *center, float *qp,
                       const float *amax, _Float16 *q16, hipStream_t st);
 // the split-f16 segment screen (ia_screen16.hip) of M queries over the DB ->
 // segmin[M][db_nsegs(nrows)] (screen units); q16 holds qrows_alloc(M) rows
-int launch_screen16(const void *db, long nrows, const _Float16 *q16, int M, float *segmin,
-                    hipStream_t st);
+// img (nullable): the DB's image form (ImgDb, whole chunks) streamed instead of the rows
+// (same minima, bit for bit)
+int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16 *q16, int M,
+                    float *segmin, hipStream_t st);
 // the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
 // stats (nullable): rows rescored, candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);
 // ev0 / ev1 (nullable) are recorded on st immediately before / after the screen launch.
 // fin (nullable, single shard only): the exact stage also runs the per-pixel tail of the
 // wave (coherence, kappa, B'/s/im update) in the same kernel.
-int launch_match(const DbSrc &src, long row0, long nrows, const void *db, const float *qp,
-                 const _Float16 *q16, int M, const double *q64, const double *nq,
+// dbi (nullable): the DB's image form for the screen (ia_db_build_image)
+int launch_match(const DbSrc &src, long row0, long nrows, const void *db, const void *dbi,
+                 const float *qp, const _Float16 *q16, int M, const double *q64, const double *nq,
                  const float *amax, void *scratch, Best *best, unsigned long long *stats,
                  hipStream_t st,
                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,

@@ -480,16 +480,19 @@ size_t match_scratch_bytes(int qrows, long nrows) {
            align_up(n * sizeof(Best), 256) + align_up((size_t)qrows * sizeof(QSel), 256);
 }
 
-int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const float *qp,
-                 const _Float16 *q16, int M, const double *q64, const double *nq,
+int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const void *dbi,
+                 const float *qp, const _Float16 *q16, int M, const double *q64, const double *nq,
                  const float *amax, void *scratch, Best *best, unsigned long long *stats,
                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, const FinishArgs *fin) {
     int rc;
     IA_ARG(q16, "launch_match: no split-f16 query rows");
     const half8 *db = reinterpret_cast<const half8 *>(dbv);
+    ImgDb img;
+    IA_ARG(!dbi || img_db_layout(src.A.h, src.A.w, src.A.hs, src.A.ws, 1, row0, nrows, dbi, img, nullptr),
+           "launch_match: an image-form DB for a level it does not apply to");
     const SegWs ws = seg_ws(scratch, M, nrows);
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
-    if ((rc = launch_screen16(db, nrows, q16, M, ws.segmin, st))) return rc;
+    if ((rc = launch_screen16(db, dbi ? &img : nullptr, nrows, q16, M, ws.segmin, st))) return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
     const int rm = rescore_mode();
@@ -623,8 +626,8 @@ int ia_match_batch(const IaMatchArgs *a, void *stream) {
                 return rc;
         } else {
             if ((rc = launch_query_rows(q, M, a->center, qp, nq, a->amax, q16, st))) return rc;
-            if ((rc = launch_match(src, a->row0, a->nrows, a->db, qp, q16, M, q, nq, a->amax,
-                                   scratch, best, nullptr, st)))
+            if ((rc = launch_match(src, a->row0, a->nrows, a->db, a->dbi, qp, q16, M, q, nq,
+                                   a->amax, scratch, best, nullptr, st)))
                 return rc;
         }
         k_split_best<<<(M + 255) / 256, 256, 0, st>>>(best, M, a->idx ? a->idx + m0 : nullptr,
@@ -675,7 +678,17 @@ int ia_diag_set_rescore_mode(int mode) {
 int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *segmin,
                      void *stream) {
     IA_ARG(db && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16: bad args");
-    return launch_screen16(db, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin,
+    return launch_screen16(db, nullptr, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin,
+                           S(stream));
+}
+
+int ia_diag_screen16_image(const IaSrcLevel *src, long row0, long nrows, const void *dbi,
+                           const void *q16, int M, float *segmin, void *stream) {
+    IA_ARG(src && dbi && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16_image: bad args");
+    ImgDb img;
+    IA_ARG(img_db_layout(src->Ah, src->Aw, src->A_hs, src->A_ws, src->nAp, row0, nrows, dbi, img, nullptr),
+           "ia_diag_screen16_image: the image form does not apply to this level");
+    return launch_screen16(nullptr, &img, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin,
                            S(stream));
 }
 

@@ -29,6 +29,7 @@
 #include "ia_split16.h"
 
 #include <float.h>
+#include <stdint.h>
 #include <type_traits>
 
 namespace ia {
@@ -62,23 +63,94 @@ __device__ __forceinline__ int fkey(float x) {
 }
 __device__ __forceinline__ float fkey_inv(int b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
 
-// wave W's share of one chunk: NS query tiles (T0 .. T0 + NS - 1 of the block's G), its
-// chains of every stage, and the segment minima of its tiles into smin[seg][G * 32]
-template <int G, int W>
-__device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
-                                           long ctile0, int nstage, int tps,
-                                           const half8 *__restrict__ q16) {
-    constexpr int T0 = bal_t0(G, W), NS = bal_ns(G, W);
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
+// wave W's MFMA chains of one 4-tile stage (operand sb in LDS) into its running minima
+template <int G, int W, int NS>
+__device__ __forceinline__ void stage_mfma(const half8 *sb, const half8 (&bq)[NS][Q16_GROUPS],
+                                           float (&mn)[NS], int lane) {
+    const floatx16 zero = {};
+    static_for<0, STAGE_TILES>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        half8 a[DB16_GROUPS];
+        const half8 *p = sb + u * TILE_H8 + lane;
+#pragma unroll
+        for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+        floatx16 acc[NS];
+        static_for<0, NS>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (bal_on(G, W, k, u))
+                acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[k][0], zero, 0, 0, 0);
+        });
+#pragma unroll
+        for (int m = 1; m < MFMA16; ++m)
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u))
+                    acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[k][mfma_b(m)],
+                                                                     acc[k], 0, 0, 0);
+            });
+        // running minimum: 8 v_min3_f32 per accumulator, dependency depth 3
+        static_for<0, NS>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (bal_on(G, W, k, u)) {
+                const floatx16 &x = acc[k];
+                const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+                const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+                const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+                const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+                mn[k] = fminf(fminf(mn[k], u0), u1);
+            }
+        });
+    });
+}
+
+// after stage s: when it closes a segment, fold the wave's minima into smin[seg][G * 32]
+template <int G, int W, int NS>
+__device__ __forceinline__ void stage_close(int s, int tps, int *smin, float (&mn)[NS], int lane) {
+    constexpr int T0 = bal_t0(G, W);
+    const int done = (s + 1) * STAGE_TILES;
+    if (done % tps == 0) {   // segment done / tps - 1 of the chunk closed
+        int *sm = smin + (done / tps - 1) * (G * 32);
+        const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            // the two lane halves hold different rows of the same queries
+            const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
+            if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
+            mn[k] = FLT_MAX;
+        }
+    }
+}
+
+template <int G, int W, int NS>
+__device__ __forceinline__ void load_queries(const half8 *__restrict__ q16, half8 (&bq)[NS][Q16_GROUPS],
+                                             int lane) {
+    constexpr int T0 = bal_t0(G, W);
     const int j = lane & 31, h = lane >> 5;
-    half8 bq[NS][Q16_GROUPS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         const half8 *p = q16 + (long)((T0 + k) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
 #pragma unroll
         for (int m = 0; m < Q16_GROUPS; ++m) bq[k][m] = p[m];
     }
+}
+
+// every wave's copies of the next stage retired, then the barrier (the compiler's own wait
+// before __syncthreads() does not cover global_load_lds)
+__device__ __forceinline__ void copies_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// row form: wave W's share of one chunk, the DB rows streamed into LDS stage by stage
+template <int G, int W>
+__device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
+                                           long ctile0, int nstage, int tps,
+                                           const half8 *__restrict__ q16) {
+    constexpr int NS = bal_ns(G, W);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    half8 bq[NS][Q16_GROUPS];
+    load_queries<G, W, NS>(q16, bq, lane);
     auto issue = [&](int s, int buf) {
         const half8 *src = db16 + (ctile0 + (long)s * STAGE_TILES) * TILE_H8 + tid;
 #pragma unroll
@@ -87,66 +159,127 @@ __device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8
                                              (void *)(sbuf + buf * STAGE_H8 + k * 256 + W * 64),
                                              16, 0, 2);
     };
-    // every wave's copies of the next stage retired, then the barrier (the compiler's own
-    // wait before __syncthreads() does not cover global_load_lds)
-    auto stage_barrier = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+    float mn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    issue(0, 0);
+    copies_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        stage_mfma<G, W, NS>(sbuf + (s & 1) * STAGE_H8, bq, mn, lane);
+        stage_close<G, W, NS>(s, tps, smin, mn, lane);
+        copies_barrier();   // stage s+1 landed and stage s is free again
+    }
+}
+
+// image form (ia_internal.h ImgDb): a stage is 128 pixels of one scanline, built in LDS
+// from image windows — fine rows y-2..y+2 of A and y-2..y of A' (34 x 16-B pieces each),
+// coarse rows of both (18 pieces), the stage's 128 norm slots — 6.6 KB instead of 28 KB
+// of rows; the window is expanded into the row form's operand layout in LDS, then the
+// same MFMA stage runs.  Windows are double-buffered (the next one's copies fly during the
+// expansion and MFMAs of this one); the operand is built and consumed between two barriers.
+constexpr int WF_PC = 34, WC_PC = 18;                                 // 16-B pieces per window row
+constexpr int WB_FINE = 8 * WF_PC * 16, WB_COARSE = 6 * WC_PC * 16, WB_NORM = 128 * 4;
+constexpr int WIN_B = WB_FINE + WB_COARSE + WB_NORM;                  // 6592 B
+constexpr int WIN_PIECES = WIN_B / 16;                                // 412
+static_assert(WIN_PIECES <= 448, "waves 0-2 x two wave-instructions + wave 3 x one stage the window");
+
+// byte offset of feature k's hi half in the window minus its lane term (pixel p of the stage:
+// 4 p for fine features, 4 (p / 2) for coarse ones); lo halves are 2 bytes on
+__host__ __device__ constexpr int win_off(int k) {
+    return k < 9 ? WB_FINE + (k / 3) * WC_PC * 16 + (k % 3 + 3) * 4
+         : k < 34 ? ((k - 9) / 5) * WF_PC * 16 + ((k - 9) % 5 + 2) * 4
+         : k < 43 ? WB_FINE + (3 + (k - 34) / 3) * WC_PC * 16 + ((k - 34) % 3 + 3) * 4
+         : k < 55 ? (5 + (k - 43) / 5) * WF_PC * 16 + ((k - 43) % 5 + 2) * 4
+         : WB_FINE + WB_COARSE;
+}
+__host__ __device__ constexpr bool win_coarse(int k) { return k < 9 || (k >= 34 && k < 43); }
+__host__ __device__ constexpr int grp_k0(int h, int g) {
+    return h == 0 ? (g < 4 ? 8 * g : 8 * (g - 4)) : (g < 3 ? 32 + 8 * g : (g == 3 ? 24 : 32 + 8 * (g - 4)));
+}
+__host__ __device__ constexpr bool grp_hi(int h, int g) { return h == 0 ? g < 4 : g < 3; }
+
+// expand groups [G0, G1) of this wave's operand slot (tile 2 (W >> 1) + lane / 32, row
+// lane % 32, lane half W & 1) from window wb into the stage operand E: ds_read_u16 at
+// compile-time offsets from two per-lane bases, one ds_write_b128 per group
+template <int W, int G0, int G1>
+__device__ __forceinline__ void expand_groups(const char *wb, half8 *E, int lane) {
+    constexpr int H = W & 1;
+    const int tile = 2 * (W >> 1) + (lane >> 5), j = lane & 31;
+    const int px = 32 * tile + j;
+    const char *bf = wb + px * 4, *bc = wb + (px >> 1) * 4;
+    half8 *e = E + tile * TILE_H8 + H * 32 + j;
+    static_for<G0, G1>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        constexpr int k0 = grp_k0(H, g);
+        constexpr bool hi = grp_hi(H, g);
+        half8 o;
+        static_for<0, 8>([&](auto ec) {
+            constexpr int k = k0 + decltype(ec)::value;
+            constexpr int off = win_off(k) + (hi ? 0 : 2);
+            const char *b = (k < 55 && win_coarse(k)) ? bc : bf;
+            o[decltype(ec)::value] = *reinterpret_cast<const _Float16 *>(b + off);
+        });
+        e[g * 64] = o;
+    });
+}
+
+// Per stage: expand the window into the operand (all waves), barrier, the row form's MFMA
+// stage, barrier.  The window of the next stage is in flight meanwhile (two window
+// buffers, one operand buffer: 63.7 KB of LDS, 2 blocks per CU, which overlap one block's
+// expansion with the other's MFMAs).  Measured against a pipelined form (two operand
+// buffers, the next stage expanded before this one's MFMAs, one barrier per stage, 81.8 KB):
+// c4 1615-1635 vs 1650-1656 ms/step (tools/gpu_img_check.sh, profiles/r02_image_form_ab.txt).
+template <int G, int W>
+__device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, int *smin,
+                                         long crow0, int nstage, int tps,
+                                         const half8 *__restrict__ q16) {
+    constexpr int NS = bal_ns(G, W);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    half8 bq[NS][Q16_GROUPS];
+    load_queries<G, W, NS>(q16, bq, lane);
+    auto issue = [&](int s, int buf) {
+        const long lrow = crow0 + (long)s * 128;
+        const long g = im.row0 + lrow;
+        const long img = g / im.hw;
+        const long rem = g - img * im.hw;
+        const int y = (int)(rem / im.W), x0 = (int)(rem - (long)y * im.W);
+        const uint32_t *fp = im.ap + img * im.apstride;
+        const uint32_t *cp = fp + im.apc;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            if (t == 1 && W == 3) continue;     // pieces 448.. are past the window
+            const int i = (t * 4 + W) * 64 + lane;
+            const uint32_t *src;
+            if (i < 8 * WF_PC) {                // fine: padded row = image row + IMG_PY
+                const int r = i / WF_PC, pc = i - r * WF_PC;
+                src = (r < 5 ? im.fa + (long)(y + r) * im.Wp : fp + (long)(y + r - 5) * im.Wp) + x0 + 4 * pc;
+            } else if (i < 8 * WF_PC + 6 * WC_PC) {
+                const int q = i - 8 * WF_PC, r = q / WC_PC, pc = q - r * WC_PC;
+                src = (r < 3 ? im.ca + (long)((y >> 1) + 1 + r) * im.Wcp
+                             : cp + (long)((y >> 1) + r - 2) * im.Wcp) + (x0 >> 1) + 4 * pc;
+            } else {
+                src = im.norm + lrow + 4 * (i - 8 * WF_PC - 6 * WC_PC);
+            }
+            if (i < WIN_PIECES)
+                __builtin_amdgcn_global_load_lds((const void *)src,
+                                                 (void *)(wbuf + buf * WIN_B + (t * 4 + W) * 1024),
+                                                 16, 0, 2);
+        }
     };
     float mn[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
-    const floatx16 zero = {};
     issue(0, 0);
-    stage_barrier();
+    copies_barrier();
     for (int s = 0; s < nstage; ++s) {
         if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
-        const half8 *sb = sbuf + (s & 1) * STAGE_H8;
-        static_for<0, STAGE_TILES>([&](auto uc) {
-            constexpr int u = decltype(uc)::value;
-            half8 a[DB16_GROUPS];
-            const half8 *p = sb + u * TILE_H8 + lane;
-#pragma unroll
-            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
-            floatx16 acc[NS];
-            static_for<0, NS>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                if constexpr (bal_on(G, W, k, u))
-                    acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[k][0], zero, 0, 0, 0);
-            });
-#pragma unroll
-            for (int m = 1; m < MFMA16; ++m)
-                static_for<0, NS>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    if constexpr (bal_on(G, W, k, u))
-                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[k][mfma_b(m)],
-                                                                         acc[k], 0, 0, 0);
-                });
-            // running minimum: 8 v_min3_f32 per accumulator, dependency depth 3
-            static_for<0, NS>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                if constexpr (bal_on(G, W, k, u)) {
-                    const floatx16 &x = acc[k];
-                    const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
-                    const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
-                    const float t4 = fminf(fminf(x[12], x[13]), x[14]);
-                    const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
-                    mn[k] = fminf(fminf(mn[k], u0), u1);
-                }
-            });
-        });
-        const int done = (s + 1) * STAGE_TILES;
-        if (done % tps == 0) {   // segment done / tps - 1 of the chunk closed
-            int *sm = smin + (done / tps - 1) * (G * 32);
-#pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                // the two lane halves hold different rows of the same queries
-                const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
-                if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
-                mn[k] = FLT_MAX;
-            }
-        }
-        stage_barrier();   // stage s+1 landed and stage s is free again
+        expand_groups<W, 0, DB16_GROUPS>(wbuf + (s & 1) * WIN_B, E, lane);
+        __syncthreads();   // the stage operand is complete
+        stage_mfma<G, W, NS>(E, bq, mn, lane);
+        stage_close<G, W, NS>(s, tps, smin, mn, lane);
+        copies_barrier();   // the operand is consumed and window s + 1 has landed
     }
 }
 
@@ -188,11 +321,45 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     }
 }
 
+template <int G>
+__global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int ch, int seg_rows,
+                                                      const half8 *__restrict__ q16, int M,
+                                                      int groups, float *__restrict__ segmin,
+                                                      long nseg) {
+    __shared__ half8 E[STAGE_H8];
+    __shared__ __attribute__((aligned(16))) char wbuf[2 * WIN_B];
+    __shared__ int smin[SPC_MAX * G * 32];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;   // uniform over the block, before any barrier
+    const int spc = ch / seg_rows;
+    for (int i = threadIdx.x; i < spc * G * 32; i += 256) smin[i] = 0x7fffffff;
+    const int nstage = ch / (STAGE_TILES * 32);
+    const int tps = seg_rows >> 5;
+    const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
+    const long crow0 = (long)chunk * ch;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) img_body<G, 0>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    else if (wv == 1) img_body<G, 1>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    else if (wv == 2) img_body<G, 2>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    else img_body<G, 3>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    __syncthreads();
+    // the chunk's minima, spc consecutive segments per query (as k_screen16)
+    const long seg0 = (long)chunk * spc;
+    const int q0 = group * G * 32;
+    for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
+        const int ql = i / spc, sg = i - ql * spc;
+        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
+    }
+}
+
 // query tiles per launch group: T tiles in ceil(T / 11) equal groups
 static inline int screen_groups(int T) { return (T + MAX_G - 1) / MAX_G; }
 
-int launch_screen16(const void *db, long nrows, const _Float16 *q16, int M, float *segmin,
-                    hipStream_t st) {
+int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16 *q16, int M,
+                    float *segmin, hipStream_t st) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -200,6 +367,7 @@ int launch_screen16(const void *db, long nrows, const _Float16 *q16, int M, floa
     IA_ARG(M > 0 && ch % (STAGE_TILES * 32) == 0 && seg_rows % (STAGE_TILES * 32) == 0 &&
                ch / seg_rows <= SPC_MAX,
            "launch_screen16: bad chunking");
+    IA_ARG(!img || db_rows_padded(nrows) == nrows, "launch_screen16: image form needs whole chunks");
     const half8 *db16 = reinterpret_cast<const half8 *>(db);
     const half8 *q = reinterpret_cast<const half8 *>(q16);
     const int T = (M + 31) / 32;
@@ -209,8 +377,12 @@ int launch_screen16(const void *db, long nrows, const _Float16 *q16, int M, floa
     IA_ARG(nb < (1L << 31), "screen grid too large");
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
-        k_screen16<GG><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M,    \
-                                                     groups, segmin, nseg);                     \
+        if (img)                                                                                \
+            k_screen16i<GG><<<(unsigned)nb, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, q, \
+                                                          M, groups, segmin, nseg);             \
+        else                                                                                    \
+            k_screen16<GG><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q,  \
+                                                         M, groups, segmin, nseg);              \
         break;
     switch (G) {
         IA_SCREEN16_CASE(1)

@@ -335,7 +335,7 @@ struct LevelRun {
                                        ws.best_local, prof ? ws.stats : nullptr, sq)))
                 return rc;
             if (e1) IA_HIP(hipEventRecord(e1, sq));
-        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, ws.qp, ws.q16, M, ws.q64, ws.nq,
+        } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, a->dbi, ws.qp, ws.q16, M, ws.q64, ws.nq,
                                       a->amax, ws.scratch, ws.best_local,
                                       prof ? ws.stats : nullptr, sq, e0, e1,
                                       (fused || (a->comm && shard_tail())) ? &fa : nullptr))) {
@@ -383,7 +383,7 @@ struct LevelRun {
             const FinishArgs fr{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg,
                                 a->s, a->im, a->dbg_px, a->dbg_dist, ws.rec_all + (long)r * M,
                                 ws.coh};
-            if ((rc = launch_match(src, sim[r].row0, sim[r].nrows, sim[r].db, ws.qp, ws.q16, M,
+            if ((rc = launch_match(src, sim[r].row0, sim[r].nrows, sim[r].db, sim[r].dbi, ws.qp, ws.q16, M,
                                    ws.q64, ws.nq, sim[r].amax, ws.scratch, ws.best_local, nullptr,
                                    sq, nullptr, nullptr, &fr)))
                 return rc;

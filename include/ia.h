@@ -93,6 +93,15 @@ size_t ia_db_bytes(long nrows);
 int ia_db_chunk_rows(long nrows);
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 void *db, float *amax, void *stream);
+/* the DB's image form: each pixel's split-f16 pair once, in images padded by
+ * reflection, plus the rows' norm slots — 59 MB instead of 940 MB at the c4 finest level; the
+ * screen builds its stages from it in LDS.  Applies when the level width and row0 are
+ * multiples of 128 and the rows fill whole chunks: ia_db_image_bytes returns 0 otherwise.
+ * Call after ia_db_build (the norm slots and amax come from it); center must be constant
+ * over k < 34 and over k >= 34 (as ia_center_fill makes it). */
+size_t ia_db_image_bytes(const IaSrcLevel *src, long row0, long nrows);
+int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                      const void *db, const float *amax, void *dbi, void *stream);
 /* per-dimension screening centre: k < 34 -> mA, k >= 34 -> mAp (host scalars). */
 int ia_center_fill(double *center, double mA, double mAp, void *stream);
 
@@ -133,6 +142,8 @@ typedef struct {
     double *dist;              /* out M                                    */
     void *workspace;
     const IaLsh *lsh;          /* NULL: exact matcher                      */
+    const void *dbi;           /* NULL, or ia_db_build_image output: the screen streams the
+                                  image form instead of the rows (same results)  */
 } IaMatchArgs;
 size_t ia_match_workspace_bytes(int M, long nrows);
 int ia_match_batch(const IaMatchArgs *a, void *stream);
@@ -180,6 +191,8 @@ typedef struct {
      * candidate}; dbg_dist: H*W x 2 fp64 {d_app, d_coh} (zeros without a candidate) */
     int32_t *dbg_px;
     double *dbg_dist;
+    const void *dbi;    /* NULL, or this shard's ia_db_build_image output (the screen's DB
+                           stream; same results) */
 } IaSynthArgs;
 #define IA_SYNTH_EAGER 1
 #define IA_SYNTH_PROF 2

@@ -24,6 +24,10 @@ int ia_diag_query_rows16(const double *q64, int M, const double *center, const f
  * minima segmin[M][nseg] (screen units; nseg = ia_db_rows_padded / segment rows) */
 int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *segmin,
                      void *stream);
+/* the same screen streaming the DB's image form (ia_db_build_image) of rows
+ * [row0, row0 + nrows) of src: the same minima bit for bit */
+int ia_diag_screen16_image(const IaSrcLevel *src, long row0, long nrows, const void *dbi,
+                           const void *q16, int M, float *segmin, void *stream);
 /* exact stage form for this process: 0 one workgroup per query (k_rescore), 1 the work list
  * (k_select / k_items / k_gather), -1 the default (work list above 2^20 rows); other values
  * leave it; returns the previous value */
@@ -46,6 +50,7 @@ typedef struct {
     const void *db;
     long row0, nrows;
     const float *amax;
+    const void *dbi;    /* NULL or the shard's image form */
 } IaShardDb;
 int ia_diag_synth_level_shards(const IaSynthArgs *a, const IaShardDb *shards, int n,
                                void *stream);

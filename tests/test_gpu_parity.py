@@ -395,7 +395,8 @@ def test_sharded_reduction_with_the_real_kernels(gpu, G):
         call = ia._LevelCall(level, L, full, B_d[level - 1], B_d[level], Bp_d[level - 1],
                              Bp_d[level], wd, 3.0)
         arr = (_ia.IaShardDb * G)(*[_ia.IaShardDb(_ia.ptr(x.db).value, x.row0, x.nrows,
-                                                  _ia.ptr(x.amax).value) for x in shards])
+                                                  _ia.ptr(x.amax).value, x.dbi_ptr())
+                                    for x in shards])
         _ia.check(_ia.lib().ia_diag_synth_level_shards(ctypes.byref(call.args), arr, G,
                                                         _ia.stream()),
                   'ia_diag_synth_level_shards')

@@ -1,6 +1,7 @@
 """The split-f16 screen on the GPU: its segment minima stay inside the
 error bound eps16 the exact stage relies on (every block shape of the launcher), and the
 matcher / synthesis built on it stay bit-exact with either form of the exact stage."""
+import ctypes
 import math
 
 import numpy as np
@@ -88,10 +89,18 @@ def _screen_vs_fp64(idx, As, Q, Ms):
         E = np.concatenate([E, np.repeat(E[-1:], npad - N, 0)])      # padding repeats the last row
         exact[m0:m0 + 64] = E.reshape(nseg, seg, -1).min(axis=1).T
     worst = 0.0
+    seg_img = torch.empty_like(segmin)
     for M in Ms:
         segmin.fill_(float('nan'))
         _ia.check(lib.ia_diag_screen16(_ia.ptr(idx.db), N, _ia.ptr(q16), M, _ia.ptr(segmin), st),
                   'ia_diag_screen16')
+        if idx.dbi is not None:      # the image-form stream: the same minima bit for bit
+            seg_img.fill_(float('nan'))
+            _ia.check(lib.ia_diag_screen16_image(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.dbi),
+                                                 _ia.ptr(q16), M, _ia.ptr(seg_img), st),
+                      'ia_diag_screen16_image')
+            torch.cuda.synchronize()
+            assert torch.equal(seg_img[:M].view(torch.int32), segmin[:M].view(torch.int32)), M
         torch.cuda.synchronize()
         got = segmin[:M].cpu().numpy().astype(np.float64)
         assert np.isfinite(got).all(), M
@@ -120,7 +129,8 @@ def test_split16_screen_every_query_split(gpu):
     """k_screen16 at query counts that hit every block shape (G = 1..11 query tiles, and
     launches of more than 11 tiles split into equal groups) on a 1M-row level (8192-row
     chunks: 16 segments per chunk, many stages): every segment minimum within eps16 of
-    the fp64 value."""
+    the fp64 value, and the image-form stream (k_screen16i) gives the same minima bit for
+    bit."""
     import algorithms
     A, Aps, _ = analogy_inputs(45, (1024, 1024), (8, 8), n_ap=1)
     A_pyr = o.compute_gaussian_pyramid(A, 3, cap=2)
@@ -132,6 +142,7 @@ def test_split16_screen_every_query_split(gpu):
     Q = np.vstack([As[rs.randint(0, len(As), 400)] + rs.randn(400, 55) * 0.01,
                    rs.rand(300, 55)])
     Ms = [1, 20, 64, 65, 100, 128, 160, 192, 224, 256, 288, 320, 342, 353, 500, 700]
+    assert idx.dbi is not None                # 1024 wide: the image form applies
     worst = _screen_vs_fp64(idx, As, Q, Ms)
     print('split16 screen (1M rows): worst |segmin - exact| / eps16 = %.3g' % worst)
     assert worst < 1.0
@@ -193,6 +204,26 @@ def graph():
     prev = _ia.graph_mode()
     yield _ia.graph_mode
     _ia.graph_mode(prev)
+
+
+@pytest.mark.parametrize('image', [True, False])
+def test_synthesis_with_image_form_db(gpu, monkeypatch, image):
+    """A 128 x 256 analogy (two A' images; levels of width 256 and 128 take the DB's image
+    form, the 64-wide coarsest level the row form): B', s and im equal the oracle's with the
+    image form on and off."""
+    import image_analogies as ia
+    monkeypatch.setenv('IA_DB_IMAGE', '1' if image else '0')
+    A, Aps, B = analogy_inputs(48, (128, 256), (64, 128), n_ap=2)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=48, cap=3)
+    w = o.compute_weights(3, 5, 12, 1)
+    ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 1.0, w)
+    Bp_dev = [dev(b) for b in Bp_pyr]
+    out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                            [dev(p) for p in B_pyr], Bp_dev, L, 1.0, w)
+    for l in ref:
+        assert np.array_equal(out[l][0].cpu().numpy(), ref[l][1]), l
+        assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
+        assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l
 
 
 @pytest.mark.parametrize('gmode', [0, 2])

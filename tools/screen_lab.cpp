@@ -7,13 +7,16 @@
 //   6  loads re-read the chunk's first two stages (L2-resident: the issue cost without HBM)
 //   7  plain loads (cache policy 0)          8  sc1 loads          9  sc0 loads
 //  10  the next stage's 7 loads interleaved with the first tile's MFMAs (one per MFMA)
+//  20  the DB stream from per-pixel split images expanded in LDS (W % 128 == 0)
 //  14, 15, 16  persistent 512 / 256 / 1024 blocks pulling 2048-row chunks from a queue
 //  11, 12, 13  variants 0, 1, 6 with s_memtime / s_memrealtime stamps around each block's
 //      loop (wave 0): prints the median in-kernel clock and the MFMA share of its cycles
 // Prints per-variant median time and whether its minima equal the library screen's
 // (variants 0 and 5 must; the others are timing probes).
 //
-//   screen_lab [--M 342] [--reps 5] [--rounds 5] [--V 0,1,2,3,4,5]
+//   screen_lab [--M 342] [--reps 5] [--rounds 5] [--V 0,1,2,3,4,5] [--gap 1]
+// (--gap 1: each screen launch is followed by a per-query scan kernel, and the time per
+// launch pair is reported)
 #include "screen_setup.h"
 
 #include <float.h>
@@ -385,6 +388,267 @@ static void launch_q(const ScreenSetup &su, int M, float *out, int nblocks) {
     CK(hipGetLastError());
 }
 
+
+// ---- variant 20: the DB stream from per-pixel split images ------------------------------
+// A row's 55 features are its neighbours' pixels, so the stage (128 consecutive pixels of
+// one scanline; W % 128 == 0) is built in LDS from image windows: fine rows y-2..y+2 of A,
+// y-2..y of A' (136 padded columns), coarse rows of both (72), and the stage's 128 norm
+// slots, each pixel stored once as its (hi, lo) f16 pair (4 B), the images padded by
+// reflection so every window row is one contiguous run.  6.6 KB per stage instead of 28 KB.
+constexpr int WF_PC = 34, WC_PC = 18;                        // 16-B pieces per window row
+constexpr int WB_FINE = 8 * WF_PC * 16, WB_COARSE = 6 * WC_PC * 16, WB_NORM = 128 * 4;
+constexpr int WIN_B = WB_FINE + WB_COARSE + WB_NORM;         // 6592
+constexpr int WIN_PIECES = WIN_B / 16;                       // 412
+static_assert(WIN_PIECES <= 512, "two wave-instructions per wave stage the window");
+
+struct ImgDb {
+    const uint32_t *fa, *fp, *ca, *cp, *norm;
+    int W, Wp, Wcp;       // image width, padded fine / coarse widths
+};
+
+// constant byte offset of feature k's (hi) value in the window, and whether its lane term is
+// the pixel (fine) or pixel / 2 (coarse)
+__host__ __device__ constexpr int win_off(int k) {
+    return k < 9 ? WB_FINE + (k / 3) * WC_PC * 16 + (k % 3 + 3) * 4
+         : k < 34 ? ((k - 9) / 5) * WF_PC * 16 + ((k - 9) % 5 + 2) * 4
+         : k < 43 ? WB_FINE + (3 + (k - 34) / 3) * WC_PC * 16 + ((k - 34) % 3 + 3) * 4
+         : k < 55 ? (5 + (k - 43) / 5) * WF_PC * 16 + ((k - 43) % 5 + 2) * 4
+         : WB_FINE + WB_COARSE;
+}
+__host__ __device__ constexpr bool win_coarse(int k) { return k < 9 || (k >= 34 && k < 43); }
+
+template <int G, int W>
+__device__ __forceinline__ void img_body(ImgDb im, half8 *E, char *wbuf, int *smin, long crow0,
+                                         int nstage, int tps, const half8 *__restrict__ q16) {
+    constexpr int T0 = bal_t0(G, W), NS = bal_ns(G, W);
+    constexpr int H = W & 1;                    // this wave expands lane half H of 2 tiles
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int j = lane & 31, h = lane >> 5;
+    half8 bq[NS][Q16_GROUPS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const half8 *p = q16 + (long)((T0 + k) * 32 + j) * Q16_ROW + h * Q16_GROUPS;
+#pragma unroll
+        for (int m = 0; m < Q16_GROUPS; ++m) bq[k][m] = p[m];
+    }
+    auto issue = [&](int s, int buf) {
+        const long row0 = crow0 + (long)s * 128;
+        const int y = (int)(row0 / im.W), x0 = (int)(row0 - (long)y * im.W);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            if (t == 1 && W == 3) continue;     // pieces 448.. are past the window
+            const int i = (t * 4 + W) * 64 + lane;
+            const uint32_t *src;
+            if (i < 8 * WF_PC) {
+                const int r = i / WF_PC, pc = i - r * WF_PC;
+                src = (r < 5 ? im.fa + (long)(y + r) * im.Wp : im.fp + (long)(y + r - 5) * im.Wp) + x0 + 4 * pc;
+            } else if (i < 8 * WF_PC + 6 * WC_PC) {
+                const int q = i - 8 * WF_PC, r = q / WC_PC, pc = q - r * WC_PC;
+                src = (r < 3 ? im.ca + (long)((y >> 1) + 1 + r) * im.Wcp
+                             : im.cp + (long)((y >> 1) + r - 2) * im.Wcp) + (x0 >> 1) + 4 * pc;
+            } else {
+                src = im.norm + row0 + 4 * (i - 8 * WF_PC - 6 * WC_PC);
+            }
+            if (i < WIN_PIECES)
+                __builtin_amdgcn_global_load_lds((const void *)src,
+                                                 (void *)(wbuf + buf * WIN_B + (t * 4 + W) * 1024),
+                                                 16, 0, 2);
+        }
+    };
+    auto wait_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    float mn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    const floatx16 zero = {};
+    // expansion slot of this thread: tile u = 2 (W >> 1) + lane / 32, row j, half H
+    const int px = 32 * (2 * (W >> 1) + h) + j;
+    issue(0, 0);
+    wait_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        {   // expand the window into the stage's MFMA operand layout
+            const char *wb = wbuf + (s & 1) * WIN_B;
+            const char *bf = wb + px * 4, *bc = wb + (px >> 1) * 4;
+            half8 *e = E + (2 * (W >> 1) + h) * (DB16_GROUPS * 64) + H * 32 + j;
+            static_for<0, DB16_GROUPS>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                constexpr int k0 = H == 0 ? (g < 4 ? 8 * g : 8 * (g - 4)) : (g < 3 ? 32 + 8 * g : (g == 3 ? 24 : 32 + 8 * (g - 4)));
+                constexpr bool hi = H == 0 ? g < 4 : g < 3;
+                half8 o;
+                static_for<0, 8>([&](auto ec) {
+                    constexpr int k = k0 + decltype(ec)::value;
+                    constexpr int off = win_off(k) + (hi ? 0 : 2);
+                    const char *b = k == 55 ? wb + px * 4 : (win_coarse(k) ? bc : bf);
+                    o[decltype(ec)::value] = *reinterpret_cast<const _Float16 *>(b + off);
+                });
+                e[g * 64] = o;
+            });
+        }
+        __syncthreads();   // the stage operand is complete
+        static_for<0, STAGE_TILES>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            half8 a[DB16_GROUPS];
+            const half8 *p = E + u * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[g] = p[g * 64];
+            floatx16 acc[NS];
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u))
+                    acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bq[k][0], zero, 0, 0, 0);
+            });
+#pragma unroll
+            for (int m = 1; m < MFMA16; ++m)
+                static_for<0, NS>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (bal_on(G, W, k, u))
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[mfma_a(m)], bq[k][mfma_b(m)],
+                                                                         acc[k], 0, 0, 0);
+                });
+            static_for<0, NS>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if constexpr (bal_on(G, W, k, u)) {
+                    const floatx16 &x = acc[k];
+                    const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+                    const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+                    const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+                    const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+                    mn[k] = fminf(fminf(mn[k], u0), u1);
+                }
+            });
+        });
+        const int done = (s + 1) * STAGE_TILES;
+        if (done % tps == 0) {
+            int *sm = smin + (done / tps - 1) * (G * 32);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
+                if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
+                mn[k] = FLT_MAX;
+            }
+        }
+        wait_barrier();   // the operand is consumed and window s + 1 has landed
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(256, 2) void k_lab_img(ImgDb im, int nchunks, int ch, int seg_rows,
+                                                    const half8 *__restrict__ q16, int M, int groups,
+                                                    float *__restrict__ segmin, long nseg) {
+    __shared__ half8 E[STAGE_H8];
+    __shared__ __attribute__((aligned(16))) char wbuf[2 * WIN_B];
+    __shared__ int smin[SPC_MAX * G * 32];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;
+    const int spc = ch / seg_rows;
+    for (int i = threadIdx.x; i < spc * G * 32; i += 256) smin[i] = 0x7fffffff;
+    const int nstage = ch / 128;
+    const int tps = seg_rows >> 5;
+    const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
+    const long crow0 = (long)chunk * ch;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) img_body<G, 0>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    else if (wv == 1) img_body<G, 1>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    else if (wv == 2) img_body<G, 2>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    else img_body<G, 3>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    __syncthreads();
+    const long seg0 = (long)chunk * spc;
+    const int q0 = group * G * 32;
+    for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
+        const int ql = i / spc, sg = i - ql * spc;
+        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
+    }
+}
+
+static ImgDb g_img;
+static inline int symi_h(int i, int n) {
+    const int p = 2 * n; i %= p; if (i < 0) i += p; return i >= n ? p - 1 - i : i;
+}
+static uint32_t split_pack(float v) {
+    const _Float16 hi = (_Float16)v;
+    const _Float16 lo = (_Float16)(v - (float)hi);
+    uint16_t a, b;
+    memcpy(&a, &hi, 2); memcpy(&b, &lo, 2);
+    return (uint32_t)a | ((uint32_t)b << 16);
+}
+// the image-form DB of the harness level: padded split images + per-row norm slots
+static void build_img(const ScreenSetup &su) {
+    int e = su.amax > 0.f ? ilogbf(su.amax) : 0;
+    e = e < -60 ? -60 : (e > 60 ? 60 : e);
+    const int ea = 13 - e, R = e + 1;
+    const int H = su.H, W = su.W, hs = su.hs, ws = su.ws;
+    const int Wp = W + 8, Hp = H + 4, Wcp = ws + 8, Hcp = hs + 4;
+    auto pad = [&](const std::vector<double> &img, int h, int w, int hp, int wp, double c) {
+        std::vector<uint32_t> o((size_t)hp * wp);
+        for (int r = 0; r < hp; ++r)
+            for (int q = 0; q < wp; ++q)
+                o[(size_t)r * wp + q] = split_pack(ldexpf((float)(img[(size_t)symi_h(r - 2, h) * w + symi_h(q - 4, w)] - c), ea));
+        return o;
+    };
+    std::vector<uint32_t> fa = pad(su.A, H, W, Hp, Wp, su.mA), fp = pad(su.Ap, H, W, Hp, Wp, su.mAp);
+    std::vector<uint32_t> ca = pad(su.Asm, hs, ws, Hcp, Wcp, su.mA), cp = pad(su.Apsm, hs, ws, Hcp, Wcp, su.mAp);
+    std::vector<uint32_t> nr((size_t)su.npad);
+    for (long ix = 0; ix < su.npad; ++ix) {
+        const long ixe = ix < su.N ? ix : su.N - 1;
+        const int r = (int)(ixe / W), c = (int)(ixe % W);
+        double n2 = 0.0;
+        auto add = [&](double v, double cc) { const double d = v - cc; n2 += d * d; };
+        for (int t = 0; t < 9; ++t) add(su.Asm[(size_t)symi_h(r / 2 + t / 3 - 1, hs) * ws + symi_h(c / 2 + t % 3 - 1, ws)], su.mA);
+        for (int t = 0; t < 25; ++t) add(su.A[(size_t)symi_h(r + t / 5 - 2, H) * W + symi_h(c + t % 5 - 2, W)], su.mA);
+        for (int t = 0; t < 9; ++t) add(su.Apsm[(size_t)symi_h(r / 2 + t / 3 - 1, hs) * ws + symi_h(c / 2 + t % 3 - 1, ws)], su.mAp);
+        for (int t = 0; t < 12; ++t) add(su.Ap[(size_t)symi_h(r + t / 5 - 2, H) * W + symi_h(c + t % 5 - 2, W)], su.mAp);
+        nr[ix] = split_pack(ldexpf((float)n2, ea - R));
+    }
+    auto up = [&](const std::vector<uint32_t> &v) {
+        uint32_t *d; CK(hipMalloc(&d, v.size() * 4 + 64));
+        CK(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+        return (const uint32_t *)d;
+    };
+    g_img = ImgDb{up(fa), up(fp), up(ca), up(cp), up(nr), W, Wp, Wcp};
+    printf("image-form DB: %.1f MB (row form %.1f MB)\n",
+           (2.0 * fa.size() + 2.0 * ca.size() + nr.size()) * 4 / 1e6, su.npad * 224 / 1e6);
+}
+
+static void launch_img(const ScreenSetup &su, int M, float *out) {
+    const int ch = ia_db_chunk_rows(su.N);
+    const long nchunks = su.npad / ch;
+    const int seg_rows = ch < 512 ? ch : 512;
+    const int T = (M + 31) / 32;
+    const int groups = (T + 10) / 11;
+    const int G = (T + groups - 1) / groups;
+    const long nb = ((nchunks + 7) / 8) * 8 * groups;
+    const half8 *q = reinterpret_cast<const half8 *>(su.q16);
+    switch (G) {
+        case 11: k_lab_img<11><<<(unsigned)nb, 256, 0, su.st>>>(g_img, (int)nchunks, ch, seg_rows, q, M, groups, out, su.nseg); break;
+        case 8: k_lab_img<8><<<(unsigned)nb, 256, 0, su.st>>>(g_img, (int)nchunks, ch, seg_rows, q, M, groups, out, su.nseg); break;
+        default: fprintf(stderr, "lab img: G=%d not instantiated\n", G); exit(1);
+    }
+    CK(hipGetLastError());
+}
+
+// --gap: after every screen launch, a latency-bound per-query pass over its minima (one
+// workgroup per query, like the exact stage's segment scan), so launches alternate as in
+// the synthesis wave loop instead of running back to back
+__global__ __launch_bounds__(256) void k_scan(const float *__restrict__ segmin, long nseg,
+                                              float *__restrict__ out) {
+    __shared__ float red[4];
+    float m = FLT_MAX;
+    for (long i = threadIdx.x; i < nseg; i += 256) m = fminf(m, segmin[blockIdx.x * nseg + i]);
+    for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+}
+static int g_gap = 0;
+static float *g_scan_out;
+
 static unsigned long long *g_stamps;
 static void run(int V, const ScreenSetup &su, int M, float *out) {
     switch (V) {
@@ -405,26 +669,35 @@ static void run(int V, const ScreenSetup &su, int M, float *out) {
         case 14: launch_q(su, M, out, 512); break;
         case 15: launch_q(su, M, out, 256); break;
         case 16: launch_q(su, M, out, 1024); break;
+        case 20: launch_img(su, M, out); break;
         default: fprintf(stderr, "bad variant %d\n", V); exit(1);
+    }
+    if (g_gap) {
+        k_scan<<<M, 256, 0, su.st>>>(out, su.nseg, g_scan_out);
+        CK(hipGetLastError());
     }
 }
 
 int main(int argc, char **argv) {
     int reps = 5, rounds = 5;
-    std::vector<int> Ms = {342}, Vs = {0, 14, 15, 16, 0, 14};
+    std::vector<int> Ms = {342}, Vs = {0, 20, 0, 20};
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--M")) Ms = parse_list(argv[i + 1]);
         else if (!strcmp(argv[i], "--V")) Vs = parse_list(argv[i + 1]);
         else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--rounds")) rounds = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "--gap")) g_gap = atoi(argv[i + 1]);
     }
     int Mmax = 0; for (int m : Ms) Mmax = std::max(Mmax, m);
     const ScreenSetup su = make_setup(2048, Mmax);
+    CK(hipMalloc(&g_scan_out, sizeof(float) * 4096));
     float *lab;
     CK(hipMalloc(&lab, sizeof(float) * (size_t)su.qrows * su.nseg));
     const long nblk_max = 1 << 16;
     CK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4 * nblk_max));
     CK(hipMalloc(&g_ctr, 2 * sizeof(int)));
+    for (int V : Vs)
+        if (V == 20) { build_img(su); break; }
     CK(hipMemset(g_ctr, 0, 2 * sizeof(int)));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int M : Ms) {

@@ -49,6 +49,12 @@ struct ScreenSetup {
     void *db, *q16;
     float *segmin;
     hipStream_t st;
+    // host copies of the level (for harness-side layouts): fine A, A' (H x W), coarse
+    // (hs x ws), the centre values and the split bound
+    int H, W, hs, ws;
+    std::vector<double> A, Ap, Asm, Apsm;
+    double mA, mAp;
+    float amax;
 };
 
 static void box_blur(std::vector<double> &img, int H, int W, int r) {
@@ -137,5 +143,7 @@ static ScreenSetup make_setup(int S, int Mmax) {
     const long nseg = npad / (ch < 512 ? ch : 512);
     float *segmin;
     CK(hipMalloc(&segmin, sizeof(float) * (size_t)qrows * nseg));
-    return ScreenSetup{N, npad, nseg, ch, qrows, db, q16, segmin, st};
+    float amax_h; CK(hipMemcpy(&amax_h, amax, sizeof(float), hipMemcpyDeviceToHost));
+    return ScreenSetup{N, npad, nseg, ch, qrows, db, q16, segmin, st, H, W, hs, ws,
+                       A, Ap, Asm, Apsm, means[0], means[1], amax_h};
 }
