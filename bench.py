@@ -509,7 +509,10 @@ def main():
     traffic, pmc = None, screen_pmc()
     if pmc and args.config == 'c4' and world == 1 and domG == 11 and lsh is None:
         traffic = pmc['bytes']
-    roof = {'bound': 'mfma', 'kernel': 'k_screen16<%s>' % domG, 'achieved': achieved,
+    # the finest level's screen streams the DB's image form when it applies (k_screen16i)
+    img_form = _ia.db_image_enabled() and jobs[0].A.shape[1] % 128 == 0 and lsh is None
+    roof = {'bound': 'mfma', 'kernel': ('k_screen16i<%s>' if img_form else 'k_screen16<%s>') % domG,
+            'achieved': achieved,
             'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
             'frac': achieved / F16_MFMA_PEAK_TFLOPS, 'traffic': traffic,
             'algorithmic': '%d f16 flop per (query,row) pair; %d launches, %.4g pairs (mean M '
@@ -528,10 +531,11 @@ def main():
                            'fp32_equivalent_tflops':
                                2.0 * 55 * pairs / (screen_ms * 1e-3) / 1e12 if screen_ms else 0.0}}
     if traffic is not None:
-        roof['traffic_note'] = ('HBM bytes per launch (mean of %d dispatches), PMC FETCH_SIZE x 2 '
-                                '+ WRITE_SIZE of bench.py under rocprofv3 (%s); algorithmic: the '
-                                '939.5 MB split-f16 DB read once + 11 MB of segment minima'
-                                % (pmc['dispatches'], pmc['source']))
+        roof['traffic_note'] = ('HBM bytes per launch (mean of %d dispatches of %s), PMC FETCH_SIZE '
+                                'x 2 + WRITE_SIZE of bench.py under rocprofv3 (%s); algorithmic: '
+                                'the DB read once (image form: 59 MB of split pixel pairs and '
+                                'norm slots; row form: 939.5 MB) + 11 MB of segment minima'
+                                % (pmc['dispatches'], pmc['kernel'], pmc['source']))
     if lsh is not None:
         # k_lsh_query is a gather: each examined row costs its 55 fp64 features (440 B)
         examined = sum(p['rows_rescored'] for p in prof if p['timed_screens'])

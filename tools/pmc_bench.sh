@@ -7,6 +7,8 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out/pmc_bench
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+# a stream sync every 64 waves: rocprofv3 --pmc crashes with thousands of dispatches in flight
+export IA_SYNC_EVERY=${IA_SYNC_EVERY:-64}
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv -d "$OUT/$C" -o p -- \
       python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS} > "$OUT/$C.json" 2> "$OUT/$C.err"
