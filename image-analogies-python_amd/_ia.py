@@ -98,6 +98,17 @@ _SIGS = {
     'ia_synth_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long,
                                                    ctypes.c_int]),
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_synth_level3': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_synth3_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long]),
+    'ia_db3_bytes': (ctypes.c_size_t, [ctypes.c_long]),
+    'ia_match3_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_long]),
+    'ia_match3_batch': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp, _dp, _dp]),
+    'ia_coherence_pick3': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp]),
+    'ia_wdist3_batch': (ctypes.c_int, [_dp, _dp, _dp, ctypes.c_int, _dp, _dp]),
+    'ia_db3_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp,
+                                    _dp]),
+    'ia_level_features3_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, _dp, _dp]),
     'ia_synth_levels': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
     'ia_lsh_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp,

@@ -34,16 +34,28 @@ def level_features_dev(sm, lg, full_feat):
     return out
 
 
+def level_features3_dev(sm, lg, full_feat):
+    """One level of compute_feature_array for 3-channel images (h, w, 3): (h*w, 102 or
+    63) fp64, windows flattened (row, col, channel)."""
+    hs, ws = sm.shape[:2]
+    h, w = lg.shape[:2]
+    out = torch.empty((h * w, 102 if full_feat else 63), dtype=torch.float64, device=lg.device)
+    _ia.check(_ia.lib().ia_level_features3_f64(_ia.ptr(sm.contiguous()), hs, ws,
+                                               _ia.ptr(lg.contiguous()), h, w,
+                                               1 if full_feat else 0, _ia.ptr(out),
+                                               _ia.stream()), 'ia_level_features3_f64')
+    return out
+
+
 def compute_feature_array(im_pyr, c, full_feat):
     """Per-level [3x3 coarse | 5x5 (or half) fine] neighbourhood rows
-    (algorithms.py:11-47); entry 0 is an empty placeholder as in the reference."""
-    if np.asarray(im_pyr[0]).ndim != 2:
-        raise NotImplementedError('multi-channel features are not supported by this build '
-                                  '(luminance / YIQ matching only)')
+    (algorithms.py:11-47), 1 or 3 channels; entry 0 is an empty placeholder as in the
+    reference."""
     dev = [_ia.to_dev(p) for p in im_pyr]
+    fn = level_features3_dev if dev[0].dim() == 3 else level_features_dev
     feats = [[]]
     for level in range(1, len(im_pyr)):
-        feats.append(level_features_dev(dev[level - 1], dev[level], full_feat).cpu().numpy())
+        feats.append(fn(dev[level - 1], dev[level], full_feat).cpu().numpy())
     return feats
 
 
@@ -172,8 +184,53 @@ class LevelIndex:
         return torch.cat(rows, 0)
 
 
+class LevelIndex3:
+    """As[level] for 3-channel images (num_ch = 3): the materialised fp64 rows
+    [A full | A'_i half], 165 values each (ia_db3_build), searched exhaustively in fp64
+    (ia_match3_batch) — exact like LevelIndex."""
+
+    def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg):
+        self.A_sm, self.A_lg = A_sm.contiguous(), A_lg.contiguous()
+        self.Ap_sm, self.Ap_lg = Ap_sm.contiguous(), Ap_lg.contiguous()
+        src = _ia.IaSrcLevel()
+        src.A_sm, src.A_lg, src.Ap_sm, src.Ap_lg = (_ia.ptr(self.A_sm).value, _ia.ptr(self.A_lg).value,
+                                                    _ia.ptr(self.Ap_sm).value, _ia.ptr(self.Ap_lg).value)
+        src.A_hs, src.A_ws = self.A_sm.shape[:2]
+        src.Ah, src.Aw = self.A_lg.shape[:2]
+        src.nAp = self.Ap_lg.shape[0]
+        self.src = src
+        self.N = int(src.nAp * src.Ah * src.Aw)
+        self.shape = (self.N, 165)
+        lib = _ia.lib()
+        self.db3 = torch.empty(lib.ia_db3_bytes(self.N) // 8, dtype=torch.float64,
+                               device=A_lg.device)
+        _ia.check(lib.ia_db3_build(ctypes.byref(src), 0, self.N, _ia.ptr(self.db3), _ia.stream()),
+                  'ia_db3_build')
+        self.lsh = None
+
+    def match(self, Q, exact=None):
+        """1-NN rows (global index, fp64 distance) of queries Q (M x 165)."""
+        dev = self.A_lg.device
+        Q = torch.as_tensor(Q, dtype=torch.float64)
+        if Q.dim() == 1:
+            Q = Q[None]
+        Q = Q.to(dev).contiguous()
+        M = Q.shape[0]
+        idx = torch.empty(M, dtype=torch.int64, device=dev)
+        dist = torch.empty(M, dtype=torch.float64, device=dev)
+        ws = _ia.workspace(_ia.lib().ia_match3_workspace_bytes(M, self.N))
+        _ia.check(_ia.lib().ia_match3_batch(_ia.ptr(self.db3), self.N, _ia.ptr(Q), M, _ia.ptr(idx),
+                                            _ia.ptr(dist), _ia.ptr(ws), _ia.stream()),
+                  'ia_match3_batch')
+        return idx, dist
+
+    def features(self):
+        """The full fp64 As[level] matrix (N x 165)."""
+        return self.db3.view(self.N, 168)[:, :165]
+
+
 class _LazyAs(list):
-    """``As`` of the reference: As[level] is the (N, 55) fp64 feature matrix.  Levels are
+    """``As`` of the reference: As[level] is the (N, 55) (3 channels: 165) fp64 feature matrix.  Levels are
     materialised from the device index only when a caller indexes them."""
 
     def __init__(self, index):
@@ -216,7 +273,15 @@ def create_index(A_pyr, Ap_pyr_list, c):
     A_dev = [_ia.to_dev(p) for p in A_pyr]
     Ap_dev = [[_ia.to_dev(p) for p in pyr] for pyr in Ap_pyr_list]
     lsh = lsh_params(c)
-    index = create_index_dev(A_dev, Ap_dev, c.max_levels, lsh=lsh)
+    if A_dev[0].dim() == 3:      # 3 channels: materialised rows, exact search
+        if lsh is not None:
+            raise NotImplementedError('3-channel matching runs with the exact matcher only')
+        index = [None] + [LevelIndex3(A_dev[l - 1], A_dev[l],
+                                      torch.stack([p[l - 1] for p in Ap_dev]),
+                                      torch.stack([p[l] for p in Ap_dev]))
+                          for l in range(1, c.max_levels)]
+    else:
+        index = create_index_dev(A_dev, Ap_dev, c.max_levels, lsh=lsh)
     if lsh is None:
         desc = {'algorithm': 'brute', 'exact': True, 'device': str(dev)}
     else:
@@ -274,8 +339,9 @@ def best_coherence_match(As, A_shape, BBp_feat, s, im, px, Bp_w, c):
     feats = _ia.to_dev(np.asarray(As[np.array(rows)], dtype=np.float64))
     q = _ia.to_dev(np.asarray(BBp_feat, dtype=np.float64))
     out = torch.empty(1, dtype=torch.int32, device=q.device)
-    _ia.check(_ia.lib().ia_coherence_pick(_ia.ptr(feats), len(rows), _ia.ptr(q), _ia.ptr(out),
-                                          _ia.stream()), 'ia_coherence_pick')
+    pick = _ia.lib().ia_coherence_pick3 if feats.shape[1] == 165 else _ia.lib().ia_coherence_pick
+    _ia.check(pick(_ia.ptr(feats), len(rows), _ia.ptr(q), _ia.ptr(out), _ia.stream()),
+              'ia_coherence_pick')
     (rr, cc), img = cands[int(out.item())]
     sr = s[rr * Bp_w + cc]
     return np.array([int(sr[0]) + row - rr, int(sr[1]) + col - cc]), img, np.array([rr, cc])
@@ -286,6 +352,7 @@ def compute_distance(AAp_p, BBp_q, weights):
     assert AAp_p.shape == BBp_q.shape == weights.shape
     a, q, w = (_ia.to_dev(np.asarray(x, dtype=np.float64)) for x in (AAp_p, BBp_q, weights))
     out = torch.empty(1, dtype=torch.float64, device=a.device)
-    _ia.check(_ia.lib().ia_wdist_batch(_ia.ptr(a), _ia.ptr(q), _ia.ptr(w), 1, _ia.ptr(out),
-                                       _ia.stream()), 'ia_wdist_batch')
+    fn = _ia.lib().ia_wdist3_batch if a.numel() == 165 else _ia.lib().ia_wdist_batch
+    _ia.check(fn(_ia.ptr(a), _ia.ptr(q), _ia.ptr(w), 1, _ia.ptr(out), _ia.stream()),
+              'ia_wdist_batch')
     return float(out.item())

@@ -130,6 +130,66 @@ def pipeline_default():
     return os.environ.get('IA_PIPELINE', '1') != '0'
 
 
+def _src_level3(A_sm, A_lg, Ap_sm, Ap_lg):
+    """IaSrcLevel over 3-channel device tensors (A_*: (h, w, 3); Ap_*: (nAp, h, w, 3))."""
+    src = _ia.IaSrcLevel()
+    src.A_sm, src.A_lg, src.Ap_sm, src.Ap_lg = (_ia.ptr(A_sm).value, _ia.ptr(A_lg).value,
+                                                _ia.ptr(Ap_sm).value, _ia.ptr(Ap_lg).value)
+    src.A_hs, src.A_ws = A_sm.shape[:2]
+    src.Ah, src.Aw = A_lg.shape[:2]
+    src.nAp = Ap_lg.shape[0]
+    return src
+
+
+def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels=None,
+                    debug=False):
+    """3-channel synthesis (num_ch = 3: convert=False on colour images, 165-dim rows), one
+    level at a time through ia_synth_level3: the materialised fp64 database
+    (ia_db3_build), exhaustive exact search, the coherence / kappa tail and the 3-channel
+    B' update.  Same return value as synthesize_dev."""
+    lib = _ia.lib()
+    st = _ia.stream()
+    weights = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
+    out = {}
+    for level in range(1, max_levels):
+        if levels is not None and level not in levels:
+            continue
+        A_sm, A_lg = A_pyr[level - 1].contiguous(), A_pyr[level].contiguous()
+        Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list]).contiguous()
+        Ap_lg = torch.stack([p[level] for p in Ap_pyr_list]).contiguous()
+        src = _src_level3(A_sm, A_lg, Ap_sm, Ap_lg)
+        N = src.nAp * src.Ah * src.Aw
+        dev = A_lg.device
+        db3 = torch.empty(lib.ia_db3_bytes(N) // 8, dtype=torch.float64, device=dev)
+        _ia.check(lib.ia_db3_build(ctypes.byref(src), 0, N, _ia.ptr(db3), st), 'ia_db3_build')
+        B_sm, B_lg = B_pyr[level - 1].contiguous(), B_pyr[level].contiguous()
+        Bp_sm, Bp_lg = Bp_pyr[level - 1], Bp_pyr[level]
+        assert Bp_lg.is_contiguous() and Bp_sm.is_contiguous()
+        H, W = B_lg.shape[:2]
+        s = torch.empty((H * W, 2), dtype=torch.int32, device=dev)
+        im = torch.empty(H * W, dtype=torch.int32, device=dev)
+        dbg = None
+        if debug:
+            dbg = (torch.zeros((H * W, 7), dtype=torch.int32, device=dev),
+                   torch.zeros((H * W, 2), dtype=torch.float64, device=dev))
+        ws = _ia.workspace(lib.ia_synth3_workspace_bytes(H, W, N))
+        a = _ia.IaSynthArgs()
+        a.src = src
+        a.db, a.row0, a.nrows, a.N_total = _ia.ptr(db3).value, 0, N, N
+        a.B_sm, a.B_lg = _ia.ptr(B_sm).value, _ia.ptr(B_lg).value
+        a.B_hs, a.B_ws = B_sm.shape[:2]
+        a.H, a.W = H, W
+        a.Bp_sm, a.Bp_lg = _ia.ptr(Bp_sm).value, _ia.ptr(Bp_lg).value
+        a.weights = _ia.ptr(weights).value
+        a.kappa_factor = kappa_factor(level, max_levels, k)
+        a.s, a.im, a.workspace = _ia.ptr(s).value, _ia.ptr(im).value, _ia.ptr(ws).value
+        if dbg is not None:
+            a.dbg_px, a.dbg_dist = _ia.ptr(dbg[0]).value, _ia.ptr(dbg[1]).value
+        _ia.check(lib.ia_synth_level3(ctypes.byref(a), st), 'ia_synth_level3')
+        out[level] = (s, im) if dbg is None else (s, im, dbg)
+    return out
+
+
 def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
                    comm=None, rank=0, nranks=1, prof=False, levels=None, lsh=None, eager=False,
                    pipeline=None, debug=False):
@@ -140,6 +200,11 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     pipelined).  pipeline: run the levels concurrently (ia_synth_levels; default
     pipeline_default()), else one after the other.
     Returns {level: (s, im[, debug])} device tensors."""
+    if B_pyr[-1].dim() == 3:     # 3-channel matching (num_ch = 3)
+        if comm is not None or nranks > 1 or lsh is not None:
+            raise NotImplementedError('3-channel matching runs on one GPU with the exact matcher')
+        return synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
+                               levels=levels, debug=debug)
     w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
     if pipeline is None:
         pipeline = pipeline_default() and not eager
@@ -200,9 +265,10 @@ def setup_dev(A_orig, Ap_orig_list, B_orig, c):
     Returns device (A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list) and sets c.*."""
     assert len(A_orig.shape) == len(B_orig.shape)
     if not c.convert and np.ndim(A_orig) == 3:
-        raise NotImplementedError('3-channel matching (convert=False on colour images, 165-dim '
-                                  'features) is not supported by this build yet; use '
-                                  'convert=True (YIQ luminance) or greyscale inputs')
+        if c.remap_lum:
+            raise ValueError('remap_lum requires convert (config.py:11-12)')
+        if getattr(c, 'matcher', 'brute') != 'brute':
+            raise NotImplementedError('3-channel matching runs with the exact matcher only')
     dev = _ia.require_device()
     for Ap in Ap_orig_list:
         assert A_orig.shape == Ap.shape
@@ -265,7 +331,7 @@ def color_output(level, Bp_lvl, s, im, color_pyr_list, c):
     B' and I/Q from B's pyramid (the reference takes color_pyr_list[i] with the LAST
     pixel's i; there is one colour pyramid then), clipped; otherwise the A' colour of each
     pixel's source."""
-    H, W = Bp_lvl.shape
+    H, W = Bp_lvl.shape[:2]
     if c.convert:
         yiq = torch.stack([Bp_lvl, color_pyr_list[0][level][:, :, 1], color_pyr_list[0][level][:, :, 2]], -1)
         out = torch.empty_like(yiq)

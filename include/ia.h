@@ -157,6 +157,33 @@ int ia_coherence_pick(const double *rows, int n, const double *q, int32_t *out,
 int ia_wdist_batch(const double *a, const double *q, const double *w, int n, double *out,
                    void *stream);
 
+/* ---- 3-channel matching (config.py:29-42 num_ch = 3: convert=False on colour images) ----
+ * Images are h x w x 3 fp64, channel-interleaved; IaSrcLevel / IaSynthArgs keep their
+ * meaning with every image pointer 3-channel.  Feature rows have 165 values (the reference's
+ * extract_patches_2d windows flattened (row, col, channel)); distances follow numpy's
+ * pairwise summation for n = 165.
+ * ia_db3_build: the materialised fp64 rows [A full | A'_i half] (168 doubles per row,
+ *   ia_db3_bytes) of rows [row0, row0 + nrows).
+ * ia_level_features3_f64: compute_feature_array (algorithms.py:11-47) of one level pair,
+ *   h*w x 102 (full) or x 63 (half).
+ * ia_synth_level3: one level on one GPU with the exact matcher (exhaustive fp64 search of
+ *   the materialised rows), the coherence / kappa tail and the 3-channel B' update;
+ *   a->db = ia_db3_build output over all rows; workspace of ia_synth3_workspace_bytes. */
+size_t ia_db3_bytes(long nrows);
+int ia_db3_build(const IaSrcLevel *src, long row0, long nrows, double *db3, void *stream);
+int ia_level_features3_f64(const double *sm, int hs, int ws, const double *lg, int h, int w,
+                           int full, double *out, void *stream);
+size_t ia_synth3_workspace_bytes(int H, int W, long nrows);
+/* the per-pixel API for 165-dim rows: exact 1-NN of M queries (M x 165) over the
+ * materialised rows (workspace of ia_match3_workspace_bytes), the coherence argmin over n
+ * <= 64 candidate rows (n x 165) and weighted distances (n pairs of 165-dim rows) */
+size_t ia_match3_workspace_bytes(int M, long nrows);
+int ia_match3_batch(const double *db3, long nrows, const double *q165, int M, int64_t *idx,
+                    double *dist, void *workspace, void *stream);
+int ia_coherence_pick3(const double *rows, int n, const double *q, int32_t *out, void *stream);
+int ia_wdist3_batch(const double *a, const double *q, const double *w, int n, double *out,
+                    void *stream);
+
 /* ---- a12-a15: image_analogies.py:130-220 — synthesize one pyramid level on device,
  * skewed wavefront t = x + 3y (exactly the scanline semantics).
  * B_sm/B_lg: B at levels l-1 (B_hs x B_ws) and l (H x W); Bp_sm: B' level l-1;
@@ -198,6 +225,7 @@ typedef struct {
 #define IA_SYNTH_PROF 2
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);
+int ia_synth_level3(const IaSynthArgs *a, void *stream);
 /* n consecutive levels (coarse to fine: levels[j].Bp_sm == levels[j-1].Bp_lg) at once, with
  * the same results as n ia_synth_level calls in order: each level runs on its own stream
  * and wave t of level j waits only for the waves of level j-1 its 3x3 coarse windows read

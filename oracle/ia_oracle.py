@@ -321,25 +321,28 @@ def Ap_px2ix(px, img_num, h, w):
 
 def _window(img, rows, cols, pad, k):
     """k x k window (row-major) around (rows, cols) with symmetric padding.
-    rows/cols: 1-D int arrays of centres.  Returns (len, k*k)."""
-    H, W = img.shape
+    rows/cols: 1-D int arrays of centres.  Returns (len, k*k*C), a C-channel image's
+    window flattened (row, col, channel) as extract_patches_2d + flatten do."""
+    H, W = img.shape[:2]
+    C = img.shape[2] if img.ndim == 3 else 1
     offs = np.arange(-pad, pad + 1)
     rr = sym_index(rows[:, None] + offs[None, :], H)          # (n, k)
     cc = sym_index(cols[:, None] + offs[None, :], W)          # (n, k)
-    return img[rr[:, :, None], cc[:, None, :]].reshape(len(rows), k * k)
+    return img[rr[:, :, None], cc[:, None, :]].reshape(len(rows), k * k * C)
 
 
 def level_features(img_sm, img_lg, full_feat):
     """One level of compute_feature_array (algorithms.py:11-47), 1 channel:
     row (r, c) = [3x3 of coarse at (r//2, c//2) | 5x5 of fine at (r, c)] with
     symmetric padding; half features keep the first n_half fine samples."""
-    H, W = img_lg.shape
+    H, W = img_lg.shape[:2]
+    C = img_lg.shape[2] if img_lg.ndim == 3 else 1
     rows = np.repeat(np.arange(H), W)
     cols = np.tile(np.arange(W), H)
     sm = _window(img_sm, rows // 2, cols // 2, PAD_SM, N_SM)
     lg = _window(img_lg, rows, cols, PAD_LG, N_LG)
     if not full_feat:
-        lg = lg[:, :N_HALF]
+        lg = lg[:, :N_HALF * C]                     # algorithms.py:31 c.num_ch * c.n_half
     return np.hstack([sm, lg])
 
 
@@ -373,7 +376,8 @@ def extract_pixel_feature(img_sm, img_lg, px, full_feat):
     sm = _window(img_sm, r // 2, c // 2, PAD_SM, N_SM)[0]
     lg = _window(img_lg, r, c, PAD_LG, N_LG)[0]
     f = np.hstack([sm, lg])
-    return f if full_feat else f[:N_SM * N_SM + N_HALF]
+    C = img_lg.shape[2] if img_lg.ndim == 3 else 1
+    return f if full_feat else f[:C * (N_SM * N_SM + N_HALF)]   # algorithms.py:89
 
 
 def best_coherence_match(As_level, A_shape, BBp_feat, s, im, px, Bp_w):
@@ -494,7 +498,8 @@ def setup_luminance(A, Ap_list, B, AB_weight=1, remap_lum=False, min_size=N_SM,
 def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, levels=None):
     """image_analogies.py:119-220: all levels (or the given subset), scanline order.
     Returns {level: (Bp_level, s, im)}; Bp_pyr is updated in place."""
-    weights = compute_weights(N_SM, N_LG, N_HALF, 1)
+    num_ch = A_pyr[0].shape[2] if A_pyr[0].ndim == 3 else 1     # config.py:29-42
+    weights = compute_weights(N_SM, N_LG, N_HALF, num_ch)
     As = create_index(A_pyr, Ap_pyr_list, max_levels)
     out = {}
     for level in range(1, max_levels):

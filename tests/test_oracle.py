@@ -257,3 +257,27 @@ def test_c3_fixture_reproduces_coarse_levels():
     for l, (bp, s, im) in out.items():
         assert np.array_equal(s, g['s%d' % l]) and np.array_equal(im, g['im%d' % l])
         assert hashlib.sha256(bp.tobytes()).hexdigest() == str(g['bp_sha%d' % l])
+
+
+@pytest.mark.parametrize('full', [True, False])
+def test_level_features_3ch_match_extract_patches_2d(full):
+    """The oracle's 3-channel feature rows equal the reference's construction
+    (algorithms.py:11-47): symmetric np.pad, sklearn extract_patches_2d, flatten, the
+    c.num_ch * c.n_half cut of the fine half, coarse patch at (row // 2) * ceil(w / 2) +
+    col // 2."""
+    from sklearn.feature_extraction.image import extract_patches_2d
+    rs = np.random.RandomState(5)
+    lg = rs.rand(9, 12, 3)
+    sm = rs.rand(5, 6, 3)
+    pad = lambda x, p: np.pad(x, ((p, p), (p, p), (0, 0)), mode='symmetric')  # noqa: E731
+    psm = extract_patches_2d(pad(sm, 1), (3, 3))
+    plg = extract_patches_2d(pad(lg, 2), (5, 5))
+    plg = plg.reshape(plg.shape[0], -1)
+    if not full:
+        plg = plg[:, :3 * 12]
+    h, w = lg.shape[:2]
+    ref = np.vstack([np.hstack([psm[(r // 2) * int(np.ceil(w / 2.)) + c // 2].flatten(),
+                                plg[r * w + c].flatten()])
+                     for r in range(h) for c in range(w)])
+    got = o.level_features(sm, lg, full)
+    assert got.shape == ref.shape and np.array_equal(got, ref)
