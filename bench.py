@@ -227,9 +227,15 @@ def hbm_kernels(dev, reps=20):
       yiq        ia_rgb_to_yiq, 2048x2048 uint8 RGB -> YIQ + Y fp64: 3 + 32 B/px
       pyr_reduce ia_pyr_reduce_f64 (k_init_minmax + fused k_pyr_reduce + k_pyr_clip),
                  2048^2 -> 1024^2 fp64: 8 B per input + 8 B per output pixel
-      db_build   ia_db_build (LDS-tiled k_db_norms_t + k_db_build_t), the c4 finest level, 4,194,304
-                 rows: 224 B written per row (split-f16 rows) + the fp64 pyramids read
-                 once (A, A' fine: 8 B per row each; coarse: 8 B per 4 rows each)
+      db_build   ia_db_build (k_db_range + k_db_bound + LDS-tiled k_db_build_t), the c4
+                 finest level, 4,194,304 rows: 224 B written per row (split-f16 rows) + the
+                 fp64 pyramids read once (A, A' fine: 8 B per row each; coarse: 8 B per 4
+                 rows each)
+      db_image   ia_db_build_image without a row form (what the product builds where the
+                 image form applies: k_db_range + k_db_bound + k_img_pad + the tiled norm
+                 pass), same level: the fp64 pyramids read once (20 B per row) + the padded
+                 u32 split pairs (A, A' fine: 4 B per row each; coarse: 4 B per 4 rows each)
+                 and the norm slots (4 B per row) written once: 34 B per row
     """
     import algorithms
     st = torch.cuda.current_stream(dev)
@@ -279,13 +285,21 @@ def hbm_kernels(dev, reps=20):
         'ia_pyr_reduce_f64 (k_init_minmax + fused k_pyr_reduce + k_pyr_clip) 2048^2 -> 1024^2')
     Ap_lg, Ap_sm = img[None].clone(), sm[None].clone()
     N = H * W
-    ix = algorithms.LevelIndex(sm, img, Ap_sm, Ap_lg)
+    ix = algorithms.LevelIndex(sm, img, Ap_sm, Ap_lg, rows=True)
 
     def build():
         _ia.check(lib.ia_db_build(ctypes.byref(ix.src), 0, ix.nrows, _ia.ptr(ix.center),
                                   _ia.ptr(ix.db), _ia.ptr(ix.amax), _ia.stream()), 'ia_db_build')
     put('db_build', timed(build), N * 224 + 8 * 2 * (N + 1024 * 1024),
-        'ia_db_build (LDS-tiled k_db_norms_t + k_db_build_t), 4,194,304 rows')
+        'ia_db_build (k_db_range + k_db_bound + LDS-tiled k_db_build_t), 4,194,304 rows')
+    if ix.dbi is not None:
+        def build_image():
+            _ia.check(lib.ia_db_build_image(ctypes.byref(ix.src), 0, ix.nrows, _ia.ptr(ix.center),
+                                            None, _ia.ptr(ix.amax), _ia.ptr(ix.dbi), _ia.stream()),
+                      'ia_db_build_image')
+        put('db_image', timed(build_image), N * 34,
+            'ia_db_build_image without rows (k_db_range + k_db_bound + k_img_pad + tiled norm '
+            'pass), 4,194,304 rows')
     return out
 
 

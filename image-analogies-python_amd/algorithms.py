@@ -84,12 +84,13 @@ class LevelIndex:
     """Device-resident As[level] for rows [row0, row0 + nrows) (a shard when sharded).
 
     Holds the fp64 A / A' pyramid levels (the exact rescore gathers features straight
-    from them) and the split-f16 screening database built by ia_db_build.  Centre = the means
+    from them) and the split-f16 screening database: its image form (ia_db_build_image, one
+    split pair per pixel) where the level allows it, else the 224-B rows of ia_db_build.  Centre = the means
     of A (34 A dims) and of the A' images (21 A' dims): any centre is exact for the
     distances; centring only tightens the screen's error bound.
     """
 
-    def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg, row0=0, nrows=None):
+    def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg, row0=0, nrows=None, rows=None):
         self.A_sm, self.A_lg = A_sm.contiguous(), A_lg.contiguous()
         self.Ap_sm, self.Ap_lg = Ap_sm.contiguous(), Ap_lg.contiguous()
         self.src = _ia.src_level(self.A_sm, self.A_lg, self.Ap_sm, self.Ap_lg)
@@ -104,16 +105,19 @@ class LevelIndex:
         mAp = _ia.mean_dev(self.Ap_lg)
         self.center = torch.empty(55, dtype=torch.float64, device=dev)
         _ia.check(lib.ia_center_fill(_ia.ptr(self.center), mA, mAp, st), 'ia_center_fill')
-        nbytes = lib.ia_db_bytes(self.nrows)      # split-f16 rows, 224 B each
-        self.db = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
-        _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
-                                  _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),
-                                  st), 'ia_db_build')
-        # the image form the screen streams where it applies
-        ibytes = lib.ia_db_image_bytes(ctypes.byref(self.src), self.row0, self.nrows)
-        self.dbi = None
-        if ibytes and _ia.db_image_enabled():
+        # the image form where it applies: the matcher then reads only it, and
+        # the 224-B rows are built only on request (rows=True: tests, the row-form bench leg)
+        ibytes = (lib.ia_db_image_bytes(ctypes.byref(self.src), self.row0, self.nrows)
+                  if _ia.db_image_enabled() else 0)
+        self.db = self.dbi = None
+        if rows or not ibytes:
+            nbytes = lib.ia_db_bytes(self.nrows)      # split-f16 rows, 224 B each
+            self.db = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            _ia.check(lib.ia_db_build(ctypes.byref(self.src), self.row0, self.nrows,
+                                      _ia.ptr(self.center), _ia.ptr(self.db), _ia.ptr(self.amax),
+                                      st), 'ia_db_build')
+        if ibytes:
             self.dbi = torch.empty(ibytes, dtype=torch.uint8, device=dev)
             _ia.check(lib.ia_db_build_image(ctypes.byref(self.src), self.row0, self.nrows,
                                             _ia.ptr(self.center), _ia.ptr(self.db),
@@ -245,15 +249,16 @@ class _LazyAs(list):
         return cur
 
 
-def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None):
+def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None, rows=None):
     """Device index of one level from device pyramids.  row_range(level, N) ->
     (row0, nrows) selects this rank's shard of the rows; lsh (dict of build_lsh
-    arguments) switches it to the LSH matcher."""
+    arguments) switches it to the LSH matcher; rows=True keeps the row form next to the
+    image form."""
     Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list])
     Ap_lg = torch.stack([p[level] for p in Ap_pyr_list])
     N = Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2]
     r0, nr = (0, N) if row_range is None else row_range(level, N)
-    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr)
+    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr, rows=rows)
     if lsh is not None:
         index.build_lsh(**lsh)
     return index

@@ -53,6 +53,7 @@ __device__ __forceinline__ void db_row(const DbSrc &src, long ix, const double *
 // which only widens the exact stage's thresholds by that factor.  Per-block partials go to
 // the head of the db buffer (overwritten by pass 2).
 constexpr int DBB_BLOCKS = 1024;   // partials: 64 KiB < the smallest db buffer (512 rows)
+static_assert(IMG_SCRATCH >= DBB_BLOCKS * 8 * sizeof(double), "the image form's scratch holds the partials");
 
 // Blocks are dealt to the four images in proportion to their sizes (image g gets blocks
 // [first[g], first[g + 1])); each thread keeps 8 x 16 B loads in flight per step (a loop of
@@ -247,10 +248,13 @@ __device__ __forceinline__ void db_win_features(const DbWinCtx &c, F &&f) {
 // Pass 2 (tiled): each thread splits its own row and writes its 14 half8 groups straight to
 // the MFMA operand layout ((tile, g) blocks of 64 half8, lane = h * 32 + j): for each (g, h)
 // the 32 rows of a tile write one contiguous 512 B run.
+// NORM_ONLY (the image form without a row form): only the norm slot pair, to norm[row]
+template <bool NORM_ONLY>
 __global__ __launch_bounds__(256) void k_db_build_t(DbSrc src, long row0, long nrows,
                                                     const double *__restrict__ center,
                                                     const float *__restrict__ amax,
-                                                    half8 *__restrict__ db16) {
+                                                    half8 *__restrict__ db16,
+                                                    uint32_t *__restrict__ norm) {
     __shared__ double win[DBT_TILES * WIN];
     const DbWinCtx c = db_stage(src, row0, nrows, blockIdx.x, win);
     float my[IA_DP];
@@ -262,6 +266,14 @@ __global__ __launch_bounds__(256) void k_db_build_t(DbSrc src, long row0, long n
     });
     my[55] = (float)n2;
     const Split16Db s = split16_db_scale(amax[0]);
+    if constexpr (NORM_ONLY) {   // the same pair as k_img_norm reads back from the row form
+        const long lr = (long)blockIdx.x * 256 + threadIdx.x;
+        _Float16 h, l;
+        split16f(ldexpf(my[55], s.ea - s.R), h, l);
+        if (lr < nrows)
+            norm[lr] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+        return;
+    }
     _Float16 xh[IA_DP], xl[IA_DP];
 #pragma unroll
     for (int k = 0; k < IA_DP; ++k)
@@ -472,33 +484,39 @@ int ia_diag_set_db_build_form(int tiled) {
     return prev;
 }
 
+// amax = max(amax, the bound of the level's four value ranges): k_db_range partials (part:
+// DBB_BLOCKS x 8 doubles of scratch), then k_db_bound
+static int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
+                          double *part, hipStream_t st) {
+    DbSpans sp;   // blocks per image in proportion to its size, at least one each
+    sp.x[0] = src->A_sm; sp.n[0] = d.hws;
+    sp.x[1] = src->A_lg; sp.n[1] = d.hw;
+    sp.x[2] = src->Ap_sm; sp.n[2] = (long)src->nAp * d.hws;
+    sp.x[3] = src->Ap_lg; sp.n[3] = (long)src->nAp * d.hw;
+    const long tot = sp.n[0] + sp.n[1] + sp.n[2] + sp.n[3];
+    sp.first[0] = 0;
+    for (int g = 0; g < 4; ++g) {
+        const long want = std::max<long>(1, (long)((double)(DBB_BLOCKS - 4) * sp.n[g] / tot));
+        sp.first[g + 1] = sp.first[g] + (int)want;
+    }
+    k_db_range<<<sp.first[4], 256, 0, st>>>(sp, part);
+    IA_LAUNCH_CHECK("k_db_range");
+    k_db_bound<<<1, DBB_BLOCKS, 0, st>>>(part, sp.first[4], center, amax);
+    IA_LAUNCH_CHECK("k_db_bound");
+    return IA_OK;
+}
+
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 void *db, float *amax, void *stream) {
     IA_ARG(src && center && db && amax && nrows > 0 && row0 >= 0, "ia_db_build: bad args");
     IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build: rows out of range");
     const long npad = db_rows_padded(nrows);
     DbSrc d = make_dbsrc(*src);
-    double *part = reinterpret_cast<double *>(db);   // DBB_BLOCKS x 8 doubles, < db_bytes
-    {   // blocks per image in proportion to its size, at least one each
-        DbSpans sp;
-        sp.x[0] = src->A_sm; sp.n[0] = d.hws;
-        sp.x[1] = src->A_lg; sp.n[1] = d.hw;
-        sp.x[2] = src->Ap_sm; sp.n[2] = (long)src->nAp * d.hws;
-        sp.x[3] = src->Ap_lg; sp.n[3] = (long)src->nAp * d.hw;
-        const long tot = sp.n[0] + sp.n[1] + sp.n[2] + sp.n[3];
-        sp.first[0] = 0;
-        for (int g = 0; g < 4; ++g) {
-            const long want = std::max<long>(1, (long)((double)(DBB_BLOCKS - 4) * sp.n[g] / tot));
-            sp.first[g + 1] = sp.first[g] + (int)want;
-        }
-        k_db_range<<<sp.first[4], 256, 0, S(stream)>>>(sp, part);
-        IA_LAUNCH_CHECK("k_db_range");
-        k_db_bound<<<1, DBB_BLOCKS, 0, S(stream)>>>(part, sp.first[4], center, amax);
-    }
-    IA_LAUNCH_CHECK("k_db_bound");
+    int rc = launch_db_amax(src, d, center, amax, reinterpret_cast<double *>(db), S(stream));
+    if (rc) return rc;   // partials: DBB_BLOCKS x 8 doubles, < db_bytes
     if (g_db_tiled && src->Aw % 32 == 0 && row0 % 32 == 0) {   // tiled form (npad is a multiple of 256)
-        k_db_build_t<<<(unsigned)(npad / 256), 256, 0, S(stream)>>>(d, row0, nrows, center, amax,
-                                                                    reinterpret_cast<half8 *>(db));
+        k_db_build_t<false><<<(unsigned)(npad / 256), 256, 0, S(stream)>>>(
+            d, row0, nrows, center, amax, reinterpret_cast<half8 *>(db), nullptr);
         IA_LAUNCH_CHECK("k_db_build_t");
         return IA_OK;
     }
@@ -517,13 +535,19 @@ size_t ia_db_image_bytes(const IaSrcLevel *src, long row0, long nrows) {
 }
 
 int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double *center,
-                      const void *db, const float *amax, void *dbi, void *stream) {
-    IA_ARG(src && center && db && amax && dbi && nrows > 0 && row0 >= 0, "ia_db_build_image: bad args");
+                      const void *db, float *amax, void *dbi, void *stream) {
+    IA_ARG(src && center && amax && dbi && nrows > 0 && row0 >= 0, "ia_db_build_image: bad args");
     IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build_image: rows out of range");
     ImgDb v;
     IA_ARG(img_db_layout(src->Ah, src->Aw, src->A_hs, src->A_ws, src->nAp, row0, nrows, dbi, v, nullptr),
            "ia_db_build_image: the image form needs width and row0 multiples of 128 and whole chunks");
     hipStream_t st = S(stream);
+    const DbSrc d = make_dbsrc(*src);
+    if (!db) {   // no row form: amax here, from the scratch section's partials
+        const int rc = launch_db_amax(src, d, center, amax,
+                                      reinterpret_cast<double *>(reinterpret_cast<char *>(dbi) + v.scr), st);
+        if (rc) return rc;
+    }
     auto pad = [&](const double *img, int h, int w, int wp, long n, int ck, const uint32_t *out) {
         k_img_pad<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(img, h, w, wp, n, center, ck, amax,
                                                               const_cast<uint32_t *>(out));
@@ -537,9 +561,15 @@ int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double
             f + v.apc);
     }
     IA_LAUNCH_CHECK("k_img_pad");
-    k_img_norm<<<(unsigned)((nrows + 255) / 256), 256, 0, st>>>(reinterpret_cast<const half8 *>(db), nrows,
-                                                               const_cast<uint32_t *>(v.norm));
-    IA_LAUNCH_CHECK("k_img_norm");
+    if (db) {
+        k_img_norm<<<(unsigned)((nrows + 255) / 256), 256, 0, st>>>(reinterpret_cast<const half8 *>(db), nrows,
+                                                                   const_cast<uint32_t *>(v.norm));
+        IA_LAUNCH_CHECK("k_img_norm");
+    } else {     // nrows is a multiple of 512 here (whole chunks, ia_internal.h)
+        k_db_build_t<true><<<(unsigned)(nrows / 256), 256, 0, st>>>(d, row0, nrows, center, amax, nullptr,
+                                                                    const_cast<uint32_t *>(v.norm));
+        IA_LAUNCH_CHECK("k_db_build_t<norm>");
+    }
     return IA_OK;
 }
 

@@ -41,8 +41,8 @@ static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_
 // stages (128 pixels of one scanline) from the images instead of from 224-B rows: every
 // pixel's split-f16 pair (hi | lo << 16) stored once, the images padded by reflection
 // (IMG_PX columns, IMG_PY rows on each side) so every window row is one contiguous run.
-// Buffer: [A fine][A coarse][norm slots of the rows][for each A' image: fine, coarse], each
-// section 256-B aligned.  Applies when the level width and row0 are multiples of 128 and
+// Buffer: [A fine][A coarse][norm slots of the rows][for each A' image: fine, coarse][scratch
+// of the build], each section 256-B aligned.  Applies when the level width and row0 are multiples of 128 and
 // the rows fill whole chunks (no padding rows): see img_db_applies.
 constexpr int IMG_PX = 4, IMG_PY = 2;
 struct ImgDb {
@@ -51,7 +51,9 @@ struct ImgDb {
     long fsz, csz, apstride, apc;           // padded image sizes (u32), A' image stride,
                                             // offset of an A' image's coarse section
     long hw, row0;                          // rows per image, global row of local row 0
+    long scr;                               // byte offset of the build's scratch section
 };
+constexpr size_t IMG_SCRATCH = 1024 * 8 * sizeof(double);   // ia_db_build_image's amax partials
 static inline bool img_db_applies(int W, long row0, long nrows) {
     return W % 128 == 0 && row0 % 128 == 0 && db_rows_padded(nrows) == nrows;
 }
@@ -70,7 +72,8 @@ static inline bool img_db_layout(int H, int W, int hs, int ws, int nAp, long row
     const size_t fb = img_align(v.fsz * 4), cb = img_align(v.csz * 4), nb = img_align(nrows * 4);
     v.apstride = (long)((fb + cb) / 4);
     v.apc = (long)(fb / 4);
-    if (bytes) *bytes = fb + cb + nb + (size_t)nAp * (fb + cb);
+    v.scr = (long)(fb + cb + nb + (size_t)nAp * (fb + cb));
+    if (bytes) *bytes = (size_t)v.scr + IMG_SCRATCH;
     const char *p = reinterpret_cast<const char *>(dbi);
     v.fa = reinterpret_cast<const uint32_t *>(p);
     v.ca = reinterpret_cast<const uint32_t *>(p + fb);

@@ -21,6 +21,7 @@
 // candidate segments would serialise k_rescore).  On a single shard the last kernel also
 // runs the per-pixel tail of the synthesis step (ia_finish.h).
 #include "ia_finish.h"
+#include "ia_imgwin.h"
 #include "ia_split16.h"
 
 #include <float.h>
@@ -86,6 +87,55 @@ __device__ __forceinline__ float rescreen16(const half8 (&g0)[DB16_GROUPS],
         acc = fmaf(x, k < 55 ? qf[(k & 1) * 28 + (k >> 1)] : twoR, acc);
     }
     return acc;
+}
+
+// the same re-screen values for pixels p and p + 64 of a staged image-form window
+// (ia_imgwin.h): the same 56 terms x_h + x_l in the same order as rescreen16, so the same
+// fp32 values; one pass over k for both (each query factor read once)
+__device__ __forceinline__ float win_x(const char *bf, const char *bc, int k) {
+    const uint32_t v = *reinterpret_cast<const uint32_t *>(((k < 55 && win_coarse(k)) ? bc : bf) + win_off(k));
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)) +
+           (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16));
+}
+__device__ __forceinline__ void rescreen_win2(const char *wb, int p, const float *qf, float twoR,
+                                              float &e0, float &e1) {
+    const char *bf0 = wb + 4 * p, *bc0 = wb + 4 * (p >> 1);
+    const char *bf1 = bf0 + 256, *bc1 = bc0 + 128;
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < IA_DP; ++k) {
+        const float f = k < 55 ? qf[(k & 1) * 28 + (k >> 1)] : twoR;
+        a0 = fmaf(win_x(bf0, bc0, k), f, a0);
+        a1 = fmaf(win_x(bf1, bc1, k), f, a1);
+    }
+    e0 = a0;
+    e1 = a1;
+}
+
+// this lane's pieces of the window of the stage at local row lrow (a wave stages a whole
+// window: pieces lane + 64 j), loaded into registers / stored into the wave's LDS window
+constexpr int WIN_PPL = (WIN_PIECES + 63) / 64;   // 7
+__device__ __forceinline__ void win_load(const ImgDb &im, long lrow, int lane, uint4 (&pc)[WIN_PPL]) {
+    const WinSrc ws = win_src(im, lrow);
+#pragma unroll
+    for (int j = 0; j < WIN_PPL; ++j) {
+        const int i = lane + 64 * j;
+        if (i < WIN_PIECES) pc[j] = *reinterpret_cast<const uint4 *>(win_piece(im, ws, i));
+    }
+}
+__device__ __forceinline__ void win_store(char *wb, int lane, const uint4 (&pc)[WIN_PPL]) {
+#pragma unroll
+    for (int j = 0; j < WIN_PPL; ++j) {
+        const int i = lane + 64 * j;
+        if (i < WIN_PIECES) reinterpret_cast<uint4 *>(wb)[i] = pc[j];
+    }
+}
+// the wave's own LDS writes are visible to all its lanes (LDS executes a wave's operations
+// in order; this keeps the compiler from moving them)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
@@ -184,10 +234,10 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
 // Exact stage, one workgroup per query: waves 0-3 screen and rescore; with the pixel tail
 // (MODE 1, 2: exact_tail) a fifth wave picks the coherence candidate meanwhile (it needs
 // only s / im of earlier waves), so the tail after the winner is one gather round.
-template <int MODE>
-__global__ __launch_bounds__(MODE == 0 ? 256 : 320) void k_rescore(
+template <int MODE, bool IMG>
+__global__ __launch_bounds__(MODE == 0 ? 256 : 320, IMG ? 2 : 1) void k_rescore(
         DbSrc src, long row0, long nrows, long nseg, int seg_rows,
-        const float *__restrict__ segmin, const half8 *__restrict__ db,
+        const float *__restrict__ segmin, const half8 *__restrict__ db, ImgDb im,
         const float *__restrict__ qp, const double *__restrict__ q64,
         const double *__restrict__ nq, const float *__restrict__ amax, Best *__restrict__ best,
         unsigned long long *stats, FinishArgs fa) {
@@ -204,6 +254,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 320) void k_rescore(
     __shared__ unsigned int nresc;
     __shared__ long rlist[RESCORE_ROWCAP];
     __shared__ int rcount;
+    __shared__ __attribute__((aligned(16))) char wins[IMG ? 4 * WIN_B : 16];   // one window per wave
 
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
@@ -231,32 +282,53 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 320) void k_rescore(
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
     unsigned int mine = 0;
-    // rows of the candidate segments, RESCORE_RPT per thread per step with all their DB
-    // loads issued together (seg_rows <= 512 = RESCORE_RPT * 256: one step per segment);
-    // rows within Trow go to a list rescored one per thread after the loop (one round of
-    // feature gathers); a list overflow is rescored in place
+    // rows within Trow go to a list rescored one per thread after the re-screen (one round
+    // of feature gathers); a list overflow is rescored in place
     const long nrs = ex ? nscan * seg_rows : 0;
-    for (long base = 0; base < nrs; base += RESCORE_RPT * 256) {
-        float e[RESCORE_RPT];
-        long lr[RESCORE_RPT];
-#pragma unroll
-        for (int u = 0; u < RESCORE_RPT; ++u) {
-            const long k = base + u * 256 + tid;
-            const long seg = k < nrs ? (full ? k / seg_rows : slist[k / seg_rows]) : 0;
-            lr[u] = k < nrs ? seg * seg_rows + k % seg_rows : nrows;
-            // out-of-range rows read row 0 and are discarded below
-            half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
-            load_row16(db, lr[u] < nrows ? lr[u] : 0, g0, g1);
-            e[u] = rescreen16(g0, g1, qf, twoR);
+    auto take = [&](long lr, float e) {     // lr: local row
+        if (lr < nrows && (double)e <= Trow) {
+            ++mine;
+            const int pos = atomicAdd(&rcount, 1);
+            if (pos < RESCORE_ROWCAP) rlist[pos] = lr;
+            else best_update(bd, bi, row_dist2(src, row0 + lr, qs), row0 + lr);
         }
+    };
+    if constexpr (IMG) {
+        // image form: wave w re-screens the 128-row stage k0 = base + 128 w of each 512-row
+        // step from its own LDS window (no block barrier: the fifth wave is free meanwhile)
+        const int wv = tid >> 6, lane = tid & 63;
+        char *wb = wins + (wv & 3) * WIN_B;
+        for (long k0 = 128L * wv; k0 < nrs; k0 += RESCORE_RPT * 256) {
+            const long seg = full ? k0 / seg_rows : slist[k0 / seg_rows];
+            const long lrow = seg * seg_rows + k0 % seg_rows;
+            uint4 pc[WIN_PPL];
+            win_load(im, lrow, lane, pc);
+            wave_lds_sync();                // the previous window's reads are done
+            win_store(wb, lane, pc);
+            wave_lds_sync();
+            float e0, e1;
+            rescreen_win2(wb, lane, qf, twoR, e0, e1);
+            take(lrow + lane, e0);
+            take(lrow + lane + 64, e1);
+        }
+    } else {
+        // rows of the candidate segments, RESCORE_RPT per thread per step with all their DB
+        // loads issued together (seg_rows <= 512 = RESCORE_RPT * 256: one step per segment)
+        for (long base = 0; base < nrs; base += RESCORE_RPT * 256) {
+            float e[RESCORE_RPT];
+            long lr[RESCORE_RPT];
 #pragma unroll
-        for (int u = 0; u < RESCORE_RPT; ++u) {
-            if (lr[u] < nrows && (double)e[u] <= Trow) {
-                ++mine;
-                const int pos = atomicAdd(&rcount, 1);
-                if (pos < RESCORE_ROWCAP) rlist[pos] = lr[u];
-                else best_update(bd, bi, row_dist2(src, row0 + lr[u], qs), row0 + lr[u]);
+            for (int u = 0; u < RESCORE_RPT; ++u) {
+                const long k = base + u * 256 + tid;
+                const long seg = k < nrs ? (full ? k / seg_rows : slist[k / seg_rows]) : 0;
+                lr[u] = k < nrs ? seg * seg_rows + k % seg_rows : nrows;
+                // out-of-range rows read row 0 and are discarded below
+                half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
+                load_row16(db, lr[u] < nrows ? lr[u] : 0, g0, g1);
+                e[u] = rescreen16(g0, g1, qf, twoR);
             }
+#pragma unroll
+            for (int u = 0; u < RESCORE_RPT; ++u) take(lr[u], e[u]);
         }
     }
     if (MODE != 0 && !ex) {                  // the fifth wave: coherence pick
@@ -342,10 +414,11 @@ __global__ __launch_bounds__(256) void k_select(long nseg, const float *__restri
     for (int i = tid; i < cnt; i += 256) items[base + i] = WItem{q, full ? i : slist[i], twoR, Trow};
 }
 
-__global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows, int seg_rows,
+template <bool IMG>
+__global__ __launch_bounds__(256, IMG ? 2 : 1) void k_items(DbSrc src, long row0, long nrows, int seg_rows,
                                                const WItem *__restrict__ items,
                                                const int *__restrict__ ctr,
-                                               const half8 *__restrict__ db,
+                                               const half8 *__restrict__ db, ImgDb im,
                                                const float *__restrict__ qp,
                                                const double *__restrict__ q64,
                                                Best *__restrict__ ibest,
@@ -356,19 +429,28 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
     __shared__ long long redi[4];
     __shared__ int plist[RESCORE_RPT * 256];
     __shared__ int pcount;
+    __shared__ __attribute__((aligned(16))) char wins[IMG ? 4 * WIN_B : 16];   // one window per wave
     const int n = *ctr;
     const int tid = threadIdx.x;
+    const int wv = tid >> 6, lane = tid & 63;
     for (int it = blockIdx.x; it < n; it += gridDim.x) {
         const WItem w = items[it];
-        // this thread's rows of the segment, issued before the query is staged so that the
-        // two round trips overlap
-        half8 x0[RESCORE_RPT][DB16_GROUPS], x1[RESCORE_RPT][DB16_GROUPS];
+        // this thread's rows of the segment (row form) or its wave's window (image form: wave
+        // wv takes the segment's 128-row stage wv), issued before the query is staged so that
+        // the two round trips overlap
+        half8 x0[IMG ? 1 : RESCORE_RPT][DB16_GROUPS], x1[IMG ? 1 : RESCORE_RPT][DB16_GROUPS];
         long lr[RESCORE_RPT];
+        uint4 pc[WIN_PPL];
+        const bool wstage = IMG && wv * 128 < seg_rows;
+        if constexpr (IMG) {
+            if (wstage) win_load(im, (long)w.seg * seg_rows + wv * 128, lane, pc);
+        } else {
 #pragma unroll
-        for (int u = 0; u < RESCORE_RPT; ++u) {
-            const int k = u * 256 + tid;
-            lr[u] = k < seg_rows ? (long)w.seg * seg_rows + k : nrows;
-            load_row16(db, lr[u] < nrows ? lr[u] : 0, x0[u], x1[u]);
+            for (int u = 0; u < RESCORE_RPT; ++u) {
+                const int k = u * 256 + tid;
+                lr[u] = k < seg_rows ? (long)w.seg * seg_rows + k : nrows;
+                load_row16(db, lr[u] < nrows ? lr[u] : 0, x0[u], x1[u]);
+            }
         }
         __syncthreads();                       // the previous item's LDS reads are done
         if (tid < IA_DP) {
@@ -376,13 +458,23 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
             qf[tid] = qp[(long)w.q * IA_DP + tid];
         }
         if (tid == 0) pcount = 0;
+        if (wstage) win_store(wins + wv * WIN_B, lane, pc);
         __syncthreads();
         // fp32 re-screen; rows within Trow go to one list, rescored one per thread below
         // (a single round of feature gathers, however the passing rows fall over lanes)
+        if constexpr (IMG) {
+            if (wstage) {
+                float e0, e1;
+                rescreen_win2(wins + wv * WIN_B, lane, qf, w.twoR, e0, e1);
+                if ((double)e0 <= w.trow) plist[atomicAdd(&pcount, 1)] = wv * 128 + lane;
+                if ((double)e1 <= w.trow) plist[atomicAdd(&pcount, 1)] = wv * 128 + lane + 64;
+            }
+        } else {
 #pragma unroll
-        for (int u = 0; u < RESCORE_RPT; ++u) {
-            const float acc = rescreen16(x0[u], x1[u], qf, w.twoR);
-            if (lr[u] < nrows && (double)acc <= w.trow) plist[atomicAdd(&pcount, 1)] = u * 256 + tid;
+            for (int u = 0; u < RESCORE_RPT; ++u) {
+                const float acc = rescreen16(x0[u], x1[u], qf, w.twoR);
+                if (lr[u] < nrows && (double)acc <= w.trow) plist[atomicAdd(&pcount, 1)] = u * 256 + tid;
+            }
         }
         __syncthreads();
         const int np = pcount;
@@ -400,7 +492,7 @@ __global__ __launch_bounds__(256) void k_items(DbSrc src, long row0, long nrows,
         if ((tid & 63) == 0) { redd[tid >> 6] = bd; redi[tid >> 6] = bi; }
         __syncthreads();
         if (tid == 0) {
-            for (int wv = 1; wv < 4; ++wv) best_update(bd, bi, redd[wv], redi[wv]);
+            for (int v = 1; v < 4; ++v) best_update(bd, bi, redd[v], redi[v]);
             ibest[it] = Best{bd, bi};
             if (stats) atomicAdd(&stats_slot(stats, w.q)[0], (unsigned long long)np);
         }
@@ -487,15 +579,19 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     int rc;
     IA_ARG(q16, "launch_match: no split-f16 query rows");
     const half8 *db = reinterpret_cast<const half8 *>(dbv);
-    ImgDb img;
+    ImgDb img{};
     IA_ARG(!dbi || img_db_layout(src.A.h, src.A.w, src.A.hs, src.A.ws, 1, row0, nrows, dbi, img, nullptr),
            "launch_match: an image-form DB for a level it does not apply to");
+    IA_ARG(db || dbi, "launch_match: no DB (row form or image form)");
     const SegWs ws = seg_ws(scratch, M, nrows);
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
     if ((rc = launch_screen16(db, dbi ? &img : nullptr, nrows, q16, M, ws.segmin, st))) return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
     const int rm = rescore_mode();
+    // the exact stage re-screens from the image form whenever there is one (the row form
+    // need not exist then)
+    const bool im = dbi != nullptr;
     // default: the work list for levels above 2^20 rows (where k_rescore's per-query
     // serialisation costs most); k_rescore below, with or without the fused tail (a
     // sharded rank's 0.5 M-row shard: 13.9 vs 19.9 us per wave, profiles/r01_shard_sim_g8.txt)
@@ -505,8 +601,12 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         k_select<<<M, 256, 0, st>>>(nseg, ws.segmin, nq, amax, ws.ctr, ws.items, ws.sel, stats);
         IA_LAUNCH_CHECK("k_select");
         const int grid = 2 * M + 64;
-        k_items<<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr, db, qp,
-                                      q64, ws.ibest, stats);
+        if (im)
+            k_items<true><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr,
+                                                db, img, qp, q64, ws.ibest, stats);
+        else
+            k_items<false><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr,
+                                                 db, img, qp, q64, ws.ibest, stats);
         IA_LAUNCH_CHECK("k_items");
         if (mode == 2)
             k_gather<2><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
@@ -517,13 +617,19 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         IA_LAUNCH_CHECK("k_gather");
         return IA_OK;
     }
-#define IA_RESCORE_CASE(MD)                                                                      \
-    k_rescore<MD><<<M, MD == 0 ? 256 : 320, 0, st>>>(src, row0, nrows, db_nsegs(nrows),          \
-                                                     db_seg_rows(nrows), ws.segmin, db, qp, q64, \
-                                                     nq, amax, best, stats, fa)
-    if (mode == 2) IA_RESCORE_CASE(2);
-    else if (mode == 1) IA_RESCORE_CASE(1);
-    else IA_RESCORE_CASE(0);
+#define IA_RESCORE_CASE(MD, IM)                                                                  \
+    k_rescore<MD, IM><<<M, MD == 0 ? 256 : 320, 0, st>>>(src, row0, nrows, db_nsegs(nrows),      \
+                                                         db_seg_rows(nrows), ws.segmin, db, img, \
+                                                         qp, q64, nq, amax, best, stats, fa)
+    if (im) {
+        if (mode == 2) IA_RESCORE_CASE(2, true);
+        else if (mode == 1) IA_RESCORE_CASE(1, true);
+        else IA_RESCORE_CASE(0, true);
+    } else {
+        if (mode == 2) IA_RESCORE_CASE(2, false);
+        else if (mode == 1) IA_RESCORE_CASE(1, false);
+        else IA_RESCORE_CASE(0, false);
+    }
 #undef IA_RESCORE_CASE
     IA_LAUNCH_CHECK("k_rescore");
     return IA_OK;
@@ -595,8 +701,8 @@ size_t ia_match_workspace_bytes(int M, long nrows) {
 }
 
 int ia_match_batch(const IaMatchArgs *a, void *stream) {
-    IA_ARG(a && a->db && a->q64 && a->center && a->amax && a->workspace && a->M >= 0 &&
-               a->nrows > 0,
+    IA_ARG(a && (a->db || a->dbi || a->lsh) && a->q64 && a->center && a->amax && a->workspace &&
+               a->M >= 0 && a->nrows > 0,
            "ia_match_batch: bad args");
     if (a->M == 0) return IA_OK;
     hipStream_t st = S(stream);

@@ -25,7 +25,7 @@
 // minima need no masking.  Built with -fno-honor-nans (the min-reductions need no NaN
 // canonicalisation: inputs are finite by construction) and -amdgpu-mfma-vgpr-form (MFMA
 // results in VGPRs: the reductions read them without v_accvgpr_read copies).
-#include "ia_internal.h"
+#include "ia_imgwin.h"
 #include "ia_split16.h"
 
 #include <float.h>
@@ -178,22 +178,7 @@ __device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8
 // of rows; the window is expanded into the row form's operand layout in LDS, then the
 // same MFMA stage runs.  Windows are double-buffered (the next one's copies fly during the
 // expansion and MFMAs of this one); the operand is built and consumed between two barriers.
-constexpr int WF_PC = 34, WC_PC = 18;                                 // 16-B pieces per window row
-constexpr int WB_FINE = 8 * WF_PC * 16, WB_COARSE = 6 * WC_PC * 16, WB_NORM = 128 * 4;
-constexpr int WIN_B = WB_FINE + WB_COARSE + WB_NORM;                  // 6592 B
-constexpr int WIN_PIECES = WIN_B / 16;                                // 412
 static_assert(WIN_PIECES <= 448, "waves 0-2 x two wave-instructions + wave 3 x one stage the window");
-
-// byte offset of feature k's hi half in the window minus its lane term (pixel p of the stage:
-// 4 p for fine features, 4 (p / 2) for coarse ones); lo halves are 2 bytes on
-__host__ __device__ constexpr int win_off(int k) {
-    return k < 9 ? WB_FINE + (k / 3) * WC_PC * 16 + (k % 3 + 3) * 4
-         : k < 34 ? ((k - 9) / 5) * WF_PC * 16 + ((k - 9) % 5 + 2) * 4
-         : k < 43 ? WB_FINE + (3 + (k - 34) / 3) * WC_PC * 16 + ((k - 34) % 3 + 3) * 4
-         : k < 55 ? (5 + (k - 43) / 5) * WF_PC * 16 + ((k - 43) % 5 + 2) * 4
-         : WB_FINE + WB_COARSE;
-}
-__host__ __device__ constexpr bool win_coarse(int k) { return k < 9 || (k >= 34 && k < 43); }
 __host__ __device__ constexpr int grp_k0(int h, int g) {
     return h == 0 ? (g < 4 ? 8 * g : 8 * (g - 4)) : (g < 3 ? 32 + 8 * g : (g == 3 ? 24 : 32 + 8 * (g - 4)));
 }
@@ -240,30 +225,13 @@ __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, 
     half8 bq[NS][Q16_GROUPS];
     load_queries<G, W, NS>(q16, bq, lane);
     auto issue = [&](int s, int buf) {
-        const long lrow = crow0 + (long)s * 128;
-        const long g = im.row0 + lrow;
-        const long img = g / im.hw;
-        const long rem = g - img * im.hw;
-        const int y = (int)(rem / im.W), x0 = (int)(rem - (long)y * im.W);
-        const uint32_t *fp = im.ap + img * im.apstride;
-        const uint32_t *cp = fp + im.apc;
+        const WinSrc ws = win_src(im, crow0 + (long)s * 128);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             if (t == 1 && W == 3) continue;     // pieces 448.. are past the window
             const int i = (t * 4 + W) * 64 + lane;
-            const uint32_t *src;
-            if (i < 8 * WF_PC) {                // fine: padded row = image row + IMG_PY
-                const int r = i / WF_PC, pc = i - r * WF_PC;
-                src = (r < 5 ? im.fa + (long)(y + r) * im.Wp : fp + (long)(y + r - 5) * im.Wp) + x0 + 4 * pc;
-            } else if (i < 8 * WF_PC + 6 * WC_PC) {
-                const int q = i - 8 * WF_PC, r = q / WC_PC, pc = q - r * WC_PC;
-                src = (r < 3 ? im.ca + (long)((y >> 1) + 1 + r) * im.Wcp
-                             : cp + (long)((y >> 1) + r - 2) * im.Wcp) + (x0 >> 1) + 4 * pc;
-            } else {
-                src = im.norm + lrow + 4 * (i - 8 * WF_PC - 6 * WC_PC);
-            }
             if (i < WIN_PIECES)
-                __builtin_amdgcn_global_load_lds((const void *)src,
+                __builtin_amdgcn_global_load_lds((const void *)win_piece(im, ws, i),
                                                  (void *)(wbuf + buf * WIN_B + (t * 4 + W) * 1024),
                                                  16, 0, 2);
         }

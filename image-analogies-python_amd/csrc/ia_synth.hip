@@ -244,7 +244,7 @@ static int shard_tail() {
 }
 
 static int check_args(const IaSynthArgs *a) {
-    IA_ARG(a && a->db && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
+    IA_ARG(a && (a->db || a->dbi || a->lsh) && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
                a->weights && a->s && a->im && a->workspace,
            "ia_synth_level: null argument");
     IA_ARG(a->H > 0 && a->W > 0 && a->nrows > 0 && a->row0 >= 0 &&
@@ -577,7 +577,7 @@ int ia_diag_synth_level_shards(const IaSynthArgs *a, const IaShardDb *shards, in
     IA_ARG(a && shards && n >= 1 && !a->comm && !a->lsh, "ia_diag_synth_level_shards: bad args");
     long total = 0;
     for (int r = 0; r < n; ++r) {
-        IA_ARG(shards[r].db && shards[r].amax && shards[r].row0 == total && shards[r].nrows > 0,
+        IA_ARG((shards[r].db || shards[r].dbi) && shards[r].amax && shards[r].row0 == total && shards[r].nrows > 0,
                "ia_diag_synth_level_shards: shards must tile the rows in order");
         total += shards[r].nrows;
     }

@@ -95,13 +95,15 @@ int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *cent
                 void *db, float *amax, void *stream);
 /* the DB's image form: each pixel's split-f16 pair once, in images padded by
  * reflection, plus the rows' norm slots — 59 MB instead of 940 MB at the c4 finest level; the
- * screen builds its stages from it in LDS.  Applies when the level width and row0 are
+ * screen builds its stages from it in LDS and the exact stage re-screens from it.  Applies when the level width and row0 are
  * multiples of 128 and the rows fill whole chunks: ia_db_image_bytes returns 0 otherwise.
- * Call after ia_db_build (the norm slots and amax come from it); center must be constant
- * over k < 34 and over k >= 34 (as ia_center_fill makes it). */
+ * db (nullable): the row form from ia_db_build, whose amax and norm slots are then reused;
+ * with db NULL the image form is built alone (amax as ia_db_build computes it: zero it
+ * first) and the matcher runs from it alone — screen and exact stage, no 224-B rows.
+ * center must be constant over k < 34 and over k >= 34 (as ia_center_fill makes it). */
 size_t ia_db_image_bytes(const IaSrcLevel *src, long row0, long nrows);
 int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double *center,
-                      const void *db, const float *amax, void *dbi, void *stream);
+                      const void *db, float *amax, void *dbi, void *stream);
 /* per-dimension screening centre: k < 34 -> mA, k >= 34 -> mAp (host scalars). */
 int ia_center_fill(double *center, double mA, double mAp, void *stream);
 
@@ -132,7 +134,7 @@ int ia_lsh_bits(long nrows);
  * approximate LSH matcher over the same rows instead. */
 typedef struct {
     IaSrcLevel src;
-    const void *db;            /* ia_db_build output                       */
+    const void *db;            /* ia_db_build output (NULL with dbi: image form only) */
     long row0, nrows;          /* this shard's global row range            */
     const double *center;      /* 55 (device)                              */
     const float *amax;         /* device scalar from ia_db_build           */
@@ -142,8 +144,8 @@ typedef struct {
     double *dist;              /* out M                                    */
     void *workspace;
     const IaLsh *lsh;          /* NULL: exact matcher                      */
-    const void *dbi;           /* NULL, or ia_db_build_image output: the screen streams the
-                                  image form instead of the rows (same results)  */
+    const void *dbi;           /* NULL, or ia_db_build_image output: the screen and the exact
+                                  stage read the image form instead of the rows (same results) */
 } IaMatchArgs;
 size_t ia_match_workspace_bytes(int M, long nrows);
 int ia_match_batch(const IaMatchArgs *a, void *stream);
@@ -218,8 +220,8 @@ typedef struct {
      * candidate}; dbg_dist: H*W x 2 fp64 {d_app, d_coh} (zeros without a candidate) */
     int32_t *dbg_px;
     double *dbg_dist;
-    const void *dbi;    /* NULL, or this shard's ia_db_build_image output (the screen's DB
-                           stream; same results) */
+    const void *dbi;    /* NULL, or this shard's ia_db_build_image output (the matcher reads
+                           it instead of the rows; db may then be NULL; same results) */
 } IaSynthArgs;
 #define IA_SYNTH_EAGER 1
 #define IA_SYNTH_PROF 2

@@ -365,20 +365,25 @@ def test_concurrent_jobs_on_streams_match_oracle(gpu):
             assert np.array_equal(out[l][1], ref[l][2]), l
 
 
-@pytest.mark.parametrize('G', [2, 3])
-def test_sharded_reduction_with_the_real_kernels(gpu, G):
+@pytest.mark.parametrize('G,image', [(2, False), (3, False), (2, True)])
+def test_sharded_reduction_with_the_real_kernels(gpu, G, image):
     # (the in-process shard path always uses the ShardRec tail: exact stage MODE 2 +
     # k_finish; the RCCL tests above run the default IA_SHARD_TAIL=0 form)
     """The sharded path's per-wave reduction run by the product kernels on one GPU: every
     level's database split into G shards (each built from its own rows, its own amax);
     per wave each shard's exact stage writes its (distance, row, weighted distance)
     records and k_finish reduces them as after the RCCL exchange
-    (ia_diag_synth_level_shards).  Flat regions put exact ties across shard boundaries."""
+    (ia_diag_synth_level_shards).  Flat regions put exact ties across shard boundaries.
+    image: 128-wide levels whose shards are whole chunks, so every shard runs from the
+    image form alone (no row form), as a c4 rank does."""
     import ctypes
     import _ia
     import algorithms
     import image_analogies as ia
-    A, Aps, B = analogy_inputs(34, (46, 57), (41, 49), n_ap=2, flat=True)
+    if image:
+        A, Aps, B = analogy_inputs(35, (128, 256), (64, 128), n_ap=2, flat=True)
+    else:
+        A, Aps, B = analogy_inputs(34, (46, 57), (41, 49), n_ap=2, flat=True)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=34)
     w = o.compute_weights(3, 5, 12, 1)
     ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 3.0, w)
@@ -387,11 +392,14 @@ def test_sharded_reduction_with_the_real_kernels(gpu, G):
     B_d = [dev(p) for p in B_pyr]
     Bp_d = [dev(b) for b in Bp_pyr]
     wd = dev(w)
+    image_levels = 0
     for level in range(1, L):
         full = algorithms.level_index(A_d, Ap_d, level)
         shards = [algorithms.level_index(A_d, Ap_d, level,
                                          lambda lv, n, r=r: ia.shard_rows(n, r, G))
                   for r in range(G)]
+        image_only = all(x.db is None and x.dbi is not None for x in shards)
+        image_levels += image_only
         call = ia._LevelCall(level, L, full, B_d[level - 1], B_d[level], Bp_d[level - 1],
                              Bp_d[level], wd, 3.0)
         arr = (_ia.IaShardDb * G)(*[_ia.IaShardDb(_ia.ptr(x.db).value, x.row0, x.nrows,
@@ -404,3 +412,4 @@ def test_sharded_reduction_with_the_real_kernels(gpu, G):
         assert np.array_equal(s.cpu().numpy(), ref[level][1]), level
         assert np.array_equal(im.cpu().numpy(), ref[level][2]), level
         assert np.array_equal(Bp_d[level].cpu().numpy(), ref[level][0]), level
+    assert image_levels >= (1 if image else 0), image_levels

@@ -43,7 +43,7 @@ def _index(A, Aps):
     Ap_pyr = [o.compute_gaussian_pyramid(x, 3) for x in Aps]
     L = len(A_pyr)
     idx = algorithms.level_index([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_pyr],
-                                 L - 1)
+                                 L - 1, rows=True)
     return idx, o.create_index(A_pyr, Ap_pyr, L)[L - 1]
 
 
@@ -136,7 +136,8 @@ def test_split16_screen_every_query_split(gpu):
     A_pyr = o.compute_gaussian_pyramid(A, 3, cap=2)
     Ap_pyr = o.compute_gaussian_pyramid(Aps[0], 3, cap=2)
     L = len(A_pyr)
-    idx = algorithms.level_index([dev(p) for p in A_pyr], [[dev(p) for p in Ap_pyr]], L - 1)
+    idx = algorithms.level_index([dev(p) for p in A_pyr], [[dev(p) for p in Ap_pyr]], L - 1,
+                                 rows=True)
     As = o.create_index(A_pyr, [Ap_pyr], L)[L - 1]
     rs = np.random.RandomState(7)
     Q = np.vstack([As[rs.randint(0, len(As), 400)] + rs.randn(400, 55) * 0.01,
@@ -168,7 +169,8 @@ def test_db_build_tiled_equals_per_row(gpu, shape, n_ap, shards):
         for form in (1, 0):
             prev = _ia.db_build_form(form)
             try:
-                idx = algorithms.level_index(A_pyr, Ap_pyr, L, lambda l, n: (r0, r1 - r0))
+                idx = algorithms.level_index(A_pyr, Ap_pyr, L, lambda l, n: (r0, r1 - r0),
+                                             rows=True)
                 torch.cuda.synchronize()
                 got.append((idx.db.cpu().numpy().copy(), float(idx.amax.item())))
             finally:
@@ -206,13 +208,15 @@ def graph():
     _ia.graph_mode(prev)
 
 
-@pytest.mark.parametrize('image', [True, False])
-def test_synthesis_with_image_form_db(gpu, monkeypatch, image):
+@pytest.mark.parametrize('image,mode', [(True, 0), (True, 1), (False, -1)])
+def test_synthesis_with_image_form_db(gpu, monkeypatch, rescore, image, mode):
     """A 128 x 256 analogy (two A' images; levels of width 256 and 128 take the DB's image
     form, the 64-wide coarsest level the row form): B', s and im equal the oracle's with the
-    image form on and off."""
+    image form on (no row form built; both forms of the exact stage re-screen from it) and
+    off."""
     import image_analogies as ia
     monkeypatch.setenv('IA_DB_IMAGE', '1' if image else '0')
+    rescore(mode)
     A, Aps, B = analogy_inputs(48, (128, 256), (64, 128), n_ap=2)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=48, cap=3)
     w = o.compute_weights(3, 5, 12, 1)
@@ -248,3 +252,47 @@ def test_synthesis_bit_exact_with_either_exact_stage(gpu, rescore, graph, mode, 
         assert np.array_equal(out[l][1].cpu().numpy(), ref[l][2]), l
         assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l
     _ia.check(_ia.lib().ia_release_thread_resources(), 'ia_release_thread_resources')
+
+
+def test_image_form_alone_equals_image_form_from_rows(gpu):
+    """ia_db_build_image without a row form (amax from the value ranges, norm slots from the
+    LDS-tiled build's norm pass) writes the same bytes and amax as from ia_db_build's rows;
+    the matcher run from it alone (screen + both exact stages) gives the brute-force 1-NN."""
+    import _ia
+    import algorithms
+    A, Aps, _ = analogy_inputs(49, (256, 384), (8, 8), n_ap=2)
+    A_pyr = o.compute_gaussian_pyramid(A, 3, cap=2)
+    Ap_pyr = [o.compute_gaussian_pyramid(x, 3, cap=2) for x in Aps]
+    L = len(A_pyr)
+    Ad, Apd = [dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_pyr]
+    both = algorithms.level_index(Ad, Apd, L - 1, rows=True)
+    alone = algorithms.level_index(Ad, Apd, L - 1)
+    assert alone.db is None and alone.dbi is not None and both.db is not None
+    # rebuilt into zeroed buffers (the sections' alignment gaps are never written)
+    lib = _ia.lib()
+    n = lib.ia_db_image_bytes(ctypes.byref(alone.src), 0, alone.nrows) - 65536
+    z_rows, z_alone = torch.zeros_like(both.dbi), torch.zeros_like(alone.dbi)
+    amax = torch.zeros(1, dtype=torch.float32, device='cuda')
+    _ia.check(lib.ia_db_build_image(ctypes.byref(both.src), 0, both.nrows, _ia.ptr(both.center),
+                                    _ia.ptr(both.db), _ia.ptr(both.amax), _ia.ptr(z_rows),
+                                    _ia.stream()), 'ia_db_build_image')
+    _ia.check(lib.ia_db_build_image(ctypes.byref(alone.src), 0, alone.nrows, _ia.ptr(alone.center),
+                                    None, _ia.ptr(amax), _ia.ptr(z_alone), _ia.stream()),
+              'ia_db_build_image')
+    torch.cuda.synchronize()
+    assert float(alone.amax.item()) == float(both.amax.item()) == float(amax.item())
+    assert torch.equal(z_alone[:n], z_rows[:n])         # all but the build's scratch
+    As = o.create_index(A_pyr, Ap_pyr, L)[L - 1]
+    rs = np.random.RandomState(5)
+    Q = np.vstack([As[rs.randint(0, len(As), 40)] + rs.randn(40, 55) * 0.003, rs.rand(24, 55)])
+    for mode in (0, 1):
+        prev = _ia.rescore_mode(mode)
+        try:
+            i, d = alone.match(Q)
+        finally:
+            _ia.rescore_mode(prev)
+        i, d = i.cpu().numpy(), d.cpu().numpy()
+        for qi, q in enumerate(Q):
+            dd = np.add.reduce((As - q) ** 2, axis=1)
+            j = int(np.argmin(dd))
+            assert (d[qi], i[qi]) == (dd[j], j), (mode, qi)
