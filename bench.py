@@ -222,10 +222,11 @@ def cpu_baseline(job, seconds=10.0):
 
 def hbm_kernels(dev, reps=20):
     """Achieved HBM rate of the bandwidth-bound kernels: each C-ABI entry
-    timed with HIP events on the stream it launches on, median of `reps`, against
+    timed with HIP events on the stream it launches on (10 back-to-back calls per
+    measurement, per call), median of `reps`, against
     algorithmic bytes (every input element read once, every output written once):
       yiq        ia_rgb_to_yiq, 2048x2048 uint8 RGB -> YIQ + Y fp64: 3 + 32 B/px
-      pyr_reduce ia_pyr_reduce_f64 (k_init_minmax + fused k_pyr_reduce + k_pyr_clip),
+      pyr_reduce ia_pyr_reduce_f64 (one-pass k_pyr_wave + k_pyr_clip_p),
                  2048^2 -> 1024^2 fp64: 8 B per input + 8 B per output pixel
       db_build   ia_db_build (k_db_range + k_db_bound + LDS-tiled k_db_build_t), the c4
                  finest level, 4,194,304 rows: 224 B written per row (split-f16 rows) + the
@@ -240,16 +241,20 @@ def hbm_kernels(dev, reps=20):
     import algorithms
     st = torch.cuda.current_stream(dev)
 
-    def timed(fn):
+    def timed(fn, batch=10):
+        # `batch` back-to-back calls between the two events (as the product issues them: a
+        # pyramid's levels, the levels' DB builds), per call: the host's launch latency is
+        # not in the window (a lone call between two events measures ~5 us of it)
         fn()
         ts = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            fn()
+            for _ in range(batch):
+                fn()
             e1.record(st)
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e-3)
+            ts.append(e0.elapsed_time(e1) * 1e-3 / batch)
         ts.sort()
         return ts[len(ts) // 2]
 
@@ -282,7 +287,7 @@ def hbm_kernels(dev, reps=20):
         _ia.check(lib.ia_pyr_reduce_f64(_ia.ptr(img), H, W, _ia.ptr(sm), 1024, 1024, coef, taps,
                                         _ia.ptr(ws), _ia.stream()), 'ia_pyr_reduce_f64')
     put('pyr_reduce', timed(reduce), 8 * (H * W + 1024 * 1024),
-        'ia_pyr_reduce_f64 (k_init_minmax + fused k_pyr_reduce + k_pyr_clip) 2048^2 -> 1024^2')
+        'ia_pyr_reduce_f64 (k_pyr_wave + k_pyr_clip_p) 2048^2 -> 1024^2')
     Ap_lg, Ap_sm = img[None].clone(), sm[None].clone()
     N = H * W
     ix = algorithms.LevelIndex(sm, img, Ap_sm, Ap_lg, rows=True)

@@ -129,6 +129,7 @@ _SIGS = {
     'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_graph_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_pyr_form': (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
@@ -293,3 +294,10 @@ def mean_dev(t):
     ws = workspace(lib().ia_mean_workspace_bytes(t.numel()))
     check(lib().ia_mean_f64(ptr(t), t.numel(), ptr(out), ptr(ws), stream()), 'ia_mean_f64')
     return float(out.item())
+
+
+def pyr_form(stream=-1, oh=0):
+    """ia_pyr_reduce_f64's kernels for this process (1 the one-pass k_pyr_wave where the
+    coefficients are a halving [default], 0 the tiled k_pyr_reduce only); returns the
+    previous flag."""
+    return lib().ia_diag_set_pyr_form(int(stream), int(oh))

@@ -295,21 +295,34 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 320, IMG ? 2 : 1) void k_rescore(
     };
     if constexpr (IMG) {
         // image form: wave w re-screens the 128-row stage k0 = base + 128 w of each 512-row
-        // step from its own LDS window (no block barrier: the fifth wave is free meanwhile)
+        // step from its own LDS window (no block barrier: the fifth wave is free meanwhile);
+        // the next step's window loads fly while this one is re-screened
         const int wv = tid >> 6, lane = tid & 63;
         char *wb = wins + (wv & 3) * WIN_B;
-        for (long k0 = 128L * wv; k0 < nrs; k0 += RESCORE_RPT * 256) {
+        auto stage_row = [&](long k0) {
             const long seg = full ? k0 / seg_rows : slist[k0 / seg_rows];
-            const long lrow = seg * seg_rows + k0 % seg_rows;
-            uint4 pc[WIN_PPL];
+            return seg * seg_rows + k0 % seg_rows;
+        };
+        uint4 pc[WIN_PPL];
+        long k0 = 128L * wv, lrow = 0;
+        if (k0 < nrs) {
+            lrow = stage_row(k0);
             win_load(im, lrow, lane, pc);
+        }
+        for (; k0 < nrs; k0 += RESCORE_RPT * 256) {
             wave_lds_sync();                // the previous window's reads are done
             win_store(wb, lane, pc);
             wave_lds_sync();
+            long lnext = 0;
+            if (k0 + RESCORE_RPT * 256 < nrs) {
+                lnext = stage_row(k0 + RESCORE_RPT * 256);
+                win_load(im, lnext, lane, pc);
+            }
             float e0, e1;
             rescreen_win2(wb, lane, qf, twoR, e0, e1);
             take(lrow + lane, e0);
             take(lrow + lane + 64, e1);
+            lrow = lnext;
         }
     } else {
         // rows of the candidate segments, RESCORE_RPT per thread per step with all their DB

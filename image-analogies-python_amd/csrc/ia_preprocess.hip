@@ -376,6 +376,191 @@ __global__ __launch_bounds__(256) void k_pyr_reduce(const double *__restrict__ s
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Wave pyramid_reduce (the halving case: 1.25 <= s <= 2 + 1e-9, 0 <= t < 1 in both
+// directions, no sample outside the image — what skimage's fit gives for h = ceil(H/2); the
+// host checks).  Each wave is independent (no LDS, no barrier): it owns <= PW_OW output
+// columns and <= PW_OH output rows, one input column per lane (the blurred columns it needs
+// plus 3 on each side: <= 64).  It loads every input row of its strip first (one memory
+// round trip), then walks the blurred rows: vertical pass from registers, horizontal pass
+// from the neighbour lanes (DPP wave shifts), and every output row as soon as its two
+// sample rows are the current / previous blurred row (lane shuffles gather the two sample
+// columns).  Operation orders are k_blur's and k_resample's.  Per wave: the min / max of
+// its owned blurred pixels (coverage of the clip range, as k_pyr_reduce) and of its outputs
+// -> part[wave][4] as keys; k_pyr_clip_p reduces them.  (An LDS-tiled strip form — 256
+// columns per block, rows staged through LDS — ran at 24-33 us for 2048^2: LDS-bound.)
+// ---------------------------------------------------------------------------------
+constexpr int PW_OW = 28, PW_OH = 16;
+constexpr int PW_NB = 2 * PW_OH + 2;         // blurred rows of a wave (s <= 2)
+
+__device__ __forceinline__ double dpp_shr1(double x) {   // lane l <- lane l - 1
+    const int2 v = __builtin_bit_cast(int2, x);
+    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_update_dpp(0, v.x, 0x138, 0xf, 0xf, false),
+                                                __builtin_amdgcn_update_dpp(0, v.y, 0x138, 0xf, 0xf, false)));
+}
+__device__ __forceinline__ double dpp_shl1(double x) {   // lane l <- lane l + 1
+    const int2 v = __builtin_bit_cast(int2, x);
+    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_update_dpp(0, v.x, 0x130, 0xf, 0xf, false),
+                                                __builtin_amdgcn_update_dpp(0, v.y, 0x130, 0xf, 0xf, false)));
+}
+
+__global__ __launch_bounds__(256) void k_pyr_wave(const double *__restrict__ src, int H, int W,
+                                                  double *__restrict__ dst, int h, int w,
+                                                  int nstrip, int nunit, double sx, double tx,
+                                                  double sy, double ty, double w0, double w1,
+                                                  double w2, double w3, long long *__restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (unit >= nunit) return;                // uniform over the wave; no barriers below
+    const int ui = unit % nstrip, uj = unit / nstrip;
+    const int x0 = ui * PW_OW, x1 = min(x0 + PW_OW, w);
+    const int y0 = uj * PW_OH, y1 = min(y0 + PW_OH, h);
+    // sample columns / rows are monotone and inside the image (host): the extremes are those
+    // of the first and last output
+    auto lo_of = [](double v) { return (int)floor(v); };
+    auto hi_of = [](double v) { return (int)ceil(v); };
+    const int oR0 = uj == 0 ? 0 : max(0, min(H, lo_of((double)y0 * sy + ty)));
+    const int oR1 = y1 == h ? H : max(0, min(H, lo_of((double)y1 * sy + ty)));
+    const int oC0 = ui == 0 ? 0 : max(0, min(W, lo_of((double)x0 * sx + tx)));
+    const int oC1 = x1 == w ? W : max(0, min(W, lo_of((double)x1 * sx + tx)));
+    const int sR0 = lo_of((double)y0 * sy + ty), sR1 = hi_of((double)(y1 - 1) * sy + ty);
+    const int sC0 = lo_of((double)x0 * sx + tx), sC1 = hi_of((double)(x1 - 1) * sx + tx);
+    const int BR0 = min(sR0, oR0), BR1 = max(sR1, oR1 - 1);
+    const int BC0 = min(sC0, oC0), BC1 = max(sC1, oC1 - 1);
+    const int NB = BR1 - BR0 + 1;            // <= PW_NB, BC1 - BC0 + 7 <= 64 (host: s <= 2)
+    // this lane's input column (blurred column BC0 - 3 + lane), reflected (W >= 4)
+    int cix = min(BC0 - 3 + lane, BC1 + 3);
+    cix = cix < 0 ? -1 - cix : cix;
+    cix = cix >= W ? 2 * W - 1 - cix : cix;
+    const double *col = src + cix;
+    const int bc = BC0 - 3 + lane;
+    const bool hown = lane >= 3 && bc <= BC1 && bc >= oC0 && bc < oC1;
+    // this lane's output column (x0 + lane): its sample lanes and weight
+    int L0 = 0, L1 = 0;
+    double dc = 0.0;
+    if (lane < x1 - x0) {
+        const double c = (double)(x0 + lane) * sx + tx;
+        const double fc = floor(c);
+        L0 = (int)fc - BC0 + 3;
+        L1 = (int)ceil(c) - BC0 + 3;
+        dc = c - fc;
+    }
+    // every input row first; rows past the wave's re-read its last one
+    double I[PW_NB + 6];
+#pragma unroll
+    for (int i = 0; i < PW_NB + 6; ++i) {
+        int r = BR0 - 3 + min(i, NB + 5);
+        r = r < 0 ? -1 - r : r;
+        r = r >= H ? 2 * H - 1 - r : r;
+        I[i] = col[(long)r * W];
+    }
+    double bmin = INFINITY, bmax = -INFINITY, omin = INFINITY, omax = -INFINITY;
+    double Bp = 0.0, Bc = 0.0;
+    int yn = y0;                             // next output row
+    double *out = dst + x0 + lane;
+#pragma unroll
+    for (int i = 0; i < PW_NB; ++i) {
+        if (i < NB) {
+            double v = I[i + 3] * w0;          // vertical pass (k_blur's order)
+            v = v + (I[i] + I[i + 6]) * w3;
+            v = v + (I[i + 1] + I[i + 5]) * w2;
+            v = v + (I[i + 2] + I[i + 4]) * w1;
+            const double m1 = dpp_shr1(v), m2 = dpp_shr1(m1), m3 = dpp_shr1(m2);
+            const double p1 = dpp_shl1(v), p2 = dpp_shl1(p1), p3 = dpp_shl1(p2);
+            double b = v * w0;                 // horizontal pass
+            b = b + (m3 + p3) * w3;
+            b = b + (m2 + p2) * w2;
+            b = b + (m1 + p1) * w1;
+            Bp = Bc;
+            Bc = b;
+            const int row = BR0 + i;
+            if (hown && row >= oR0 && row < oR1) {
+                bmin = fmin(bmin, b);
+                bmax = fmax(bmax, b);
+            }
+            if (yn < y1) {
+                const double r = (double)yn * sy + ty;
+                const double fr = floor(r);
+                const int r0 = (int)fr, r1 = (int)ceil(r);
+                if (r1 == row) {               // both sample rows done (r0 = row or row - 1)
+                    const double dr = r - fr;
+                    const double T = r0 == row ? Bc : Bp;
+                    const double tl = __shfl(T, L0), tr = __shfl(T, L1);
+                    const double bl = __shfl(Bc, L0), br = __shfl(Bc, L1);
+                    const double top = (1 - dc) * tl + dc * tr;
+                    const double bot = (1 - dc) * bl + dc * br;
+                    const double val = (1 - dr) * top + dr * bot;
+                    if (lane < x1 - x0) {
+                        out[(long)yn * w] = val;
+                        omin = fmin(omin, val);
+                        omax = fmax(omax, val);
+                    }
+                    ++yn;
+                }
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        bmin = fmin(bmin, __shfl_xor(bmin, o));
+        bmax = fmax(bmax, __shfl_xor(bmax, o));
+        omin = fmin(omin, __shfl_xor(omin, o));
+        omax = fmax(omax, __shfl_xor(omax, o));
+    }
+    if (lane < 4) {
+        const double v = lane == 0 ? bmin : lane == 1 ? bmax : lane == 2 ? omin : omax;
+        part[(long)unit * 4 + lane] = dkey(v);
+    }
+}
+
+// warp's clip after k_pyr_wave: every block reduces the np wave partials (blurred min /
+// max, output min / max keys) and returns when the outputs lie inside the blurred range (the
+// usual case); otherwise the grid clips the level.  The partials come from fmin / fmax, so a
+// zero bound may carry either sign; that never changes the level: a value is replaced only
+// when it lies strictly outside [lo, hi], and with lo = 0 every blurred value, hence every
+// bilinear sample (non-negative weights), is >= 0 (likewise hi = 0).
+__global__ __launch_bounds__(256) void k_pyr_clip_p(double *__restrict__ dst, long n,
+                                                    const long long *__restrict__ part, int np) {
+    __shared__ long long red[4][4];
+    __shared__ double clip[2];
+    __shared__ int skip;
+    const int tid = threadIdx.x;
+    long long v[4] = {0x7fffffffffffffffLL, (long long)0x8000000000000000ULL,
+                      0x7fffffffffffffffLL, (long long)0x8000000000000000ULL};
+    for (int i = tid; i < np; i += 256) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long long x = part[(long)i * 4 + k];
+            v[k] = (k & 1) ? (x > v[k] ? x : v[k]) : (x < v[k] ? x : v[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long x = __shfl_xor(v[k], o);
+            v[k] = (k & 1) ? (x > v[k] ? x : v[k]) : (x < v[k] ? x : v[k]);
+        }
+        if ((tid & 63) == 0) red[k][tid >> 6] = v[k];
+    }
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            for (int i = 1; i < 4; ++i)
+                v[k] = (k & 1) ? (red[k][i] > v[k] ? red[k][i] : v[k]) : (red[k][i] < v[k] ? red[k][i] : v[k]);
+        clip[0] = dkey_inv(v[0]);
+        clip[1] = dkey_inv(v[1]);
+        skip = v[2] >= v[0] && v[3] <= v[1];
+    }
+    __syncthreads();
+    if (skip) return;
+    const double lo = clip[0], hi = clip[1];
+    for (long i = (long)blockIdx.x * 256 + tid; i < n; i += (long)gridDim.x * 256) {
+        const double x = dst[i];
+        if (x < lo) dst[i] = lo;
+        else if (x > hi) dst[i] = hi;
+    }
+}
+
 // warp's clip of the resampled level to [min, max] of the blurred image (np.clip; only
 // values outside the range, which bilinear weights can produce by rounding, are written).
 // k_pyr_reduce also recorded the min / max of its outputs: when they lie inside the range
@@ -495,6 +680,30 @@ int ia_axpb_f64(const double *x, long n, int mode, double a, double m, double b,
     return IA_OK;
 }
 
+// pyramid_reduce form (ia_diag_set_pyr_form): 1 the wave kernel where it applies (default),
+// 0 the tiled fused kernel / two-kernel path only
+static int g_pyr_stream = env_int("IA_PYR_STREAM", 1);
+int ia_diag_set_pyr_form(int stream, int oh) {
+    (void)oh;
+    const int prev = g_pyr_stream;
+    if (stream == 0 || stream == 1) g_pyr_stream = stream;
+    return prev;
+}
+// k_pyr_wave's preconditions, in the device's own arithmetic (no FMA contraction here
+// either): halving scales, every sample row / column of the first and last output inside
+// the image (the maps are monotone), and a wave's blurred span within its 64 lanes
+static bool pyr_wave_applies(int H, int W, int h, int w, const double coef[4]) {
+    const double sx = coef[0], tx = coef[1], sy = coef[2], ty = coef[3];
+    if (H < 4 || W < 4 || !(sx >= 1.25 && sx <= 2.0 + 1e-9 && sy >= 1.25 && sy <= 2.0 + 1e-9))
+        return false;
+    if (!(tx >= 0 && tx < 1.0 && ty >= 0 && ty < 1.0)) return false;
+    const double cmax = (double)(w - 1) * sx + tx, rmax = (double)(h - 1) * sy + ty;
+    if (std::ceil(cmax) > W - 1 || std::ceil(rmax) > H - 1) return false;
+    // blurred columns of a wave: <= (PW_OW - 1) s + 2 sampled, PW_OW s + 1 owned
+    return (PW_OW - 1) * sx + 2 + 6 <= 64 && PW_OW * sx + 1 + 6 <= 64 &&
+           (PW_OH - 1) * sy + 2 <= PW_NB && PW_OH * sy + 1 <= PW_NB;
+}
+
 size_t ia_pyr_workspace_bytes(int H, int W) {
     return align_up((size_t)H * W * sizeof(double), 256) + MM_SLOTS * MM_STRIDE * 8;
 }
@@ -509,14 +718,29 @@ int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w
     unsigned long long *mm = reinterpret_cast<unsigned long long *>(
         reinterpret_cast<char *>(workspace) + align_up((size_t)H * W * sizeof(double), 256));
     hipStream_t st = S(stream);
-    k_init_minmax<<<1, MM_SLOTS, 0, st>>>(mm);
-    IA_LAUNCH_CHECK("k_init_minmax");
     // fused form when every output tile's sample rows / cols fit the LDS region (skimage's
     // coefficients of a halving: s <= 2 up to rounding (its fit gives 2.0000000000000004),
     // 0 <= t < 1; the region has 8 spare rows / cols; anything else takes the two-kernel path)
     const bool fused = coef[0] > 0 && coef[0] <= 2.01 && coef[2] > 0 && coef[2] <= 2.01 &&
                        coef[1] >= 0 && coef[1] < 1.0 && coef[3] >= 0 && coef[3] < 1.0 &&
                        H >= 2 && W >= 2;
+    if (g_pyr_stream && pyr_wave_applies(H, W, h, w, coef)) {
+        const int nstrip = (w + PW_OW - 1) / PW_OW;
+        const int nunit = nstrip * ((h + PW_OH - 1) / PW_OH);
+        IA_ARG((size_t)nunit * 4 * sizeof(long long) <= ia_pyr_workspace_bytes(H, W),
+               "ia_pyr_reduce_f64: workspace too small for the partials");
+        long long *part = reinterpret_cast<long long *>(workspace);
+        k_pyr_wave<<<(unsigned)((nunit + 3) / 4), 256, 0, st>>>(src, H, W, dst, h, w, nstrip, nunit,
+                                                               coef[0], coef[1], coef[2], coef[3],
+                                                               taps[0], taps[1], taps[2], taps[3], part);
+        IA_LAUNCH_CHECK("k_pyr_wave");
+        const long n = (long)h * w;
+        k_pyr_clip_p<<<(unsigned)std::min<long>(nblk(n, 256), 64), 256, 0, st>>>(dst, n, part, nunit);
+        IA_LAUNCH_CHECK("k_pyr_clip_p");
+        return IA_OK;
+    }
+    k_init_minmax<<<1, MM_SLOTS, 0, st>>>(mm);
+    IA_LAUNCH_CHECK("k_init_minmax");
     if (fused) {
         dim3 g(nblk(w, PT_W), nblk(h, PT_H));
         k_pyr_reduce<<<g, 256, 0, st>>>(src, H, W, dst, h, w, coef[0], coef[1], coef[2], coef[3],

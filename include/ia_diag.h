@@ -36,6 +36,10 @@ int ia_diag_set_rescore_mode(int mode);
  * width and row0 are multiples of 32, 0 always the per-row gather kernels (same bytes);
  * other values leave it; returns the previous value */
 int ia_diag_set_db_build_form(int tiled);
+/* pyramid_reduce form for this process: stream 1 = the one-pass k_pyr_wave where the
+ * coefficients are a halving (default), 0 = the tiled k_pyr_reduce / two-kernel path only;
+ * oh is unused.  Returns the previous stream flag. */
+int ia_diag_set_pyr_form(int stream, int oh);
 /* HIP-graph capture of ia_synth_level's wave loop for this process (overrides IA_GRAPH):
  * 0 off, 1 levels of <= 2^18 rows, 2 every single-GPU level; other values leave it;
  * returns the previous value */

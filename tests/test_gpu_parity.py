@@ -73,6 +73,33 @@ def test_pyramid_kernel_vs_oracle_large(gpu, shape, cap):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize('shape', [(2048, 2048), (517, 300), (33, 1000), (4, 5), (2, 2), (3, 255),
+                                   (257, 124)])
+@pytest.mark.parametrize('kind', ['noise', 'flat'])
+def test_pyramid_streaming_form_equals_tiled(gpu, shape, kind):
+    """k_pyr_wave (one LDS-free pass, waves of 28 output columns x 16 rows, the clip from
+    per-wave partials) writes the same level as the tiled k_pyr_reduce + k_pyr_clip, bit for
+    bit, and the oracle's; 'flat' images (saturated regions) exercise the clip itself."""
+    import _ia
+    import img_preprocess as ip
+    rs = np.random.RandomState(sum(shape))
+    img = rs.rand(*shape)
+    if kind == 'flat':
+        img = np.minimum(1.0, img * 3.0)          # ~2/3 of the pixels exactly 1.0
+    x = dev(img)
+    outs = []
+    for form, oh in [(0, 0), (1, 0)]:
+        prev = _ia.pyr_form(form, oh if oh else 16)
+        try:
+            outs.append(ip.pyramid_reduce_dev(x).cpu().numpy())
+        finally:
+            _ia.pyr_form(prev, 16)
+    for o_ in outs[1:]:
+        assert np.array_equal(o_.view(np.int64), outs[0].view(np.int64))
+    if max(shape) <= 600:
+        assert np.array_equal(outs[1], o.pyramid_reduce(img))
+
+
 # ---- a9 features ---------------------------------------------------------------------------------
 
 def test_feature_kernel_kat_and_oracle(gpu):
