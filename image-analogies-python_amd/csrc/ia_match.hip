@@ -144,11 +144,19 @@ constexpr int RESCORE_RPT = 2;         // candidate rows per thread per step
 constexpr int RESCORE_ROWCAP = 512;    // rows to rescore held in LDS per query
 static_assert(DB_SEG_MAX <= RESCORE_RPT * 256, "one re-screen step per segment");
 
+// a uniform index the compiler must treat as per-lane: the load it feeds is a vector load
+// issued in program order with the others (a scalar load of it would be scheduled after
+// their wait: one more memory round trip)
+__device__ __forceinline__ int vidx(int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+}
+
 // e* of query q over its nseg segment minima (float4 reads, nseg a multiple of 4); the
 // first RESCORE_REG float4s per thread stay in v[] for the selection pass
-// (threads >= 256 of a block take no part but meet the barrier)
-__device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, float4 (&v)[RESCORE_REG],
-                                             float *redf) {
+// (threads >= 256 of a block take no part but meet the barrier).  segmin_load issues the
+// loads only, so the caller can put its other independent loads in the same round trip.
+__device__ __forceinline__ void segmin_load(const float4 *sq4, long n4, float4 (&v)[RESCORE_REG]) {
     const int tid = threadIdx.x;
     const long lim = tid < 256 ? n4 : 0;
 #pragma unroll
@@ -156,6 +164,11 @@ __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, float4 
         const long i = tid + (long)j * 256;
         v[j] = i < lim ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
     }
+}
+__device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
+                                             float *redf) {
+    const int tid = threadIdx.x;
+    const long lim = tid < 256 ? n4 : 0;
     float emin = FLT_MAX;
 #pragma unroll
     for (int j = 0; j < RESCORE_REG; ++j)
@@ -259,20 +272,30 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 320, IMG ? 2 : 1) void k_rescore(
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
     const bool ex = tid < 256;               // the exact stage's waves
+    // every independent load in one round trip: the query rows, its norm, the DB bound and
+    // the segment minima (the LDS stores of the query come after all of them are issued)
+    double qsv = 0.0;
+    float qfv = 0.f;
     if (tid < IA_DP) {
-        qs[tid] = q64[(long)q * IA_DP + tid];
-        qf[tid] = qp[(long)q * IA_DP + tid];
+        qsv = q64[(long)q * IA_DP + tid];
+        qfv = qp[(long)q * IA_DP + tid];
     }
-    if (tid == 0) { scount = 0; nresc = 0; rcount = 0; }
-    const double nqq = nq[q];
+    const double nqq = nq[vidx(q)];
+    const float am = amax[vidx(0)];
     const long n4 = nseg / 4;
     const float4 *sq4 = reinterpret_cast<const float4 *>(segmin + (long)q * nseg);
     float4 v[RESCORE_REG];
+    segmin_load(sq4, n4, v);
+    if (tid == 0) { scount = 0; nresc = 0; rcount = 0; }
     const float emin = segmin_scan(sq4, n4, v, redf);
+    if (tid < IA_DP) {                       // read after the selection's barrier
+        qs[tid] = qsv;
+        qf[tid] = qfv;
+    }
     double Tseg, Trow;
     bool force_full;
-    rescore_thresholds(emin, amax[0], nqq, Tseg, Trow, force_full);
-    const float twoR = ldexpf(1.f, split16_db_scale(amax[0]).R);
+    rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+    const float twoR = ldexpf(1.f, split16_db_scale(am).R);
     segmin_select(sq4, n4, v, Tseg, slist, &scount);
     __syncthreads();
     const int ns = scount;
@@ -398,15 +421,17 @@ __global__ __launch_bounds__(256) void k_select(long nseg, const float *__restri
     __shared__ float redf[4];
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
-    if (tid == 0) scount = 0;
-    const double nqq = nq[q];
+    const double nqq = nq[vidx(q)];          // one round trip for all independent loads
+    const float am = amax[vidx(0)];
     const long n4 = nseg / 4;
     const float4 *sq4 = reinterpret_cast<const float4 *>(segmin + (long)q * nseg);
     float4 v[RESCORE_REG];
+    segmin_load(sq4, n4, v);
+    if (tid == 0) scount = 0;
     const float emin = segmin_scan(sq4, n4, v, redf);
     double Tseg, Trow;
     bool force_full;
-    rescore_thresholds(emin, amax[0], nqq, Tseg, Trow, force_full);
+    rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
     segmin_select(sq4, n4, v, Tseg, slist, &scount);
     __syncthreads();
     const int ns = scount;
@@ -423,7 +448,7 @@ __global__ __launch_bounds__(256) void k_select(long nseg, const float *__restri
     }
     __syncthreads();
     const int base = sbase;
-    const float twoR = ldexpf(1.f, split16_db_scale(amax[0]).R);
+    const float twoR = ldexpf(1.f, split16_db_scale(am).R);
     for (int i = tid; i < cnt; i += 256) items[base + i] = WItem{q, full ? i : slist[i], twoR, Trow};
 }
 

@@ -63,7 +63,16 @@ __global__ __launch_bounds__(128) void k_finish_gather(DbSrc src, const Best *__
     __shared__ CohSel cs;
     const int m = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (threadIdx.x < IA_DP) qs[threadIdx.x] = q64[(long)m * IA_DP + threadIdx.x];
+    // the query and (wave 0) the first 8 ranks' winners in one memory round trip
+    const double qv = threadIdx.x < IA_DP ? q64[(long)m * IA_DP + threadIdx.x] : 0.0;
+    constexpr int NB0 = 8;
+    Best b0[NB0];
+    if (wv == 0) {
+#pragma unroll
+        for (int g = 0; g < NB0; ++g)
+            b0[g] = g < nranks ? best_all[(long)g * M + m] : Best{INFINITY, 0x7fffffffffffffffLL};
+    }
+    if (threadIdx.x < IA_DP) qs[threadIdx.x] = qv;
     __syncthreads();
     double ad = INFINITY;
     long long app = 0x7fffffffffffffffLL;
@@ -71,7 +80,9 @@ __global__ __launch_bounds__(128) void k_finish_gather(DbSrc src, const Best *__
         const CohSel c = coh_pick(src, m, f, qs, lane);
         if (lane == 0) cs = c;
     } else {
-        for (int g = 0; g < nranks; ++g) {
+#pragma unroll
+        for (int g = 0; g < NB0; ++g) fin_best(ad, app, b0[g].d, b0[g].idx);
+        for (int g = NB0; g < nranks; ++g) {
             const Best b = best_all[(long)g * M + m];
             fin_best(ad, app, b.d, b.idx);
         }
