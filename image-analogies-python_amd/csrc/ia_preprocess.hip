@@ -404,6 +404,11 @@ __device__ __forceinline__ double dpp_shl1(double x) {   // lane l <- lane l + 1
                                                 __builtin_amdgcn_update_dpp(0, v.y, 0x130, 0xf, 0xf, false)));
 }
 
+// AF: the exact halving map (host-checked for every output row and column: floor(y s + t)
+// = 2y, ceil = 2y + 1, likewise x): output row j is emitted at blurred row 2j + 1 from the
+// previous and current rows, and its samples sit in lanes 2j + 3 and 2j + 4 (one DPP shift),
+// so the emission needs no per-row sample-row test and no lane shuffle.
+template <bool AF>
 __global__ __launch_bounds__(256) void k_pyr_wave(const double *__restrict__ src, int H, int W,
                                                   double *__restrict__ dst, int h, int w,
                                                   int nstrip, int nunit, double sx, double tx,
@@ -435,16 +440,20 @@ __global__ __launch_bounds__(256) void k_pyr_wave(const double *__restrict__ src
     const double *col = src + cix;
     const int bc = BC0 - 3 + lane;
     const bool hown = lane >= 3 && bc <= BC1 && bc >= oC0 && bc < oC1;
-    // this lane's output column (x0 + lane): its sample lanes and weight
+    // this lane's output column: x0 + lane (its sample lanes L0, L1), or with AF x0 + (lane
+    // - 3) / 2 for the odd lanes 3 .. 2 (x1 - x0) + 1 (samples in this lane and the next)
     int L0 = 0, L1 = 0;
     double dc = 0.0;
-    if (lane < x1 - x0) {
-        const double c = (double)(x0 + lane) * sx + tx;
+    const int oj = AF ? (lane - 3) >> 1 : lane;
+    const bool olane = AF ? (lane >= 3 && (lane & 1) && oj < x1 - x0) : lane < x1 - x0;
+    if (olane) {
+        const double c = (double)(x0 + oj) * sx + tx;
         const double fc = floor(c);
         L0 = (int)fc - BC0 + 3;
         L1 = (int)ceil(c) - BC0 + 3;
         dc = c - fc;
     }
+    const double omdc = 1 - dc;
     // every input row first; rows past the wave's re-read its last one
     double I[PW_NB + 6];
 #pragma unroll
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(256) void k_pyr_wave(const double *__restrict__ src
     double bmin = INFINITY, bmax = -INFINITY, omin = INFINITY, omax = -INFINITY;
     double Bp = 0.0, Bc = 0.0;
     int yn = y0;                             // next output row
-    double *out = dst + x0 + lane;
+    double *out = dst + x0 + oj;
 #pragma unroll
     for (int i = 0; i < PW_NB; ++i) {
         if (i < NB) {
@@ -478,7 +487,21 @@ __global__ __launch_bounds__(256) void k_pyr_wave(const double *__restrict__ src
                 bmin = fmin(bmin, b);
                 bmax = fmax(bmax, b);
             }
-            if (yn < y1) {
+            if (AF) {
+                if ((i & 1) && y0 + (i >> 1) < y1) {  // output row y0 + i / 2, rows 2j and 2j + 1
+                    const int y = y0 + (i >> 1);
+                    const double r = (double)y * sy + ty;
+                    const double dr = r - floor(r);
+                    const double top = omdc * Bp + dc * dpp_shl1(Bp);
+                    const double bot = omdc * Bc + dc * dpp_shl1(Bc);
+                    const double val = (1 - dr) * top + dr * bot;
+                    if (olane) {
+                        out[(long)y * w] = val;
+                        omin = fmin(omin, val);
+                        omax = fmax(omax, val);
+                    }
+                }
+            } else if (yn < y1) {
                 const double r = (double)yn * sy + ty;
                 const double fr = floor(r);
                 const int r0 = (int)fr, r1 = (int)ceil(r);
@@ -487,10 +510,10 @@ __global__ __launch_bounds__(256) void k_pyr_wave(const double *__restrict__ src
                     const double T = r0 == row ? Bc : Bp;
                     const double tl = __shfl(T, L0), tr = __shfl(T, L1);
                     const double bl = __shfl(Bc, L0), br = __shfl(Bc, L1);
-                    const double top = (1 - dc) * tl + dc * tr;
-                    const double bot = (1 - dc) * bl + dc * br;
+                    const double top = omdc * tl + dc * tr;
+                    const double bot = omdc * bl + dc * br;
                     const double val = (1 - dr) * top + dr * bot;
-                    if (lane < x1 - x0) {
+                    if (olane) {
                         out[(long)yn * w] = val;
                         omin = fmin(omin, val);
                         omax = fmax(omax, val);
@@ -692,6 +715,15 @@ int ia_diag_set_pyr_form(int stream, int oh) {
 // k_pyr_wave's preconditions, in the device's own arithmetic (no FMA contraction here
 // either): halving scales, every sample row / column of the first and last output inside
 // the image (the maps are monotone), and a wave's blurred span within its 64 lanes
+// the exact halving map k_pyr_wave<true> assumes: floor(v s + t) = 2v and ceil = 2v + 1 for
+// every output row / column v (the device evaluates v * s + t the same way: no contraction)
+static bool pyr_halving_exact(int n, double s, double t) {
+    for (int v = 0; v < n; ++v) {
+        const double c = (double)v * s + t;
+        if (std::floor(c) != 2.0 * v || std::ceil(c) != 2.0 * v + 1) return false;
+    }
+    return true;
+}
 static bool pyr_wave_applies(int H, int W, int h, int w, const double coef[4]) {
     const double sx = coef[0], tx = coef[1], sy = coef[2], ty = coef[3];
     if (H < 4 || W < 4 || !(sx >= 1.25 && sx <= 2.0 + 1e-9 && sy >= 1.25 && sy <= 2.0 + 1e-9))
@@ -730,9 +762,13 @@ int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w
         IA_ARG((size_t)nunit * 4 * sizeof(long long) <= ia_pyr_workspace_bytes(H, W),
                "ia_pyr_reduce_f64: workspace too small for the partials");
         long long *part = reinterpret_cast<long long *>(workspace);
-        k_pyr_wave<<<(unsigned)((nunit + 3) / 4), 256, 0, st>>>(src, H, W, dst, h, w, nstrip, nunit,
-                                                               coef[0], coef[1], coef[2], coef[3],
-                                                               taps[0], taps[1], taps[2], taps[3], part);
+        const unsigned grid = (unsigned)((nunit + 3) / 4);
+        if (pyr_halving_exact(h, coef[2], coef[3]) && pyr_halving_exact(w, coef[0], coef[1]))
+            k_pyr_wave<true><<<grid, 256, 0, st>>>(src, H, W, dst, h, w, nstrip, nunit, coef[0], coef[1],
+                                                   coef[2], coef[3], taps[0], taps[1], taps[2], taps[3], part);
+        else
+            k_pyr_wave<false><<<grid, 256, 0, st>>>(src, H, W, dst, h, w, nstrip, nunit, coef[0], coef[1],
+                                                    coef[2], coef[3], taps[0], taps[1], taps[2], taps[3], part);
         IA_LAUNCH_CHECK("k_pyr_wave");
         const long n = (long)h * w;
         k_pyr_clip_p<<<(unsigned)std::min<long>(nblk(n, 256), 64), 256, 0, st>>>(dst, n, part, nunit);

@@ -73,8 +73,8 @@ def test_pyramid_kernel_vs_oracle_large(gpu, shape, cap):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize('shape', [(2048, 2048), (517, 300), (33, 1000), (4, 5), (2, 2), (3, 255),
-                                   (257, 124)])
+@pytest.mark.parametrize('shape', [(2048, 2048), (96, 130), (8, 4), (517, 300), (33, 1000), (4, 5),
+                                   (2, 2), (3, 255), (257, 124)])
 @pytest.mark.parametrize('kind', ['noise', 'flat'])
 def test_pyramid_streaming_form_equals_tiled(gpu, shape, kind):
     """k_pyr_wave (one LDS-free pass, waves of 28 output columns x 16 rows, the clip from
