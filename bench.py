@@ -308,32 +308,23 @@ def hbm_kernels(dev, reps=20):
     return out
 
 
-def init_comm(rank, world):
-    """RCCL communicator of libia (one per process/GPU); the unique id travels over the
-    gloo process group."""
-    uid = torch.zeros(128, dtype=torch.uint8)
-    if rank == 0:
-        buf = ctypes.create_string_buffer(128)
-        _ia.check(_ia.lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
-        uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
-    dist.broadcast(uid, 0)
-    h = ctypes.c_void_p()
-    _ia.check(_ia.lib().ia_comm_init(uid.numpy().tobytes(), world, rank, ctypes.byref(h)),
-              'ia_comm_init')
-    return h
-
-
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
         sk.bind(('127.0.0.1', 0))
         return sk.getsockname()[1]
 
 
+def share_gpu():
+    """IA_SHARE_GPU=1 (tests on a one-GPU box only): every rank runs on cuda:0.  The
+    device-side exchange works between processes of one GPU; RCCL refuses it."""
+    return os.environ.get('IA_SHARE_GPU', '0') == '1'
+
+
 def launch_ranks(args):
     """`--gpus N` (N > 1) outside torch.distributed.run: start the N rank processes with it
     as a child (this process has made no GPU call: torch.cuda.device_count() does not
     initialise the device on this image) and exit with its status."""
-    if not args.dry_run:
+    if not args.dry_run and not share_gpu():
         ndev = torch.cuda.device_count()
         if ndev < args.gpus:
             print('bench.py: --gpus %d but only %d GPU(s) visible' % (args.gpus, ndev),
@@ -389,6 +380,8 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    if share_gpu():
+        local = 0
     if torch.cuda.device_count() <= local:
         print('bench.py: rank %d needs GPU %d, %d visible' % (rank, local,
                                                             torch.cuda.device_count()),
@@ -400,10 +393,11 @@ def main():
 
     comm = None
     if world > 1 and args.config != 'c5':
-        # one RCCL communicator per sharded level: the levels run pipelined, each exchange
-        # stream-ordered on its own level's stream
+        # one exchange per sharded level (the levels run pipelined, each exchange ordered
+        # on its own level's stream): the device-side exchange (IA_EXCHANGE=peer, default)
+        # or one RCCL all-gather per wave (IA_EXCHANGE=rccl)
         nshard = Job(conf, 0, dev).sharded_levels(world)
-        comm = [init_comm(rank, world) for _ in range(max(nshard, 1))]
+        comm = [_ia.exchange(rank, world) for _ in range(max(nshard, 1))]
 
     lsh = None
     if args.matcher == 'lsh':
@@ -464,6 +458,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof = _ia.prof_end()
+    for cm in comm or []:
+        _ia.exchange_status(cm)     # raises if a device-side exchange wait timed out
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -589,7 +585,9 @@ def main():
                    'levels_cap': conf['levels'], 'jobs_per_gpu': len(jobs), 'streams_per_gpu': nstreams,
                    'pixels_per_step': pixels_per_step,
                    'parallelism': ('jobs%d' % world) if args.config == 'c5' else
-                                  ('db-shard%d' % world if world > 1 else 'single')},
+                                  ('db-shard%d' % world if world > 1 else 'single'),
+                   **({'exchange': _ia.exchange_kind() + (' (ranks share one GPU)' if share_gpu() else '')}
+                      if comm is not None else {})},
         'roofline': roof,
         'matcher': {'kind': 'lsh' if lsh is not None else 'exact',
                     'rows_rescored_fp64': sum(p['rows_rescored'] for p in prof),

@@ -119,6 +119,12 @@ _SIGS = {
                                     ctypes.POINTER(ctypes.c_void_p)]),
     'ia_comm_destroy': (ctypes.c_int, [_dp]),
     'ia_comm_nranks': (ctypes.c_int, [_dp]),
+    'ia_peer_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p]),
+    'ia_peer_connect': (ctypes.c_int, [_dp, ctypes.c_char_p]),
+    'ia_peer_check': (ctypes.c_int, [_dp, _dp]),
+    'ia_peer_status': (ctypes.c_int, [_dp]),
+    'ia_peer_mem_kind': (ctypes.c_int, [_dp]),
     'ia_prof_begin': (ctypes.c_int, []),
     'ia_prof_prepare': (ctypes.c_int, [ctypes.c_long]),
     'ia_prof_end': (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
@@ -135,6 +141,9 @@ _SIGS = {
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
     'ia_diag_screen16_image': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long,
                                               ctypes.c_long, _dp, _dp, ctypes.c_int, _dp, _dp]),
+    'ia_diag_peer_stress': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int), _dp]),
+    'ia_diag_peer_trace': (ctypes.c_int, [_dp, _dp]),
     'ia_diag_synth_level_shards': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs),
                                                   ctypes.POINTER(IaShardDb), ctypes.c_int, _dp]),
 }
@@ -294,6 +303,58 @@ def mean_dev(t):
     ws = workspace(lib().ia_mean_workspace_bytes(t.numel()))
     check(lib().ia_mean_f64(ptr(t), t.numel(), ptr(out), ptr(ws), stream()), 'ia_mean_f64')
     return float(out.item())
+
+
+def exchange_kind():
+    """The per-wave exchange of sharded levels (IA_EXCHANGE): 'peer' [default] the
+    device-side exchange (IPC-mapped receive boxes written by the exact stage's kernel),
+    'rccl' one ncclAllGather per wave plus a finish kernel.  Same results."""
+    k = os.environ.get('IA_EXCHANGE', 'peer')
+    if k not in ('peer', 'rccl'):
+        raise ValueError('IA_EXCHANGE must be peer or rccl, not %r' % k)
+    return k
+
+
+def exchange(rank, world, kind=None, mcap=4096):
+    """One exchange object (the IaSynthArgs.comm of one sharded level) over the initialised
+    torch.distributed process group: every rank calls it at the same point.  'rccl': an
+    RCCL communicator (the unique id broadcast from rank 0).  'peer': receive boxes for
+    waves of up to mcap queries, handles all-gathered, mapped, then a handshake wave
+    (include/ia.h).  Release with ia_comm_destroy."""
+    import torch.distributed as dist
+    kind = kind or exchange_kind()
+    h = ctypes.c_void_p()
+    if kind == 'rccl':
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            check(lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
+            uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        if world > 1:
+            dist.broadcast(uid, 0)
+        check(lib().ia_comm_init(uid.numpy().tobytes(), world, rank, ctypes.byref(h)),
+              'ia_comm_init')
+        return h
+    hd = ctypes.create_string_buffer(64)
+    check(lib().ia_peer_create(world, rank, mcap, ctypes.byref(h), hd), 'ia_peer_create')
+    mine = torch.frombuffer(bytearray(hd.raw[:64]), dtype=torch.uint8).clone()
+    parts = [torch.zeros(64, dtype=torch.uint8) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(parts, mine)
+    else:
+        parts = [mine]
+    check(lib().ia_peer_connect(h, b''.join(p.numpy().tobytes() for p in parts)),
+          'ia_peer_connect')
+    if world > 1:
+        dist.barrier()
+    check(lib().ia_peer_check(h, stream()), 'ia_peer_check')
+    return h
+
+
+def exchange_status(comm):
+    """Raise if a device-side exchange timed out waiting for another rank (no-op for RCCL)."""
+    if comm and lib().ia_peer_mem_kind(comm) >= 0:
+        check(lib().ia_peer_status(comm), 'ia_peer_status')
 
 
 def pyr_form(stream=-1, oh=0):

@@ -124,6 +124,83 @@ __device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, in
     }
 }
 
+// ---- device-side exchange of a sharded level (PeerView, ia_internal.h) ----------------
+// granules of (slot, source rank, query) in a receive box
+__device__ __forceinline__ unsigned long long *peer_cell(unsigned long long *box, const PeerView &p,
+                                                         int src, int q) {
+    return box + (((long)(p.epoch & 1) * p.nranks + src) * p.mcap + q) * 3;
+}
+// rank g's box pointer (selects over the kernel argument, not an indexed private copy)
+__device__ __forceinline__ unsigned long long *peer_box(const PeerView &p, int g) {
+    unsigned long long *box = p.box[0];
+#pragma unroll
+    for (int k = 1; k < IA_PEER_MAX; ++k) box = g == k ? p.box[k] : box;
+    return box;
+}
+// lanes g < nranks of one wave: this rank's winner of query q into rank g's box (system-
+// scope 8-byte stores: each granule arrives whole, over xGMI for a peer GPU's box)
+__device__ __forceinline__ void peer_publish(const PeerView &p, int q, double d, long long row,
+                                             int lane) {
+    if (lane >= p.nranks) return;
+    unsigned long long *dst = peer_cell(peer_box(p, lane), p, p.rank, q);
+    const unsigned long long tag = (unsigned long long)p.epoch << 32;
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+    __hip_atomic_store(dst, tag | (bits & 0xffffffffULL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 2, tag | (unsigned long long)(unsigned int)row, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// 10 s at the 100 MHz real-time counter: a peer that never publishes (a dead rank, or
+// memory the peer's stores do not reach) sets the error word instead of hanging the GPU;
+// once it is set every later wait of this rank gives up at once (ia_peer_status reports it)
+constexpr unsigned long long PEER_TIMEOUT_TICKS = 1000000000ULL;
+// one whole wave: lane g < nranks reads rank g's granules of query q from this rank's box
+// until all three carry this wave's epoch; then the lexicographic (distance, row) minimum
+// over the ranks, valid in every lane.  bd / bi: this rank's own winner (uniform) on entry;
+// kept as the result on timeout (false; the error word is then set).
+__device__ __forceinline__ bool peer_collect(const PeerView &p, int q, int lane, double &bd,
+                                             long long &bi, unsigned long long *raw = nullptr) {
+    const bool mine = lane < p.nranks;
+    const unsigned long long *src = peer_cell(peer_box(p, p.rank), p, mine ? lane : 0, q);
+    unsigned long long g0 = 0, g1 = 0, g2 = 0;
+    bool dead = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok;
+    for (;;) {
+        ok = true;
+        if (mine) {
+            g0 = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            g1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            g2 = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = (unsigned)(g0 >> 32) == p.epoch && (unsigned)(g1 >> 32) == p.epoch &&
+                 (unsigned)(g2 >> 32) == p.epoch;
+        }
+        if (__all(ok) || dead) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
+            if (lane == 0) __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            dead = true;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (raw && lane < 2) { raw[3 * lane] = g0; raw[3 * lane + 1] = g1; raw[3 * lane + 2] = g2; }
+    if (dead) return false;
+    double d = INFINITY;
+    long long i = 0x7fffffffffffffffLL;
+    if (mine) {
+        d = __longlong_as_double((long long)(((g1 & 0xffffffffULL) << 32) | (g0 & 0xffffffffULL)));
+        i = (long long)(g2 & 0xffffffffULL);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(d, o);
+        const long long oi = __shfl_xor(i, o);
+        fin_best(d, i, od, oi);
+    }
+    bd = d;
+    bi = i;
+    return true;
+}
+
 // The tail kernels run coh_pick on one wave and app_wdist + finish_apply on another.
 // (Picking the coherence candidate ahead, on a side stream beside the screen, measured 5 %
 // slower on c4: the per-wave cross-stream event waits cost more than the two gather rounds

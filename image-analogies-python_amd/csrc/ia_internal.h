@@ -109,6 +109,24 @@ static inline int qrows_alloc(int Mmax) {
     return (T + (T + 10) / 11) * 32;
 }
 
+// Device-side exchange of a sharded level (ia_comm.hip, ia_finish.h): every rank owns a
+// receive box in uncached device memory, IPC-mapped into every other rank's process.  Per
+// wave each rank writes its (distance, row) winner of query q straight into every rank's
+// box as three 8-byte granules {epoch << 32 | 32-bit payload} (the data carries its own
+// flag, so a reader needs no fence), and reads the G ranks' granules of q from its own
+// box until all carry the wave's epoch.  Two slots (epoch parity): a rank can be at most
+// one wave ahead of a slower one's reads (its next record needs the slower rank's next
+// record first).
+constexpr int IA_PEER_MAX = 16;
+struct PeerView {
+    unsigned long long *box[IA_PEER_MAX];   // box[g]: rank g's receive box (box[rank]: own)
+    unsigned int *err;                      // this rank's timeout word (0: fine)
+    double *trace;                          // diagnostic (nullable): ia_diag_peer_trace
+    int nranks, rank, mcap;                 // nranks 0: not a peer exchange
+    unsigned int epoch;                     // this wave's tag (>= 1, one per wave)
+};
+static inline size_t peer_box_words(int nranks, int mcap) { return (size_t)2 * nranks * mcap * 3; }
+
 // the level state one wave of the per-pixel tail updates (ia_finish.h)
 struct FinishArgs {
     int t, y_lo, W;
@@ -123,6 +141,9 @@ struct FinishArgs {
     // its coherence pick (CohSel, ia_finish.h) here instead of finishing the pixel
     ShardRec *shard_out;
     void *coh_out;
+    // sharded DB with the device-side exchange (px.nranks > 0): the exact stage publishes
+    // its shard's winner, collects every rank's, and finishes the pixel in the same kernel
+    PeerView px{};
 };
 
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS

@@ -226,6 +226,36 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
     __syncthreads();
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double d_app = 0.0;
+    if (MODE == 3) {
+        // device-side exchange: wave 0 hands this shard's winner to every rank, collects
+        // every rank's (ia_finish.h peer_publish / peer_collect) and weighs the global
+        // winner; wave 1 picks the coherence candidate meanwhile (unless already picked)
+        // (win / bd come from LDS words lane 0 of wave 0 wrote just before the call: only
+        // that lane's copy is certain, and every publishing lane needs it)
+        bd = __shfl(bd, 0);
+        win = __shfl(win, 0);
+        double gd = bd;
+        long long gw = win;
+        if (wv == 0) {
+            peer_publish(fa.px, q, bd, win, lane);
+            const bool tron = fa.px.trace && q < 8 && fa.px.epoch < 1024;
+            unsigned long long *tr = tron ? reinterpret_cast<unsigned long long *>(fa.px.trace) +
+                                                ((long)fa.px.epoch * 8 + q) * 12
+                                          : nullptr;
+            peer_collect(fa.px, q, lane, gd, gw, tr ? tr + 4 : nullptr);
+            if (tr && lane == 0) {
+                tr[0] = __double_as_longlong(bd); tr[1] = win;
+                tr[2] = __double_as_longlong(gd); tr[3] = gw;
+            }
+            d_app = app_wdist(src, gw, fa, qs, lane);
+        } else if (wv == 1 && !have_cs) {
+            const CohSel c = coh_pick(src, q, fa, qs, lane);
+            if (lane == 0) *cs = c;
+        }
+        if (!have_cs) __syncthreads();
+        if (wv == 0) finish_apply(src, gw, q, fa, *cs, d_app, lane);
+        return;
+    }
     if (wv == 1 && !have_cs) {
         const CohSel c = coh_pick(src, q, fa, qs, lane);
         if (lane == 0) *cs = c;
@@ -633,7 +663,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     // default: the work list for levels above 2^20 rows (where k_rescore's per-query
     // serialisation costs most); k_rescore below, with or without the fused tail (a
     // sharded rank's 0.5 M-row shard: 13.9 vs 19.9 us per wave, profiles/r01_shard_sim_g8.txt)
-    const int mode = !fin ? 0 : (fin->shard_out ? 2 : 1);
+    const int mode = !fin ? 0 : fin->shard_out ? 2 : fin->px.nranks ? 3 : 1;
     if (rm == 1 || (rm < 0 && nrows > (1L << 20))) {
         const long nseg = db_nsegs(nrows);
         k_select<<<M, 256, 0, st>>>(nseg, ws.segmin, nq, amax, ws.ctr, ws.items, ws.sel, stats);
@@ -646,7 +676,9 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
             k_items<false><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr,
                                                  db, img, qp, q64, ws.ibest, stats);
         IA_LAUNCH_CHECK("k_items");
-        if (mode == 2)
+        if (mode == 3)
+            k_gather<3><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
+        else if (mode == 2)
             k_gather<2><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
         else if (mode == 1)
             k_gather<1><<<M, 128, 0, st>>>(src, ws.sel, ws.ibest, ws.ctr, best, fa, q64);
@@ -660,11 +692,13 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
                                                          db_seg_rows(nrows), ws.segmin, db, img, \
                                                          qp, q64, nq, amax, best, stats, fa)
     if (im) {
-        if (mode == 2) IA_RESCORE_CASE(2, true);
+        if (mode == 3) IA_RESCORE_CASE(3, true);
+        else if (mode == 2) IA_RESCORE_CASE(2, true);
         else if (mode == 1) IA_RESCORE_CASE(1, true);
         else IA_RESCORE_CASE(0, true);
     } else {
-        if (mode == 2) IA_RESCORE_CASE(2, false);
+        if (mode == 3) IA_RESCORE_CASE(3, false);
+        else if (mode == 2) IA_RESCORE_CASE(2, false);
         else if (mode == 1) IA_RESCORE_CASE(1, false);
         else IA_RESCORE_CASE(0, false);
     }

@@ -243,6 +243,8 @@ static int graph_mode() { return g_graph_mode.load(std::memory_order_relaxed); }
 
 int comm_allgather(void *comm, const void *send, void *recv, size_t bytes, hipStream_t st);
 int comm_nranks(void *comm);
+PeerView comm_peer_wave(void *comm);
+int comm_peer_mcap(void *comm);
 
 // sharded tail form (IA_SHARD_TAIL): 0 [default] the exchange carries (distance, row) and
 // k_finish_gather does the coherence pick and the weighting after it; 1 the exact stage
@@ -281,7 +283,7 @@ struct LevelRun {
     DbSrc src{};
     ImgPair B{}, Bp{};
     int H = 0, W = 0, nw = 0, nranks = 1;
-    bool prof = false, timed = false, fused = false;
+    bool prof = false, timed = false, fused = false, peer = false;
     size_t ev0 = 0;
     unsigned long long *hstats = nullptr;
     double pairs = 0.0;
@@ -314,6 +316,11 @@ struct LevelRun {
         // on a sharded DB it prepares the tail (coherence pick, the winner's weighted
         // distance) before the exchange
         fused = !a->comm && !a->lsh && !sim;
+        // sharded level over the device-side exchange: the exact stage's kernel exchanges
+        // and finishes each pixel (no RCCL call, no finish launch)
+        peer = a->comm && comm_peer_mcap(a->comm) > 0;
+        IA_ARG(!peer || comm_peer_mcap(a->comm) >= Mmax,
+               "ia_synth_level: the peer exchange's box holds fewer queries than a wave");
         return IA_OK;
     }
 
@@ -336,10 +343,11 @@ struct LevelRun {
             return rc;
         hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
         hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
-        const FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
-                            a->im, a->dbg_px, a->dbg_dist,
-                            a->comm && shard_tail() ? ws.rec_local : nullptr,
-                            a->comm && shard_tail() ? ws.coh : nullptr};
+        FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
+                      a->im, a->dbg_px, a->dbg_dist,
+                      a->comm && !peer && shard_tail() ? ws.rec_local : nullptr,
+                      a->comm && !peer && shard_tail() ? ws.coh : nullptr};
+        if (peer) fa.px = comm_peer_wave(a->comm);
         if (a->lsh) {   // approximate matcher: the events bracket the LSH query kernel
             if (e0) IA_HIP(hipEventRecord(e0, sq));
             if ((rc = launch_lsh_match(a->lsh, src, a->row0, a->nrows, M, ws.q64, a->center,
@@ -349,7 +357,7 @@ struct LevelRun {
         } else if ((rc = launch_match(src, a->row0, a->nrows, a->db, a->dbi, ws.qp, ws.q16, M, ws.q64, ws.nq,
                                       a->amax, ws.scratch, ws.best_local,
                                       prof ? ws.stats : nullptr, sq, e0, e1,
-                                      (fused || (a->comm && shard_tail())) ? &fa : nullptr))) {
+                                      (fused || peer || (a->comm && shard_tail())) ? &fa : nullptr))) {
             return rc;
         }
         ++nscreen;
@@ -359,7 +367,7 @@ struct LevelRun {
         // dispatches in flight (rocprofv3 --pmc runs of the whole bench crash otherwise)
         static const int sync_every = env_int("IA_SYNC_EVERY", 0);
         if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
-        if (fused) return IA_OK;   // the exact stage already ran the per-pixel tail
+        if (fused || peer) return IA_OK;   // the exact stage already ran the per-pixel tail
         if (a->lsh) {   // one shard, LSH winners: the tail in k_lsh_finish form
             k_lsh_tail<<<M, 128, 0, sq>>>(src, ws.best_local, M, fa, ws.q64);
             IA_LAUNCH_CHECK("k_lsh_tail");

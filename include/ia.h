@@ -258,6 +258,21 @@ int ia_comm_unique_id(uint8_t out[128]);
 int ia_comm_init(const uint8_t uid[128], int nranks, int rank, void **comm);
 int ia_comm_destroy(void *comm);
 int ia_comm_nranks(void *comm);
+/* The device-side form of the same per-wave exchange (no RCCL call per wave): each rank
+ * owns a receive box (2 x nranks x mcap x 24 B of uncached device memory; mcap >= the most
+ * queries of any wave of the levels it serves), shared by IPC handle.  Per wave the exact
+ * stage's kernel writes its shard's (distance, row) winner into every rank's box, reads all
+ * ranks' winners from its own and finishes the pixel.  Usable wherever a
+ * communicator is (IaSynthArgs.comm, one per concurrently sharded level); destroyed by
+ * ia_comm_destroy.  Protocol: ia_peer_create on every rank -> exchange the 64-byte handles
+ * (rank order) -> ia_peer_connect -> a barrier -> ia_peer_check (a handshake wave; every
+ * rank at once).  ia_peer_status: IA_E_COMM if any wait of this rank timed out (10 s).
+ * ia_peer_mem_kind: 0 uncached, 1 fine-grained, 2 plain device memory. */
+int ia_peer_create(int nranks, int rank, int mcap, void **comm, uint8_t handle[64]);
+int ia_peer_connect(void *comm, const uint8_t *handles);
+int ia_peer_check(void *comm, void *stream);
+int ia_peer_status(void *comm);
+int ia_peer_mem_kind(void *comm);
 
 #ifdef __cplusplus
 }

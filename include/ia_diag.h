@@ -59,6 +59,16 @@ typedef struct {
 int ia_diag_synth_level_shards(const IaSynthArgs *a, const IaShardDb *shards, int n,
                                void *stream);
 
+/* the device-side exchange's protocol alone (ia.h ia_peer_*): nwaves waves of M queries,
+ * every rank publishing a known record per (wave, query); *bad = the number of (wave,
+ * query) whose collected records or minimum differ from the expected ones.  Every rank
+ * of the exchange calls it at once. */
+int ia_diag_peer_stress(void *comm, int nwaves, int M, int *bad, void *stream);
+/* with IA_PEER_TRACE=1 at ia_peer_create: per epoch < 1024 and query < 8 of the exact
+ * stage's exchange {own distance, own row, collected distance, collected row} (1024 x 8 x 4
+ * doubles) */
+int ia_diag_peer_trace(void *comm, double *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,9 +1,11 @@
 """Per-rank cost of the sharded c4 synthesis, simulated on one GPU (diagnostic).
 
 Runs the synthesis as rank `r` of G database shards (each level's rows
-`shard_rows(N, r, G)`), with a 1-rank RCCL communicator: the per-wave path is the
-sharded one (unfused exact stage, all-gather, k_finish), but the all-gather moves one
-shard's winners only, so the time excludes the real collective's xGMI latency.  The
+`shard_rows(N, r, G)`), with a 1-rank exchange (IA_EXCHANGE: rccl — unfused exact stage,
+all-gather, k_finish_gather; peer [default] — the exact stage's kernel publishes to and
+collects from its own box and finishes the pixel): the per-wave path is the sharded one,
+but the exchange moves one shard's winners only, so the time excludes the real xGMI
+latency.  The
 winners are this shard's, so B' differs from the real result: timing only.
 Per level wall time between torch.cuda.synchronize() calls (levels one at a time), and the
 whole step with the levels pipelined (ia_synth_levels, one communicator per sharded
@@ -11,7 +13,6 @@ level); second repetition reported.
 
 Usage: python tools/shard_sim.py G [G ...]        (G = 1 runs the sharded path unsharded)
 """
-import ctypes
 import os
 import sys
 import time
@@ -25,11 +26,7 @@ ip, cfg, ia, _ia = bench.ip, bench.cfg, bench.ia, bench._ia
 
 
 def one_rank_comm():
-    buf = ctypes.create_string_buffer(128)
-    _ia.check(_ia.lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
-    h = ctypes.c_void_p()
-    _ia.check(_ia.lib().ia_comm_init(buf.raw, 1, 0, ctypes.byref(h)), 'ia_comm_init')
-    return h
+    return _ia.exchange(0, 1)
 
 
 def main():
@@ -59,10 +56,11 @@ def main():
                               comm=comms, rank=0, nranks=G, pipeline=True)
             torch.cuda.synchronize()
             pipe.append((time.perf_counter() - t0) * 1e3)
-        print('G=%d rank0 %.1f ms/step (levels one at a time: ' % (G, tot) +
+        print('[%s] G=%d rank0 %.1f ms/step (levels one at a time: ' % (_ia.exchange_kind(), G, tot) +
               ' '.join('L%d %.1f' % (l, t) for l, t in sorted(res.items())) +
               '); pipelined %.1f ms/step' % min(pipe[1:]), flush=True)
     for cm in comms:
+        _ia.exchange_status(cm)
         _ia.lib().ia_comm_destroy(cm)
 
 
