@@ -12,6 +12,7 @@ library or a HIP device is missing.
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import torch  # noqa: F401  (must precede libia.so, see module doc)
@@ -305,14 +306,28 @@ def mean_dev(t):
     return float(out.item())
 
 
+_EXCHANGE_FALLBACK = []   # reasons the device-side exchange was replaced by RCCL
+
+
 def exchange_kind():
     """The per-wave exchange of sharded levels (IA_EXCHANGE): 'peer' [default] the
     device-side exchange (IPC-mapped receive boxes written by the exact stage's kernel),
-    'rccl' one ncclAllGather per wave plus a finish kernel.  Same results."""
+    'rccl' one ncclAllGather per wave plus a finish kernel.  Same results.  'peer' reads
+    'peer->rccl' once a peer exchange could not be set up on every rank (exchange())."""
     k = os.environ.get('IA_EXCHANGE', 'peer')
     if k not in ('peer', 'rccl'):
         raise ValueError('IA_EXCHANGE must be peer or rccl, not %r' % k)
-    return k
+    return 'peer->rccl' if k == 'peer' and _EXCHANGE_FALLBACK else k
+
+
+def _all_ok(ok, world):
+    """Every rank's flag (gloo/RCCL process group): True only if all ranks are ok."""
+    if world == 1:
+        return ok
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
 
 
 def exchange(rank, world, kind=None, mcap=4096):
@@ -320,10 +335,14 @@ def exchange(rank, world, kind=None, mcap=4096):
     torch.distributed process group: every rank calls it at the same point.  'rccl': an
     RCCL communicator (the unique id broadcast from rank 0).  'peer': receive boxes for
     waves of up to mcap queries, handles all-gathered, mapped, then a handshake wave
-    (include/ia.h).  Release with ia_comm_destroy."""
+    (include/ia.h).  If mapping or the handshake fails on any rank, every rank agrees on
+    it and falls back to RCCL (the reason is kept in _EXCHANGE_FALLBACK; exchange_kind()
+    then reports 'peer->rccl').  Release with ia_comm_destroy."""
     import torch.distributed as dist
     kind = kind or exchange_kind()
     h = ctypes.c_void_p()
+    if kind == 'peer->rccl':
+        kind = 'rccl'
     if kind == 'rccl':
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
@@ -343,12 +362,22 @@ def exchange(rank, world, kind=None, mcap=4096):
         dist.all_gather(parts, mine)
     else:
         parts = [mine]
-    check(lib().ia_peer_connect(h, b''.join(p.numpy().tobytes() for p in parts)),
-          'ia_peer_connect')
-    if world > 1:
-        dist.barrier()
-    check(lib().ia_peer_check(h, stream()), 'ia_peer_check')
-    return h
+    why = None
+    if lib().ia_peer_connect(h, b''.join(p.numpy().tobytes() for p in parts)) != 0:
+        why = 'rank %d: %s' % (rank, lib().ia_last_error().decode())
+    if _all_ok(why is None, world):
+        if lib().ia_peer_check(h, stream()) != 0:
+            why = 'rank %d: %s' % (rank, lib().ia_last_error().decode())
+        if _all_ok(why is None, world):
+            return h
+    # some rank could not map or reach the others' boxes: every rank drops its peer
+    # exchange and takes the RCCL one
+    torch.cuda.synchronize()
+    lib().ia_comm_destroy(h)
+    _EXCHANGE_FALLBACK.append(why or 'another rank failed')
+    print('ia: device-side exchange unusable (%s); falling back to RCCL' % _EXCHANGE_FALLBACK[-1],
+          file=sys.stderr, flush=True)
+    return exchange(rank, world, 'rccl', mcap)
 
 
 def exchange_status(comm):

@@ -273,3 +273,74 @@ def test_threaded_oracle_scan_equals_serial():
     ref = [int(np.argmin(np.add.reduce((As - q) ** 2, axis=1))) for q in Q]
     assert list(i1) == ref == serial == par and list(i5) == ref
     assert np.array_equal(d1, d5)
+
+
+# ---- device-side exchange setup: agreed fallback to RCCL (gloo, 2 ranks, fake library) ---------
+
+class _FakeLib:
+    """Stands in for libia.so's exchange entries: rank `bad` cannot map a peer's box."""
+    def __init__(self, rank, bad, log):
+        self.rank, self.bad, self.log = rank, bad, log
+
+    def ia_peer_create(self, world, rank, mcap, h, hd):
+        self.log.append('peer_create')
+        return 0
+
+    def ia_peer_connect(self, h, handles):
+        self.log.append('peer_connect')
+        return 7 if self.rank == self.bad else 0
+
+    def ia_peer_check(self, h, st):
+        self.log.append('peer_check')
+        return 0
+
+    def ia_comm_destroy(self, h):
+        self.log.append('destroy')
+        return 0
+
+    def ia_last_error(self):
+        return b'hipIpcOpenMemHandle: invalid argument'
+
+    def ia_comm_unique_id(self, buf):
+        self.log.append('unique_id')
+        return 0
+
+    def ia_comm_init(self, uid, world, rank, h):
+        self.log.append('comm_init')
+        return 0
+
+
+def _fallback_worker(rank, world, port, bad, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ.pop('IA_EXCHANGE', None)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import _ia
+    log = []
+    fake = _FakeLib(rank, bad, log)
+    _ia.lib = lambda: fake
+    _ia.stream = lambda: None
+    torch.cuda.synchronize = lambda *a: None
+    _ia.exchange(rank, world)
+    out[rank] = (log, _ia.exchange_kind())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('bad', [-1, 1])
+def test_peer_exchange_setup_falls_back_to_rccl_on_every_rank(bad):
+    """_ia.exchange: when one rank cannot map the others' receive boxes, every rank (not
+    only the failing one) drops the device-side exchange and builds the RCCL one, so the
+    ranks never disagree on the per-wave protocol; with every rank fine, no RCCL setup."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 31500 + np.random.RandomState(bad + 5).randint(0, 2000)
+    mp.spawn(_fallback_worker, args=(world, port, bad, out), nprocs=world, join=True)
+    for r in range(world):
+        log, kind = out[r]
+        if bad < 0:
+            assert log == ['peer_create', 'peer_connect', 'peer_check'] and kind == 'peer'
+        else:
+            assert log[:2] == ['peer_create', 'peer_connect'] and 'peer_check' not in log
+            assert log[2:] == ['destroy'] + (['unique_id'] if r == 0 else []) + ['comm_init']
+            assert kind == 'peer->rccl'
