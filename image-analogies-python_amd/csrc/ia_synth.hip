@@ -653,9 +653,31 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
         blk[j].assign((run[j].nw + PIPE_BLOCK - 1) / PIPE_BLOCK, nullptr);
     }
     // enqueue level j through wave `target` (and the coarse waves it needs, first)
-    std::function<int(int, int)> advance = [&](int j, int target) -> int {
+    // Levels whose DB is sharded over several ranks never overlap one another: each one's first wave
+    // waits for the previous multi-rank level's last.  Their exact stages wait in-kernel
+    // for the other ranks' records (or in RCCL's kernels); two such levels resident at once
+    // on every rank can fill the CUs with waiting workgroups (k_rescore: 2 per CU) while
+    // the workgroups they wait for sit queued behind them on another rank: a cross-level
+    // deadlock (seen with two ranks on one GPU; on separate GPUs c4's two sharded levels
+    // hold up to 513 such workgroups for 512 slots).  One level at a time, a rank's only
+    // waiting kernel is the wave every other rank is also on.  Replicated levels still
+    // overlap them.
+    auto multi_rank = [&](int j) {
+        return levels[j].comm != nullptr && levels[j].nrows < levels[j].N_total;
+    };
+    std::function<int(int, int)> advance;
+    advance = [&](int j, int target) -> int {
         hipStream_t sj = g_pipe.streams[j];
         if (target > run[j].nw - 1) target = run[j].nw - 1;
+        if (next[j] == 0 && target >= 0 && multi_rank(j)) {
+            for (int i = j - 1; i >= 0; --i) {
+                if (!multi_rank(i)) continue;
+                int rc = advance(i, run[i].nw - 1);
+                if (rc) return rc;
+                IA_HIP(hipStreamWaitEvent(sj, blk[i].back(), 0));
+                break;
+            }
+        }
         while (next[j] <= target) {
             const int t = next[j];
             if (j > 0) {
