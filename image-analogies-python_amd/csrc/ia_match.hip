@@ -660,11 +660,13 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     // the exact stage re-screens from the image form whenever there is one (the row form
     // need not exist then)
     const bool im = dbi != nullptr;
-    // default: the work list for levels above 2^20 rows (where k_rescore's per-query
-    // serialisation costs most); k_rescore below, with or without the fused tail (a
-    // sharded rank's 0.5 M-row shard: 13.9 vs 19.9 us per wave, profiles/r01_shard_sim_g8.txt)
+    // default: k_rescore (one workgroup per query, with or without the fused tail; a
+    // sharded rank's 0.5 M-row shard: 13.9 vs 19.9 us per wave, profiles/r01_shard_sim_g8.txt),
+    // except on row-form levels above 2^20 rows, where its per-query serialisation costs
+    // most and the work list wins.  On the image form k_rescore wins at every size (c4's
+    // 4.19 M-row finest level: 1637-1643 vs 1667-1669 ms/step, profiles/r02_ab_rescore.txt)
     const int mode = !fin ? 0 : fin->shard_out ? 2 : fin->px.nranks ? 3 : 1;
-    if (rm == 1 || (rm < 0 && nrows > (1L << 20))) {
+    if (rm == 1 || (rm < 0 && !im && nrows > (1L << 20))) {
         const long nseg = db_nsegs(nrows);
         k_select<<<M, 256, 0, st>>>(nseg, ws.segmin, nq, amax, ws.ctr, ws.items, ws.sel, stats);
         IA_LAUNCH_CHECK("k_select");
