@@ -401,7 +401,7 @@ constexpr int WIN_B = WB_FINE + WB_COARSE + WB_NORM;         // 6592
 constexpr int WIN_PIECES = WIN_B / 16;                       // 412
 static_assert(WIN_PIECES <= 512, "two wave-instructions per wave stage the window");
 
-struct ImgDb {
+struct LabImgDb {
     const uint32_t *fa, *fp, *ca, *cp, *norm;
     int W, Wp, Wcp;       // image width, padded fine / coarse widths
 };
@@ -418,7 +418,7 @@ __host__ __device__ constexpr int win_off(int k) {
 __host__ __device__ constexpr bool win_coarse(int k) { return k < 9 || (k >= 34 && k < 43); }
 
 template <int G, int W>
-__device__ __forceinline__ void img_body(ImgDb im, half8 *E, char *wbuf, int *smin, long crow0,
+__device__ __forceinline__ void img_body(LabImgDb im, half8 *E, char *wbuf, int *smin, long crow0,
                                          int nstage, int tps, const half8 *__restrict__ q16) {
     constexpr int T0 = bal_t0(G, W), NS = bal_ns(G, W);
     constexpr int H = W & 1;                    // this wave expands lane half H of 2 tiles
@@ -536,7 +536,7 @@ __device__ __forceinline__ void img_body(ImgDb im, half8 *E, char *wbuf, int *sm
 }
 
 template <int G>
-__global__ __launch_bounds__(256, 2) void k_lab_img(ImgDb im, int nchunks, int ch, int seg_rows,
+__global__ __launch_bounds__(256, 2) void k_lab_img(LabImgDb im, int nchunks, int ch, int seg_rows,
                                                     const half8 *__restrict__ q16, int M, int groups,
                                                     float *__restrict__ segmin, long nseg) {
     __shared__ half8 E[STAGE_H8];
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void k_lab_img(ImgDb im, int nchunks, int c
     }
 }
 
-static ImgDb g_img;
+static LabImgDb g_img;
 static inline int symi_h(int i, int n) {
     const int p = 2 * n; i %= p; if (i < 0) i += p; return i >= n ? p - 1 - i : i;
 }
@@ -611,7 +611,7 @@ static void build_img(const ScreenSetup &su) {
         CK(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
         return (const uint32_t *)d;
     };
-    g_img = ImgDb{up(fa), up(fp), up(ca), up(cp), up(nr), W, Wp, Wcp};
+    g_img = LabImgDb{up(fa), up(fp), up(ca), up(cp), up(nr), W, Wp, Wcp};
     printf("image-form DB: %.1f MB (row form %.1f MB)\n",
            (2.0 * fa.size() + 2.0 * ca.size() + nr.size()) * 4 / 1e6, su.npad * 224 / 1e6);
 }
