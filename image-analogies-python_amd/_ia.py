@@ -18,7 +18,8 @@ import numpy as np
 import torch  # noqa: F401  (must precede libia.so, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libia.so')
+# IA_LIB_PATH: another build of the same library (A/B of build variants, tools/ab_lib.sh)
+LIB_PATH = os.environ.get('IA_LIB_PATH') or os.path.join(_HERE, 'libia.so')
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'ia.h')
 
 IA_D = 55

@@ -274,11 +274,23 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
     }
 }
 
-// Exact stage, one workgroup per query: waves 0-3 screen and rescore; with the pixel tail
-// (MODE 1, 2: exact_tail) a fifth wave picks the coherence candidate meanwhile (it needs
-// only s / im of earlier waves), so the tail after the winner is one gather round.
+// IA_RESCORE_FIFTH (build switch, default 0): with 1, MODE 1-3 add a fifth wave that picks
+// the coherence candidate during the row loop.  The kernel needs ~250 VGPRs (2 waves per
+// SIMD), so a 5-wave workgroup leaves room for one per CU: 256 resident, and c4's 342-query
+// waves ran in two rounds.  4 waves fit two per CU (all 342 at once; wave 1 picks coherence
+// in the tail beside wave 0's weighting instead; profiles/r02_ab_fifth.txt).
+// (Forcing 3 waves per SIMD instead spills ~110 VGPRs: 1,700 ms/step, r02_ab_rescore_occ.)
+#ifndef IA_RESCORE_FIFTH
+#define IA_RESCORE_FIFTH 0
+#endif
+constexpr bool RESCORE_FIFTH = IA_RESCORE_FIFTH != 0;
+constexpr int rescore_threads(int mode) { return mode != 0 && RESCORE_FIFTH ? 320 : 256; }
+
+// Exact stage, one workgroup per query: waves 0-3 screen and rescore, then the pixel tail
+// (MODE 1-3: exact_tail; with IA_RESCORE_FIFTH a fifth wave picks the coherence candidate
+// during the row loop, since it needs only s / im of earlier waves).
 template <int MODE, bool IMG>
-__global__ __launch_bounds__(MODE == 0 ? 256 : 320, IMG ? 2 : 1) void k_rescore(
+__global__ __launch_bounds__(rescore_threads(MODE), IMG ? 2 : 1) void k_rescore(
         DbSrc src, long row0, long nrows, long nseg, int seg_rows,
         const float *__restrict__ segmin, const half8 *__restrict__ db, ImgDb im,
         const float *__restrict__ qp, const double *__restrict__ q64,
@@ -427,7 +439,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 320, IMG ? 2 : 1) void k_rescore(
             atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
-    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, true);
+    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, RESCORE_FIFTH);
 }
 
 // ---------------------------------------------------------------------------------
@@ -690,7 +702,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         return IA_OK;
     }
 #define IA_RESCORE_CASE(MD, IM)                                                                  \
-    k_rescore<MD, IM><<<M, MD == 0 ? 256 : 320, 0, st>>>(src, row0, nrows, db_nsegs(nrows),      \
+    k_rescore<MD, IM><<<M, rescore_threads(MD), 0, st>>>(src, row0, nrows, db_nsegs(nrows),      \
                                                          db_seg_rows(nrows), ws.segmin, db, img, \
                                                          qp, q64, nq, amax, best, stats, fa)
     if (im) {
