@@ -274,23 +274,20 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
     }
 }
 
-// IA_RESCORE_FIFTH (build switch, default 0): with 1, MODE 1-3 add a fifth wave that picks
-// the coherence candidate during the row loop.  The kernel needs ~250 VGPRs (2 waves per
-// SIMD), so a 5-wave workgroup leaves room for one per CU: 256 resident, and c4's 342-query
-// waves ran in two rounds.  4 waves fit two per CU (all 342 at once; wave 1 picks coherence
-// in the tail beside wave 0's weighting instead; profiles/r02_ab_fifth.txt).
-// (Forcing 3 waves per SIMD instead spills ~110 VGPRs: 1,700 ms/step, r02_ab_rescore_occ.)
-#ifndef IA_RESCORE_FIFTH
-#define IA_RESCORE_FIFTH 0
-#endif
-constexpr bool RESCORE_FIFTH = IA_RESCORE_FIFTH != 0;
-constexpr int rescore_threads(int mode) { return mode != 0 && RESCORE_FIFTH ? 320 : 256; }
+// The fifth wave (FIFTH, MODE 1-3): picks the coherence candidate during the row loop
+// instead of in the tail.  k_rescore needs ~250 VGPRs (2 waves per SIMD, 8 per CU), so a
+// 5-wave workgroup leaves room for one per CU (256 resident) and 4-wave ones for two
+// (512).  A wave of more than 256 queries (c4's plateau: 342) runs 4-wave, in one round
+// instead of two; smaller waves keep the fifth wave's overlap (profiles/r02_ab_fifth.txt).
+// (Forcing 3 waves per SIMD spills ~110 VGPRs: r02_ab_rescore_occ.)
+constexpr int RESCORE_FIFTH_MAX_M = 256;
+constexpr int rescore_threads(int mode, bool fifth) { return mode != 0 && fifth ? 320 : 256; }
 
 // Exact stage, one workgroup per query: waves 0-3 screen and rescore, then the pixel tail
 // (MODE 1-3: exact_tail; with IA_RESCORE_FIFTH a fifth wave picks the coherence candidate
 // during the row loop, since it needs only s / im of earlier waves).
-template <int MODE, bool IMG>
-__global__ __launch_bounds__(rescore_threads(MODE), IMG ? 2 : 1) void k_rescore(
+template <int MODE, bool IMG, bool FIFTH>
+__global__ __launch_bounds__(rescore_threads(MODE, FIFTH), IMG ? 2 : 1) void k_rescore(
         DbSrc src, long row0, long nrows, long nseg, int seg_rows,
         const float *__restrict__ segmin, const half8 *__restrict__ db, ImgDb im,
         const float *__restrict__ qp, const double *__restrict__ q64,
@@ -439,7 +436,7 @@ __global__ __launch_bounds__(rescore_threads(MODE), IMG ? 2 : 1) void k_rescore(
             atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
-    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, RESCORE_FIFTH);
+    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, FIFTH && MODE != 0);
 }
 
 // ---------------------------------------------------------------------------------
@@ -701,10 +698,15 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         IA_LAUNCH_CHECK("k_gather");
         return IA_OK;
     }
+#define IA_RESCORE_LAUNCH(MD, IM, F)                                                            \
+    k_rescore<MD, IM, F><<<M, rescore_threads(MD, F), 0, st>>>(src, row0, nrows, db_nsegs(nrows), \
+                                                               db_seg_rows(nrows), ws.segmin, db, \
+                                                               img, qp, q64, nq, amax, best, stats, fa)
 #define IA_RESCORE_CASE(MD, IM)                                                                  \
-    k_rescore<MD, IM><<<M, rescore_threads(MD), 0, st>>>(src, row0, nrows, db_nsegs(nrows),      \
-                                                         db_seg_rows(nrows), ws.segmin, db, img, \
-                                                         qp, q64, nq, amax, best, stats, fa)
+    do {                                                                                         \
+        if (MD != 0 && M <= RESCORE_FIFTH_MAX_M) IA_RESCORE_LAUNCH(MD, IM, true);                \
+        else IA_RESCORE_LAUNCH(MD, IM, false);                                                   \
+    } while (0)
     if (im) {
         if (mode == 3) IA_RESCORE_CASE(3, true);
         else if (mode == 2) IA_RESCORE_CASE(2, true);
@@ -716,6 +718,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         else if (mode == 1) IA_RESCORE_CASE(1, false);
         else IA_RESCORE_CASE(0, false);
     }
+#undef IA_RESCORE_LAUNCH
 #undef IA_RESCORE_CASE
     IA_LAUNCH_CHECK("k_rescore");
     return IA_OK;
