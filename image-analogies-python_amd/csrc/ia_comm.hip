@@ -8,9 +8,9 @@
 // collective.
 //
 // The second form of the same exchange is device-side (PeerView, ia_internal.h): each rank's
-// receive box is IPC-mapped into every rank, and the exact stage's kernel itself publishes
-// its winner into every box, collects all ranks' winners from its own box and finishes the
-// pixel — no host call, no collective kernel and no separate finish launch per wave.
+// receive box is IPC-mapped into every rank; the exact stage's kernel publishes its winner
+// into every box, and k_peer_finish collects all ranks' winners from its own box and
+// finishes the pixel — no host call and no collective kernel per wave.
 #include "ia_finish.h"
 
 #include <rccl/rccl.h>

@@ -227,33 +227,15 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double d_app = 0.0;
     if (MODE == 3) {
-        // device-side exchange: wave 0 hands this shard's winner to every rank, collects
-        // every rank's (ia_finish.h peer_publish / peer_collect) and weighs the global
-        // winner; wave 1 picks the coherence candidate meanwhile (unless already picked)
+        // device-side exchange: wave 0 hands this shard's winner to every rank's receive box
+        // (ia_finish.h peer_publish); k_peer_finish (ia_synth.hip), the next launch,
+        // collects every rank's and finishes the pixel.  Nothing here waits on another
+        // rank, so this kernel's large workgroups never hold CUs while they wait.
         // (win / bd come from LDS words lane 0 of wave 0 wrote just before the call: only
         // that lane's copy is certain, and every publishing lane needs it)
         bd = __shfl(bd, 0);
         win = __shfl(win, 0);
-        double gd = bd;
-        long long gw = win;
-        if (wv == 0) {
-            peer_publish(fa.px, q, bd, win, lane);
-            const bool tron = fa.px.trace && q < 8 && fa.px.epoch < 1024;
-            unsigned long long *tr = tron ? reinterpret_cast<unsigned long long *>(fa.px.trace) +
-                                                ((long)fa.px.epoch * 8 + q) * 12
-                                          : nullptr;
-            peer_collect(fa.px, q, lane, gd, gw, tr ? tr + 4 : nullptr);
-            if (tr && lane == 0) {
-                tr[0] = __double_as_longlong(bd); tr[1] = win;
-                tr[2] = __double_as_longlong(gd); tr[3] = gw;
-            }
-            d_app = app_wdist(src, gw, fa, qs, lane);
-        } else if (wv == 1 && !have_cs) {
-            const CohSel c = coh_pick(src, q, fa, qs, lane);
-            if (lane == 0) *cs = c;
-        }
-        if (!have_cs) __syncthreads();
-        if (wv == 0) finish_apply(src, gw, q, fa, *cs, d_app, lane);
+        if (wv == 0) peer_publish(fa.px, q, bd, win, lane);
         return;
     }
     if (wv == 1 && !have_cs) {
@@ -281,7 +263,7 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
 // instead of two; smaller waves keep the fifth wave's overlap (profiles/r02_ab_fifth.txt).
 // (Forcing 3 waves per SIMD spills ~110 VGPRs: r02_ab_rescore_occ.)
 constexpr int RESCORE_FIFTH_MAX_M = 256;
-constexpr int rescore_threads(int mode, bool fifth) { return mode != 0 && fifth ? 320 : 256; }
+constexpr int rescore_threads(int mode, bool fifth) { return mode != 0 && mode != 3 && fifth ? 320 : 256; }
 
 // Exact stage, one workgroup per query: waves 0-3 screen and rescore, then the pixel tail
 // (MODE 1-3: exact_tail; with IA_RESCORE_FIFTH a fifth wave picks the coherence candidate
@@ -436,7 +418,7 @@ __global__ __launch_bounds__(rescore_threads(MODE, FIFTH), IMG ? 2 : 1) void k_r
             atomicAdd(&sl[2], full ? 1ULL : 0ULL);
         }
     }
-    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, FIFTH && MODE != 0);
+    exact_tail<MODE>(src, q, win, wind, fa, qs, &cs, FIFTH && MODE != 0 && MODE != 3);
 }
 
 // ---------------------------------------------------------------------------------
@@ -605,7 +587,7 @@ __global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restric
         }
         if (m == 0 && lane == 0) *ctr = 0;   // every k_items block has read it
         if (lane == 0) {
-            if (MODE == 0) best[m] = Best{bd, bi};
+            if (MODE == 0 || MODE == 3) best[m] = Best{bd, bi};
             win = bi;
             wind = bd;
         }
@@ -704,7 +686,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
                                                                img, qp, q64, nq, amax, best, stats, fa)
 #define IA_RESCORE_CASE(MD, IM)                                                                  \
     do {                                                                                         \
-        if (MD != 0 && M <= RESCORE_FIFTH_MAX_M) IA_RESCORE_LAUNCH(MD, IM, true);                \
+        if (MD != 0 && MD != 3 && M <= RESCORE_FIFTH_MAX_M) IA_RESCORE_LAUNCH(MD, IM, true);                \
         else IA_RESCORE_LAUNCH(MD, IM, false);                                                   \
     } while (0)
     if (im) {

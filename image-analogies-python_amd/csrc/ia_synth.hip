@@ -92,6 +92,44 @@ __global__ __launch_bounds__(128) void k_finish_gather(DbSrc src, const Best *__
     if (wv == 0) finish_apply(src, app, m, f, cs, d_app, lane);
 }
 
+// Sharded DB over the device-side exchange: the exact stage published this shard's winner
+// (k_rescore<3> / k_gather<3>, which also left it in best[m]); wave 0 collects every
+// rank's from this rank's receive box and weighs the global winner while wave 1 picks the
+// coherence candidate, then wave 0 finishes the pixel.  The waits live in these small
+// 2-wave workgroups, not in the exact stage's 4-wave, 250-VGPR ones: ranks sharing a GPU,
+// or a rank's other streams, keep room to run the kernels the waits depend on (the fused
+// form deadlocked two ranks on one GPU).  On timeout the shard's own winner.
+__global__ __launch_bounds__(128) void k_peer_finish(DbSrc src, const Best *__restrict__ best,
+                                                     FinishArgs f, const double *__restrict__ q64) {
+    __shared__ double qs[IA_DP];
+    __shared__ CohSel cs;
+    const int m = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double qv = threadIdx.x < IA_DP ? q64[(long)m * IA_DP + threadIdx.x] : 0.0;
+    const Best own = best[m];
+    if (threadIdx.x < IA_DP) qs[threadIdx.x] = qv;
+    __syncthreads();
+    double gd = own.d;
+    long long gw = own.idx;
+    if (wv == 1) {
+        const CohSel c = coh_pick(src, m, f, qs, lane);
+        if (lane == 0) cs = c;
+    } else {
+        const bool tron = f.px.trace && m < 8 && f.px.epoch < 1024;
+        unsigned long long *tr = tron ? reinterpret_cast<unsigned long long *>(f.px.trace) +
+                                            ((long)f.px.epoch * 8 + m) * 12
+                                      : nullptr;
+        peer_collect(f.px, m, lane, gd, gw, tr ? tr + 4 : nullptr);
+        if (tr && lane == 0) {
+            tr[0] = __double_as_longlong(own.d); tr[1] = own.idx;
+            tr[2] = __double_as_longlong(gd); tr[3] = gw;
+        }
+    }
+    const double d_app = wv == 0 ? app_wdist(src, gw, f, qs, lane) : 0.0;
+    __syncthreads();
+    if (wv == 0) finish_apply(src, gw, m, f, cs, d_app, lane);
+}
+
 // LSH matcher (one shard): wave 1 picks the coherence candidate while wave 0 weighs the
 // LSH winner, then wave 0 finishes the pixel (ia_finish.h)
 __global__ __launch_bounds__(128) void k_lsh_tail(DbSrc src, const Best *__restrict__ best, int M,
@@ -316,8 +354,8 @@ struct LevelRun {
         // on a sharded DB it prepares the tail (coherence pick, the winner's weighted
         // distance) before the exchange
         fused = !a->comm && !a->lsh && !sim;
-        // sharded level over the device-side exchange: the exact stage's kernel exchanges
-        // and finishes each pixel (no RCCL call, no finish launch)
+        // sharded level over the device-side exchange: the exact stage's kernel publishes,
+        // k_peer_finish collects and finishes each pixel (no RCCL call)
         peer = a->comm && comm_peer_mcap(a->comm) > 0;
         IA_ARG(!peer || comm_peer_mcap(a->comm) >= Mmax,
                "ia_synth_level: the peer exchange's box holds fewer queries than a wave");
@@ -367,7 +405,12 @@ struct LevelRun {
         // dispatches in flight (rocprofv3 --pmc runs of the whole bench crash otherwise)
         static const int sync_every = env_int("IA_SYNC_EVERY", 0);
         if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
-        if (fused || peer) return IA_OK;   // the exact stage already ran the per-pixel tail
+        if (fused) return IA_OK;   // the exact stage already ran the per-pixel tail
+        if (peer) {                // collect the ranks' winners, finish the pixel
+            k_peer_finish<<<M, 128, 0, sq>>>(src, ws.best_local, fa, ws.q64);
+            IA_LAUNCH_CHECK("k_peer_finish");
+            return IA_OK;
+        }
         if (a->lsh) {   // one shard, LSH winners: the tail in k_lsh_finish form
             k_lsh_tail<<<M, 128, 0, sq>>>(src, ws.best_local, M, fa, ws.q64);
             IA_LAUNCH_CHECK("k_lsh_tail");

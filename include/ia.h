@@ -261,8 +261,9 @@ int ia_comm_nranks(void *comm);
 /* The device-side form of the same per-wave exchange (no RCCL call per wave): each rank
  * owns a receive box (2 x nranks x mcap x 24 B of uncached device memory; mcap >= the most
  * queries of any wave of the levels it serves), shared by IPC handle.  Per wave the exact
- * stage's kernel writes its shard's (distance, row) winner into every rank's box, reads all
- * ranks' winners from its own and finishes the pixel.  Usable wherever a
+ * stage's kernel writes its shard's (distance, row) winner into every rank's box, and a
+ * small finish kernel reads all ranks' winners from its own and finishes the pixel
+ * (DESIGN.md §7).  Usable wherever a
  * communicator is (IaSynthArgs.comm, one per concurrently sharded level); destroyed by
  * ia_comm_destroy.  Protocol: ia_peer_create on every rank -> exchange the 64-byte handles
  * (rank order) -> ia_peer_connect -> a barrier -> ia_peer_check (a handshake wave; every
