@@ -696,17 +696,22 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
         blk[j].assign((run[j].nw + PIPE_BLOCK - 1) / PIPE_BLOCK, nullptr);
     }
     // enqueue level j through wave `target` (and the coarse waves it needs, first)
-    // Levels whose DB is sharded over several ranks never overlap one another: each one's first wave
-    // waits for the previous multi-rank level's last.  Their exact stages wait in-kernel
-    // for the other ranks' records (or in RCCL's kernels); two such levels resident at once
-    // on every rank can fill the CUs with waiting workgroups (k_rescore: 2 per CU) while
-    // the workgroups they wait for sit queued behind them on another rank: a cross-level
-    // deadlock (seen with two ranks on one GPU; on separate GPUs c4's two sharded levels
-    // hold up to 513 such workgroups for 512 slots).  One level at a time, a rank's only
-    // waiting kernel is the wave every other rank is also on.  Replicated levels still
-    // overlap them.
+    // Levels whose DB is sharded over several ranks and exchanged over RCCL never overlap
+    // one another: each one's first wave waits for the previous such level's last.  RCCL's
+    // kernels wait in-kernel for the other ranks, and two communicators in flight on
+    // different streams can deadlock when the waiting kernels hold the CUs the awaited
+    // ones need.  The same held for the first device-side exchange, whose waits sat inside
+    // the exact stage's 4-wave, 250-VGPR workgroups (two bench ranks on one GPU deadlocked
+    // on c3 with the levels pipelined).  Its waits now live in k_peer_finish's small 2-wave
+    // workgroups (c4: at most (171 + 342) x 2 waves of 152 VGPRs when two sharded levels
+    // overlap, a quarter of a GPU's wave slots), so those levels overlap: 3 ranks sharing
+    // one GPU with every c3 level sharded and overlapping complete, and the simulated
+    // G = 8 rank gains 3.6 % (profiles/r02_shard_overlap.txt).  IA_SHARD_OVERLAP=0
+    // serializes them too.
+    static const int overlap = env_int("IA_SHARD_OVERLAP", 1);
     auto multi_rank = [&](int j) {
-        return levels[j].comm != nullptr && levels[j].nrows < levels[j].N_total;
+        if (levels[j].comm == nullptr || levels[j].nrows >= levels[j].N_total) return false;
+        return !(overlap && comm_peer_mcap(levels[j].comm) > 0);
     };
     std::function<int(int, int)> advance;
     advance = [&](int j, int target) -> int {
