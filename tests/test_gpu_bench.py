@@ -50,3 +50,24 @@ def test_bench_contract_c5_streams(gpu):
     check_contract(d, 1, 1)
     assert d['scaling'] == 'weak' and d['config']['streams_per_gpu'] == 2
     assert d['checks']['concurrent_identical'] is True
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_sharing_the_gpu_equal_one_rank(gpu):
+    """bench.py --gpus 2 as the driver's multi-GPU run starts it (its own launcher), both
+    ranks on the box's one GPU (IA_SHARE_GPU=1) with every c1 level sharded over the
+    device-side exchange: one JSON line with n_gpus 2, identical replicas, and the 1-rank
+    checksum (the sharded synthesis is exact)."""
+    one = run_bench('--config', 'c1', '--steps', '1', '--warmup', '0', '--no-cpu-baseline')
+    env = dict(os.environ, IA_SHARE_GPU='1', IA_SHARD_MIN_ROWS='0')
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--config', 'c1', '--steps', '1', '--warmup', '0', '--no-cpu-baseline'],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    two = json.loads(lines[0])
+    assert two['n_gpus'] == 2 and two['config']['parallelism'] == 'db-shard2'
+    assert two['config']['exchange'].startswith('peer')
+    assert two['checks']['replicas_identical'] is True
+    assert two['checks']['checksum'] == one['checks']['checksum']
