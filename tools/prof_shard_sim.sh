@@ -12,7 +12,7 @@ d = collections.defaultdict(list)
 rows = list(csv.DictReader(open(sys.argv[1])))
 for r in rows:
     n = r['Kernel_Name']
-    if any(k in n for k in ('k_rescore', 'finish_gather', 'k_query_wave', 'copyBuffer', 'k_screen16iILi11', 'k_gather', 'k_items', 'k_select')):
+    if any(k in n for k in ('k_rescore', 'finish_gather', 'k_peer_finish', 'k_query_wave', 'copyBuffer', 'k_screen16iILi11', 'k_gather', 'k_items', 'k_select')):
         d[n.split('(')[0][:40]].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
 for k, v in d.items():
     print(k, len(v), 'p10 %.1f p50 %.1f p90 %.1f us' % tuple(np.percentile(np.array(v), [10, 50, 90])))
