@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0
 # level's plateau waves: 321-342 queries x 4,194,304 rows), from rocprofv3 PMC passes of
 # bench.py itself (tools/pmc_bench.sh: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process)
-SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r02_screen_traffic_bench_pmc.json')
+SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r02_final_screen_traffic_bench_pmc.json')
 
 
 def screen_pmc():
