@@ -112,6 +112,7 @@ _SIGS = {
     'ia_level_features3_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int, _dp, _dp]),
     'ia_synth_levels': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
+    'ia_synth_status': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
     'ia_lsh_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp,
                                     ctypes.POINTER(IaLsh), _dp]),
@@ -136,6 +137,7 @@ _SIGS = {
     # diagnostics (include/ia_diag.h)
     'ia_diag_set_rescore_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_graph_mode': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_xwave': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_pyr_form': (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
@@ -195,6 +197,13 @@ def graph_mode(mode=-1):
     """HIP-graph capture of the synthesis wave loop for this process (0 off [default],
     1 levels <= 2^18 rows, 2 all single-GPU levels); returns the previous value."""
     return lib().ia_diag_set_graph_mode(int(mode))
+
+
+def xwave(on=-1):
+    """The fused per-wave kernel for this process (1: one launch per wave after the screen
+    runs the exact stage, the device-side exchange, the per-pixel tail and the next wave's
+    query rows [default, IA_XWAVE]; 0: the separate kernels); returns the previous value."""
+    return lib().ia_diag_set_xwave(int(on))
 
 
 def db_image_enabled():

@@ -26,8 +26,7 @@ __global__ void k_level_features(ImgPair p, int full, double *out) {
     }
 }
 
-// MFMA operand order of element k = 2s + h: position h*28 + s (the fp32 query rows qp).
-__device__ __forceinline__ int perm56(int k) { return (k & 1) * 28 + (k >> 1); }
+// (perm56, the MFMA operand order of the fp32 query rows qp: ia_split16.h)
 
 // Centred row of DB row ix: my[k] = fl32(a_k - c_k) (k < 55), my[55] = fl32(|a - c|^2)
 // (fp64 sum in feature order).

@@ -128,7 +128,7 @@ __device__ __forceinline__ void finish_apply(const DbSrc &src, long long app, in
 // granules of (slot, source rank, query) in a receive box
 __device__ __forceinline__ unsigned long long *peer_cell(unsigned long long *box, const PeerView &p,
                                                          int src, int q) {
-    return box + (((long)(p.epoch & 1) * p.nranks + src) * p.mcap + q) * 3;
+    return box + (((long)(p.epoch & 1) * p.nranks + src) * p.mcap + q) * PEER_CELL;
 }
 // rank g's box pointer (selects over the kernel argument, not an indexed private copy)
 __device__ __forceinline__ unsigned long long *peer_box(const PeerView &p, int g) {
@@ -198,6 +198,83 @@ __device__ __forceinline__ bool peer_collect(const PeerView &p, int q, int lane,
     }
     bd = d;
     bi = i;
+    return true;
+}
+
+// ---- the fused per-wave kernel's records (k_xwave, ia_xwave.hip) ---------------------
+// one rank's exact winner of one query: distance, global row, the row's weighted (kappa)
+// distance to the query and its A' value (the B' value it would write)
+struct XRec {
+    double d;
+    long long i;
+    double wd, val;
+};
+__device__ __forceinline__ void xrec_take(XRec &b, const XRec &o) {
+    if (o.d < b.d || (o.d == b.d && o.i < b.i)) b = o;
+}
+// lexicographic (distance, row) minimum over the wave, valid in every lane
+__device__ __forceinline__ XRec xrec_wave_min(XRec b) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const XRec x{__shfl_xor(b.d, o), __shfl_xor(b.i, o), __shfl_xor(b.wd, o), __shfl_xor(b.val, o)};
+        xrec_take(b, x);
+    }
+    return b;
+}
+// lanes g < nranks: this rank's record of query q into rank g's box, 7 granules
+// {epoch << 32 | 32-bit payload} (d lo/hi, row, wd lo/hi, val lo/hi); rows < 2^32 (checked
+// on the host)
+__device__ __forceinline__ void peer_publish_rec(const PeerView &p, int q, const XRec &r, int lane) {
+    if (lane >= p.nranks) return;
+    unsigned long long *dst = peer_cell(peer_box(p, lane), p, p.rank, q);
+    const unsigned long long tag = (unsigned long long)p.epoch << 32;
+    const unsigned long long bd = (unsigned long long)__double_as_longlong(r.d);
+    const unsigned long long bw = (unsigned long long)__double_as_longlong(r.wd);
+    const unsigned long long bv = (unsigned long long)__double_as_longlong(r.val);
+    auto put = [&](int k, unsigned long long v) {
+        __hip_atomic_store(dst + k, tag | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    put(0, bd & 0xffffffffULL);
+    put(1, bd >> 32);
+    put(2, (unsigned long long)(unsigned int)r.i);
+    put(3, bw & 0xffffffffULL);
+    put(4, bw >> 32);
+    put(5, bv & 0xffffffffULL);
+    put(6, bv >> 32);
+}
+// one whole wave: lane g < nranks polls rank g's record of query q in this rank's box until
+// all 7 granules carry this wave's epoch; r = the lexicographic minimum over the ranks
+// (valid in every lane).  On timeout (or an earlier one on this exchange) r is left as the
+// caller's own record and false is returned (the error word is set).
+__device__ __forceinline__ bool peer_collect_rec(const PeerView &p, int q, int lane, XRec &r) {
+    const bool mine = lane < p.nranks;
+    const unsigned long long *src = peer_cell(peer_box(p, p.rank), p, mine ? lane : 0, q);
+    unsigned long long g0 = 0, g1 = 0, g2 = 0, g3 = 0, g4 = 0, g5 = 0, g6 = 0;
+    bool dead = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    auto ld = [&](int k) { return __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    auto tagged = [&](unsigned long long v) { return (unsigned)(v >> 32) == p.epoch; };
+    for (;;) {
+        bool ok = true;
+        if (mine) {
+            g0 = ld(0); g1 = ld(1); g2 = ld(2); g3 = ld(3); g4 = ld(4); g5 = ld(5); g6 = ld(6);
+            ok = tagged(g0) && tagged(g1) && tagged(g2) && tagged(g3) && tagged(g4) && tagged(g5) &&
+                 tagged(g6);
+        }
+        if (__all(ok) || dead) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
+            if (lane == 0) __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            dead = true;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (dead) return false;
+    auto dbl = [](unsigned long long lo, unsigned long long hi) {
+        return __longlong_as_double((long long)(((hi & 0xffffffffULL) << 32) | (lo & 0xffffffffULL)));
+    };
+    XRec x{INFINITY, 0x7fffffffffffffffLL, 0.0, 0.0};
+    if (mine) x = XRec{dbl(g0, g1), (long long)(g2 & 0xffffffffULL), dbl(g3, g4), dbl(g5, g6)};
+    r = xrec_wave_min(x);
     return true;
 }
 

@@ -125,7 +125,11 @@ struct PeerView {
     int nranks, rank, mcap;                 // nranks 0: not a peer exchange
     unsigned int epoch;                     // this wave's tag (>= 1, one per wave)
 };
-static inline size_t peer_box_words(int nranks, int mcap) { return (size_t)2 * nranks * mcap * 3; }
+// granules per (slot, source rank, query) cell: 3 for the (distance, row) records of
+// k_rescore<3>, 7 for the fused per-wave kernel's {distance, row, weighted distance, A'
+// value} (ia_xwave.hip); cells are 64 B
+constexpr int PEER_CELL = 8;
+static inline size_t peer_box_words(int nranks, int mcap) { return (size_t)2 * nranks * mcap * PEER_CELL; }
 
 // the level state one wave of the per-pixel tail updates (ia_finish.h)
 struct FinishArgs {
@@ -146,6 +150,34 @@ struct FinishArgs {
     PeerView px{};
 };
 
+// one launch of the fused per-wave kernel k_xwave (ia_xwave.hip): wave t's exact stage,
+// exchange (f.px) and per-pixel tail, and wave t + 1's query rows
+struct XArgs {
+    DbSrc src;
+    ImgDb im;                     // image-form DB (IMG) ...
+    const void *db;               // ... or the split-f16 rows (half8)
+    long row0, nrows, nseg;
+    int seg_rows;
+    const float *segmin;          // [M][nseg], this wave's screen
+    const double *q64;            // this wave's query rows (M)
+    const float *qp;
+    const double *nq;
+    const float *amax;
+    const double *center;
+    double *q64n;                 // wave t + 1's query rows (M_n), written here
+    float *qpn;
+    double *nqn;
+    _Float16 *q16n;
+    ImgPair B, Bp;                // B / B' at levels l - 1, l (the query's features)
+    int H, M, y_lo_n, M_n;        // wave t: M pixels from f.y_lo; wave t + 1: M_n from y_lo_n
+    unsigned long long *dbox;     // decision granules, 2 per row
+    unsigned int *tickets;        // [2]: this launch uses tickets[t & 1]
+    unsigned int *err;            // set when a wait for a neighbour's decision times out
+    unsigned long long *stats;    // nullable: rows rescored, candidate segments, full scans
+    FinishArgs f;                 // t, y_lo, W, ..., px (sharded DB: the device-side exchange)
+};
+int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st);
+
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS
 // cache lines so that the atomics of a wave's M queries do not serialise on one address;
 // the host sums the slots.
@@ -154,6 +186,16 @@ constexpr size_t STATS_BYTES = (size_t)STATS_SLOTS * STATS_LINE * sizeof(unsigne
 __device__ __forceinline__ unsigned long long *stats_slot(unsigned long long *s, int q) {
     return s + (q & (STATS_SLOTS - 1)) * STATS_LINE;
 }
+
+// the exact matcher's scratch (match_scratch_bytes): a 256-B head (the work list's counter),
+// then the segment minima [M][nseg]
+constexpr size_t MATCH_HEAD = 256;
+static inline float *match_segmin(void *scratch) {
+    return reinterpret_cast<float *>(reinterpret_cast<char *>(scratch) + MATCH_HEAD);
+}
+// the exact stage's form for this process (ia_diag_set_rescore_mode): 0 per-query
+// workgroups, 1 the work list, -1 default
+int exact_stage_mode();
 
 // ---- launchers ------------------------------------------------------------------
 // query rows of wave t: q64 (fp64 features), qp (fp32 rows of the exact stage's

@@ -20,196 +20,14 @@
 // and the work list k_select -> k_items -> k_gather (larger levels, where a query with many
 // candidate segments would serialise k_rescore).  On a single shard the last kernel also
 // runs the per-pixel tail of the synthesis step (ia_finish.h).
+#include "ia_exact.h"
 #include "ia_finish.h"
-#include "ia_imgwin.h"
-#include "ia_split16.h"
 
 #include <float.h>
 
 namespace ia {
 
-constexpr int TILE_H8 = DB16_GROUPS * 64;  // half8 per 32-row tile of the split-f16 DB
-
-__device__ __forceinline__ void best_update(double &bd, long long &bi, double d, long long i) {
-    if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
-}
-
-// Thresholds of the exact stage from the minimum segment minimum emin (screen units):
-// Tseg for segment minima (screen units), Trow for the fp32 VALU re-screen (in units of
-// sa, the re-screen's scale).  e* = emin / (sa sq) exactly; Tseg = e* + 2 eps16,
-// Trow = e* + eps16 + eps_q (+ a 1e-12 relative allowance for the fp64 rounding of d and
-// of the centring); force_full when the query's norm slot nears the f16 floor
-// (|q'| > 2^24 Amax).  eps_q = 70 u (2 A|q'| + A^2) bounds the re-screen (§4): fp32
-// conversions 2u on the 2A|q'| term and u on A^2, the split residual |x - x_h - x_l| <=
-// 4u|x|, a 56-term fp32 chain in any order <= 56u (1 + O(u)): 62u + O(u^2) in all.
-__device__ __forceinline__ void rescore_thresholds(float emin, float amax0, double nqq,
-                                                   double &Tseg, double &Trow, bool &force_full) {
-    constexpr double U32 = 5.9604644775390625e-08;
-    const double A = (double)amax0;
-    const double eps = 70.0 * U32 * (2.0 * A * sqrt(nqq) + A * A);
-    const Split16Db sc = split16_db_scale(amax0);
-    const int eq = split16_q_scale(nqq, sc.R);
-    const int e2 = sc.ea + eq;
-    const double em = ldexp((double)emin, -e2);
-    const double eps16 = U32 * (300.0 * A * sqrt(nqq) + 50.0 * A * A);
-    const double slack = 1e-12 * (fabs(em) + nqq + A * A);
-    Tseg = ldexp(em + 2.0 * eps16 + slack, e2);
-    Trow = ldexp(em + eps16 + eps + slack, sc.ea);
-    force_full = eq + sc.R < -10;
-}
-
-// The 14 register groups of DB row r (split-f16, ia_split16.h): g0 = lane half 0, g1 = 1
-__device__ __forceinline__ void load_row16(const half8 *__restrict__ db16, long r,
-                                           half8 (&g0)[DB16_GROUPS], half8 (&g1)[DB16_GROUPS]) {
-    const half8 *t = db16 + (r >> 5) * TILE_H8 + (r & 31);
-#pragma unroll
-    for (int g = 0; g < DB16_GROUPS; ++g) {
-        g0[g] = t[g * 64];
-        g1[g] = t[g * 64 + 32];
-    }
-}
-
-// fp32 re-screen value of a row from its split record, in units of sa: the same 56-term
-// dot product [a', |a'|^2] . [-2 q', 1] as the screen (qf: the fp32 query row, MFMA
-// operand order perm56), each value reassembled exactly as x_h + x_l in fp32; the norm
-// slot carries sa 2^-R |a'|^2, so its query factor is 2^R.  Any summation order (§4).
-__device__ __forceinline__ float rescreen16(const half8 (&g0)[DB16_GROUPS],
-                                            const half8 (&g1)[DB16_GROUPS], const float *qf,
-                                            float twoR) {
-    float acc = 0.f;
-#pragma unroll
-    for (int k = 0; k < IA_DP; ++k) {
-        _Float16 hi, lo;
-        if (k < 24) { hi = g0[k >> 3][k & 7]; lo = g0[4 + (k >> 3)][k & 7]; }
-        else if (k < 32) { hi = g0[3][k & 7]; lo = g1[3][k & 7]; }
-        else { hi = g1[(k - 32) >> 3][k & 7]; lo = g1[4 + ((k - 32) >> 3)][k & 7]; }
-        const float x = (float)hi + (float)lo;
-        acc = fmaf(x, k < 55 ? qf[(k & 1) * 28 + (k >> 1)] : twoR, acc);
-    }
-    return acc;
-}
-
-// the same re-screen values for pixels p and p + 64 of a staged image-form window
-// (ia_imgwin.h): the same 56 terms x_h + x_l in the same order as rescreen16, so the same
-// fp32 values; one pass over k for both (each query factor read once)
-__device__ __forceinline__ float win_x(const char *bf, const char *bc, int k) {
-    const uint32_t v = *reinterpret_cast<const uint32_t *>(((k < 55 && win_coarse(k)) ? bc : bf) + win_off(k));
-    return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)) +
-           (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16));
-}
-__device__ __forceinline__ void rescreen_win2(const char *wb, int p, const float *qf, float twoR,
-                                              float &e0, float &e1) {
-    const char *bf0 = wb + 4 * p, *bc0 = wb + 4 * (p >> 1);
-    const char *bf1 = bf0 + 256, *bc1 = bc0 + 128;
-    float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-    for (int k = 0; k < IA_DP; ++k) {
-        const float f = k < 55 ? qf[(k & 1) * 28 + (k >> 1)] : twoR;
-        a0 = fmaf(win_x(bf0, bc0, k), f, a0);
-        a1 = fmaf(win_x(bf1, bc1, k), f, a1);
-    }
-    e0 = a0;
-    e1 = a1;
-}
-
-// this lane's pieces of the window of the stage at local row lrow (a wave stages a whole
-// window: pieces lane + 64 j), loaded into registers / stored into the wave's LDS window
-constexpr int WIN_PPL = (WIN_PIECES + 63) / 64;   // 7
-__device__ __forceinline__ void win_load(const ImgDb &im, long lrow, int lane, uint4 (&pc)[WIN_PPL]) {
-    const WinSrc ws = win_src(im, lrow);
-#pragma unroll
-    for (int j = 0; j < WIN_PPL; ++j) {
-        const int i = lane + 64 * j;
-        if (i < WIN_PIECES) pc[j] = *reinterpret_cast<const uint4 *>(win_piece(im, ws, i));
-    }
-}
-__device__ __forceinline__ void win_store(char *wb, int lane, const uint4 (&pc)[WIN_PPL]) {
-#pragma unroll
-    for (int j = 0; j < WIN_PPL; ++j) {
-        const int i = lane + 64 * j;
-        if (i < WIN_PIECES) reinterpret_cast<uint4 *>(wb)[i] = pc[j];
-    }
-}
-// the wave's own LDS writes are visible to all its lanes (LDS executes a wave's operations
-// in order; this keeps the compiler from moving them)
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-constexpr int RESCORE_SEGCAP = 1024;   // candidate segments held in LDS per query
-constexpr int RESCORE_REG = 8;         // float4s of segment minima per thread kept in VGPRs
-constexpr int RESCORE_RPT = 2;         // candidate rows per thread per step
-constexpr int RESCORE_ROWCAP = 512;    // rows to rescore held in LDS per query
-static_assert(DB_SEG_MAX <= RESCORE_RPT * 256, "one re-screen step per segment");
-
-// a uniform index the compiler must treat as per-lane: the load it feeds is a vector load
-// issued in program order with the others (a scalar load of it would be scheduled after
-// their wait: one more memory round trip)
-__device__ __forceinline__ int vidx(int i) {
-    asm volatile("" : "+v"(i));
-    return i;
-}
-
-// e* of query q over its nseg segment minima (float4 reads, nseg a multiple of 4); the
-// first RESCORE_REG float4s per thread stay in v[] for the selection pass
-// (threads >= 256 of a block take no part but meet the barrier).  segmin_load issues the
-// loads only, so the caller can put its other independent loads in the same round trip.
-__device__ __forceinline__ void segmin_load(const float4 *sq4, long n4, float4 (&v)[RESCORE_REG]) {
-    const int tid = threadIdx.x;
-    const long lim = tid < 256 ? n4 : 0;
-#pragma unroll
-    for (int j = 0; j < RESCORE_REG; ++j) {
-        const long i = tid + (long)j * 256;
-        v[j] = i < lim ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
-    }
-}
-__device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
-                                             float *redf) {
-    const int tid = threadIdx.x;
-    const long lim = tid < 256 ? n4 : 0;
-    float emin = FLT_MAX;
-#pragma unroll
-    for (int j = 0; j < RESCORE_REG; ++j)
-        emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
-    for (long i = tid + (long)RESCORE_REG * 256; i < lim; i += 256) {
-        const float4 x = sq4[i];
-        emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
-    }
-    for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
-    if ((tid & 63) == 0 && tid < 256) redf[tid >> 6] = emin;
-    __syncthreads();
-    return fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
-}
-
-// candidate segments (minimum <= Tseg) -> slist (LDS, first RESCORE_SEGCAP), count in *scount
-__device__ __forceinline__ void segmin_select(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
-                                              double Tseg, int *slist, int *scount) {
-    const int tid = threadIdx.x;
-    if (tid >= 256) return;
-    auto push = [&](float e, long s) {
-        if ((double)e <= Tseg) {
-            const int pos = atomicAdd(scount, 1);
-            if (pos < RESCORE_SEGCAP) slist[pos] = (int)s;
-        }
-    };
-#pragma unroll
-    for (int j = 0; j < RESCORE_REG; ++j) {
-        const long i = tid + (long)j * 256;
-        push(v[j].x, 4 * i);
-        push(v[j].y, 4 * i + 1);
-        push(v[j].z, 4 * i + 2);
-        push(v[j].w, 4 * i + 3);
-    }
-    for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
-        const float4 x = sq4[i];
-        push(x.x, 4 * i);
-        push(x.y, 4 * i + 1);
-        push(x.z, 4 * i + 2);
-        push(x.w, 4 * i + 3);
-    }
-}
+// (thresholds, re-screen and window helpers: ia_exact.h)
 
 // The end of the exact stage for query q once its winner win (distance bd) is known, by
 // the block's waves 0 and 1 (all threads call it; every wave reaches the barriers).
@@ -347,7 +165,7 @@ __global__ __launch_bounds__(rescore_threads(MODE, FIFTH), IMG ? 2 : 1) void k_r
             const long seg = full ? k0 / seg_rows : slist[k0 / seg_rows];
             return seg * seg_rows + k0 % seg_rows;
         };
-        uint4 pc[WIN_PPL];
+        piece_t pc[WIN_PPL];
         long k0 = 128L * wv, lrow = 0;
         if (k0 < nrs) {
             lrow = stage_row(k0);
@@ -499,7 +317,7 @@ __global__ __launch_bounds__(256, IMG ? 2 : 1) void k_items(DbSrc src, long row0
         // the two round trips overlap
         half8 x0[IMG ? 1 : RESCORE_RPT][DB16_GROUPS], x1[IMG ? 1 : RESCORE_RPT][DB16_GROUPS];
         long lr[RESCORE_RPT];
-        uint4 pc[WIN_PPL];
+        piece_t pc[WIN_PPL];
         const bool wstage = IMG && wv * 128 < seg_rows;
         if constexpr (IMG) {
             if (wstage) win_load(im, (long)w.seg * seg_rows + wv * 128, lane, pc);
@@ -602,11 +420,12 @@ __global__ __launch_bounds__(128) void k_gather(DbSrc src, const QSel *__restric
 // ia_diag_set_rescore_mode
 static std::atomic<int> g_rescore_mode{env_int("IA_RESCORE", -1)};
 static int rescore_mode() { return g_rescore_mode.load(std::memory_order_relaxed); }
+int exact_stage_mode() { return rescore_mode(); }
 
 // matcher scratch: [list counter | segment minima | items | item winners | per-query
 // records]; the counter sits at a fixed offset (it carries over between calls, emptied by
 // k_gather)
-static constexpr size_t WL_HEAD = 256;
+static constexpr size_t WL_HEAD = MATCH_HEAD;
 struct SegWs {
     int *ctr;
     float *segmin;

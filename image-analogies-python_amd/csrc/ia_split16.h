@@ -65,6 +65,10 @@ __device__ __forceinline__ int split16_q_scale(double nq, int R) {
     return eq < -120 ? -120 : eq;
 }
 
+// MFMA operand order of element k = 2s + h: position h*28 + s (the fp32 query rows qp, the
+// exact stage's re-screen operand).
+__device__ __forceinline__ int perm56(int k) { return (k & 1) * 28 + (k >> 1); }
+
 // x = h + l (+ the f16 rounding of l)
 __device__ __forceinline__ void split16f(float x, _Float16 &h, _Float16 &l) {
     h = (_Float16)x;

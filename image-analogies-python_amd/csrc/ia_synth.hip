@@ -162,7 +162,17 @@ struct SynthWs {
     ShardRec *rec_all;
     CohSel *coh;
     unsigned long long *stats;
+    // the fused per-wave kernel (k_xwave): the query rows of odd waves (even waves use
+    // q64 / qp / q16 / nq), the decision granules (2 per row) and the control words
+    // {tickets[2], error}
+    double *q64b;
+    float *qpb;
+    _Float16 *q16b;
+    double *nqb;
+    unsigned long long *dbox;
+    unsigned int *ctl;
 };
+constexpr int XW_CTL_ERR = 2;
 
 static inline int wave_max_queries(int H, int W) {
     const int byw = (W + 2) / 3;   // ceil(W/3)
@@ -185,6 +195,12 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     w.rec_all = (ShardRec *)take((size_t)Mmax * nranks * sizeof(ShardRec));
     w.coh = (CohSel *)take((size_t)Mmax * sizeof(CohSel));
     w.stats = (unsigned long long *)take(STATS_BYTES);
+    w.q64b = (double *)take((size_t)Mmax * IA_DP * sizeof(double));
+    w.qpb = (float *)take((size_t)qr * IA_DP * sizeof(float));
+    w.q16b = (_Float16 *)take((size_t)qr * Q16_ROW * 16);
+    w.nqb = (double *)take((size_t)qr * sizeof(double));
+    w.dbox = (unsigned long long *)take((size_t)H * 2 * sizeof(unsigned long long));
+    w.ctl = (unsigned int *)take(256);
     if (ws) *ws = w;
     return off;
 }
@@ -294,6 +310,12 @@ static int shard_tail() {
     return v;
 }
 
+// the fused per-wave kernel (k_xwave, ia_xwave.hip): after each screen ONE launch runs the
+// exact stage, the device-side exchange, the per-pixel tail and the next wave's query rows
+// (IA_XWAVE / ia_diag_set_xwave: 1 [default] wherever it applies, 0 the separate kernels)
+static std::atomic<int> g_xwave{env_int("IA_XWAVE", 1)};
+static int xwave_on() { return g_xwave.load(std::memory_order_relaxed); }
+
 static int check_args(const IaSynthArgs *a) {
     IA_ARG(a && (a->db || a->dbi || a->lsh) && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
                a->weights && a->s && a->im && a->workspace,
@@ -321,7 +343,7 @@ struct LevelRun {
     DbSrc src{};
     ImgPair B{}, Bp{};
     int H = 0, W = 0, nw = 0, nranks = 1;
-    bool prof = false, timed = false, fused = false, peer = false;
+    bool prof = false, timed = false, fused = false, peer = false, xw = false;
     size_t ev0 = 0;
     unsigned long long *hstats = nullptr;
     double pairs = 0.0;
@@ -359,6 +381,18 @@ struct LevelRun {
         peer = a->comm && comm_peer_mcap(a->comm) > 0;
         IA_ARG(!peer || comm_peer_mcap(a->comm) >= Mmax,
                "ia_synth_level: the peer exchange's box holds fewer queries than a wave");
+        IA_ARG(!peer || a->N_total < (1L << 32),
+               "ia_synth_level: the peer exchange carries 32-bit rows (N_total >= 2^32)");
+        // one launch per wave after the screen (k_xwave) wherever the exact matcher runs
+        // on one GPU or over the device-side exchange (not the LSH matcher, the RCCL
+        // exchange, the in-process shard simulation or a forced work list)
+        xw = xwave_on() && !a->lsh && !sim && (!a->comm || peer) && exact_stage_mode() != 1;
+        IA_HIP(hipMemsetAsync(ws.ctl, 0, 256, st));   // tickets, error word (ia_synth_status)
+        if (xw) {
+            IA_HIP(hipMemsetAsync(ws.qpb, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
+            IA_HIP(hipMemsetAsync(ws.q16b, 0, (size_t)qrows_alloc(Mmax) * Q16_ROW * 16, st));
+            IA_HIP(hipMemsetAsync(ws.dbox, 0, (size_t)H * 2 * sizeof(unsigned long long), st));
+        }
         return IA_OK;
     }
 
@@ -376,6 +410,7 @@ struct LevelRun {
         if (M <= 0) return IA_OK;
         int rc;
         if (sim) return sim_wave(t, y_lo, M, sq);
+        if (xw) return xw_wave(t, y_lo, M, sq);
         if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
                                     ws.q16, sq)))
             return rc;
@@ -431,6 +466,65 @@ struct LevelRun {
             return rc;
         k_finish<<<M, 64, 0, sq>>>(src, ws.rec_all, ws.coh, nranks, M, fa);
         IA_LAUNCH_CHECK("k_finish");
+        return IA_OK;
+    }
+
+    // wave t on the fused path: [wave 0's query rows,] the screen, then k_xwave (exact
+    // stage, exchange, tail, and wave t + 1's query rows into the other buffer set)
+    int xw_wave(int t, int y_lo, int M, hipStream_t sq) {
+        int rc;
+        double *q64s[2] = {ws.q64, ws.q64b};
+        float *qps[2] = {ws.qp, ws.qpb};
+        _Float16 *q16s[2] = {ws.q16, ws.q16b};
+        double *nqs[2] = {ws.nq, ws.nqb};
+        const int b = t & 1;
+        if (t == 0 && (rc = launch_query_wave(B, Bp, 0, y_lo, M, a->center, q64s[0], qps[0], nqs[0],
+                                              a->amax, q16s[0], sq)))
+            return rc;
+        ImgDb img{};
+        const bool im = a->dbi != nullptr;
+        IA_ARG(!im || img_db_layout(src.A.h, src.A.w, src.A.hs, src.A.ws, 1, a->row0, a->nrows, a->dbi, img,
+                                    nullptr),
+               "ia_synth_level: an image-form DB for a level it does not apply to");
+        IA_ARG(im || a->db, "ia_synth_level: no DB (row form or image form)");
+        float *segmin = match_segmin(ws.scratch);
+        hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
+        hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
+        if (e0) IA_HIP(hipEventRecord(e0, sq));
+        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, q16s[b], M, segmin, sq))) return rc;
+        if (e1) IA_HIP(hipEventRecord(e1, sq));
+        int y_lo_n = 0, M_n = 0;
+        if (t + 1 < nw) wave_rows(H, W, t + 1, y_lo_n, M_n);
+        XArgs x{};
+        x.src = src;
+        x.im = img;
+        x.db = a->db;
+        x.row0 = a->row0;
+        x.nrows = a->nrows;
+        x.nseg = db_nsegs(a->nrows);
+        x.seg_rows = db_seg_rows(a->nrows);
+        x.segmin = segmin;
+        x.q64 = q64s[b]; x.qp = qps[b]; x.nq = nqs[b];
+        x.amax = a->amax;
+        x.center = a->center;
+        x.q64n = q64s[b ^ 1]; x.qpn = qps[b ^ 1]; x.nqn = nqs[b ^ 1]; x.q16n = q16s[b ^ 1];
+        x.B = B;
+        x.Bp = Bp;
+        x.H = H; x.M = M; x.y_lo_n = y_lo_n; x.M_n = M_n;
+        x.dbox = ws.dbox;
+        x.tickets = ws.ctl;
+        x.err = ws.ctl + XW_CTL_ERR;
+        x.stats = prof ? ws.stats : nullptr;
+        x.f = FinishArgs{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
+                         a->im, a->dbg_px, a->dbg_dist, nullptr, nullptr};
+        if (peer) x.f.px = comm_peer_wave(a->comm);
+        const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
+        if ((rc = launch_xwave(x, R, im, sq))) return rc;
+        ++nscreen;
+        pairs += (double)M * (double)a->nrows;
+        if (prof) Ms.push_back(M);
+        static const int sync_every = env_int("IA_SYNC_EVERY", 0);
+        if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
         return IA_OK;
     }
 
@@ -514,6 +608,34 @@ static thread_local PipeRes g_pipe;
 using namespace ia;
 
 extern "C" {
+
+int ia_diag_set_xwave(int on) {
+    const int prev = xwave_on();
+    if (on == 0 || on == 1) g_xwave.store(on);
+    return prev;
+}
+
+int ia_synth_status(const IaSynthArgs *levels, int n, void *stream) {
+    IA_ARG(levels && n >= 1, "ia_synth_status: bad args");
+    IA_HIP(hipStreamSynchronize(S(stream)));
+    for (int j = 0; j < n; ++j) {
+        const IaSynthArgs &a = levels[j];
+        IA_ARG(a.workspace && a.H > 0 && a.W > 0 && a.nrows > 0, "ia_synth_status: bad level");
+        SynthWs w;
+        carve(&w, reinterpret_cast<char *>(a.workspace), a.H, a.W, a.nrows, comm_nranks(a.comm));
+        unsigned int e = 0;
+        IA_HIP(hipMemcpy(&e, w.ctl + XW_CTL_ERR, sizeof(e), hipMemcpyDeviceToHost));
+        if (e) {
+            set_error("ia_synth_status: a wait for a neighbouring pixel's decision timed out");
+            return IA_E_COMM;
+        }
+        if (comm_peer_mcap(a.comm) > 0) {
+            const int rc = ia_peer_status(a.comm);
+            if (rc) return rc;
+        }
+    }
+    return IA_OK;
+}
 
 int ia_diag_set_graph_mode(int mode) {
     const int prev = graph_mode();
@@ -708,7 +830,10 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
     // one GPU with every c3 level sharded and overlapping complete, and the simulated
     // G = 8 rank gains 3.6 % (profiles/r02_shard_overlap.txt).  IA_SHARD_OVERLAP=0
     // serializes them too.
-    static const int overlap = env_int("IA_SHARD_OVERLAP", 1);
+    // Ranks sharing ONE GPU (IA_SHARE_GPU=1, the tests' multi-rank mode) serialize them as
+    // well: their waiting workgroups (k_xwave's, up to ~343 per level and rank) could then
+    // fill the one GPU's slots while a third rank's awaited ones cannot start.
+    static const int overlap = env_int("IA_SHARD_OVERLAP", 1) && !env_int("IA_SHARE_GPU", 0);
     auto multi_rank = [&](int j) {
         if (levels[j].comm == nullptr || levels[j].nrows >= levels[j].N_total) return false;
         return !(overlap && comm_peer_mcap(levels[j].comm) > 0);
@@ -729,7 +854,8 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
         while (next[j] <= target) {
             const int t = next[j];
             if (j > 0) {
-                int w = coarse_need(&levels[j], t);
+                // on the fused path wave t's launch also builds wave t + 1's query rows
+                int w = coarse_need(&levels[j], run[j].xw && t + 1 < run[j].nw ? t + 1 : t);
                 need_max[j] = w > need_max[j] ? w : need_max[j];
                 w = need_max[j];
                 if (w > waited[j]) {

@@ -1,0 +1,457 @@
+// ia_xwave.hip — everything a wave needs after its screen, in ONE launch (SURVEY §8(a) rows
+// a11-a15, §8(e)).
+//
+// The reference's pixel loop (image_analogies.py:161-220) does, per pixel: query build
+// (:166-168), approximate match (:175, algorithms.py:73-75), coherence match (:193,
+// algorithms.py:92-130), two weighted distances and the kappa test (:200-211), and the
+// B'/s/im update (:213-220).  On the wavefront t = x + 3y the screen (ia_screen16.hip) is
+// the only step with real arithmetic; every other step is a few dependent memory round
+// trips, and as separate launches (query build, exact stage, exchange + finish) they cost
+// more per wave than the screen itself once the DB is sharded over 8 GPUs.  k_xwave runs
+// them all for wave t, one 4-wave workgroup per pixel:
+//
+//   1. exact stage: e* over the pixel's segment minima, candidate segments, fp32 re-screen
+//      of their rows (4 waves in parallel), fp64 rescore of the rows within the bound
+//      (lane-parallel gathers, numpy's pairwise order from LDS), the lexicographic winner
+//      with its weighted distance and A' value;
+//   2. meanwhile wave 1 picks the coherence candidate (best_coherence_match: the 15
+//      causal window positions gathered lane-parallel, sqrt distances, first minimum);
+//   3. sharded DB: the winner goes to every rank's receive box and every rank's winner of
+//      this pixel is collected from this rank's box (PeerView, ia_finish.h), nothing waits
+//      before this workgroup has published;
+//   4. kappa test and the B'/s/im (+ debug) update; the new B' value is published as two
+//      tagged 8-byte granules (the decision box, one entry per row);
+//   5. the query row of the SAME row in wave t + 1, pixel (y, x + 1): of its 55 features only
+//      two can come from wave t — this pixel (y, x) and the upper neighbour's (y - 1, x + 3)
+//      (the only wave-t pixels inside its causal windows, reflections included) — so they
+//      come from this workgroup's registers and from the neighbour's decision granules;
+//      every other feature is read from memory (earlier waves, the coarse level, B).
+//
+// Workgroups take their pixel from a ticket counter, so a workgroup only ever waits for
+// the decision of a lower ticket (dispatched earlier), and it publishes its own record
+// and decision before any wait: no wait can hold a slot another workgroup needs to make
+// the awaited progress (forward progress).
+#include "ia_exact.h"
+#include "ia_finish.h"
+#include "../../include/ia_diag.h"
+
+#include <climits>
+
+namespace ia {
+
+// address of feature k (0..54) of pixel (r, c) of a pair X (full: k < 34) | Y (half:
+// k >= 34), the layout of emit_feature (ia_common.h), and its sample (rr, cc) in that
+// feature's image
+__device__ __forceinline__ const double *feat_addr(const ImgPair &X, const ImgPair &Y, int r, int c,
+                                                   int k, int &rr, int &cc) {
+    const bool yk = k >= 34;
+    const int kk = yk ? k - 34 : k;
+    const bool coarse = kk < 9;
+    const int t = coarse ? kk : kk - 9;
+    const int h = yk ? (coarse ? Y.hs : Y.h) : (coarse ? X.hs : X.h);
+    const int w = yk ? (coarse ? Y.ws : Y.w) : (coarse ? X.ws : X.w);
+    const double *base = yk ? (coarse ? Y.sm : Y.lg) : (coarse ? X.sm : X.lg);
+    const int r0 = coarse ? (r >> 1) + t / 3 - 1 : r + t / 5 - 2;
+    const int c0 = coarse ? (c >> 1) + t % 3 - 1 : c + t % 5 - 2;
+    rr = symi2(r0, h);
+    cc = symi2(c0, w);
+    return base + (long)rr * w + cc;
+}
+// feature k of DB row (A' image img, pixel (r, c)) (algorithms.py:63-67)
+__device__ __forceinline__ double db_feat(const DbSrc &src, int img, int r, int c, int k) {
+    ImgPair ap = src.Ap;
+    ap.sm += (long)img * src.hws;
+    ap.lg += (long)img * src.hw;
+    int rr, cc;
+    return *feat_addr(src.A, ap, r, c, k, rr, cc);
+}
+
+// numpy pairwise_sum of v[0..54] (Pw55's order, ia_common.h) from LDS
+__device__ __forceinline__ double pw55_lds(const double *v) {
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = v[j];
+#pragma unroll
+    for (int k = 8; k < 48; ++k) r[k & 7] += v[k];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int k = 48; k < IA_D; ++k) res += v[k];
+    return res;
+}
+
+// (XArgs: ia_internal.h)
+
+// the record of one DB row rescored by one thread (the row list's overflow: never on the
+// measured configs; out of line so that its 55-load gathers do not inflate the common path)
+__device__ __attribute__((noinline)) XRec row_rec(const DbSrc &src, long g, const double *qs,
+                                                  const double *wts) {
+    return XRec{row_dist2(src, g, qs), g, row_wdist(src, g, qs, wts), src.Ap.lg[g]};
+}
+
+constexpr int XW_ROWCAP = 256;   // rows within Trow rescored lane-parallel (the rest in place)
+constexpr int XW_RPW = 4;        // rows per rescoring wave and batch
+constexpr int XW_NCOH = 15;      // coherence window positions (3 x 5, algorithms.py:101-102)
+constexpr size_t XW_STAGE_B = (size_t)4 * XW_RPW * IA_DP * 8 * 2;   // 4 waves x (x^2, (x w)^2)
+
+__device__ __forceinline__ unsigned long long dgran(unsigned int tag, unsigned int bits) {
+    return ((unsigned long long)tag << 32) | bits;
+}
+
+template <bool IMG>
+__global__ __launch_bounds__(256, 3) void k_xwave(XArgs a) {
+    constexpr size_t POOL = IMG ? (size_t)4 * WIN_SLOT : 0;
+    __shared__ __attribute__((aligned(16))) char pool[POOL > XW_STAGE_B ? POOL : XW_STAGE_B];
+    __shared__ double cx[XW_NCOH][IA_DP], cw[XW_NCOH][IA_DP];
+    __shared__ double qs[IA_DP], wts[IA_DP];
+    __shared__ float qf[IA_DP];
+    __shared__ int slist[RESCORE_SEGCAP];
+    __shared__ long rlist[XW_ROWCAP];
+    __shared__ int tk, scount, rcount;
+    __shared__ unsigned int nresc;
+    __shared__ float redf[4];
+    __shared__ XRec wbest[4];
+    __shared__ CohSel cs;
+    __shared__ double csval;
+    // long-lived per-lane values kept in LDS (not VGPRs across the exact stage): wave 0's
+    // prefetched next-query features and centre, wave 1's coherence candidates
+    __shared__ double nxv[IA_DP], nxc[IA_DP];
+    __shared__ int nxd[IA_DP];
+    __shared__ long long ccix[XW_NCOH];
+    __shared__ int cpos[XW_NCOH][3];
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const FinishArgs &f = a.f;
+    const DbSrc &src = a.src;
+    const int t = f.t, W = f.W;
+    if (tid == 0) tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
+    __syncthreads();
+    const int i = tk;
+    // the counter of launch t + 1 was launch t - 1's: empty it for the next launch
+    if (i == 0 && tid == 0) __hip_atomic_store(&a.tickets[(t + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int y = f.y_lo + i, x = t - 3 * y;
+    const bool cur = i < a.M;                                    // pixel (y, x) is in wave t
+    const bool nxt = y >= a.y_lo_n && y < a.y_lo_n + a.M_n;       // (y, x + 1) is in wave t + 1
+
+    // wave 0: the next query's features that do not depend on wave t, issued first
+    // (kept in registers until the first barrier, then in LDS: the load's wait must not
+    // come before the exact stage's own loads are issued)
+    double pv = 0.0, pc0 = 0.0;
+    int pdep = 0;
+    if (wv == 0 && nxt && lane < IA_D) {
+        int rr, cc;
+        const double *p = feat_addr(a.B, a.Bp, y, x + 1, lane, rr, cc);
+        // 1: this pixel's new value, 2: the upper neighbour's
+        pdep = lane < 43 ? 0 : (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
+        pv = pdep ? 0.0 : *p;
+        pc0 = a.center[lane];
+    }
+    auto park_next = [&]() {
+        if (wv == 0 && lane < IA_DP) {
+            nxv[lane] = pv;
+            nxc[lane] = pc0;
+            nxd[lane] = pdep;
+        }
+    };
+
+    double own = 0.0;            // this pixel's new B' value (wave 0)
+    if (cur) {
+        // ---- 1. loads of one round trip: query, norm, bound, segment minima, coherence window
+        double qsv = 0.0, wk = 0.0;
+        float qfv = 0.f;
+        if (tid < IA_DP) {
+            qsv = a.q64[(long)i * IA_DP + tid];
+            qfv = a.qp[(long)i * IA_DP + tid];
+            wk = tid < IA_D ? f.weights[tid] : 0.0;
+        }
+        const double nqq = a.nq[vidx(i)];
+        const float am = a.amax[vidx(0)];
+        const long n4 = a.nseg / 4;
+        const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
+        float4 v[RESCORE_REG];
+        segmin_load(sq4, n4, v);
+        // wave 1, lane l < 15: coherence candidate of window position l (algorithms.py:
+        // 101-119): r strictly before q in scanline order, p_r = s(r) + q - r inside A'
+        if (wv == 1 && lane < XW_NCOH) {
+            long long cix = -1;
+            int csr = 0, csc = 0, cim = 0;
+            const int rr = y - 2 + lane / 5, rc = x - 2 + lane % 5;
+            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
+                const long sidx = (long)rr * W + rc;
+                const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
+                const int simg = f.im[sidx];
+                if (sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w) {
+                    cix = ((long)src.A.h * simg + sr) * src.A.w + sc;
+                    csr = sr; csc = sc; cim = simg;
+                }
+            }
+            ccix[lane] = cix;
+            cpos[lane][0] = csr; cpos[lane][1] = csc; cpos[lane][2] = cim;
+        }
+        if (tid == 0) { scount = 0; nresc = 0; rcount = 0; }
+        const float emin = segmin_scan(sq4, n4, v, redf);
+        if (tid < IA_DP) {
+            qs[tid] = qsv;
+            qf[tid] = qfv;
+            wts[tid] = wk;
+        }
+        park_next();
+        double Tseg, Trow;
+        bool force_full;
+        rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+        const float twoR = ldexpf(1.f, split16_db_scale(am).R);
+        segmin_select(sq4, n4, v, Tseg, slist, &scount);
+        __syncthreads();
+        const int ns = scount;
+        const bool full = ns > RESCORE_SEGCAP || force_full;
+        const long nscan = full ? a.nseg : ns;
+        const long nrs = nscan * a.seg_rows;
+
+        // ---- 2. fp32 re-screen of the candidate segments' rows; rows within Trow to the
+        // list (overflow rows rescored in place: never on the measured configs)
+        unsigned int mine = 0;
+        XRec ob{INFINITY, LLONG_MAX, 0.0, 0.0};
+        auto take = [&](long lr, float e) {
+            if (lr < a.nrows && (double)e <= Trow) {
+                ++mine;
+                const int pos = atomicAdd(&rcount, 1);
+                if (pos < XW_ROWCAP) {
+                    rlist[pos] = lr;
+                } else {
+                    const long g = a.row0 + lr;
+                    xrec_take(ob, row_rec(src, g, qs, wts));
+                }
+            }
+        };
+        if constexpr (IMG) {
+            // wave w re-screens the 128-row stage base + 128 w of each 512-row step from its
+            // own LDS slot, the window copied in by LDS DMA (one step: one round trip; more
+            // than one candidate segment per query is rare)
+            char *wb = pool + wv * WIN_SLOT;
+            for (long k0 = 128L * wv; k0 < nrs; k0 += 512) {
+                const long seg = full ? k0 / a.seg_rows : slist[k0 / a.seg_rows];
+                const long lrow = seg * a.seg_rows + k0 % a.seg_rows;
+                wave_lds_sync();   // the previous step's reads of the slot are done
+                win_dma(a.im, lrow, lane, wb);
+                win_dma_wait();
+                float e0, e1;
+                rescreen_win2(wb, lane, qf, twoR, e0, e1);
+                take(lrow + lane, e0);
+                take(lrow + lane + 64, e1);
+            }
+        } else {
+            // row form: one row per thread per step (224-B split rows)
+            for (long k = tid; k < nrs; k += 256) {
+                const long seg = full ? k / a.seg_rows : slist[k / a.seg_rows];
+                const long lr = seg * a.seg_rows + k % a.seg_rows;
+                half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
+                load_row16(reinterpret_cast<const half8 *>(a.db), lr < a.nrows ? lr : 0, g0, g1);
+                take(lr, rescreen16(g0, g1, qf, twoR));
+            }
+        }
+        if (mine) atomicAdd(&nresc, mine);
+        __syncthreads();   // the row list is complete; the windows are free
+
+        // ---- 3. fp64 rescore of the listed rows (waves 2, 3, 0 in turn, XW_RPW rows per
+        // batch: lane k gathers feature k, the squares go through LDS, lane j sums row j in
+        // numpy's order) | wave 1: the coherence pick
+        const int nl = rcount < XW_ROWCAP ? rcount : XW_ROWCAP;
+        XRec b = ob;
+        if (wv != 1) {
+            const int rk = wv == 2 ? 0 : (wv == 3 ? 1 : 2);
+            double *rx = reinterpret_cast<double *>(pool) + (size_t)wv * XW_RPW * IA_DP * 2;
+            for (int base = rk * XW_RPW; base < nl; base += 3 * XW_RPW) {
+                // lane j < XW_RPW locates row base + j once; every lane then gathers
+                int li = 0, lr_ = 0, lc = 0;
+                long lg = 0;
+                if (lane < XW_RPW && base + lane < nl) {
+                    lg = a.row0 + rlist[base + lane];
+                    const long img = lg / src.hw, rem = lg - img * src.hw;
+                    li = (int)img;
+                    lr_ = (int)(rem / src.A.w);
+                    lc = (int)(rem - (long)lr_ * src.A.w);
+                }
+                double g[XW_RPW];
+#pragma unroll
+                for (int j = 0; j < XW_RPW; ++j) {
+                    const int ri = __shfl(li, j), rr = __shfl(lr_, j), rc = __shfl(lc, j);
+                    const long rg = __shfl(lg, j);
+                    g[j] = 0.0;
+                    if (base + j < nl) {
+                        if (lane < IA_D) g[j] = db_feat(src, ri, rr, rc, lane);
+                        else if (lane == IA_D) g[j] = src.Ap.lg[rg];
+                    }
+                }
+                wave_lds_sync();   // the previous batch's sums are done with rx
+#pragma unroll
+                for (int j = 0; j < XW_RPW; ++j) {
+                    if (base + j < nl) {
+                        if (lane < IA_D) {
+                            const double xx = g[j] - qs[lane];
+                            const double xw = xx * wts[lane];
+                            rx[j * IA_DP + lane] = xx * xx;
+                            rx[(XW_RPW + j) * IA_DP + lane] = xw * xw;
+                        } else if (lane == IA_D) {
+                            rx[j * IA_DP + IA_D] = g[j];   // the row's A' value (slot 55)
+                        }
+                    }
+                }
+                wave_lds_sync();
+                if (lane < XW_RPW && base + lane < nl) {
+                    const double d = pw55_lds(rx + lane * IA_DP);
+                    const double s = sqrt(pw55_lds(rx + (XW_RPW + lane) * IA_DP));
+                    xrec_take(b, XRec{d, lg, s * s, rx[lane * IA_DP + IA_D]});
+                }
+            }
+        } else {
+            // best_coherence_match (algorithms.py:92-130) + the winner's compute_distance
+            // (:133-135): all candidates' features in one round trip (lane = feature)
+            double g[XW_NCOH];
+            const long long cix = lane < XW_NCOH ? ccix[lane] : -1;
+            const double cvl = cix >= 0 ? src.Ap.lg[cix] : 0.0;
+#pragma unroll
+            for (int c = 0; c < XW_NCOH; ++c)
+                g[c] = (ccix[c] >= 0 && lane < IA_D) ? db_feat(src, cpos[c][2], cpos[c][0], cpos[c][1], lane) : 0.0;
+#pragma unroll
+            for (int c = 0; c < XW_NCOH; ++c) {
+                if (ccix[c] >= 0 && lane < IA_D) {
+                    const double xx = g[c] - qs[lane];
+                    const double xw = xx * wts[lane];
+                    cx[c][lane] = xx * xx;
+                    cw[c][lane] = xw * xw;
+                }
+            }
+            wave_lds_sync();
+            double cd = INFINITY, cwd = 0.0;
+            long long cl = LLONG_MAX;
+            if (lane < XW_NCOH && cix >= 0) {
+                cd = sqrt(pw55_lds(cx[lane]));
+                const double s = sqrt(pw55_lds(cw[lane]));
+                cwd = s * s;
+                cl = lane;
+            }
+            double bd = cd;
+            long long bl = cl;
+            for (int o = 32; o > 0; o >>= 1) {
+                const double od = __shfl_xor(bd, o);
+                const long long ol = __shfl_xor(bl, o);
+                fin_best(bd, bl, od, ol);
+            }
+            const int win = bl == LLONG_MAX ? 0 : (int)bl;
+            const long long wix = ccix[win];
+            const int wr = cpos[win][0], wc = cpos[win][1], wim = cpos[win][2];
+            const double wd = __shfl(cwd, win), wval = __shfl(cvl, win);
+            if (lane == 0) {
+                cs = bl == LLONG_MAX ? CohSel{0, 0, 0, 0, 0, 0, 0, 0.0}
+                                     : CohSel{wix, wr, wc, wim, y - 2 + win / 5, x - 2 + win % 5, 1, wd};
+                csval = wval;
+            }
+        }
+        b = xrec_wave_min(b);
+        if (lane == 0) wbest[wv] = b;
+        __syncthreads();
+        if (wv != 0) return;
+
+        // ---- 4. this rank's winner; sharded DB: publish it, collect every rank's
+        XRec lb = wbest[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) xrec_take(lb, wbest[w]);
+        XRec gb = lb;
+        if (f.px.nranks > 0) {
+            peer_publish_rec(f.px, i, lb, lane);
+            if (!peer_collect_rec(f.px, i, lane, gb)) gb = lb;
+        }
+        if (a.stats && lane == 0) {
+            unsigned long long *sl = stats_slot(a.stats, i);
+            atomicAdd(&sl[0], (unsigned long long)nresc);
+            atomicAdd(&sl[1], (unsigned long long)ns);
+            atomicAdd(&sl[2], full ? 1ULL : 0ULL);
+        }
+        // ---- kappa test and update (image_analogies.py:200-220; finish_apply's rules)
+        const CohSel c = cs;
+        const long long app = (gb.i < 0 || gb.i >= f.N_total) ? 0 : gb.i;
+        const long hw = src.hw;
+        const int Aw = src.A.w;
+        long img = app / hw;
+        const long rem = app - img * hw;
+        const int ar = (int)(rem / Aw), ac = (int)(rem - (long)(rem / Aw) * Aw);
+        int pr = ar, pc = ac;
+        double val = gb.val;
+        if (c.valid && c.dcoh <= gb.wd * f.kappa_factor) {
+            pr = c.wr; pc = c.wc; img = c.wim;
+            val = csval;
+        }
+        own = val;
+        if (lane == 0) {
+            const long q = (long)y * W + x;
+            if (f.dbg_px) {
+                int32_t *o = f.dbg_px + 7 * q;
+                o[0] = ar; o[1] = ac;
+                o[2] = c.valid ? c.wr : 0;
+                o[3] = c.valid ? c.wc : 0;
+                o[4] = c.valid ? c.rr : 0;
+                o[5] = c.valid ? c.rc : 0;
+                o[6] = c.valid;
+                f.dbg_dist[2 * q] = c.valid ? gb.wd : 0.0;
+                f.dbg_dist[2 * q + 1] = c.valid ? c.dcoh : 0.0;
+            }
+            f.Bp_lg[q] = val;
+            f.s[2 * q] = pr;
+            f.s[2 * q + 1] = pc;
+            f.im[q] = (int32_t)img;
+            // the decision for the lower neighbour's next query (step 5)
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(val);
+            unsigned long long *d = a.dbox + 2 * (long)y;
+            __hip_atomic_store(d, dgran(t + 1, (unsigned int)bits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d + 1, dgran(t + 1, (unsigned int)(bits >> 32)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (wv != 0 || !nxt) return;
+    if (!cur) park_next();
+
+    // ---- 5. the query row of (y, x + 1) for wave t + 1 (k_query_wave's arithmetic)
+    const int dep = lane < IA_D ? nxd[lane] : 0;
+    double nb = 0.0;
+    if (__any(dep == 2)) {   // the upper neighbour (ticket i - 1) decided (y - 1, x + 3)
+        const unsigned long long *d = a.dbox + 2 * (long)(y - 1);
+        unsigned long long g0 = 0, g1 = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            g0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(g0 >> 32) == (unsigned)(t + 1) && (unsigned)(g1 >> 32) == (unsigned)(t + 1)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
+                if (lane == 0) atomicOr(a.err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        nb = __longlong_as_double((long long)(((g1 & 0xffffffffULL) << 32) | (g0 & 0xffffffffULL)));
+    }
+    const double vq = dep == 1 ? own : (dep == 2 ? nb : (lane < IA_D ? nxv[lane] : 0.0));
+    const double ncen = lane < IA_D ? nxc[lane] : 0.0;
+    const int m = y - a.y_lo_n;
+    double d = 0.0;
+    if (lane < IA_D) {
+        a.q64n[(long)m * IA_DP + lane] = vq;
+        d = vq - ncen;
+        a.qpn[(long)m * IA_DP + perm56(lane)] = -2.0f * (float)d;
+    } else if (lane == IA_D) {
+        a.q64n[(long)m * IA_DP + IA_D] = 0.0;
+        a.qpn[(long)m * IA_DP + perm56(IA_D)] = 1.0f;
+    }
+    double d2 = d * d;
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
+    if (lane == 0) a.nqn[m] = d2;
+    split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, a.amax[0]);
+}
+
+int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st) {
+    if (nblocks <= 0) return IA_OK;
+    if (img) k_xwave<true><<<nblocks, 256, 0, st>>>(a);
+    else k_xwave<false><<<nblocks, 256, 0, st>>>(a);
+    IA_LAUNCH_CHECK("k_xwave");
+    return IA_OK;
+}
+
+}  // namespace ia

@@ -192,14 +192,15 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
 
 def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
                    comm=None, rank=0, nranks=1, prof=False, levels=None, lsh=None, eager=False,
-                   pipeline=None, debug=False):
+                   pipeline=None, debug=False, check=True):
     """Synthesise levels 1..max_levels-1 (image_analogies.py:119-220) from device
     pyramids.  Bp_pyr (list of device tensors) is updated in place.  lsh: None (exact
     matcher) or LevelIndex.build_lsh arguments (approximate matcher).  comm: one
     communicator, or a list (one per sharded level, needed when sharded levels run
     pipelined).  pipeline: run the levels concurrently (ia_synth_levels; default
-    pipeline_default()), else one after the other.
-    Returns {level: (s, im[, debug])} device tensors."""
+    pipeline_default()), else one after the other.  check: synchronise at the end and raise
+    if a wait inside the device schedule timed out (ia_synth_status: the results would be
+    wrong).  Returns {level: (s, im[, debug])} device tensors."""
     if B_pyr[-1].dim() == 3:     # 3-channel matching (num_ch = 3)
         if comm is not None or nranks > 1 or lsh is not None:
             raise NotImplementedError('3-channel matching runs on one GPU with the exact matcher')
@@ -213,15 +214,19 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     sharded = [l for l in todo            # (the LSH matcher runs unsharded, replicated)
                if comm is not None and lsh is None and
                shard_level(level_rows(Ap_pyr_list, l), nranks)]
-    if pipeline and comms is None and len(sharded) > 1:
-        pipeline = False      # one communicator cannot serve concurrent levels
+    if pipeline and len(sharded) > 1 and (comms is None or len(comms) < len(sharded)):
+        # one exchange cannot serve two levels running at once (their records would share
+        # the exchange's box cells): levels one at a time then
+        pipeline = False
     out = {}
     t_start = time.time()
     calls = []
+    done = []
     for level in todo:
         lcomm, row_range = None, None
         if level in sharded:
-            lcomm = comms[sharded.index(level) % len(comms)] if comms else comm
+            # one exchange per sharded level; fewer only with the levels one at a time
+            lcomm = comms[min(sharded.index(level), len(comms) - 1)] if comms else comm
             row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
         index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range, lsh)
         call = _LevelCall(level, max_levels, index, B_pyr[level - 1], B_pyr[level],
@@ -232,7 +237,8 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         _ia.check(_ia.lib().ia_synth_level(ctypes.byref(call.args), _ia.stream()),
                   'ia_synth_level')
         out[level] = call.result()
-        del index, call
+        done.append(call)
+        del index
         if os.environ.get('IA_VERBOSE'):
             torch.cuda.synchronize()
             print('[ia] level %d/%d done %.3f s' % (level, max_levels - 1, time.time() - t_start),
@@ -247,6 +253,12 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         for (level, _), r in zip(calls[i:j], res):
             out[level] = r
         i = j
+    done += [c for _, c in calls]
+    if check and done:
+        # waits inside the device schedule (a neighbour's decision, another rank's records)
+        # that timed out leave wrong pixels: raise instead of returning them
+        arr = (_ia.IaSynthArgs * len(done))(*[c.args for c in done])
+        _ia.check(_ia.lib().ia_synth_status(arr, len(done), _ia.stream()), 'ia_synth_status')
     return out
 
 

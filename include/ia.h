@@ -234,6 +234,12 @@ int ia_synth_level3(const IaSynthArgs *a, void *stream);
  * (coarse pixel (y/2 + 1, x/2 + 1) and before), so the levels overlap and the critical
  * path is about the finest level's waves.  Sharded levels need one communicator each. */
 int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream);
+/* after ia_synth_level(s) calls on `stream`: synchronises the stream and returns IA_E_COMM if
+ * any wait inside those levels' synthesis timed out (a neighbouring pixel's decision inside
+ * the fused per-wave kernel, or another rank's records on a device-side exchange): the
+ * results are then wrong.  The reference has no such wait (image_analogies.py:161-220 is one
+ * thread); this is the device schedule's own integrity check. */
+int ia_synth_status(const IaSynthArgs *levels, int n, void *stream);
 
 /* profiling of ia_synth_level calls flagged IA_SYNTH_PROF (process-wide, thread-safe):
  * ia_prof_begin opens a profile (the caller has synchronised); ia_prof_end synchronises the

@@ -44,6 +44,11 @@ int ia_diag_set_pyr_form(int stream, int oh);
  * 0 off, 1 levels of <= 2^18 rows, 2 every single-GPU level; other values leave it;
  * returns the previous value */
 int ia_diag_set_graph_mode(int mode);
+/* the fused per-wave kernel (k_xwave: exact stage, device-side exchange, per-pixel tail and
+ * the next wave's query rows in one launch) for this process: 1 [default, IA_XWAVE] wherever
+ * it applies, 0 the separate kernels (k_query_wave, k_rescore / work list, k_peer_finish);
+ * other values leave it; returns the previous value */
+int ia_diag_set_xwave(int on);
 
 /* the sharded synthesis path in ONE process: level a (a->comm = NULL, a->db unused) with
  * its database split into n shards {db, row0, nrows, amax} (each ia_db_build'ed from its

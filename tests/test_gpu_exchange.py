@@ -73,7 +73,7 @@ def run_ranks(world, argv, timeout=100):
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), IA_TEST_DEVICE='0',
-                   IA_SHARD_MIN_ROWS='0')
+                   IA_SHARD_MIN_ROWS='0', IA_SHARE_GPU='1')
         procs.append(subprocess.Popen([sys.executable, '-u', os.path.join(HERE, 'exchange_worker.py')]
                                       + [str(a) for a in argv], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
