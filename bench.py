@@ -118,6 +118,16 @@ class Job:
                                  self.weights, comm=comm, rank=rank, nranks=nranks, prof=prof,
                                  lsh=self.lsh, eager=eager)
 
+    def prepare(self):
+        """Pyramids and the B' reset of one step (the batch path's per-job part)."""
+        A_pyr = ip.gaussian_pyramid_dev(self.A, cfg.n_sm, self.levels)
+        Ap_pyr = ip.gaussian_pyramid_dev(self.Ap, cfg.n_sm, self.levels)
+        B_pyr = ip.gaussian_pyramid_dev(self.B, cfg.n_sm, self.levels)
+        self.Ap_pyr_last = Ap_pyr
+        for dst, src in zip(self.Bp, self.Bp_init):
+            dst.copy_(src)
+        return A_pyr, [Ap_pyr], B_pyr, self.Bp
+
     def lsh_quality(self):
         """LSH vs exact on the same queries: the finest level's B / B' features (B' as
         this job's last synthesis left it), matched by both matchers over one index."""
@@ -342,16 +352,25 @@ def main():
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
-    ap.add_argument('--jobs', type=int, default=4, help='c5: jobs per GPU per step')
+    ap.add_argument('--jobs', type=int, default=32,
+                    help='c5: jobs per GPU per step (32 = the per-GPU share of the 256-job '
+                         'batch over 8 GPUs)')
+    ap.add_argument('--batch', type=int, default=0,
+                    help='c5: jobs per batched launch set (ia_synth_levels_batch; 0 = all of '
+                         'the GPU\'s jobs in one batch; 1 = one job per synthesis call, run '
+                         '--streams at a time)')
     ap.add_argument('--streams', type=int, default=4,
-                    help='c5: jobs run concurrently per GPU (one HIP stream + host thread each; '
-                         '4 = the HIP hardware queues per process)')
+                    help='c5 with --batch 1: jobs run concurrently per GPU (one HIP stream + '
+                         'host thread each; 4 = the HIP hardware queues per process)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0,
                     help='CPU work per leg of the CPU baseline (1 thread, all threads)')
     ap.add_argument('--matcher', default='brute', choices=['brute', 'lsh'],
                     help="lsh: the approximate E2LSH matcher (SURVEY §8(f)1, config c2)")
     ap.add_argument('--lsh', default='16,4,1.0', help='tables,hashes,width for --matcher lsh')
+    ap.add_argument('--strict-exchange', action='store_true',
+                    help='exit non-zero when the device-side exchange times out instead of '
+                         'measuring again over RCCL')
     ap.add_argument('--dry-run', action='store_true',
                     help='launcher check without a GPU: ranks meet over gloo, rank 0 prints '
                          'the world it saw')
@@ -421,7 +440,8 @@ def main():
     # c5: --streams S runs the GPU's jobs S at a time, each on its own HIP stream driven by
     # its own host thread (ctypes drops the GIL inside ia_synth_level, so the threads enqueue
     # their latency-bound waves concurrently); results are per job and stream-independent
-    nstreams = max(1, min(args.streams, len(jobs))) if args.config == 'c5' else 1
+    batch = (args.batch or len(jobs)) if args.config == 'c5' and lsh is None else 1
+    nstreams = max(1, min(args.streams, len(jobs))) if args.config == 'c5' and batch == 1 else 1
     pool = streams = None
     if nstreams > 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -444,54 +464,93 @@ def main():
             main.wait_stream(st)
         return [r for part in res for r in part]
 
+    def run_batches(prof=False):
+        outs = []
+        for b0 in range(0, len(jobs), batch):
+            part = jobs[b0:b0 + batch]
+            ins = [jb.prepare() for jb in part]
+            outs += ia.synthesize_batch_dev(ins, part[0].max_levels, [jb.k for jb in part],
+                                            part[0].weights, prof=prof)
+        return outs
+
     def run_step(prof=False):
+        if batch > 1:
+            return run_batches(prof)
         run_jobs(lambda jb: jb.step(comm, rank, world, prof))
 
+    def timed_pass(prof):
+        """K steps between two barrier + synchronize brackets; prof: HIP events around
+        every screen launch and the matcher statistics, read back after the region."""
+        if prof:
+            _ia.prof_begin()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_step(prof)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        return dt, (_ia.prof_end() if prof else None)
+
     def measure():
-        # warm-up steps run profiled too; the event pool is created before the timed region
+        # warm-up steps run profiled too; the event pool is created before any timed region
         nev = 2 * args.steps * sum(jb.waves for jb in jobs)
         _ia.prof_begin(nev)
         for _ in range(args.warmup):
             run_step(True)
         _ia.prof_end()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        # the timed steps: the product path, plus HIP events around every screen launch and
-        # the matcher statistics copied stream-ordered (no host synchronisation inside)
-        _ia.prof_begin()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            run_step(True)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        return time.perf_counter() - t0, _ia.prof_end()
+        # `value`: the product path alone; then the same K steps with the HIP events of the
+        # roofline (their cost is reported as events_overhead)
+        plain, _ = timed_pass(False)
+        evented, prof = timed_pass(True)
+        return plain, evented, prof
 
-    elapsed, prof = measure()
-    if comm and _ia.exchange_kind() == 'peer':
-        # a device-side exchange wait that timed out on any rank (every later wait then
-        # gives up at once, so B' is wrong): all ranks agree, take the RCCL exchange and
-        # measure again from scratch (every step rebuilds pyramids, DBs and B')
+    exchange_fallback = None
+    try:
+        elapsed, elapsed_ev, prof = measure()
+    except RuntimeError as e:
+        # a wait inside the device schedule timed out (synthesize_dev raises through
+        # ia_synth_status): with the device-side exchange, every rank agrees, takes the RCCL
+        # exchange and measures again from scratch (every step rebuilds pyramids, DBs, B')
+        if not (comm and _ia.exchange_kind() == 'peer' and 'timed out' in str(e)) or args.strict_exchange:
+            raise
+        exchange_fallback = 'device-side exchange wait timed out: %s' % e
+    if comm and exchange_fallback is None and _ia.exchange_kind() == 'peer':
         ok = all(_ia.lib().ia_peer_status(cm) == 0 for cm in comm)
         if not _ia._all_ok(ok, world):
-            for cm in comm:
-                _ia.lib().ia_comm_destroy(cm)
-            _ia._EXCHANGE_FALLBACK.append('a peer wait timed out during the run')
-            print('bench.py: device-side exchange timed out; measuring again over RCCL',
-                  file=sys.stderr, flush=True)
-            comm = [_ia.exchange(rank, world, 'rccl') for _ in comm]
-            elapsed, prof = measure()
+            exchange_fallback = 'device-side exchange wait timed out on some rank'
+    if exchange_fallback is not None:
+        if args.strict_exchange:
+            print('bench.py: %s (--strict-exchange)' % exchange_fallback, file=sys.stderr, flush=True)
+            sys.exit(3)
+        for cm in comm:
+            _ia.lib().ia_comm_destroy(cm)
+        _ia._EXCHANGE_FALLBACK.append(exchange_fallback)
+        print('bench.py: %s; measuring again over RCCL' % exchange_fallback, file=sys.stderr, flush=True)
+        comm = [_ia.exchange(rank, world, 'rccl') for _ in comm]
+        elapsed, elapsed_ev, prof = measure()
     for cm in comm or []:
         _ia.exchange_status(cm)     # raises if a device-side exchange wait timed out
-    t = torch.tensor([elapsed], dtype=torch.float64)
+    t = torch.tensor([elapsed, elapsed_ev], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, elapsed_ev = float(t[0].item()), float(t[1].item())
 
     # consistency of the result (outside the timed region): B' == A'[im][s] per level and
     # identical replicas across ranks
+    batch_ok = None
+    if batch > 1:
+        # every job of a batch equals its own one-job synthesis (same inputs, same B' init)
+        def job_sum(jb, out):
+            return sum(float(jb.Bp[l].sum().item()) + float(s_.double().sum().item())
+                       for l, (s_, _) in out.items())
+        outs = run_batches()
+        torch.cuda.synchronize()
+        bsums = [job_sum(jb, o) for jb, o in zip(jobs, outs)]
+        batch_ok = all(b == job_sum(jb, jb.step()) for b, jb in zip(bsums, jobs))
     out = jobs[0].step(comm, rank, world)
     chk = 0.0
     consistent = True
@@ -534,9 +593,10 @@ def main():
             g = (T + 10) // 11
             G = (T + g - 1) // g
             d = inst.setdefault(G, [0.0, 0, 0.0, 0])
-            d[0] += ms; d[1] += 1; d[2] += float(M) * p['rows']; d[3] += int(M)
+            nj = max(1, p.get('jobs', 1))      # a batch's launch screens every job's DB
+            d[0] += ms; d[1] += 1; d[2] += float(M) * p['rows'] * nj; d[3] += int(M)
             e = lv.setdefault(p['level'], [0.0, 0, 0.0, p['rows']])
-            e[0] += ms; e[1] += 1; e[2] += float(M) * p['rows']
+            e[0] += ms; e[1] += 1; e[2] += float(M) * p['rows'] * nj
     domG = max(inst, key=lambda G: inst[G][0]) if inst else None
     i_ms, i_n, i_pairs, i_q = inst[domG] if domG is not None else (0.0, 0, 0.0, 0)
     achieved = per_pair * i_pairs / (i_ms * 1e-3) / 1e12 if i_ms > 0 else 0.0
@@ -608,6 +668,7 @@ def main():
                                (', LSH matcher' if lsh is not None else ', brute force'),
                    'A': list(conf['A']), 'B': list(conf['B']), 'kappa': conf['k'],
                    'levels_cap': conf['levels'], 'jobs_per_gpu': len(jobs), 'streams_per_gpu': nstreams,
+                   'jobs_per_launch': batch,
                    'pixels_per_step': pixels_per_step,
                    'parallelism': ('jobs%d' % world) if args.config == 'c5' else
                                   ('db-shard%d' % world if world > 1 else 'single'),
@@ -618,11 +679,27 @@ def main():
                     'rows_rescored_fp64': sum(p['rows_rescored'] for p in prof),
                     'candidate_segments': sum(p['candidate_segments'] for p in prof),
                     'full_scans': sum(p['full_scans'] for p in prof),
-                    'queries': pixels_per_step * args.steps // (world if args.config == 'c5' else 1)},
+                    'queries': pixels_per_step * args.steps // (world if args.config == 'c5' else 1),
+                    # time the fused per-wave kernel's pixels spent waiting, summed over pixels
+                    # and divided by them: for the other ranks' records (device-side exchange)
+                    # and for the upper neighbour's decision (its next-query build)
+                    'peer_wait_us_per_pixel': sum(p['peer_wait_us'] for p in prof) /
+                        max(1, pixels_per_step * args.steps // (world if args.config == 'c5' else 1)),
+                    'neighbour_wait_us_per_pixel': sum(p['neighbour_wait_us'] for p in prof) /
+                        max(1, pixels_per_step * args.steps // (world if args.config == 'c5' else 1))},
+        'events_pass': {'ms_per_step': elapsed_ev / args.steps * 1e3,
+                        'overhead': (elapsed_ev - elapsed) / elapsed,
+                        'note': 'the same K steps again with HIP events around every screen '
+                                'launch and the matcher statistics (the roofline\'s source); '
+                                '`value` is the pass without them'},
         'checks': {'replicas_identical': replicas_ok, 'bp_equals_ap_at_s': consistent,
                    'checksum': chk,
+                   **({'exchange_fallback': exchange_fallback or _ia._EXCHANGE_FALLBACK[-1]}
+                      if (exchange_fallback or _ia._EXCHANGE_FALLBACK) else {}),
                    **({'concurrent_streams': nstreams, 'concurrent_identical': concurrent_ok}
-                      if concurrent_ok is not None else {})},
+                      if concurrent_ok is not None else {}),
+                   **({'batch_jobs': batch, 'batch_identical': batch_ok}
+                      if batch_ok is not None else {})},
     }
     if lsh is not None:
         result['lsh_quality'] = jobs[0].lsh_quality()
@@ -637,6 +714,10 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not (replicas_ok and consistent and batch_ok is not False and concurrent_ok is not False):
+        print('bench.py: result check failed (replicas_identical=%s, bp_equals_ap_at_s=%s)'
+              % (replicas_ok, consistent), file=sys.stderr, flush=True)
+        sys.exit(4)
 
 
 if __name__ == '__main__':

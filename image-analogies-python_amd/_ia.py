@@ -65,7 +65,7 @@ class IaShardDb(ctypes.Structure):
 
 IA_SYNTH_EAGER = 1
 IA_SYNTH_PROF = 2
-IA_PROF_FIELDS = 8
+IA_PROF_FIELDS = 11
 
 _SIGS = {
     'ia_last_error': (ctypes.c_char_p, []),
@@ -113,6 +113,8 @@ _SIGS = {
                                               ctypes.c_int, ctypes.c_int, _dp, _dp]),
     'ia_synth_levels': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_synth_status': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
+    'ia_synth_levels_batch': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, ctypes.c_int,
+                                             _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
     'ia_lsh_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp,
                                     ctypes.POINTER(IaLsh), _dp]),
@@ -219,7 +221,7 @@ def db_build_form(tiled=-1):
 
 
 PROF_KEYS = ('level', 'rows', 'pairs', 'screen_ms', 'timed_screens', 'rows_rescored',
-             'candidate_segments', 'full_scans')
+             'candidate_segments', 'full_scans', 'peer_wait_us', 'neighbour_wait_us', 'jobs')
 
 
 def prof_begin(nevents=0):
@@ -250,7 +252,7 @@ def prof_end():
     for r in range(n):
         rec = dict(zip(PROF_KEYS, buf[r * IA_PROF_FIELDS:(r + 1) * IA_PROF_FIELDS]))
         for k in ('level', 'rows', 'timed_screens', 'rows_rescored', 'candidate_segments',
-                  'full_scans'):
+                  'full_scans', 'jobs'):
             rec[k] = int(rec[k])
         nl = rec['timed_screens']
         ms = (ctypes.c_float * max(nl, 1))()
@@ -317,6 +319,7 @@ def mean_dev(t):
 
 
 _EXCHANGE_FALLBACK = []   # reasons the device-side exchange was replaced by RCCL
+PEER_MAX = 16             # ranks of one device-side exchange (IA_PEER_MAX, ia_internal.h)
 
 
 def exchange_kind():
@@ -364,8 +367,20 @@ def exchange(rank, world, kind=None, mcap=4096):
         check(lib().ia_comm_init(uid.numpy().tobytes(), world, rank, ctypes.byref(h)),
               'ia_comm_init')
         return h
+    if world > PEER_MAX:
+        _EXCHANGE_FALLBACK.append('%d ranks > the device-side exchange\'s %d' % (world, PEER_MAX))
+        return exchange(rank, world, 'rccl', mcap)
     hd = ctypes.create_string_buffer(64)
-    check(lib().ia_peer_create(world, rank, mcap, ctypes.byref(h), hd), 'ia_peer_create')
+    rc = lib().ia_peer_create(world, rank, mcap, ctypes.byref(h), hd)
+    if not _all_ok(rc == 0, world):
+        # no usable receive box on some rank: every rank takes the RCCL exchange
+        if rc == 0:
+            lib().ia_comm_destroy(h)
+        _EXCHANGE_FALLBACK.append('rank %d: %s' % (rank, lib().ia_last_error().decode())
+                                  if rc else 'ia_peer_create failed on another rank')
+        print('ia: device-side exchange unusable (%s); falling back to RCCL' % _EXCHANGE_FALLBACK[-1],
+              file=sys.stderr, flush=True)
+        return exchange(rank, world, 'rccl', mcap)
     mine = torch.frombuffer(bytearray(hd.raw[:64]), dtype=torch.uint8).clone()
     parts = [torch.zeros(64, dtype=torch.uint8) for _ in range(world)]
     if world > 1:
@@ -378,6 +393,14 @@ def exchange(rank, world, kind=None, mcap=4096):
     if _all_ok(why is None, world):
         if lib().ia_peer_check(h, stream()) != 0:
             why = 'rank %d: %s' % (rank, lib().ia_last_error().decode())
+        elif world > 1:
+            # many waves of known records through the boxes (a one-wave handshake can pass
+            # on cold caches where later waves would go stale)
+            bad = ctypes.c_int(0)
+            if lib().ia_diag_peer_stress(h, 16, min(mcap, 256), ctypes.byref(bad), stream()) != 0:
+                why = 'rank %d: %s' % (rank, lib().ia_last_error().decode())
+            elif bad.value:
+                why = 'rank %d: %d of 16 x %d stress records wrong' % (rank, bad.value, min(mcap, 256))
         if _all_ok(why is None, world):
             return h
     # some rank could not map or reach the others' boxes: every rank drops its peer

@@ -181,6 +181,16 @@ int ia_peer_create(int nranks, int rank, int mcap, void **comm, uint8_t handle[6
     }
     if (e != hipSuccess) {
         (void)hipGetLastError();
+        // plain (coarse-grained) memory: another GPU's stores need not become visible to
+        // this GPU's polls (they may be served from its L2), so across GPUs this form is
+        // refused and every rank takes the RCCL exchange; ranks sharing one GPU
+        // (IA_SHARE_GPU=1) meet in that GPU's own memory and may use it
+        if (nranks > 1 && !env_int("IA_SHARE_GPU", 0)) {
+            delete p;
+            set_error("ia_peer_create: neither uncached nor fine-grained device memory for the "
+                      "receive box (plain memory is not coherent across GPUs)");
+            return IA_E_UNSUPPORTED;
+        }
         e = hipMalloc(&m, p->bytes);
         p->mem_kind = 2;
     }

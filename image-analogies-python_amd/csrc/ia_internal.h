@@ -150,6 +150,32 @@ struct FinishArgs {
     PeerView px{};
 };
 
+// one job of a batch of identical-shape jobs sharing each wave's launches (the multi_script
+// workload, ia_synth_levels_batch): its own images, DB, query buffers (by wave parity),
+// outputs and control words; the screen and k_xwave take job blockIdx.y's pointers from a
+// device table of these
+struct XJob {
+    const double *A_sm, *A_lg, *Ap_sm, *Ap_lg;   // DbSrc images
+    const uint32_t *fa, *ca, *norm, *ap;          // image-form DB sections (ImgDb)
+    const void *db;                               // split-f16 rows
+    float *segmin;
+    double *q64[2];
+    float *qp[2];
+    double *nq[2];
+    _Float16 *q16[2];
+    const float *amax;
+    const double *center;
+    const double *B_sm, *B_lg, *Bp_sm;
+    double *Bp_lg;
+    const double *weights;
+    double kappa_factor;
+    int32_t *s, *im, *dbg_px;
+    double *dbg_dist;
+    unsigned long long *dbox;
+    unsigned int *ctl;                            // tickets[2], error word
+};
+constexpr int IA_BATCH_MAX = 128;
+
 // one launch of the fused per-wave kernel k_xwave (ia_xwave.hip): wave t's exact stage,
 // exchange (f.px) and per-pixel tail, and wave t + 1's query rows
 struct XArgs {
@@ -175,8 +201,9 @@ struct XArgs {
     unsigned int *err;            // set when a wait for a neighbour's decision times out
     unsigned long long *stats;    // nullable: rows rescored, candidate segments, full scans
     FinishArgs f;                 // t, y_lo, W, ..., px (sharded DB: the device-side exchange)
+    const XJob *jobs;             // nullable: a batch, job blockIdx.y's pointers override these
 };
-int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st);
+int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st, int njobs = 1);
 
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS
 // cache lines so that the atomics of a wave's M queries do not serialise on one address;
@@ -209,8 +236,11 @@ int launch_query_rows(const double *qin, int M, const double *center, float *qp,
 // segmin[M][db_nsegs(nrows)] (screen units); q16 holds qrows_alloc(M) rows
 // img (nullable): the DB's image form (ImgDb, whole chunks) streamed instead of the rows
 // (same minima, bit for bit)
+// jobs (nullable): a batch of njobs identical-shape jobs in one launch (grid y = job; each
+// job's DB sections, q16[parity] and segmin from its table entry)
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16 *q16, int M,
-                    float *segmin, hipStream_t st);
+                    float *segmin, hipStream_t st, const XJob *jobs = nullptr, int njobs = 1,
+                    int parity = 0);
 // the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
 // stats (nullable): rows rescored, candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);

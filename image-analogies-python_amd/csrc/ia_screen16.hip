@@ -259,8 +259,14 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
                                                      int ch, int seg_rows,
                                                      const half8 *__restrict__ q16, int M,
                                                      int groups, float *__restrict__ segmin,
-                                                     long nseg) {
+                                                     long nseg, const XJob *jobs, int parity) {
     __shared__ half8 sbuf[2 * STAGE_H8];
+    if (jobs) {   // batch: this job's DB, query rows and minima
+        const XJob &J = jobs[blockIdx.y];
+        db16 = reinterpret_cast<const half8 *>(J.db);
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity]);
+        segmin = J.segmin;
+    }
     __shared__ int smin[SPC_MAX * G * 32];
     const int b = blockIdx.x;
     const int slot = b >> 3;
@@ -293,8 +299,14 @@ template <int G>
 __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int ch, int seg_rows,
                                                       const half8 *__restrict__ q16, int M,
                                                       int groups, float *__restrict__ segmin,
-                                                      long nseg) {
+                                                      long nseg, const XJob *jobs, int parity) {
     __shared__ half8 E[STAGE_H8];
+    if (jobs) {   // batch: this job's image-form sections, query rows and minima
+        const XJob &J = jobs[blockIdx.y];
+        im.fa = J.fa; im.ca = J.ca; im.norm = J.norm; im.ap = J.ap;
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity]);
+        segmin = J.segmin;
+    }
     __shared__ __attribute__((aligned(16))) char wbuf[2 * WIN_B];
     __shared__ int smin[SPC_MAX * G * 32];
     const int b = blockIdx.x;
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
 static inline int screen_groups(int T) { return (T + MAX_G - 1) / MAX_G; }
 
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16 *q16, int M,
-                    float *segmin, hipStream_t st) {
+                    float *segmin, hipStream_t st, const XJob *jobs, int njobs, int parity) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -343,14 +355,16 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16
     const int G = (T + groups - 1) / groups;
     const long nb = ((nchunks + 7) / 8) * 8 * groups;
     IA_ARG(nb < (1L << 31), "screen grid too large");
+    IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || jobs), "launch_screen16: bad batch");
+    const dim3 grid((unsigned)nb, (unsigned)njobs);
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
         if (img)                                                                                \
-            k_screen16i<GG><<<(unsigned)nb, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, q, \
-                                                          M, groups, segmin, nseg);             \
+            k_screen16i<GG><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, q, M,      \
+                                                  groups, segmin, nseg, jobs, parity);          \
         else                                                                                    \
-            k_screen16<GG><<<(unsigned)nb, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q,  \
-                                                         M, groups, segmin, nseg);              \
+            k_screen16<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M,       \
+                                                 groups, segmin, nseg, jobs, parity);           \
         break;
     switch (G) {
         IA_SCREEN16_CASE(1)

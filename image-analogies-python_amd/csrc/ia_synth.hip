@@ -171,6 +171,7 @@ struct SynthWs {
     double *nqb;
     unsigned long long *dbox;
     unsigned int *ctl;
+    XJob *jtab;              // a batch's job table (ia_synth_levels_batch, job 0's workspace)
 };
 constexpr int XW_CTL_ERR = 2;
 
@@ -201,6 +202,7 @@ static size_t carve(SynthWs *ws, char *base, int H, int W, long nrows, int nrank
     w.nqb = (double *)take((size_t)qr * sizeof(double));
     w.dbox = (unsigned long long *)take((size_t)H * 2 * sizeof(unsigned long long));
     w.ctl = (unsigned int *)take(256);
+    w.jtab = (XJob *)take((size_t)IA_BATCH_MAX * sizeof(XJob));
     if (ws) *ws = w;
     return off;
 }
@@ -236,6 +238,7 @@ static thread_local GraphKeeper g_graphs;
 // launches with no host round trip (bench.py profiles its timed steps this way).
 struct ProfRec {
     int tag;
+    int jobs;                // jobs batched into each launch
     long nrows;
     double pairs;
     size_t ev0;
@@ -344,6 +347,11 @@ struct LevelRun {
     ImgPair B{}, Bp{};
     int H = 0, W = 0, nw = 0, nranks = 1;
     bool prof = false, timed = false, fused = false, peer = false, xw = false;
+    // a batch of K identical-shape jobs (ia_synth_levels_batch): this run is job 0 and owns
+    // the launches; part[k - 1] holds job k's state (member runs record no profile)
+    int K = 1;
+    bool member = false;
+    std::vector<LevelRun> part;
     size_t ev0 = 0;
     unsigned long long *hstats = nullptr;
     double pairs = 0.0;
@@ -368,7 +376,7 @@ struct LevelRun {
         src = make_dbsrc(a->src);
         B = ImgPair{a->B_sm, a->B_lg, a->B_hs, a->B_ws, H, W};
         Bp = ImgPair{a->Bp_sm, a->Bp_lg, a->B_hs, a->B_ws, H, W};
-        prof = (a->flags & IA_SYNTH_PROF) && prof_active();
+        prof = !member && (a->flags & IA_SYNTH_PROF) && prof_active();
         timed = prof;
         if (prof && (rc = prof_reserve(2 * (size_t)nw, &ev0, &hstats))) return rc;
         // fused tail (one launch + one round trip less per wave): on a single shard the exact
@@ -469,6 +477,59 @@ struct LevelRun {
         return IA_OK;
     }
 
+    // job k's table entry (the batched launches read their pointers from it)
+    XJob job_entry() const {
+        XJob J{};
+        J.A_sm = a->src.A_sm; J.A_lg = a->src.A_lg; J.Ap_sm = a->src.Ap_sm; J.Ap_lg = a->src.Ap_lg;
+        ImgDb img{};
+        if (a->dbi)
+            img_db_layout(src.A.h, src.A.w, src.A.hs, src.A.ws, 1, a->row0, a->nrows, a->dbi, img, nullptr);
+        J.fa = img.fa; J.ca = img.ca; J.norm = img.norm; J.ap = img.ap;
+        J.db = a->db;
+        J.segmin = match_segmin(ws.scratch);
+        J.q64[0] = ws.q64; J.q64[1] = ws.q64b;
+        J.qp[0] = ws.qp; J.qp[1] = ws.qpb;
+        J.nq[0] = ws.nq; J.nq[1] = ws.nqb;
+        J.q16[0] = ws.q16; J.q16[1] = ws.q16b;
+        J.amax = a->amax;
+        J.center = a->center;
+        J.B_sm = a->B_sm; J.B_lg = a->B_lg; J.Bp_sm = a->Bp_sm; J.Bp_lg = a->Bp_lg;
+        J.weights = a->weights;
+        J.kappa_factor = a->kappa_factor;
+        J.s = a->s; J.im = a->im; J.dbg_px = a->dbg_px; J.dbg_dist = a->dbg_dist;
+        J.dbox = ws.dbox;
+        J.ctl = ws.ctl;
+        return J;
+    }
+
+    // K jobs (args[0..K)) of identical shapes in one set of launches per wave; the job
+    // table is staged through `pinned` (kept alive by the caller until the copy has run)
+    int init_batch(const IaSynthArgs *args, int nj, hipStream_t st, XJob *pinned) {
+        int rc = init(&args[0], st);
+        if (rc || nj == 1) return rc;
+        IA_ARG(nj <= IA_BATCH_MAX, "ia_synth_levels_batch: too many jobs in one batch");
+        IA_ARG(xw, "ia_synth_levels_batch: batches run the exact matcher on one GPU (fused kernel)");
+        K = nj;
+        part.resize(K - 1);
+        for (int k = 1; k < K; ++k) {
+            const IaSynthArgs &b = args[k];
+            IA_ARG(b.H == a->H && b.W == a->W && b.nrows == a->nrows && b.N_total == a->N_total &&
+                       b.row0 == a->row0 && b.B_hs == a->B_hs && b.B_ws == a->B_ws &&
+                       b.src.Ah == a->src.Ah && b.src.Aw == a->src.Aw && b.src.A_hs == a->src.A_hs &&
+                       b.src.A_ws == a->src.A_ws && b.src.nAp == a->src.nAp &&
+                       !b.comm == !a->comm && !b.lsh == !a->lsh && !b.dbi == !a->dbi &&
+                       !b.dbg_px == !a->dbg_px,
+                   "ia_synth_levels_batch: the jobs of a batch must have identical shapes and forms");
+            part[k - 1].member = true;
+            if ((rc = part[k - 1].init(&b, st))) return rc;
+            IA_ARG(part[k - 1].xw, "ia_synth_levels_batch: a job without the fused kernel");
+        }
+        pinned[0] = job_entry();
+        for (int k = 1; k < K; ++k) pinned[k] = part[k - 1].job_entry();
+        IA_HIP(hipMemcpyAsync(ws.jtab, pinned, (size_t)K * sizeof(XJob), hipMemcpyHostToDevice, st));
+        return IA_OK;
+    }
+
     // wave t on the fused path: [wave 0's query rows,] the screen, then k_xwave (exact
     // stage, exchange, tail, and wave t + 1's query rows into the other buffer set)
     int xw_wave(int t, int y_lo, int M, hipStream_t sq) {
@@ -481,6 +542,13 @@ struct LevelRun {
         if (t == 0 && (rc = launch_query_wave(B, Bp, 0, y_lo, M, a->center, q64s[0], qps[0], nqs[0],
                                               a->amax, q16s[0], sq)))
             return rc;
+        for (int k = 1; k < K && t == 0; ++k) {
+            const LevelRun &p = part[k - 1];
+            if ((rc = launch_query_wave(p.B, p.Bp, 0, y_lo, M, p.a->center, p.ws.q64, p.ws.qp, p.ws.nq,
+                                        p.a->amax, p.ws.q16, sq)))
+                return rc;
+        }
+        const XJob *jt = K > 1 ? ws.jtab : nullptr;
         ImgDb img{};
         const bool im = a->dbi != nullptr;
         IA_ARG(!im || img_db_layout(src.A.h, src.A.w, src.A.hs, src.A.ws, 1, a->row0, a->nrows, a->dbi, img,
@@ -491,7 +559,8 @@ struct LevelRun {
         hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
         hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
         if (e0) IA_HIP(hipEventRecord(e0, sq));
-        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, q16s[b], M, segmin, sq))) return rc;
+        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, q16s[b], M, segmin, sq, jt, K, b)))
+            return rc;
         if (e1) IA_HIP(hipEventRecord(e1, sq));
         int y_lo_n = 0, M_n = 0;
         if (t + 1 < nw) wave_rows(H, W, t + 1, y_lo_n, M_n);
@@ -518,10 +587,11 @@ struct LevelRun {
         x.f = FinishArgs{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
                          a->im, a->dbg_px, a->dbg_dist, nullptr, nullptr};
         if (peer) x.f.px = comm_peer_wave(a->comm);
+        x.jobs = jt;
         const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
-        if ((rc = launch_xwave(x, R, im, sq))) return rc;
+        if ((rc = launch_xwave(x, R, im, sq, K))) return rc;
         ++nscreen;
-        pairs += (double)M * (double)a->nrows;
+        pairs += (double)M * (double)a->nrows * K;
         if (prof) Ms.push_back(M);
         static const int sync_every = env_int("IA_SYNC_EVERY", 0);
         if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
@@ -554,7 +624,7 @@ struct LevelRun {
     int done(hipStream_t st) {
         if (prof) {   // read back by ia_prof_end (no synchronisation here)
             IA_HIP(hipMemcpyAsync(hstats, ws.stats, STATS_BYTES, hipMemcpyDeviceToHost, st));
-            prof_push(ProfRec{a->tag, a->nrows, pairs, ev0, nscreen, timed ? 1 : 0, hstats,
+            prof_push(ProfRec{a->tag, K, a->nrows, pairs, ev0, nscreen, timed ? 1 : 0, hstats,
                               std::move(Ms)});
         }
         return IA_OK;
@@ -590,6 +660,25 @@ struct PipeRes {   // per host thread: the level streams and events of ia_synth_
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> events;
     size_t next_event = 0;
+    // pinned staging of the batch job tables: reused after the previous call's copies ran
+    void *pin = nullptr;
+    size_t pin_bytes = 0;
+    hipEvent_t staged = nullptr;
+    bool staged_rec = false;
+    hipError_t staging(size_t bytes, void **p) {
+        hipError_t r = hipSuccess;
+        if (!staged && (r = hipEventCreateWithFlags(&staged, hipEventDisableTiming)) != hipSuccess) return r;
+        if (staged_rec && (r = hipEventSynchronize(staged)) != hipSuccess) return r;
+        if (bytes > pin_bytes) {
+            if (pin && (r = hipHostFree(pin)) != hipSuccess) return r;
+            pin = nullptr;
+            if ((r = hipHostMalloc(&pin, bytes, hipHostMallocDefault)) != hipSuccess) return r;
+            pin_bytes = bytes;
+        }
+        staged_rec = true;
+        *p = pin;
+        return r;
+    }
     hipError_t event(hipEvent_t *e) {
         if (next_event == events.size()) {
             hipEvent_t x;
@@ -650,6 +739,12 @@ int ia_release_thread_resources(void) {
     for (hipEvent_t e : g_pipe.events) IA_HIP(hipEventDestroy(e));
     g_pipe.streams.clear();
     g_pipe.events.clear();
+    if (g_pipe.pin) IA_HIP(hipHostFree(g_pipe.pin));
+    if (g_pipe.staged) IA_HIP(hipEventDestroy(g_pipe.staged));
+    g_pipe.pin = nullptr;
+    g_pipe.pin_bytes = 0;
+    g_pipe.staged = nullptr;
+    g_pipe.staged_rec = false;
     g_pipe.next_event = 0;
     if (g_graphs.cap) { IA_HIP(hipStreamDestroy(g_graphs.cap)); g_graphs.cap = nullptr; }
     if (g_graphs.done) { IA_HIP(hipEventDestroy(g_graphs.done)); g_graphs.done = nullptr; }
@@ -712,6 +807,9 @@ int ia_prof_end(double *out, int maxrec) {
         o[5] = (double)st[0];
         o[6] = (double)st[1];
         o[7] = (double)st[2];
+        o[8] = (double)st[3] * 1e-2;   // 100 MHz ticks -> us
+        o[9] = (double)st[4] * 1e-2;
+        o[10] = p.jobs;
     }
     return n;
 }
@@ -777,12 +875,16 @@ int ia_diag_synth_level_shards(const IaSynthArgs *a, const IaShardDb *shards, in
     return run.done(st);
 }
 
-int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
-    IA_ARG(levels && n >= 1 && n <= 64, "ia_synth_levels: bad level count");
+// n consecutive levels of K identical-shape jobs (levels[j * K + k]: level j of job k)
+static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
+    IA_ARG(levels && n >= 1 && n <= 64 && K >= 1 && K <= IA_BATCH_MAX, "ia_synth_levels: bad level count");
+    auto lv = [&](int j) -> const IaSynthArgs & { return levels[(size_t)j * K]; };
     for (int j = 1; j < n; ++j)
-        IA_ARG(levels[j].Bp_sm == levels[j - 1].Bp_lg && levels[j].B_hs == levels[j - 1].H &&
-                   levels[j].B_ws == levels[j - 1].W,
-               "ia_synth_levels: levels must be consecutive (level j's coarse B' = level j-1's B')");
+        for (int k = 0; k < K; ++k)
+            IA_ARG(levels[(size_t)j * K + k].Bp_sm == levels[(size_t)(j - 1) * K + k].Bp_lg &&
+                       levels[(size_t)j * K + k].B_hs == levels[(size_t)(j - 1) * K + k].H &&
+                       levels[(size_t)j * K + k].B_ws == levels[(size_t)(j - 1) * K + k].W,
+                   "ia_synth_levels: levels must be consecutive (level j's coarse B' = level j-1's B')");
     hipStream_t st = S(stream);
     // one stream per level; coarser levels at high priority (IA_PIPE_PRIO, default 1) so
     // that they run ahead of the finest level instead of time-sharing with it.  Measured
@@ -807,13 +909,19 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
     hipEvent_t start;
     IA_HIP(g_pipe.event(&start));
     IA_HIP(hipEventRecord(start, st));
+    // the batch job tables go through a pinned host buffer kept by this thread (reused once
+    // the previous call's copies have run)
+    XJob *pinned = nullptr;
+    if (K > 1) {
+        IA_HIP(g_pipe.staging((size_t)n * K * sizeof(XJob), reinterpret_cast<void **>(&pinned)));
+    }
     std::vector<LevelRun> run(n);
     std::vector<std::vector<hipEvent_t>> blk(n);   // blk[j][b]: level j done through block b
     std::vector<int> next(n, 0), waited(n, -1), need_max(n, 0);
     for (int j = 0; j < n; ++j) {
         hipStream_t sj = g_pipe.streams[j];
         IA_HIP(hipStreamWaitEvent(sj, start, 0));
-        int rc = run[j].init(&levels[j], sj);
+        int rc = run[j].init_batch(&levels[(size_t)j * K], K, sj, pinned + (size_t)j * K);
         if (rc) return rc;
         blk[j].assign((run[j].nw + PIPE_BLOCK - 1) / PIPE_BLOCK, nullptr);
     }
@@ -835,8 +943,8 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
     // fill the one GPU's slots while a third rank's awaited ones cannot start.
     static const int overlap = env_int("IA_SHARD_OVERLAP", 1) && !env_int("IA_SHARE_GPU", 0);
     auto multi_rank = [&](int j) {
-        if (levels[j].comm == nullptr || levels[j].nrows >= levels[j].N_total) return false;
-        return !(overlap && comm_peer_mcap(levels[j].comm) > 0);
+        if (lv(j).comm == nullptr || lv(j).nrows >= lv(j).N_total) return false;
+        return !(overlap && comm_peer_mcap(lv(j).comm) > 0);
     };
     std::function<int(int, int)> advance;
     advance = [&](int j, int target) -> int {
@@ -855,7 +963,7 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
             const int t = next[j];
             if (j > 0) {
                 // on the fused path wave t's launch also builds wave t + 1's query rows
-                int w = coarse_need(&levels[j], run[j].xw && t + 1 < run[j].nw ? t + 1 : t);
+                int w = coarse_need(&lv(j), run[j].xw && t + 1 < run[j].nw ? t + 1 : t);
                 need_max[j] = w > need_max[j] ? w : need_max[j];
                 w = need_max[j];
                 if (w > waited[j]) {
@@ -896,7 +1004,14 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) {
         IA_HIP(hipEventRecord(e, sj));
         IA_HIP(hipStreamWaitEvent(st, e, 0));
     }
+    if (pinned) IA_HIP(hipEventRecord(g_pipe.staged, st));
     return IA_OK;
+}
+
+int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream) { return synth_levels(levels, n, 1, stream); }
+
+int ia_synth_levels_batch(const IaSynthArgs *levels, int n, int K, void *stream) {
+    return synth_levels(levels, n, K, stream);
 }
 
 }  // extern "C"

@@ -83,7 +83,7 @@ __device__ __forceinline__ double pw55_lds(const double *v) {
 
 // the record of one DB row rescored by one thread (the row list's overflow: never on the
 // measured configs; out of line so that its 55-load gathers do not inflate the common path)
-__device__ __attribute__((noinline)) XRec row_rec(const DbSrc &src, long g, const double *qs,
+__device__ __attribute__((noinline)) XRec row_rec(DbSrc src, long g, const double *qs,
                                                   const double *wts) {
     return XRec{row_dist2(src, g, qs), g, row_wdist(src, g, qs, wts), src.Ap.lg[g]};
 }
@@ -97,8 +97,43 @@ __device__ __forceinline__ unsigned long long dgran(unsigned int tag, unsigned i
     return ((unsigned long long)tag << 32) | bits;
 }
 
-template <bool IMG>
-__global__ __launch_bounds__(256, 3) void k_xwave(XArgs a) {
+// a batch's job J (blockIdx.y) in place of the launch's pointers; b = wave t's parity
+__device__ __forceinline__ void xjob_apply(XArgs &a, const XJob &J, int b) {
+    a.src.A.sm = J.A_sm; a.src.A.lg = J.A_lg; a.src.Ap.sm = J.Ap_sm; a.src.Ap.lg = J.Ap_lg;
+    a.im.fa = J.fa; a.im.ca = J.ca; a.im.norm = J.norm; a.im.ap = J.ap;
+    a.db = J.db;
+    a.segmin = J.segmin;
+    a.q64 = J.q64[b]; a.qp = J.qp[b]; a.nq = J.nq[b];
+    a.q64n = J.q64[b ^ 1]; a.qpn = J.qp[b ^ 1]; a.nqn = J.nq[b ^ 1]; a.q16n = J.q16[b ^ 1];
+    a.amax = J.amax;
+    a.center = J.center;
+    a.B.sm = J.B_sm; a.B.lg = J.B_lg; a.Bp.sm = J.Bp_sm; a.Bp.lg = J.Bp_lg;
+    a.dbox = J.dbox;
+    a.tickets = J.ctl;
+    a.err = J.ctl + 2;
+    a.f.weights = J.weights;
+    a.f.kappa_factor = J.kappa_factor;
+    a.f.Bp_lg = J.Bp_lg;
+    a.f.s = J.s; a.f.im = J.im; a.f.dbg_px = J.dbg_px; a.f.dbg_dist = J.dbg_dist;
+}
+
+// BATCH: a0.jobs holds a batch's pointers; the block copies the launch arguments into LDS
+// once and overrides them with its job's (a private copy of the arguments would live in
+// scratch memory), then reads them from there
+template <bool IMG, bool BATCH>
+__global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
+    __shared__ __attribute__((aligned(16))) char sa_raw[BATCH ? sizeof(XArgs) : 16];
+    XArgs &sa = *reinterpret_cast<XArgs *>(sa_raw);
+    if constexpr (BATCH) {
+        static_assert(sizeof(XArgs) % 8 == 0, "XArgs copied as 8-byte words");
+        const unsigned long long *w0 = reinterpret_cast<const unsigned long long *>(&a0);
+        unsigned long long *w1 = reinterpret_cast<unsigned long long *>(&sa);
+        for (int w = threadIdx.x; w < (int)(sizeof(XArgs) / 8); w += 256) w1[w] = w0[w];
+        __syncthreads();
+        if (threadIdx.x == 0) xjob_apply(sa, a0.jobs[blockIdx.y], a0.f.t & 1);
+        __syncthreads();
+    }
+    const XArgs &a = BATCH ? sa : a0;
     constexpr size_t POOL = IMG ? (size_t)4 * WIN_SLOT : 0;
     __shared__ __attribute__((aligned(16))) char pool[POOL > XW_STAGE_B ? POOL : XW_STAGE_B];
     __shared__ double cx[XW_NCOH][IA_DP], cw[XW_NCOH][IA_DP];
@@ -356,15 +391,19 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a) {
 #pragma unroll
         for (int w = 1; w < 4; ++w) xrec_take(lb, wbest[w]);
         XRec gb = lb;
+        unsigned long long waited = 0;
         if (f.px.nranks > 0) {
             peer_publish_rec(f.px, i, lb, lane);
+            const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
             if (!peer_collect_rec(f.px, i, lane, gb)) gb = lb;
+            waited = __builtin_amdgcn_s_memrealtime() - w0;
         }
         if (a.stats && lane == 0) {
             unsigned long long *sl = stats_slot(a.stats, i);
             atomicAdd(&sl[0], (unsigned long long)nresc);
             atomicAdd(&sl[1], (unsigned long long)ns);
             atomicAdd(&sl[2], full ? 1ULL : 0ULL);
+            atomicAdd(&sl[3], waited);
         }
         // ---- kappa test and update (image_analogies.py:200-220; finish_apply's rules)
         const CohSel c = cs;
@@ -416,6 +455,10 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a) {
         const unsigned long long *d = a.dbox + 2 * (long)(y - 1);
         unsigned long long g0 = 0, g1 = 0;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        auto waited = [&]() {
+            if (a.stats && lane == 0)
+                atomicAdd(&stats_slot(a.stats, i)[4], __builtin_amdgcn_s_memrealtime() - t0);
+        };
         for (;;) {
             g0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             g1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -426,6 +469,7 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        waited();
         nb = __longlong_as_double((long long)(((g1 & 0xffffffffULL) << 32) | (g0 & 0xffffffffULL)));
     }
     const double vq = dep == 1 ? own : (dep == 2 ? nb : (lane < IA_D ? nxv[lane] : 0.0));
@@ -446,10 +490,17 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a) {
     split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, a.amax[0]);
 }
 
-int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st) {
+int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st, int njobs) {
     if (nblocks <= 0) return IA_OK;
-    if (img) k_xwave<true><<<nblocks, 256, 0, st>>>(a);
-    else k_xwave<false><<<nblocks, 256, 0, st>>>(a);
+    IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || a.jobs), "launch_xwave: bad batch");
+    const dim3 grid((unsigned)nblocks, (unsigned)njobs);
+    if (njobs > 1) {
+        if (img) k_xwave<true, true><<<grid, 256, 0, st>>>(a);
+        else k_xwave<false, true><<<grid, 256, 0, st>>>(a);
+    } else {
+        if (img) k_xwave<true, false><<<grid, 256, 0, st>>>(a);
+        else k_xwave<false, false><<<grid, 256, 0, st>>>(a);
+    }
     IA_LAUNCH_CHECK("k_xwave");
     return IA_OK;
 }

@@ -262,6 +262,39 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     return out
 
 
+def synthesize_batch_dev(jobs, max_levels, k, weights, prof=False, debug=False, check=True):
+    """K independent analogies of identical shapes in ONE set of launches per wave (the
+    multi_script batch, multi_script.py:13-32: each run an image_analogies_main of its own;
+    SURVEY §8(e) config 5).  jobs: list of (A_pyr, Ap_pyr_list, B_pyr, Bp_pyr) device
+    pyramids (Bp_pyr updated in place); k: one kappa or one per job.  Every level of every
+    job is synthesised exactly as synthesize_dev would (exact matcher, one GPU); each wave's
+    screen and fused kernel serve all K jobs at once (ia_synth_levels_batch), so the batch
+    costs about one job's per-wave launch latency.  Returns one {level: (s, im[, debug])}
+    dict per job."""
+    K = len(jobs)
+    if K == 0:
+        return []
+    ks = list(k) if isinstance(k, (list, tuple)) else [k] * K
+    w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
+    if any(j[2][-1].dim() == 3 for j in jobs):
+        raise NotImplementedError('batches run 1-channel (luminance) matching')
+    levels = list(range(1, max_levels))
+    calls = []          # level-major: calls[j * K + job]
+    for level in levels:
+        for (A_pyr, Ap_list, B_pyr, Bp_pyr), kj in zip(jobs, ks):
+            index = algorithms.level_index(A_pyr, Ap_list, level, None, None)
+            calls.append(_LevelCall(level, max_levels, index, B_pyr[level - 1], B_pyr[level],
+                                    Bp_pyr[level - 1], Bp_pyr[level], w, kj, None, prof, False,
+                                    debug))
+    arr = (_ia.IaSynthArgs * len(calls))(*[c.args for c in calls])
+    _ia.check(_ia.lib().ia_synth_levels_batch(arr, len(levels), K, _ia.stream()),
+              'ia_synth_levels_batch')
+    if check:
+        _ia.check(_ia.lib().ia_synth_status(arr, len(calls), _ia.stream()), 'ia_synth_status')
+    return [{level: calls[j * K + q].result() for j, level in enumerate(levels)}
+            for q in range(K)]
+
+
 # ---- setup (image_analogies.py:17-94) ------------------------------------------------------
 
 def _read(fname):

@@ -234,6 +234,13 @@ int ia_synth_level3(const IaSynthArgs *a, void *stream);
  * (coarse pixel (y/2 + 1, x/2 + 1) and before), so the levels overlap and the critical
  * path is about the finest level's waves.  Sharded levels need one communicator each. */
 int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream);
+/* K independent jobs of identical shapes (the multi_script batch, multi_script.py:13-32;
+ * SURVEY §8(e) config 5), n consecutive levels each: levels[j * K + k] is level j of job k,
+ * every job with its own inputs, DB, workspace and outputs.  Each wave of each level is ONE
+ * screen launch and ONE fused-kernel launch for all K jobs (grid y = job), so K jobs cost
+ * about one job's launch latency; results equal K separate ia_synth_levels calls.  Exact
+ * matcher on one GPU only (comm and lsh NULL), 1 <= K <= 128. */
+int ia_synth_levels_batch(const IaSynthArgs *levels, int n, int K, void *stream);
 /* after ia_synth_level(s) calls on `stream`: synchronises the stream and returns IA_E_COMM if
  * any wait inside those levels' synthesis timed out (a neighbouring pixel's decision inside
  * the fused per-wave kernel, or another rank's records on a device-side exchange): the
@@ -245,9 +252,12 @@ int ia_synth_status(const IaSynthArgs *levels, int n, void *stream);
  * ia_prof_begin opens a profile (the caller has synchronised); ia_prof_end synchronises the
  * device and writes IA_PROF_FIELDS doubles per recorded level call, in call order:
  * {tag, DB rows, (query, row) pairs, screen ms over the timed launches, #timed screen
- * launches, #rows rescored in fp64, #candidate segments, #full scans}; returns the number
- * of records (<0: error). */
-#define IA_PROF_FIELDS 8
+ * launches, #rows rescored in fp64, #candidate segments, #full scans, microseconds waited
+ * for other ranks' records summed over the level's pixels (device-side exchange), the same
+ * for the upper neighbour's decision (fused per-wave kernel), jobs per launch (a batch:
+ * ia_synth_levels_batch; the pairs count all of them)}; returns the number of records
+ * (<0: error). */
+#define IA_PROF_FIELDS 11
 int ia_prof_begin(void);
 /* create the event pool up front (2 events per wave of every profiled level call of the
  * profile), so that no event is created inside a timed region */

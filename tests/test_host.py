@@ -278,20 +278,29 @@ def test_threaded_oracle_scan_equals_serial():
 # ---- device-side exchange setup: agreed fallback to RCCL (gloo, 2 ranks, fake library) ---------
 
 class _FakeLib:
-    """Stands in for libia.so's exchange entries: rank `bad` cannot map a peer's box."""
-    def __init__(self, rank, bad, log):
-        self.rank, self.bad, self.log = rank, bad, log
+    """Stands in for libia.so's exchange entries: rank `bad` fails at step `where` (no
+    usable receive box, cannot map a peer's box, or wrong records in the stress waves)."""
+    def __init__(self, rank, bad, where, log):
+        self.rank, self.bad, self.where, self.log = rank, bad, where, log
+
+    def _fails(self, step):
+        return self.rank == self.bad and self.where == step
 
     def ia_peer_create(self, world, rank, mcap, h, hd):
         self.log.append('peer_create')
-        return 0
+        return -4 if self._fails('create') else 0
 
     def ia_peer_connect(self, h, handles):
         self.log.append('peer_connect')
-        return 7 if self.rank == self.bad else 0
+        return 7 if self._fails('connect') else 0
 
     def ia_peer_check(self, h, st):
         self.log.append('peer_check')
+        return 0
+
+    def ia_diag_peer_stress(self, h, nwaves, M, bad, st):
+        self.log.append('peer_stress')
+        bad._obj.value = 3 if self._fails('stress') else 0
         return 0
 
     def ia_comm_destroy(self, h):
@@ -310,14 +319,14 @@ class _FakeLib:
         return 0
 
 
-def _fallback_worker(rank, world, port, bad, out):
+def _fallback_worker(rank, world, port, bad, where, out):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     os.environ.pop('IA_EXCHANGE', None)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     import _ia
     log = []
-    fake = _FakeLib(rank, bad, log)
+    fake = _FakeLib(rank, bad, where, log)
     _ia.lib = lambda: fake
     _ia.stream = lambda: None
     torch.cuda.synchronize = lambda *a: None
@@ -326,21 +335,29 @@ def _fallback_worker(rank, world, port, bad, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('bad', [-1, 1])
-def test_peer_exchange_setup_falls_back_to_rccl_on_every_rank(bad):
-    """_ia.exchange: when one rank cannot map the others' receive boxes, every rank (not
-    only the failing one) drops the device-side exchange and builds the RCCL one, so the
-    ranks never disagree on the per-wave protocol; with every rank fine, no RCCL setup."""
+@pytest.mark.parametrize('bad,where', [(-1, None), (1, 'connect'), (1, 'create'), (0, 'stress')])
+def test_peer_exchange_setup_falls_back_to_rccl_on_every_rank(bad, where):
+    """_ia.exchange: when one rank has no usable receive box, cannot map the others' boxes
+    or sees wrong records in the stress waves, every rank (not only the failing one) drops
+    the device-side exchange and builds the RCCL one, so the ranks never disagree on the
+    per-wave protocol; with every rank fine, no RCCL setup."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    port = 31500 + np.random.RandomState(bad + 5).randint(0, 2000)
-    mp.spawn(_fallback_worker, args=(world, port, bad, out), nprocs=world, join=True)
+    port = 31500 + np.random.RandomState(bad + 5 + len(where or '')).randint(0, 2000)
+    mp.spawn(_fallback_worker, args=(world, port, bad, where, out), nprocs=world, join=True)
+    rccl = lambda r: (['unique_id'] if r == 0 else []) + ['comm_init']  # noqa: E731
     for r in range(world):
         log, kind = out[r]
         if bad < 0:
-            assert log == ['peer_create', 'peer_connect', 'peer_check'] and kind == 'peer'
-        else:
+            assert log == ['peer_create', 'peer_connect', 'peer_check', 'peer_stress'] and kind == 'peer'
+            continue
+        assert kind == 'peer->rccl'
+        if where == 'create':
+            # the failing rank never got a box; the other destroys its own
+            assert log == ['peer_create'] + ([] if r == bad else ['destroy']) + rccl(r)
+        elif where == 'connect':
             assert log[:2] == ['peer_create', 'peer_connect'] and 'peer_check' not in log
-            assert log[2:] == ['destroy'] + (['unique_id'] if r == 0 else []) + ['comm_init']
-            assert kind == 'peer->rccl'
+            assert log[2:] == ['destroy'] + rccl(r)
+        else:
+            assert log == ['peer_create', 'peer_connect', 'peer_check', 'peer_stress', 'destroy'] + rccl(r)
