@@ -45,11 +45,22 @@ def test_bench_contract_c1(gpu):
 
 @pytest.mark.gpu
 def test_bench_contract_c5_streams(gpu):
-    d = run_bench('--config', 'c5', '--jobs', '2', '--streams', '2', '--steps', '1',
+    d = run_bench('--config', 'c5', '--jobs', '2', '--batch', '1', '--streams', '2', '--steps', '1',
                   '--warmup', '1', '--no-cpu-baseline')
     check_contract(d, 1, 1)
     assert d['scaling'] == 'weak' and d['config']['streams_per_gpu'] == 2
     assert d['checks']['concurrent_identical'] is True
+
+
+@pytest.mark.gpu
+def test_bench_contract_c5_batch(gpu):
+    """c5's default form: the GPU's jobs in one batch (one screen and one fused launch per
+    wave serve them all); every job's result equals its own one-job synthesis."""
+    d = run_bench('--config', 'c5', '--jobs', '3', '--steps', '1', '--warmup', '1',
+                  '--no-cpu-baseline')
+    check_contract(d, 1, 1)
+    assert d['config']['jobs_per_launch'] == 3 and d['config']['jobs_per_gpu'] == 3
+    assert d['checks']['batch_identical'] is True and d['checks']['bp_equals_ap_at_s'] is True
 
 
 @pytest.mark.gpu
@@ -70,4 +81,25 @@ def test_bench_two_ranks_sharing_the_gpu_equal_one_rank(gpu):
     assert two['n_gpus'] == 2 and two['config']['parallelism'] == 'db-shard2'
     assert two['config']['exchange'].startswith('peer')
     assert two['checks']['replicas_identical'] is True
+    assert two['checks']['checksum'] == one['checks']['checksum']
+
+
+@pytest.mark.gpu
+def test_bench_c4_two_ranks_sharing_the_gpu_equal_one_rank(gpu):
+    """c4 itself (A = A' 2048^2, B 1024^2, 5-level cap) as the driver's 2-GPU run starts it,
+    both ranks on the box's one GPU: the 4.19 M-row finest DB and the 1 M-row level sharded
+    over the device-side exchange, replicas identical, the 1-rank checksum, no fallback."""
+    one = run_bench('--config', 'c4', '--steps', '1', '--warmup', '0', '--no-cpu-baseline')
+    env = dict(os.environ, IA_SHARE_GPU='1')
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--config', 'c4', '--steps', '1', '--warmup', '0', '--no-cpu-baseline',
+                        '--strict-exchange'],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    two = json.loads(lines[0])
+    assert two['n_gpus'] == 2 and two['config']['parallelism'] == 'db-shard2'
+    assert two['config']['exchange'].startswith('peer') and 'exchange_fallback' not in two['checks']
+    assert two['checks']['replicas_identical'] is True and two['checks']['bp_equals_ap_at_s'] is True
     assert two['checks']['checksum'] == one['checks']['checksum']

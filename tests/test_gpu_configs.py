@@ -81,6 +81,33 @@ def test_c4_matcher_vs_oracle_fixture(gpu):
     assert len(bad) == 0, (len(bad), bad[:10])
 
 
+@pytest.mark.parametrize('G', [2, 8])
+def test_c4_matcher_sharded_reduction_vs_oracle_fixture(gpu, G):
+    """The sharded DB of c4's finest level (algorithms.py:63-69 rows split contiguously over
+    G ranks, each shard with its own split scale): every shard's exact winners, reduced
+    with the exchange's lexicographic (distance, lowest row) rule, equal the oracle's brute
+    force over all 4,194,304 rows (tests/golden/c4_queries.npz)."""
+    import algorithms
+    import image_analogies as ia
+    g = golden('c4_queries.npz')
+    job = _job('c4')
+    level = job.max_levels - 1
+    A_pyr, Ap_pyr = _pyr(job, job.A), _pyr(job, job.Ap)
+    best_d = np.full(len(g['q']), np.inf)
+    best_i = np.full(len(g['q']), np.iinfo(np.int64).max)
+    for r in range(G):
+        index = algorithms.level_index(A_pyr, [Ap_pyr], level,
+                                       lambda lv, N: ia.shard_rows(N, r, G))
+        si, sd = index.match(g['q'])
+        si, sd = si.cpu().numpy(), sd.cpu().numpy()
+        assert np.all((si >= index.row0) & (si < index.row0 + index.nrows))
+        take = (sd < best_d) | ((sd == best_d) & (si < best_i))
+        best_d = np.where(take, sd, best_d)
+        best_i = np.where(take, si, best_i)
+    bad = np.nonzero((best_i != g['idx']) | (best_d != g['dist']))[0]
+    assert len(bad) == 0, (len(bad), bad[:10])
+
+
 def _spot_check(job, out, level, n_rand, seed):
     import config as cfg
     A_pyr = [p.cpu().numpy() for p in _pyr(job, job.A)]
