@@ -145,6 +145,10 @@ _SIGS = {
     'ia_diag_qp_rows': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_query_rows16': (ctypes.c_int, [_dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_screen16': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp]),
+    'ia_diag_stage_map': (ctypes.c_int, [ctypes.c_long, ctypes.c_long, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_int)]),
+    'ia_diag_screen16_rows': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
+                                             _dp, _dp, ctypes.c_int, _dp, _dp]),
     'ia_diag_screen16_image': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long,
                                               ctypes.c_long, _dp, _dp, ctypes.c_int, _dp, _dp]),
     'ia_diag_peer_stress': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int,

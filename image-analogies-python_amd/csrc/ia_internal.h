@@ -36,6 +36,38 @@ static inline int db_seg_rows(long nrows) {
 }
 static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_rows(nrows); }
 
+// ---- the matcher's order of a DB's rows: chunks, stages, segments -------
+// A screen workgroup owns a chunk of ch rows and walks it in 128-row stages; a segment (one
+// minimum per query) is seg_rows / 128 consecutive stages of one chunk.  Two orders:
+//   linear  chunk c = rows [c ch, (c + 1) ch), stage s = its rows 128 s ...;
+//   strips  (a level whose shard is whole scanlines of width W % 128 == 0, with every chunk's
+//           ch / 128 scanlines inside one A' image): chunk c is the 128-pixel column strip
+//           c % (W / 128) of ch / 128 consecutive scanlines, stage s its scanline s.  The
+//           image-form screen then walks down the strip and reloads one window row per
+//           stage instead of the whole window (IA_DB_STRIPS, default 1).
+// Every kernel that maps a segment or a stage back to rows uses stage_lrow.
+struct StageMap {
+    int W;        // 0: linear; else the level width (strips)
+    int nstrip;   // W / 128
+    int sc;       // stages per chunk (ch / 128)
+};
+__host__ __device__ __forceinline__ long stage_lrow(const StageMap &m, long chunk, int s) {
+    if (m.W == 0) return (chunk * m.sc + s) * 128L;
+    const long sx = chunk % m.nstrip, yb = chunk / m.nstrip;
+    return (yb * m.sc + s) * (long)m.W + sx * 128;
+}
+// local row of element k (0 <= k < seg_rows) of segment seg
+__host__ __device__ __forceinline__ long seg_lrow(const StageMap &m, long seg, int seg_rows, long k) {
+    const int spc = (m.sc * 128) / seg_rows;   // segments per chunk
+    const long chunk = seg / spc;
+    const int s = (int)(seg - chunk * spc) * (seg_rows >> 7) + (int)(k >> 7);
+    return stage_lrow(m, chunk, s) + (k & 127);
+}
+static inline bool db_strips_enabled() {
+    static const int v = env_int("IA_DB_STRIPS", 1);
+    return v != 0;
+}
+
 // ---- the image form of a level's DB (ia_db_build_image) ---------------
 // A row's 55 features are pixels of its neighbourhood, so the screen can stage 128-row
 // stages (128 pixels of one scanline) from the images instead of from 224-B rows: every
@@ -80,6 +112,21 @@ static inline bool img_db_layout(int H, int W, int hs, int ws, int nAp, long row
     v.norm = reinterpret_cast<const uint32_t *>(p + fb + cb);
     v.ap = reinterpret_cast<const uint32_t *>(p + fb + cb + nb);
     return true;
+}
+
+// the stage order of rows [row0, row0 + nrows) of a level W wide with Himg scanlines per
+// A' image: strips where they apply (and are enabled), else linear
+static inline StageMap db_stage_map(long row0, long nrows, int W, int Himg) {
+    const int ch = db_chunk_rows(nrows);
+    StageMap m{0, 1, ch / 128};
+    if (!db_strips_enabled() || W <= 0 || W % 128 != 0 || row0 % W != 0 || nrows % W != 0 ||
+        db_rows_padded(nrows) != nrows)
+        return m;
+    const long lines = nrows / W, sc = ch / 128;
+    if (lines % sc != 0 || (row0 / W) % sc != 0 || Himg % sc != 0) return m;
+    m.W = W;
+    m.nstrip = W / 128;
+    return m;
 }
 
 struct Best {            // exact winner of a (query, shard): fp64 distance + global row
@@ -184,6 +231,7 @@ struct XArgs {
     const void *db;               // ... or the split-f16 rows (half8)
     long row0, nrows, nseg;
     int seg_rows;
+    StageMap smap;                // segment -> rows
     const float *segmin;          // [M][nseg], this wave's screen
     const double *q64;            // this wave's query rows (M)
     const float *qp;
@@ -238,9 +286,9 @@ int launch_query_rows(const double *qin, int M, const double *center, float *qp,
 // (same minima, bit for bit)
 // jobs (nullable): a batch of njobs identical-shape jobs in one launch (grid y = job; each
 // job's DB sections, q16[parity] and segmin from its table entry)
-int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16 *q16, int M,
-                    float *segmin, hipStream_t st, const XJob *jobs = nullptr, int njobs = 1,
-                    int parity = 0);
+int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
+                    const _Float16 *q16, int M, float *segmin, hipStream_t st,
+                    const XJob *jobs = nullptr, int njobs = 1, int parity = 0);
 // the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
 // stats (nullable): rows rescored, candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);

@@ -88,7 +88,7 @@ constexpr int rescore_threads(int mode, bool fifth) { return mode != 0 && mode !
 // during the row loop, since it needs only s / im of earlier waves).
 template <int MODE, bool IMG, bool FIFTH>
 __global__ __launch_bounds__(rescore_threads(MODE, FIFTH), IMG ? 2 : 1) void k_rescore(
-        DbSrc src, long row0, long nrows, long nseg, int seg_rows,
+        DbSrc src, long row0, long nrows, long nseg, int seg_rows, StageMap sm,
         const float *__restrict__ segmin, const half8 *__restrict__ db, ImgDb im,
         const float *__restrict__ qp, const double *__restrict__ q64,
         const double *__restrict__ nq, const float *__restrict__ amax, Best *__restrict__ best,
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(rescore_threads(MODE, FIFTH), IMG ? 2 : 1) void k_r
         char *wb = wins + (wv & 3) * WIN_B;
         auto stage_row = [&](long k0) {
             const long seg = full ? k0 / seg_rows : slist[k0 / seg_rows];
-            return seg * seg_rows + k0 % seg_rows;
+            return seg_lrow(sm, seg, seg_rows, k0 % seg_rows);
         };
         piece_t pc[WIN_PPL];
         long k0 = 128L * wv, lrow = 0;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(rescore_threads(MODE, FIFTH), IMG ? 2 : 1) void k_r
             for (int u = 0; u < RESCORE_RPT; ++u) {
                 const long k = base + u * 256 + tid;
                 const long seg = k < nrs ? (full ? k / seg_rows : slist[k / seg_rows]) : 0;
-                lr[u] = k < nrs ? seg * seg_rows + k % seg_rows : nrows;
+                lr[u] = k < nrs ? seg_lrow(sm, seg, seg_rows, k % seg_rows) : nrows;
                 // out-of-range rows read row 0 and are discarded below
                 half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
                 load_row16(db, lr[u] < nrows ? lr[u] : 0, g0, g1);
@@ -293,6 +293,7 @@ __global__ __launch_bounds__(256) void k_select(long nseg, const float *__restri
 
 template <bool IMG>
 __global__ __launch_bounds__(256, IMG ? 2 : 1) void k_items(DbSrc src, long row0, long nrows, int seg_rows,
+                                               StageMap sm,
                                                const WItem *__restrict__ items,
                                                const int *__restrict__ ctr,
                                                const half8 *__restrict__ db, ImgDb im,
@@ -320,12 +321,12 @@ __global__ __launch_bounds__(256, IMG ? 2 : 1) void k_items(DbSrc src, long row0
         piece_t pc[WIN_PPL];
         const bool wstage = IMG && wv * 128 < seg_rows;
         if constexpr (IMG) {
-            if (wstage) win_load(im, (long)w.seg * seg_rows + wv * 128, lane, pc);
+            if (wstage) win_load(im, seg_lrow(sm, w.seg, seg_rows, wv * 128), lane, pc);
         } else {
 #pragma unroll
             for (int u = 0; u < RESCORE_RPT; ++u) {
                 const int k = u * 256 + tid;
-                lr[u] = k < seg_rows ? (long)w.seg * seg_rows + k : nrows;
+                lr[u] = k < seg_rows ? seg_lrow(sm, w.seg, seg_rows, k) : nrows;
                 load_row16(db, lr[u] < nrows ? lr[u] : 0, x0[u], x1[u]);
             }
         }
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(256, IMG ? 2 : 1) void k_items(DbSrc src, long row0
         double bd = INFINITY;
         long long bi = 0x7fffffffffffffffLL;
         for (int i = tid; i < np; i += 256) {
-            const long row = row0 + (long)w.seg * seg_rows + plist[i];
+            const long row = row0 + seg_lrow(sm, w.seg, seg_rows, plist[i]);
             best_update(bd, bi, row_dist2(src, row, qs), row);
         }
         for (int o = 32; o > 0; o >>= 1) {
@@ -463,7 +464,8 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     IA_ARG(db || dbi, "launch_match: no DB (row form or image form)");
     const SegWs ws = seg_ws(scratch, M, nrows);
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
-    if ((rc = launch_screen16(db, dbi ? &img : nullptr, nrows, q16, M, ws.segmin, st))) return rc;
+    const StageMap sm = db_stage_map(row0, nrows, src.A.w, src.A.h);
+    if ((rc = launch_screen16(db, dbi ? &img : nullptr, nrows, sm, q16, M, ws.segmin, st))) return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
     const int rm = rescore_mode();
@@ -482,10 +484,10 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
         IA_LAUNCH_CHECK("k_select");
         const int grid = 2 * M + 64;
         if (im)
-            k_items<true><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr,
+            k_items<true><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), sm, ws.items, ws.ctr,
                                                 db, img, qp, q64, ws.ibest, stats);
         else
-            k_items<false><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), ws.items, ws.ctr,
+            k_items<false><<<grid, 256, 0, st>>>(src, row0, nrows, db_seg_rows(nrows), sm, ws.items, ws.ctr,
                                                  db, img, qp, q64, ws.ibest, stats);
         IA_LAUNCH_CHECK("k_items");
         if (mode == 3)
@@ -501,7 +503,7 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     }
 #define IA_RESCORE_LAUNCH(MD, IM, F)                                                            \
     k_rescore<MD, IM, F><<<M, rescore_threads(MD, F), 0, st>>>(src, row0, nrows, db_nsegs(nrows), \
-                                                               db_seg_rows(nrows), ws.segmin, db, \
+                                                               db_seg_rows(nrows), sm, ws.segmin, db, \
                                                                img, qp, q64, nq, amax, best, stats, fa)
 #define IA_RESCORE_CASE(MD, IM)                                                                  \
     do {                                                                                         \
@@ -674,8 +676,24 @@ int ia_diag_set_rescore_mode(int mode) {
 int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *segmin,
                      void *stream) {
     IA_ARG(db && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16: bad args");
-    return launch_screen16(db, nullptr, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin,
-                           S(stream));
+    return launch_screen16(db, nullptr, nrows, StageMap{0, 1, db_chunk_rows(nrows) / 128},
+                           reinterpret_cast<const _Float16 *>(q16), M, segmin, S(stream));
+}
+
+int ia_diag_stage_map(long row0, long nrows, int W, int Himg, int *out) {
+    IA_ARG(out && nrows > 0 && row0 >= 0, "ia_diag_stage_map: bad args");
+    const StageMap m = db_stage_map(row0, nrows, W, Himg);
+    out[0] = m.W;
+    out[1] = m.nstrip;
+    out[2] = m.sc;
+    return IA_OK;
+}
+
+int ia_diag_screen16_rows(const IaSrcLevel *src, long row0, long nrows, const void *db,
+                          const void *q16, int M, float *segmin, void *stream) {
+    IA_ARG(src && db && q16 && segmin && M > 0 && nrows > 0, "ia_diag_screen16_rows: bad args");
+    return launch_screen16(db, nullptr, nrows, db_stage_map(row0, nrows, src->Aw, src->Ah),
+                           reinterpret_cast<const _Float16 *>(q16), M, segmin, S(stream));
 }
 
 int ia_diag_screen16_image(const IaSrcLevel *src, long row0, long nrows, const void *dbi,
@@ -684,8 +702,8 @@ int ia_diag_screen16_image(const IaSrcLevel *src, long row0, long nrows, const v
     ImgDb img;
     IA_ARG(img_db_layout(src->Ah, src->Aw, src->A_hs, src->A_ws, src->nAp, row0, nrows, dbi, img, nullptr),
            "ia_diag_screen16_image: the image form does not apply to this level");
-    return launch_screen16(nullptr, &img, nrows, reinterpret_cast<const _Float16 *>(q16), M, segmin,
-                           S(stream));
+    return launch_screen16(nullptr, &img, nrows, db_stage_map(row0, nrows, src->Aw, src->Ah),
+                           reinterpret_cast<const _Float16 *>(q16), M, segmin, S(stream));
 }
 
 }  // extern "C"

@@ -144,7 +144,7 @@ __device__ __forceinline__ void copies_barrier() {
 // row form: wave W's share of one chunk, the DB rows streamed into LDS stage by stage
 template <int G, int W>
 __device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
-                                           long ctile0, int nstage, int tps,
+                                           const StageMap &sm, long chunk, int nstage, int tps,
                                            const half8 *__restrict__ q16) {
     constexpr int NS = bal_ns(G, W);
     const int tid = threadIdx.x;
@@ -152,7 +152,7 @@ __device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8
     half8 bq[NS][Q16_GROUPS];
     load_queries<G, W, NS>(q16, bq, lane);
     auto issue = [&](int s, int buf) {
-        const half8 *src = db16 + (ctile0 + (long)s * STAGE_TILES) * TILE_H8 + tid;
+        const half8 *src = db16 + (stage_lrow(sm, chunk, s) >> 5) * TILE_H8 + tid;
 #pragma unroll
         for (int k = 0; k < DB16_GROUPS; ++k)
             __builtin_amdgcn_global_load_lds((const void *)(src + k * 256),
@@ -217,7 +217,7 @@ __device__ __forceinline__ void expand_groups(const char *wb, half8 *E, int lane
 // c4 1615-1635 vs 1650-1656 ms/step (tools/gpu_img_check.sh, profiles/r02_image_form_ab.txt).
 template <int G, int W>
 __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, int *smin,
-                                         long crow0, int nstage, int tps,
+                                         const StageMap &sm, long chunk, int nstage, int tps,
                                          const half8 *__restrict__ q16) {
     constexpr int NS = bal_ns(G, W);
     const int tid = threadIdx.x;
@@ -225,7 +225,7 @@ __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, 
     half8 bq[NS][Q16_GROUPS];
     load_queries<G, W, NS>(q16, bq, lane);
     auto issue = [&](int s, int buf) {
-        const WinSrc ws = win_src(im, crow0 + (long)s * 128);
+        const WinSrc ws = win_src(im, stage_lrow(sm, chunk, s));
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             if (t == 1 && W == 3) continue;     // pieces 448.. are past the window
@@ -251,12 +251,121 @@ __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, 
     }
 }
 
+// ---- strips (StageMap with W > 0): the rolling window --------------------------------
+// A chunk is one 128-pixel column strip walked down scanline by scanline, so consecutive
+// stages' windows share all but one fine row of A and of A' (and all coarse rows every
+// second stage).  The window rows live in LDS rings indexed by their padded image row
+// (A fine 8 slots, A' fine 4, each coarse image 4, norm slots 2); per stage the block
+// copies in the rows the next stage adds (<= 5 wave instructions, ~1.9 KB instead of the
+// whole 6.6 KB window), so every image row is fetched about once per chunk.
+constexpr int FROW_B = WF_PC * 16, CROW_B = WC_PC * 16;        // 544, 288 B per window row
+constexpr int RW_FA = 0, RW_FP = RW_FA + 8 * FROW_B, RW_CA = RW_FP + 4 * FROW_B;
+constexpr int RW_CP = RW_CA + 4 * CROW_B, RW_NM = RW_CP + 4 * CROW_B, RW_B = RW_NM + 2 * 512;
+
+// window row job j of a stage at position w into the ring (one wave instruction; lanes past
+// the row's pieces idle).  kind: 0 A fine, 1 A' fine, 2 A coarse, 3 A' coarse, 4 norms;
+// r = the padded image row (fine / coarse) or unused (norms); nslot = the stage's norm slot
+__device__ __forceinline__ void rw_load(const ImgDb &im, const WinSrc &w, char *ring, int kind, int r,
+                                        int nslot, int lane) {
+    const uint32_t *src;
+    char *dst;
+    int n;
+    if (kind == 0) { src = im.fa + (long)r * im.Wp + w.x0; dst = ring + RW_FA + (r & 7) * FROW_B; n = WF_PC; }
+    else if (kind == 1) { src = w.fp + (long)r * im.Wp + w.x0; dst = ring + RW_FP + (r & 3) * FROW_B; n = WF_PC; }
+    else if (kind == 2) { src = im.ca + (long)r * im.Wcp + (w.x0 >> 1); dst = ring + RW_CA + (r & 3) * CROW_B; n = WC_PC; }
+    else if (kind == 3) { src = w.cp + (long)r * im.Wcp + (w.x0 >> 1); dst = ring + RW_CP + (r & 3) * CROW_B; n = WC_PC; }
+    else { src = im.norm + w.lrow; dst = ring + RW_NM + nslot * 512; n = 32; }
+    if (lane < n) __builtin_amdgcn_global_load_lds((const void *)(src + 4 * lane), (void *)dst, 16, 0, 2);
+}
+
+// the operand slot of wave W (as expand_groups) from the rings of the stage at image row y
+// (padded fine rows y .. y + 4 / y + 2, coarse rows c1 .. c1 + 2, norm slot ns)
+template <int W>
+__device__ __forceinline__ void expand_ring(const char *ring, int y, int ns, half8 *E, int lane) {
+    constexpr int H = W & 1;
+    const int tile = 2 * (W >> 1) + (lane >> 5), j = lane & 31;
+    const int px = 32 * tile + j;
+    const int c1 = (y >> 1) + 1;
+    const char *fa[5], *fp[3], *ca[3], *cp[3];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) fa[r] = ring + RW_FA + ((y + r) & 7) * FROW_B + px * 4;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        fp[r] = ring + RW_FP + ((y + r) & 3) * FROW_B + px * 4;
+        ca[r] = ring + RW_CA + ((c1 + r) & 3) * CROW_B + (px >> 1) * 4;
+        cp[r] = ring + RW_CP + ((c1 + r) & 3) * CROW_B + (px >> 1) * 4;
+    }
+    const char *nm = ring + RW_NM + ns * 512 + px * 4;
+    half8 *e = E + tile * TILE_H8 + H * 32 + j;
+    static_for<0, DB16_GROUPS>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        constexpr int k0 = grp_k0(H, g);
+        constexpr int hb = grp_hi(H, g) ? 0 : 2;
+        half8 o;
+        static_for<0, 8>([&](auto ec) {
+            constexpr int k = k0 + decltype(ec)::value;
+            const char *b;
+            if constexpr (k < 9) b = ca[k / 3] + (k % 3 + 3) * 4;
+            else if constexpr (k < 34) b = fa[(k - 9) / 5] + ((k - 9) % 5 + 2) * 4;
+            else if constexpr (k < 43) b = cp[(k - 34) / 3] + ((k - 34) % 3 + 3) * 4;
+            else if constexpr (k < 55) b = fp[(k - 43) / 5] + ((k - 43) % 5 + 2) * 4;
+            else b = nm;
+            o[decltype(ec)::value] = *reinterpret_cast<const _Float16 *>(b + hb);
+        });
+        e[g * 64] = o;
+    });
+}
+
+template <int G, int W>
+__device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring, int *smin,
+                                           const StageMap &sm, long chunk, int nstage, int tps,
+                                           const half8 *__restrict__ q16) {
+    constexpr int NS = bal_ns(G, W);
+    const int lane = threadIdx.x & 63;
+    half8 bq[NS][Q16_GROUPS];
+    load_queries<G, W, NS>(q16, bq, lane);
+    float mn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    // stage 0: the whole window, 15 row jobs dealt over the 4 waves
+    WinSrc w = win_src(im, stage_lrow(sm, chunk, 0));
+    for (int j = W; j < 15; j += 4) {
+        const int kind = j < 5 ? 0 : j < 8 ? 1 : j < 11 ? 2 : j < 14 ? 3 : 4;
+        const int r = j < 5 ? w.y + j : j < 8 ? w.y + j - 5 : j < 11 ? (w.y >> 1) + 1 + j - 8
+                                                                    : (w.y >> 1) + 1 + j - 11;
+        rw_load(im, w, ring, kind, r, 0, lane);
+    }
+    copies_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        const int y = w.y;
+        if (s + 1 < nstage) {
+            // the rows stage s + 1 adds (scanline y + 1 of the same image): slots stage s
+            // does not read
+            const WinSrc wn = win_src(im, stage_lrow(sm, chunk, s + 1));
+            const bool cnew = (wn.y >> 1) != (y >> 1);
+            if (W == 0) rw_load(im, wn, ring, 0, wn.y + 4, 0, lane);
+            else if (W == 1) rw_load(im, wn, ring, 1, wn.y + 2, 0, lane);
+            else if (W == 2) rw_load(im, wn, ring, 4, 0, (s + 1) & 1, lane);
+            else if (cnew) {
+                rw_load(im, wn, ring, 2, (wn.y >> 1) + 3, 0, lane);
+                rw_load(im, wn, ring, 3, (wn.y >> 1) + 3, 0, lane);
+            }
+            w = wn;
+        }
+        expand_ring<W>(ring, y, s & 1, E, lane);
+        __syncthreads();   // the stage operand is complete
+        stage_mfma<G, W, NS>(E, bq, mn, lane);
+        stage_close<G, W, NS>(s, tps, smin, mn, lane);
+        copies_barrier();  // the operand is consumed and stage s + 1's rows have landed
+    }
+}
+
 // grid: (nchunks rounded up to 8) x groups, XCD-aware: all groups of a chunk share
 // blockIdx % 8 (one XCD under round-robin dispatch), so the chunk is fetched from HBM once
 // per launch.  Group g holds query tiles [g G, g G + G).
 template <int G>
 __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ db16, int nchunks,
-                                                     int ch, int seg_rows,
+                                                     int ch, int seg_rows, StageMap sm,
                                                      const half8 *__restrict__ q16, int M,
                                                      int groups, float *__restrict__ segmin,
                                                      long nseg, const XJob *jobs, int parity) {
@@ -275,16 +384,14 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     if (chunk >= nchunks) return;   // uniform over the block, before any barrier
     const int spc = ch / seg_rows;
     for (int i = threadIdx.x; i < spc * G * 32; i += 256) smin[i] = 0x7fffffff;
-    const int tpc = ch >> 5;
-    const long ctile0 = (long)chunk * tpc;
-    const int nstage = tpc / STAGE_TILES;
+    const int nstage = ch / (STAGE_TILES * 32);
     const int tps = seg_rows >> 5;
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv == 0) chain_body<G, 0>(db16, sbuf, smin, ctile0, nstage, tps, qg);
-    else if (wv == 1) chain_body<G, 1>(db16, sbuf, smin, ctile0, nstage, tps, qg);
-    else if (wv == 2) chain_body<G, 2>(db16, sbuf, smin, ctile0, nstage, tps, qg);
-    else chain_body<G, 3>(db16, sbuf, smin, ctile0, nstage, tps, qg);
+    if (wv == 0) chain_body<G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else if (wv == 1) chain_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else if (wv == 2) chain_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else chain_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
     __syncthreads();
     // the chunk's minima, spc consecutive segments per query
     const long seg0 = (long)chunk * spc;
@@ -297,6 +404,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
 
 template <int G>
 __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int ch, int seg_rows,
+                                                      StageMap sm,
                                                       const half8 *__restrict__ q16, int M,
                                                       int groups, float *__restrict__ segmin,
                                                       long nseg, const XJob *jobs, int parity) {
@@ -307,6 +415,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
         q16 = reinterpret_cast<const half8 *>(J.q16[parity]);
         segmin = J.segmin;
     }
+    static_assert(RW_B <= 2 * WIN_B, "the rings fit the window buffers");
     __shared__ __attribute__((aligned(16))) char wbuf[2 * WIN_B];
     __shared__ int smin[SPC_MAX * G * 32];
     const int b = blockIdx.x;
@@ -319,12 +428,18 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
     const int nstage = ch / (STAGE_TILES * 32);
     const int tps = seg_rows >> 5;
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
-    const long crow0 = (long)chunk * ch;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv == 0) img_body<G, 0>(im, E, wbuf, smin, crow0, nstage, tps, qg);
-    else if (wv == 1) img_body<G, 1>(im, E, wbuf, smin, crow0, nstage, tps, qg);
-    else if (wv == 2) img_body<G, 2>(im, E, wbuf, smin, crow0, nstage, tps, qg);
-    else img_body<G, 3>(im, E, wbuf, smin, crow0, nstage, tps, qg);
+    if (sm.W > 0) {   // strips: the rolling window (wbuf holds the rings)
+        if (wv == 0) strip_body<G, 0>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 1) strip_body<G, 1>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 2) strip_body<G, 2>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else strip_body<G, 3>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+    } else {
+        if (wv == 0) img_body<G, 0>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 1) img_body<G, 1>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 2) img_body<G, 2>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else img_body<G, 3>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+    }
     __syncthreads();
     // the chunk's minima, spc consecutive segments per query (as k_screen16)
     const long seg0 = (long)chunk * spc;
@@ -338,8 +453,9 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
 // query tiles per launch group: T tiles in ceil(T / 11) equal groups
 static inline int screen_groups(int T) { return (T + MAX_G - 1) / MAX_G; }
 
-int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16 *q16, int M,
-                    float *segmin, hipStream_t st, const XJob *jobs, int njobs, int parity) {
+int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
+                    const _Float16 *q16, int M, float *segmin, hipStream_t st, const XJob *jobs,
+                    int njobs, int parity) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -348,6 +464,7 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16
                ch / seg_rows <= SPC_MAX,
            "launch_screen16: bad chunking");
     IA_ARG(!img || db_rows_padded(nrows) == nrows, "launch_screen16: image form needs whole chunks");
+    IA_ARG(sm.sc == ch / 128, "launch_screen16: stage map of another chunking");
     const half8 *db16 = reinterpret_cast<const half8 *>(db);
     const half8 *q = reinterpret_cast<const half8 *>(q16);
     const int T = (M + 31) / 32;
@@ -360,10 +477,10 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const _Float16
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
         if (img)                                                                                \
-            k_screen16i<GG><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, q, M,      \
+            k_screen16i<GG><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
                                                   groups, segmin, nseg, jobs, parity);          \
         else                                                                                    \
-            k_screen16<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, q, M,       \
+            k_screen16<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,   \
                                                  groups, segmin, nseg, jobs, parity);           \
         break;
     switch (G) {

@@ -559,7 +559,8 @@ struct LevelRun {
         hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
         hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
         if (e0) IA_HIP(hipEventRecord(e0, sq));
-        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, q16s[b], M, segmin, sq, jt, K, b)))
+        const StageMap sm = db_stage_map(a->row0, a->nrows, src.A.w, src.A.h);
+        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b)))
             return rc;
         if (e1) IA_HIP(hipEventRecord(e1, sq));
         int y_lo_n = 0, M_n = 0;
@@ -572,6 +573,7 @@ struct LevelRun {
         x.nrows = a->nrows;
         x.nseg = db_nsegs(a->nrows);
         x.seg_rows = db_seg_rows(a->nrows);
+        x.smap = sm;
         x.segmin = segmin;
         x.q64 = q64s[b]; x.qp = qps[b]; x.nq = nqs[b];
         x.amax = a->amax;

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             char *wb = pool + wv * WIN_SLOT;
             for (long k0 = 128L * wv; k0 < nrs; k0 += 512) {
                 const long seg = full ? k0 / a.seg_rows : slist[k0 / a.seg_rows];
-                const long lrow = seg * a.seg_rows + k0 % a.seg_rows;
+                const long lrow = seg_lrow(a.smap, seg, a.seg_rows, k0 % a.seg_rows);
                 wave_lds_sync();   // the previous step's reads of the slot are done
                 win_dma(a.im, lrow, lane, wb);
                 win_dma_wait();
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             // row form: one row per thread per step (224-B split rows)
             for (long k = tid; k < nrs; k += 256) {
                 const long seg = full ? k / a.seg_rows : slist[k / a.seg_rows];
-                const long lr = seg * a.seg_rows + k % a.seg_rows;
+                const long lr = seg_lrow(a.smap, seg, a.seg_rows, k % a.seg_rows);
                 half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
                 load_row16(reinterpret_cast<const half8 *>(a.db), lr < a.nrows ? lr : 0, g0, g1);
                 take(lr, rescreen16(g0, g1, qf, twoR));

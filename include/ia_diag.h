@@ -24,6 +24,16 @@ int ia_diag_query_rows16(const double *q64, int M, const double *center, const f
  * minima segmin[M][nseg] (screen units; nseg = ia_db_rows_padded / segment rows) */
 int ia_diag_screen16(const void *db, long nrows, const void *q16, int M, float *segmin,
                      void *stream);
+/* the matcher's stage order of rows [row0, row0 + nrows) of a level W wide with Himg
+ * scanlines per A' image (ia_internal.h StageMap): out = {W (0: linear chunks), strips per
+ * scanline, 128-row stages per chunk}.  With strips, chunk c is the 128-px column strip
+ * c % strips of stages-per-chunk consecutive scanlines and a segment is 4 consecutive stages
+ * of a chunk; linear: chunk c = rows [c ch, (c + 1) ch). */
+int ia_diag_stage_map(long row0, long nrows, int W, int Himg, int *out);
+/* the row-form screen over rows [row0, row0 + nrows) of src's level in the product's stage
+ * order (the same minima as the image form, bit for bit) */
+int ia_diag_screen16_rows(const IaSrcLevel *src, long row0, long nrows, const void *db,
+                          const void *q16, int M, float *segmin, void *stream);
 /* the same screen streaming the DB's image form (ia_db_build_image) of rows
  * [row0, row0 + nrows) of src: the same minima bit for bit */
 int ia_diag_screen16_image(const IaSrcLevel *src, long row0, long nrows, const void *dbi,

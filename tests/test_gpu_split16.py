@@ -56,6 +56,25 @@ def _queries(As, rs):
                       np.full((1, 55), As.mean())])                          # ~ the centre
 
 
+def _segment_order(idx, N, npad, seg):
+    """Local rows in the matcher's segment order (ia_diag_stage_map; ia_internal.h
+    stage_lrow): identity for linear chunks, column strips otherwise."""
+    import _ia
+    m = (ctypes.c_int * 3)()
+    _ia.check(_ia.lib().ia_diag_stage_map(idx.row0, N, idx.src.Aw, idx.src.Ah, m), 'ia_diag_stage_map')
+    W, nstrip, sc = m[0], m[1], m[2]
+    if W == 0:
+        return np.arange(npad)
+    ch = sc * 128
+    out = np.empty(npad, dtype=np.int64)
+    for chunk in range(npad // ch):
+        sx, yb = chunk % nstrip, chunk // nstrip
+        for s in range(sc):
+            r0 = (yb * sc + s) * W + sx * 128
+            out[chunk * ch + s * 128: chunk * ch + (s + 1) * 128] = np.arange(r0, r0 + 128)
+    return out
+
+
 def _screen_vs_fp64(idx, As, Q, Ms):
     """Run the split-f16 screen on Q[:M] for each M and return the worst
     |segmin - exact| / eps16 over all (query, segment) pairs (exact = fp64 minima of
@@ -76,6 +95,7 @@ def _screen_vs_fp64(idx, As, Q, Ms):
     npad = lib.ia_db_rows_padded(N)
     seg = min(lib.ia_db_chunk_rows(N), 512)
     nseg = npad // seg
+    order = _segment_order(idx, N, npad, seg)      # rows of segment s: order[s * seg:(s + 1) * seg]
     segmin = torch.empty((qrows, nseg), dtype=torch.float32, device='cuda')
     amax = float(idx.amax.item())
     c = idx.center.cpu().numpy()
@@ -87,13 +107,14 @@ def _screen_vs_fp64(idx, As, Q, Ms):
     for m0 in range(0, Mmax, 64):                                     # fp64, 64 queries at a time
         E = na[:, None] - 2.0 * (a @ (Q[m0:m0 + 64] - c).T)
         E = np.concatenate([E, np.repeat(E[-1:], npad - N, 0)])      # padding repeats the last row
-        exact[m0:m0 + 64] = E.reshape(nseg, seg, -1).min(axis=1).T
+        exact[m0:m0 + 64] = E[order].reshape(nseg, seg, -1).min(axis=1).T
     worst = 0.0
     seg_img = torch.empty_like(segmin)
     for M in Ms:
         segmin.fill_(float('nan'))
-        _ia.check(lib.ia_diag_screen16(_ia.ptr(idx.db), N, _ia.ptr(q16), M, _ia.ptr(segmin), st),
-                  'ia_diag_screen16')
+        _ia.check(lib.ia_diag_screen16_rows(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.db),
+                                            _ia.ptr(q16), M, _ia.ptr(segmin), st),
+                  'ia_diag_screen16_rows')
         if idx.dbi is not None:      # the image-form stream: the same minima bit for bit
             seg_img.fill_(float('nan'))
             _ia.check(lib.ia_diag_screen16_image(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.dbi),
