@@ -250,7 +250,11 @@ struct XArgs {
     unsigned long long *stats;    // nullable: rows rescored, candidate segments, full scans
     FinishArgs f;                 // t, y_lo, W, ..., px (sharded DB: the device-side exchange)
     const XJob *jobs;             // nullable: a batch, job blockIdx.y's pointers override these
+    unsigned long long *trace;    // diagnostic (nullable): phase stamps, XW_TRACE_* below
 };
+// k_xwave phase stamps (IA_XW_TRACE=<level tag>, ia_diag_xwave_trace): s_memrealtime (100
+// MHz) at XW_TRACE_N points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T
+constexpr int XW_TRACE_N = 16, XW_TRACE_PX = 8, XW_TRACE_T = 4096;
 int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st, int njobs = 1);
 
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS

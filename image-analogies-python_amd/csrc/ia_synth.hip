@@ -319,6 +319,19 @@ static int shard_tail() {
 static std::atomic<int> g_xwave{env_int("IA_XWAVE", 1)};
 static int xwave_on() { return g_xwave.load(std::memory_order_relaxed); }
 
+// diagnostic: k_xwave phase stamps of the level tagged IA_XW_TRACE (one process-wide buffer)
+static unsigned long long *g_xw_trace = nullptr;
+static unsigned long long *xw_trace(int tag) {
+    static const int want = env_int("IA_XW_TRACE", -1);
+    if (want < 0 || tag != want) return nullptr;
+    if (!g_xw_trace) {
+        const size_t n = (size_t)XW_TRACE_T * XW_TRACE_PX * XW_TRACE_N * sizeof(unsigned long long);
+        if (hipMalloc(&g_xw_trace, n) != hipSuccess) { g_xw_trace = nullptr; return nullptr; }
+        (void)hipMemset(g_xw_trace, 0, n);
+    }
+    return g_xw_trace;
+}
+
 static int check_args(const IaSynthArgs *a) {
     IA_ARG(a && (a->db || a->dbi || a->lsh) && a->center && a->amax && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg &&
                a->weights && a->s && a->im && a->workspace,
@@ -590,6 +603,7 @@ struct LevelRun {
                          a->im, a->dbg_px, a->dbg_dist, nullptr, nullptr};
         if (peer) x.f.px = comm_peer_wave(a->comm);
         x.jobs = jt;
+        x.trace = xw_trace(a->tag);
         const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
         if ((rc = launch_xwave(x, R, im, sq, K))) return rc;
         ++nscreen;
@@ -699,6 +713,14 @@ static thread_local PipeRes g_pipe;
 using namespace ia;
 
 extern "C" {
+
+int ia_diag_xwave_trace(unsigned long long *out) {
+    IA_ARG(out && g_xw_trace, "ia_diag_xwave_trace: no trace (IA_XW_TRACE=<level>)");
+    IA_HIP(hipDeviceSynchronize());
+    IA_HIP(hipMemcpy(out, g_xw_trace, (size_t)XW_TRACE_T * XW_TRACE_PX * XW_TRACE_N * 8,
+                     hipMemcpyDeviceToHost));
+    return IA_OK;
+}
 
 int ia_diag_set_xwave(int on) {
     const int prev = xwave_on();

@@ -48,9 +48,14 @@ __device__ __forceinline__ const double *feat_addr(const ImgPair &X, const ImgPa
     const int kk = yk ? k - 34 : k;
     const bool coarse = kk < 9;
     const int t = coarse ? kk : kk - 9;
-    const int h = yk ? (coarse ? Y.hs : Y.h) : (coarse ? X.hs : X.h);
-    const int w = yk ? (coarse ? Y.ws : Y.w) : (coarse ? X.ws : X.w);
-    const double *base = yk ? (coarse ? Y.sm : Y.lg) : (coarse ? X.sm : X.lg);
+    // select between field VALUES (selecting between the structs would take their address:
+    // a local ImgPair would then live in scratch memory)
+    const int xh = coarse ? X.hs : X.h, yh = coarse ? Y.hs : Y.h;
+    const int xw = coarse ? X.ws : X.w, yw = coarse ? Y.ws : Y.w;
+    const double *xb = coarse ? X.sm : X.lg, *yb = coarse ? Y.sm : Y.lg;
+    const int h = yk ? yh : xh;
+    const int w = yk ? yw : xw;
+    const double *base = yk ? yb : xb;
     const int r0 = coarse ? (r >> 1) + t / 3 - 1 : r + t / 5 - 2;
     const int c0 = coarse ? (c >> 1) + t % 3 - 1 : c + t % 5 - 2;
     rr = symi2(r0, h);
@@ -64,6 +69,19 @@ __device__ __forceinline__ double db_feat(const DbSrc &src, int img, int r, int 
     ap.lg += (long)img * src.hw;
     int rr, cc;
     return *feat_addr(src.A, ap, r, c, k, rr, cc);
+}
+
+// lane's double at p into the wave's LDS words lo[lane], hi[lane] by two 4-byte DMA copies
+// (global_load_lds: the gather is in flight without holding registers; the wave waits with
+// s_waitcnt vmcnt(0) before reading the words).  lo / hi must be wave-uniform.
+__device__ __forceinline__ void dma_f64(const double *p, bool on, unsigned *lo, unsigned *hi) {
+    if (on) {
+        __builtin_amdgcn_global_load_lds((const void *)p, (void *)lo, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const char *>(p) + 4), (void *)hi, 4, 0, 0);
+    }
+}
+__device__ __forceinline__ double lds_f64(const unsigned *lo, const unsigned *hi, int l) {
+    return __longlong_as_double((long long)(((unsigned long long)hi[l] << 32) | lo[l]));
 }
 
 // numpy pairwise_sum of v[0..54] (Pw55's order, ia_common.h) from LDS
@@ -147,20 +165,34 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
     __shared__ XRec wbest[4];
     __shared__ CohSel cs;
     __shared__ double csval;
-    // long-lived per-lane values kept in LDS (not VGPRs across the exact stage): wave 0's
-    // prefetched next-query features and centre, wave 1's coherence candidates
-    __shared__ double nxv[IA_DP], nxc[IA_DP];
-    __shared__ int nxd[IA_DP];
+    // wave 1's coherence candidates (broadcast to the wave's gathers) and their A' values;
+    // wave 0's next-query features and centre (LDS-DMA words)
     __shared__ long long ccix[XW_NCOH];
+    __shared__ unsigned cvw[2][64];
+    __shared__ unsigned nxw[4][64];
     __shared__ int cpos[XW_NCOH][3];
 
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // wv must be provably uniform: the LDS-DMA destinations derived from it go into M0 (a
+    // per-lane value would turn each copy into a 64-iteration waterfall loop)
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const FinishArgs &f = a.f;
     const DbSrc &src = a.src;
     const int t = f.t, W = f.W;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
     __syncthreads();
     const int i = tk;
+    // diagnostic phase stamps (thread 0 of the first pixels)
+    unsigned long long *trace =
+        (a.trace && i < XW_TRACE_PX && t < XW_TRACE_T) ? a.trace + ((long)t * XW_TRACE_PX + i) * XW_TRACE_N : nullptr;
+    auto stamp = [&](int k) {
+        if (trace && tid == 0) trace[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    auto wstamp = [&](int k) {   // lane 0 of any wave
+        if (trace && lane == 0) trace[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    if (trace && tid == 0) trace[0] = t_start;
+    stamp(1);
     // the counter of launch t + 1 was launch t - 1's: empty it for the next launch
     if (i == 0 && tid == 0) __hip_atomic_store(&a.tickets[(t + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int y = f.y_lo + i, x = t - 3 * y;
@@ -168,25 +200,18 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
     const bool nxt = y >= a.y_lo_n && y < a.y_lo_n + a.M_n;       // (y, x + 1) is in wave t + 1
 
     // wave 0: the next query's features that do not depend on wave t, issued first
-    // (kept in registers until the first barrier, then in LDS: the load's wait must not
-    // come before the exact stage's own loads are issued)
-    double pv = 0.0, pc0 = 0.0;
+    // (copied into LDS by DMA, consumed only at the end: their wait never delays the exact
+    // stage)
+    const float amx = a.amax[vidx(0)];
     int pdep = 0;
-    if (wv == 0 && nxt && lane < IA_D) {
-        int rr, cc;
-        const double *p = feat_addr(a.B, a.Bp, y, x + 1, lane, rr, cc);
+    if (wv == 0 && nxt) {
+        int rr = 0, cc = 0;
+        const double *p = feat_addr(a.B, a.Bp, y, x + 1, lane < IA_D ? lane : 0, rr, cc);
         // 1: this pixel's new value, 2: the upper neighbour's
-        pdep = lane < 43 ? 0 : (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
-        pv = pdep ? 0.0 : *p;
-        pc0 = a.center[lane];
+        pdep = lane < 43 || lane >= IA_D ? 0 : (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
+        dma_f64(p, lane < IA_D && pdep == 0, nxw[0], nxw[1]);
+        dma_f64(a.center + (lane < IA_D ? lane : 0), lane < IA_D, nxw[2], nxw[3]);
     }
-    auto park_next = [&]() {
-        if (wv == 0 && lane < IA_DP) {
-            nxv[lane] = pv;
-            nxc[lane] = pc0;
-            nxd[lane] = pdep;
-        }
-    };
 
     double own = 0.0;            // this pixel's new B' value (wave 0)
     if (cur) {
@@ -199,47 +224,71 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             wk = tid < IA_D ? f.weights[tid] : 0.0;
         }
         const double nqq = a.nq[vidx(i)];
-        const float am = a.amax[vidx(0)];
+        const float am = amx;
         const long n4 = a.nseg / 4;
         const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
         float4 v[RESCORE_REG];
         segmin_load(sq4, n4, v);
-        // wave 1, lane l < 15: coherence candidate of window position l (algorithms.py:
-        // 101-119): r strictly before q in scanline order, p_r = s(r) + q - r inside A'
-        if (wv == 1 && lane < XW_NCOH) {
-            long long cix = -1;
-            int csr = 0, csc = 0, cim = 0;
-            const int rr = y - 2 + lane / 5, rc = x - 2 + lane % 5;
-            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
-                const long sidx = (long)rr * W + rc;
-                const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
-                const int simg = f.im[sidx];
-                if (sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w) {
-                    cix = ((long)src.A.h * simg + sr) * src.A.w + sc;
-                    csr = sr; csc = sc; cim = simg;
-                }
-            }
-            ccix[lane] = cix;
-            cpos[lane][0] = csr; cpos[lane][1] = csc; cpos[lane][2] = cim;
+        // wave 1, lane l < 15: s / im of coherence window position l (algorithms.py:101-119),
+        // issued now, used after e*
+        const int rr0 = y - 2 + lane / 5, rc0 = x - 2 + lane % 5;
+        const bool cpos_ok = wv == 1 && lane < XW_NCOH && rr0 >= 0 && rc0 >= 0 && rc0 < W &&
+                             (rr0 < y || rc0 < x);
+        int s_r = 0, s_c = 0, s_i = 0;
+        if (cpos_ok) {
+            const long sidx = (long)rr0 * W + rc0;
+            s_r = f.s[2 * sidx];
+            s_c = f.s[2 * sidx + 1];
+            s_i = f.im[sidx];
         }
         if (tid == 0) { scount = 0; nresc = 0; rcount = 0; }
         const float emin = segmin_scan(sq4, n4, v, redf);
+        stamp(2);
         if (tid < IA_DP) {
             qs[tid] = qsv;
             qf[tid] = qfv;
             wts[tid] = wk;
         }
-        park_next();
         double Tseg, Trow;
         bool force_full;
         rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
         const float twoR = ldexpf(1.f, split16_db_scale(am).R);
         segmin_select(sq4, n4, v, Tseg, slist, &scount);
         __syncthreads();
+        stamp(3);
         const int ns = scount;
         const bool full = ns > RESCORE_SEGCAP || force_full;
         const long nscan = full ? a.nseg : ns;
         const long nrs = nscan * a.seg_rows;
+        // wave 1: the coherence candidates (p_r = s(r) + q - r inside A'), then all their
+        // features requested at once by LDS DMA (candidate c's lo / hi words in cx / cw);
+        // they land during the re-screen, which wave 1 leaves to the other three (its loads
+        // return in order: a re-screen window of its own would wait for all of these)
+        if (wv == 1) {
+            long long cix = -1;
+            if (lane < XW_NCOH) {
+                const int sr = s_r + y - rr0, sc = s_c + x - rc0;
+                if (cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w)
+                    cix = ((long)src.A.h * s_i + sr) * src.A.w + sc;
+                ccix[lane] = cix;
+                cpos[lane][0] = sr; cpos[lane][1] = sc; cpos[lane][2] = s_i;
+            }
+            dma_f64(src.Ap.lg + (cix >= 0 ? cix : 0), lane < XW_NCOH && cix >= 0, cvw[0], cvw[1]);
+            wave_lds_sync();
+            unsigned *clo = reinterpret_cast<unsigned *>(&cx[0][0]);
+            unsigned *chi = reinterpret_cast<unsigned *>(&cw[0][0]);
+#pragma unroll
+            for (int c = 0; c < XW_NCOH; ++c) {
+                const bool on = ccix[c] >= 0;
+                ImgPair ap = src.Ap;
+                ap.sm += (long)cpos[c][2] * src.hws;
+                ap.lg += (long)cpos[c][2] * src.hw;
+                int rr, cc;
+                const double *fp = feat_addr(src.A, ap, cpos[c][0], cpos[c][1], lane < IA_D ? lane : 0, rr, cc);
+                if (on) dma_f64(fp, lane < IA_D, clo + c * 64, chi + c * 64);
+            }
+            wstamp(13);
+        }
 
         // ---- 2. fp32 re-screen of the candidate segments' rows; rows within Trow to the
         // list (overflow rows rescored in place: never on the measured configs)
@@ -258,24 +307,42 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             }
         };
         if constexpr (IMG) {
-            // wave w re-screens the 128-row stage base + 128 w of each 512-row step from its
-            // own LDS slot, the window copied in by LDS DMA (one step: one round trip; more
-            // than one candidate segment per query is rare)
-            char *wb = pool + wv * WIN_SLOT;
-            for (long k0 = 128L * wv; k0 < nrs; k0 += 512) {
-                const long seg = full ? k0 / a.seg_rows : slist[k0 / a.seg_rows];
-                const long lrow = seg_lrow(a.smap, seg, a.seg_rows, k0 % a.seg_rows);
-                wave_lds_sync();   // the previous step's reads of the slot are done
-                win_dma(a.im, lrow, lane, wb);
-                win_dma_wait();
-                float e0, e1;
-                rescreen_win2(wb, lane, qf, twoR, e0, e1);
-                take(lrow + lane, e0);
-                take(lrow + lane + 64, e1);
+            // the 128-row stages of each 512-row step go to waves 0, 2, 3, 0 (wave 0 takes two,
+            // in the slots of waves 0 and 1), each window copied into LDS by DMA: one round
+            // trip per step (more than one candidate segment per query is rare)
+            if (wv != 1) {
+                const int j0 = wv == 0 ? 0 : wv - 1;          // first stage of the step
+                const int nj = wv == 0 ? 2 : 1;
+                for (long base = 0; base < nrs; base += 512) {
+                    long lrow[2] = {0, 0};
+                    wave_lds_sync();   // the previous step's reads of the slots are done
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const long k0 = base + 128L * (u == 0 ? j0 : 3);
+                        if (u < nj && k0 < nrs) {
+                            const long seg = full ? k0 / a.seg_rows : slist[k0 / a.seg_rows];
+                            lrow[u] = seg_lrow(a.smap, seg, a.seg_rows, k0 % a.seg_rows);
+                            win_dma(a.im, lrow[u], lane, pool + (u == 0 ? wv : 1) * WIN_SLOT);
+                        }
+                    }
+                    win_dma_wait();
+                    if (wv == 0 && base == 0) wstamp(11);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const long k0 = base + 128L * (u == 0 ? j0 : 3);
+                        if (u < nj && k0 < nrs) {
+                            float e0, e1;
+                            rescreen_win2<0>(pool + (u == 0 ? wv : 1) * WIN_SLOT, lane, qf, twoR, e0, e1);
+                            take(lrow[u] + lane, e0);
+                            take(lrow[u] + lane + 64, e1);
+                        }
+                    }
+                }
             }
         } else {
-            // row form: one row per thread per step (224-B split rows)
-            for (long k = tid; k < nrs; k += 256) {
+            // row form: one row per thread per step (224-B split rows), waves 0, 2, 3
+            const int rt = (wv == 0 ? 0 : wv - 1) * 64 + lane;
+            for (long k = rt; wv != 1 && k < nrs; k += 192) {
                 const long seg = full ? k / a.seg_rows : slist[k / a.seg_rows];
                 const long lr = seg_lrow(a.smap, seg, a.seg_rows, k % a.seg_rows);
                 half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
@@ -283,8 +350,10 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
                 take(lr, rescreen16(g0, g1, qf, twoR));
             }
         }
+        if (wv == 0) wstamp(12);
         if (mine) atomicAdd(&nresc, mine);
         __syncthreads();   // the row list is complete; the windows are free
+        stamp(4);
 
         // ---- 3. fp64 rescore of the listed rows (waves 2, 3, 0 in turn, XW_RPW rows per
         // batch: lane k gathers feature k, the squares go through LDS, lane j sums row j in
@@ -339,13 +408,19 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             }
         } else {
             // best_coherence_match (algorithms.py:92-130) + the winner's compute_distance
-            // (:133-135): all candidates' features in one round trip (lane = feature)
+            // (:133-135): the candidates' features, copied in before the re-screen
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_lds_sync();
             double g[XW_NCOH];
-            const long long cix = lane < XW_NCOH ? ccix[lane] : -1;
-            const double cvl = cix >= 0 ? src.Ap.lg[cix] : 0.0;
+            {
+                const unsigned *clo = reinterpret_cast<const unsigned *>(&cx[0][0]);
+                const unsigned *chi = reinterpret_cast<const unsigned *>(&cw[0][0]);
 #pragma unroll
-            for (int c = 0; c < XW_NCOH; ++c)
-                g[c] = (ccix[c] >= 0 && lane < IA_D) ? db_feat(src, cpos[c][2], cpos[c][0], cpos[c][1], lane) : 0.0;
+                for (int c = 0; c < XW_NCOH; ++c) g[c] = lds_f64(clo + c * 64, chi + c * 64, lane);
+            }
+            wave_lds_sync();   // every lane has its words before the squares overwrite them
+            const long long cix = lane < XW_NCOH ? ccix[lane] : -1;
+            const double cvl = cix >= 0 ? lds_f64(cvw[0], cvw[1], lane) : 0.0;
 #pragma unroll
             for (int c = 0; c < XW_NCOH; ++c) {
                 if (ccix[c] >= 0 && lane < IA_D) {
@@ -375,15 +450,19 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             const long long wix = ccix[win];
             const int wr = cpos[win][0], wc = cpos[win][1], wim = cpos[win][2];
             const double wd = __shfl(cwd, win), wval = __shfl(cvl, win);
+            wstamp(15);
             if (lane == 0) {
                 cs = bl == LLONG_MAX ? CohSel{0, 0, 0, 0, 0, 0, 0, 0.0}
                                      : CohSel{wix, wr, wc, wim, y - 2 + win / 5, x - 2 + win % 5, 1, wd};
                 csval = wval;
             }
         }
+        stamp(5);
+        if (wv == 2) wstamp(14);
         b = xrec_wave_min(b);
         if (lane == 0) wbest[wv] = b;
         __syncthreads();
+        stamp(6);
         if (wv != 0) return;
 
         // ---- 4. this rank's winner; sharded DB: publish it, collect every rank's
@@ -398,6 +477,7 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             if (!peer_collect_rec(f.px, i, lane, gb)) gb = lb;
             waited = __builtin_amdgcn_s_memrealtime() - w0;
         }
+        stamp(7);
         if (a.stats && lane == 0) {
             unsigned long long *sl = stats_slot(a.stats, i);
             atomicAdd(&sl[0], (unsigned long long)nresc);
@@ -445,11 +525,15 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
                                __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    stamp(8);
     if (wv != 0 || !nxt) return;
-    if (!cur) park_next();
 
     // ---- 5. the query row of (y, x + 1) for wave t + 1 (k_query_wave's arithmetic)
-    const int dep = lane < IA_D ? nxd[lane] : 0;
+    const int dep = pdep;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the prefetched words have landed
+    wave_lds_sync();
+    const double pv = lane < IA_D ? lds_f64(nxw[0], nxw[1], lane) : 0.0;
+    const double pc0 = lane < IA_D ? lds_f64(nxw[2], nxw[3], lane) : 0.0;
     double nb = 0.0;
     if (__any(dep == 2)) {   // the upper neighbour (ticket i - 1) decided (y - 1, x + 3)
         const unsigned long long *d = a.dbox + 2 * (long)(y - 1);
@@ -472,8 +556,9 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
         waited();
         nb = __longlong_as_double((long long)(((g1 & 0xffffffffULL) << 32) | (g0 & 0xffffffffULL)));
     }
-    const double vq = dep == 1 ? own : (dep == 2 ? nb : (lane < IA_D ? nxv[lane] : 0.0));
-    const double ncen = lane < IA_D ? nxc[lane] : 0.0;
+    stamp(9);
+    const double vq = dep == 1 ? own : (dep == 2 ? nb : pv);
+    const double ncen = pc0;
     const int m = y - a.y_lo_n;
     double d = 0.0;
     if (lane < IA_D) {
@@ -487,7 +572,8 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
     double d2 = d * d;
     for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
     if (lane == 0) a.nqn[m] = d2;
-    split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, a.amax[0]);
+    split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, amx);
+    stamp(10);
 }
 
 int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st, int njobs) {

@@ -59,6 +59,11 @@ int ia_diag_set_graph_mode(int mode);
  * it applies, 0 the separate kernels (k_query_wave, k_rescore / work list, k_peer_finish);
  * other values leave it; returns the previous value */
 int ia_diag_set_xwave(int on);
+/* with IA_XW_TRACE=<level tag>: the fused kernel's phase stamps of that level (100 MHz
+ * s_memrealtime) for waves < 4096 and the first 8 pixels of each, 12 stamps per pixel:
+ * {start, ticket, e*, candidates, re-screen, rescore | coherence, winner, exchange,
+ * update, neighbour, end}; 4096 x 8 x 16 u64 (slots 11-15: wave-level stamps of the re-screen, coherence and rescore) */
+int ia_diag_xwave_trace(unsigned long long *out);
 
 /* the sharded synthesis path in ONE process: level a (a->comm = NULL, a->db unused) with
  * its database split into n shards {db, row0, nrows, amax} (each ia_db_build'ed from its

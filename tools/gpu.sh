@@ -62,8 +62,8 @@ shardsim)
 trace)
     tag=$1; shift
     cmd=$(split_cmd "$@")
-    (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OLDPWD/gpurun_out/$tag" -o run -- $cmd) > gpurun_out/$tag.log 2>&1 \
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$PWD/gpurun_out/$tag" -o run -- $cmd > gpurun_out/$tag.log 2>&1 \
         || { tail -20 gpurun_out/$tag.log; exit 1; }
     python3 tools/trace_summary.py gpurun_out/$tag/run_kernel_trace.csv > gpurun_out/$tag/summary.txt
     cat gpurun_out/$tag/summary.txt
@@ -72,8 +72,8 @@ trace)
 pmc)
     tag=$1; counters=$2; shift 2
     cmd=$(split_cmd "$@")
-    (cd /tmp && timeout -s KILL 600 rocprofv3 --pmc $counters --output-format csv \
-        -d "$OLDPWD/gpurun_out/$tag" -o run -- $cmd) > gpurun_out/$tag.log 2>&1 \
+    timeout -s KILL 600 rocprofv3 --pmc $counters --output-format csv \
+        -d "$PWD/gpurun_out/$tag" -o run -- $cmd > gpurun_out/$tag.log 2>&1 \
         || { tail -20 gpurun_out/$tag.log; exit 1; }
     ls gpurun_out/$tag ;;
 abknob)
