@@ -79,24 +79,67 @@ __device__ __forceinline__ float win_x(const char *bf, const char *bc, int k) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)) +
            (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16));
 }
-// CHUNK > 0: a scheduling barrier every CHUNK terms, so that at most CHUNK terms' LDS reads
-// are in flight (fewer live registers; same order, same values)
-template <int CHUNK = 0>
+// the window's terms walked row by row (rolled loops over the window's rows, constant
+// column offsets inside): the same 56 terms in the same order as rescreen16, so the same fp32
+// values, in a few hundred bytes of code instead of several KB (the fused per-wave kernel
+// runs cold from the instruction cache every launch)
+__device__ __forceinline__ void win_terms2(const char *r0, const char *r1, const float *qf, int k,
+                                           float &a0, float &a1) {
+    const uint32_t v0 = *reinterpret_cast<const uint32_t *>(r0);
+    const uint32_t v1 = *reinterpret_cast<const uint32_t *>(r1);
+    const float f = qf[(k & 1) * 28 + (k >> 1)];
+    a0 = fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(v0 & 0xffffu)) +
+              (float)__builtin_bit_cast(_Float16, (uint16_t)(v0 >> 16)), f, a0);
+    a1 = fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(v1 & 0xffffu)) +
+              (float)__builtin_bit_cast(_Float16, (uint16_t)(v1 >> 16)), f, a1);
+}
 __device__ __forceinline__ void rescreen_win2(const char *wb, int p, const float *qf, float twoR,
                                               float &e0, float &e1) {
     const char *bf0 = wb + 4 * p, *bc0 = wb + 4 * (p >> 1);
     const char *bf1 = bf0 + 256, *bc1 = bc0 + 128;
     float a0 = 0.f, a1 = 0.f;
+    int k = 0;
+    // coarse A (k 0..8), fine A (9..33), coarse A' (34..42), fine A' (43..54): win_off's rows
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r) {
+        const int o = WB_FINE + r * WC_PC * 16 + 12;
 #pragma unroll
-    for (int k = 0; k < IA_DP; ++k) {
-        const float f = k < 55 ? qf[(k & 1) * 28 + (k >> 1)] : twoR;
-        a0 = fmaf(win_x(bf0, bc0, k), f, a0);
-        a1 = fmaf(win_x(bf1, bc1, k), f, a1);
-        if (CHUNK > 0 && k % CHUNK == CHUNK - 1) __builtin_amdgcn_sched_barrier(0);
+        for (int c = 0; c < 3; ++c, ++k) win_terms2(bc0 + o + 4 * c, bc1 + o + 4 * c, qf, k, a0, a1);
     }
+#pragma unroll 1
+    for (int r = 0; r < 5; ++r) {
+        const int o = r * WF_PC * 16 + 8;
+#pragma unroll
+        for (int c = 0; c < 5; ++c, ++k) win_terms2(bf0 + o + 4 * c, bf1 + o + 4 * c, qf, k, a0, a1);
+    }
+#pragma unroll 1
+    for (int r = 3; r < 6; ++r) {
+        const int o = WB_FINE + r * WC_PC * 16 + 12;
+#pragma unroll
+        for (int c = 0; c < 3; ++c, ++k) win_terms2(bc0 + o + 4 * c, bc1 + o + 4 * c, qf, k, a0, a1);
+    }
+#pragma unroll 1
+    for (int r = 5; r < 8; ++r) {
+        const int o = r * WF_PC * 16 + 8;
+        const int nc = r < 7 ? 5 : 2;
+#pragma unroll
+        for (int c = 0; c < 5; ++c, ++k)
+            if (c < nc) win_terms2(bf0 + o + 4 * c, bf1 + o + 4 * c, qf, k, a0, a1);
+    }
+    // the norm slot (k = 55), query factor 2^R
+    const uint32_t v0 = *reinterpret_cast<const uint32_t *>(bf0 + WB_FINE + WB_COARSE);
+    const uint32_t v1 = *reinterpret_cast<const uint32_t *>(bf1 + WB_FINE + WB_COARSE);
+    a0 = fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(v0 & 0xffffu)) +
+              (float)__builtin_bit_cast(_Float16, (uint16_t)(v0 >> 16)), twoR, a0);
+    a1 = fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(v1 & 0xffffu)) +
+              (float)__builtin_bit_cast(_Float16, (uint16_t)(v1 >> 16)), twoR, a1);
     e0 = a0;
     e1 = a1;
 }
+static_assert(win_off(0) == WB_FINE + 12 && win_off(9) == 8 && win_off(34) == WB_FINE + 3 * WC_PC * 16 + 12 &&
+                  win_off(43) == 5 * WF_PC * 16 + 8 && win_off(54) == 7 * WF_PC * 16 + 12 &&
+                  win_off(55) == WB_FINE + WB_COARSE,
+              "rescreen_win2 walks win_off's rows");
 
 // this lane's pieces of the window of the stage at local row lrow (a wave stages a whole
 // window: pieces lane + 64 j), loaded into registers / stored into the wave's LDS window
@@ -191,31 +234,45 @@ __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const f
     return fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
 }
 
-// candidate segments (minimum <= Tseg) -> slist (LDS, first RESCORE_SEGCAP), count in *scount
+// candidate segments (minimum <= Tseg) -> slist (LDS, first RESCORE_SEGCAP), count in *scount:
+// a thread's register-held candidates as one bit mask and ONE atomic per thread (unrolled
+// per-candidate atomics cost ~800 instructions of code); any order (the winner is a
+// lexicographic minimum)
 __device__ __forceinline__ void segmin_select(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
                                               double Tseg, int *slist, int *scount) {
     const int tid = threadIdx.x;
     if (tid >= 256) return;
-    auto push = [&](float e, long s) {
-        if ((double)e <= Tseg) {
-            const int pos = atomicAdd(scount, 1);
-            if (pos < RESCORE_SEGCAP) slist[pos] = (int)s;
-        }
-    };
+    static_assert(RESCORE_REG * 4 <= 32, "one 32-bit mask");
+    unsigned m = 0;
 #pragma unroll
     for (int j = 0; j < RESCORE_REG; ++j) {
-        const long i = tid + (long)j * 256;
-        push(v[j].x, 4 * i);
-        push(v[j].y, 4 * i + 1);
-        push(v[j].z, 4 * i + 2);
-        push(v[j].w, 4 * i + 3);
+        m |= ((double)v[j].x <= Tseg ? 1u : 0u) << (4 * j);
+        m |= ((double)v[j].y <= Tseg ? 1u : 0u) << (4 * j + 1);
+        m |= ((double)v[j].z <= Tseg ? 1u : 0u) << (4 * j + 2);
+        m |= ((double)v[j].w <= Tseg ? 1u : 0u) << (4 * j + 3);
+    }
+    if (m) {
+        int pos = atomicAdd(scount, __builtin_popcount(m));
+        while (m) {
+            const int b = __builtin_ctz(m);
+            m &= m - 1;
+            if (pos < RESCORE_SEGCAP) slist[pos] = 4 * (tid + (b >> 2) * 256) + (b & 3);
+            ++pos;
+        }
     }
     for (long i = tid + (long)RESCORE_REG * 256; i < n4; i += 256) {
         const float4 x = sq4[i];
-        push(x.x, 4 * i);
-        push(x.y, 4 * i + 1);
-        push(x.z, 4 * i + 2);
-        push(x.w, 4 * i + 3);
+        unsigned mt = ((double)x.x <= Tseg ? 1u : 0u) | ((double)x.y <= Tseg ? 2u : 0u) |
+                      ((double)x.z <= Tseg ? 4u : 0u) | ((double)x.w <= Tseg ? 8u : 0u);
+        if (mt) {
+            int pos = atomicAdd(scount, __builtin_popcount(mt));
+            while (mt) {
+                const int b = __builtin_ctz(mt);
+                mt &= mt - 1;
+                if (pos < RESCORE_SEGCAP) slist[pos] = (int)(4 * i + b);
+                ++pos;
+            }
+        }
     }
 }
 

@@ -38,12 +38,12 @@ struct WinSrc {
     long lrow;
 };
 __device__ __forceinline__ WinSrc win_src(const ImgDb &im, long lrow) {
-    const long g = im.row0 + lrow;
-    const long img = g / im.hw;
-    const long rem = g - img * im.hw;
+    const unsigned g = (unsigned)(im.row0 + lrow);   // < 2^31 (img_db_applies)
+    const unsigned img = g / (unsigned)im.hw;
+    const unsigned rem = g - img * (unsigned)im.hw;
     WinSrc w;
-    w.y = (int)(rem / im.W);
-    w.x0 = (int)(rem - (long)w.y * im.W);
+    w.y = (int)(rem / (unsigned)im.W);
+    w.x0 = (int)(rem - (unsigned)w.y * (unsigned)im.W);
     w.fp = im.ap + img * im.apstride;
     w.cp = w.fp + im.apc;
     w.lrow = lrow;

@@ -51,16 +51,18 @@ struct StageMap {
     int nstrip;   // W / 128
     int sc;       // stages per chunk (ch / 128)
 };
+// (chunks, stages and segments come in powers of two; row indices of a level's shard stay
+// below 2^31 wherever these run: 32-bit arithmetic, shifts instead of 64-bit divisions)
 __host__ __device__ __forceinline__ long stage_lrow(const StageMap &m, long chunk, int s) {
     if (m.W == 0) return (chunk * m.sc + s) * 128L;
-    const long sx = chunk % m.nstrip, yb = chunk / m.nstrip;
-    return (yb * m.sc + s) * (long)m.W + sx * 128;
+    const unsigned c = (unsigned)chunk, yb = c / (unsigned)m.nstrip, sx = c - yb * (unsigned)m.nstrip;
+    return ((long)yb * m.sc + s) * (long)m.W + (long)sx * 128;
 }
 // local row of element k (0 <= k < seg_rows) of segment seg
 __host__ __device__ __forceinline__ long seg_lrow(const StageMap &m, long seg, int seg_rows, long k) {
-    const int spc = (m.sc * 128) / seg_rows;   // segments per chunk
-    const long chunk = seg / spc;
-    const int s = (int)(seg - chunk * spc) * (seg_rows >> 7) + (int)(k >> 7);
+    const int lspc = __builtin_ctz((unsigned)(m.sc * 128 / seg_rows));   // log2 segments per chunk
+    const long chunk = seg >> lspc;
+    const int s = (int)(seg - (chunk << lspc)) * (seg_rows >> 7) + (int)(k >> 7);
     return stage_lrow(m, chunk, s) + (k & 127);
 }
 static inline bool db_strips_enabled() {
@@ -87,7 +89,8 @@ struct ImgDb {
 };
 constexpr size_t IMG_SCRATCH = 1024 * 8 * sizeof(double);   // ia_db_build_image's amax partials
 static inline bool img_db_applies(int W, long row0, long nrows) {
-    return W % 128 == 0 && row0 % 128 == 0 && db_rows_padded(nrows) == nrows;
+    return W % 128 == 0 && row0 % 128 == 0 && db_rows_padded(nrows) == nrows &&
+           row0 + nrows < (1L << 31);   // win_src's 32-bit row arithmetic
 }
 static inline size_t img_align(size_t b) { return (b + 255) / 256 * 256; }
 // the image-form buffer of rows [row0, row0 + nrows) of a level with fine images H x W and

@@ -62,13 +62,12 @@ __device__ __forceinline__ const double *feat_addr(const ImgPair &X, const ImgPa
     cc = symi2(c0, w);
     return base + (long)rr * w + cc;
 }
-// feature k of DB row (A' image img, pixel (r, c)) (algorithms.py:63-67)
-__device__ __forceinline__ double db_feat(const DbSrc &src, int img, int r, int c, int k) {
-    ImgPair ap = src.Ap;
-    ap.sm += (long)img * src.hws;
-    ap.lg += (long)img * src.hw;
-    int rr, cc;
-    return *feat_addr(src.A, ap, r, c, k, rr, cc);
+// image, row and column of global DB row g (< 2^31: the fused kernel's host check)
+__device__ __forceinline__ void row_pos(long g, long hw, int w, int &img, int &r, int &c) {
+    const unsigned u = (unsigned)g, im = u / (unsigned)hw, rem = u - im * (unsigned)hw;
+    img = (int)im;
+    r = (int)(rem / (unsigned)w);
+    c = (int)(rem - (unsigned)r * (unsigned)w);
 }
 
 // lane's double at p into the wave's LDS words lo[lane], hi[lane] by two 4-byte DMA copies
@@ -89,8 +88,11 @@ __device__ __forceinline__ double pw55_lds(const double *v) {
     double r[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = v[j];
+#pragma unroll 1
+    for (int k = 8; k < 48; k += 8) {
 #pragma unroll
-    for (int k = 8; k < 48; ++k) r[k & 7] += v[k];
+        for (int j = 0; j < 8; ++j) r[j] += v[k + j];
+    }
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 #pragma unroll
     for (int k = 48; k < IA_D; ++k) res += v[k];
@@ -110,6 +112,8 @@ constexpr int XW_ROWCAP = 256;   // rows within Trow rescored lane-parallel (the
 constexpr int XW_RPW = 4;        // rows per rescoring wave and batch
 constexpr int XW_NCOH = 15;      // coherence window positions (3 x 5, algorithms.py:101-102)
 constexpr size_t XW_STAGE_B = (size_t)4 * XW_RPW * IA_DP * 8 * 2;   // 4 waves x (x^2, (x w)^2)
+constexpr size_t XW_RAW_B = (size_t)4 * XW_RPW * 128 * 4;            // 4 waves x rows' lo / hi words
+constexpr int XW_COH_DMA = 2 + 2 * XW_NCOH;                          // coherence copies per lane
 
 __device__ __forceinline__ unsigned long long dgran(unsigned int tag, unsigned int bits) {
     return ((unsigned long long)tag << 32) | bits;
@@ -153,7 +157,8 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
     }
     const XArgs &a = BATCH ? sa : a0;
     constexpr size_t POOL = IMG ? (size_t)4 * WIN_SLOT : 0;
-    __shared__ __attribute__((aligned(16))) char pool[POOL > XW_STAGE_B ? POOL : XW_STAGE_B];
+    constexpr size_t RESB = XW_STAGE_B + XW_RAW_B;
+    __shared__ __attribute__((aligned(16))) char pool[POOL > RESB ? POOL : RESB];
     __shared__ double cx[XW_NCOH][IA_DP], cw[XW_NCOH][IA_DP];
     __shared__ double qs[IA_DP], wts[IA_DP];
     __shared__ float qf[IA_DP];
@@ -260,35 +265,38 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
         const bool full = ns > RESCORE_SEGCAP || force_full;
         const long nscan = full ? a.nseg : ns;
         const long nrs = nscan * a.seg_rows;
-        // wave 1: the coherence candidates (p_r = s(r) + q - r inside A'), then all their
-        // features requested at once by LDS DMA (candidate c's lo / hi words in cx / cw);
-        // they land during the re-screen, which wave 1 leaves to the other three (its loads
-        // return in order: a re-screen window of its own would wait for all of these)
+        const int lseg = __builtin_ctz((unsigned)a.seg_rows);
+        // wave 1: the coherence candidates (p_r = s(r) + q - r inside A'); an invalid one gets
+        // position (0, 0, 0) so that its (unused) copies read valid memory
         if (wv == 1) {
-            long long cix = -1;
             if (lane < XW_NCOH) {
                 const int sr = s_r + y - rr0, sc = s_c + x - rc0;
-                if (cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w)
-                    cix = ((long)src.A.h * s_i + sr) * src.A.w + sc;
-                ccix[lane] = cix;
-                cpos[lane][0] = sr; cpos[lane][1] = sc; cpos[lane][2] = s_i;
+                const bool ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
+                ccix[lane] = ok ? ((long)src.A.h * s_i + sr) * src.A.w + sc : -1;
+                cpos[lane][0] = ok ? sr : 0; cpos[lane][1] = ok ? sc : 0; cpos[lane][2] = ok ? s_i : 0;
             }
-            dma_f64(src.Ap.lg + (cix >= 0 ? cix : 0), lane < XW_NCOH && cix >= 0, cvw[0], cvw[1]);
             wave_lds_sync();
+        }
+        // wave 1: the candidates' A' values and all their features requested at once by LDS
+        // DMA (candidate c's lo / hi words in cx / cw): EXACTLY XW_COH_DMA copies, none
+        // skipped, so that a window copied in before them is waited for with vmcnt
+        // (loads return in order)
+        auto coh_issue = [&]() {
+            const long long cl = lane < XW_NCOH ? ccix[lane] : -1;
+            dma_f64(src.Ap.lg + (cl >= 0 ? cl : 0), true, cvw[0], cvw[1]);
             unsigned *clo = reinterpret_cast<unsigned *>(&cx[0][0]);
             unsigned *chi = reinterpret_cast<unsigned *>(&cw[0][0]);
-#pragma unroll
+#pragma unroll 1
             for (int c = 0; c < XW_NCOH; ++c) {
-                const bool on = ccix[c] >= 0;
                 ImgPair ap = src.Ap;
                 ap.sm += (long)cpos[c][2] * src.hws;
                 ap.lg += (long)cpos[c][2] * src.hw;
                 int rr, cc;
                 const double *fp = feat_addr(src.A, ap, cpos[c][0], cpos[c][1], lane < IA_D ? lane : 0, rr, cc);
-                if (on) dma_f64(fp, lane < IA_D, clo + c * 64, chi + c * 64);
+                dma_f64(fp, true, clo + c * 64, chi + c * 64);
             }
             wstamp(13);
-        }
+        };
 
         // ---- 2. fp32 re-screen of the candidate segments' rows; rows within Trow to the
         // list (overflow rows rescored in place: never on the measured configs)
@@ -306,45 +314,49 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
                 }
             }
         };
+        auto stage_row = [&](long k) {   // local row of re-screen element k (a stage's first)
+            const long seg = full ? (k >> lseg) : slist[k >> lseg];
+            return seg_lrow(a.smap, seg, a.seg_rows, k & (a.seg_rows - 1));
+        };
         if constexpr (IMG) {
-            // the 128-row stages of each 512-row step go to waves 0, 2, 3, 0 (wave 0 takes two,
-            // in the slots of waves 0 and 1), each window copied into LDS by DMA: one round
-            // trip per step (more than one candidate segment per query is rare)
-            if (wv != 1) {
-                const int j0 = wv == 0 ? 0 : wv - 1;          // first stage of the step
-                const int nj = wv == 0 ? 2 : 1;
-                for (long base = 0; base < nrs; base += 512) {
-                    long lrow[2] = {0, 0};
-                    wave_lds_sync();   // the previous step's reads of the slots are done
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const long k0 = base + 128L * (u == 0 ? j0 : 3);
-                        if (u < nj && k0 < nrs) {
-                            const long seg = full ? k0 / a.seg_rows : slist[k0 / a.seg_rows];
-                            lrow[u] = seg_lrow(a.smap, seg, a.seg_rows, k0 % a.seg_rows);
-                            win_dma(a.im, lrow[u], lane, pool + (u == 0 ? wv : 1) * WIN_SLOT);
-                        }
-                    }
-                    win_dma_wait();
-                    if (wv == 0 && base == 0) wstamp(11);
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const long k0 = base + 128L * (u == 0 ? j0 : 3);
-                        if (u < nj && k0 < nrs) {
-                            float e0, e1;
-                            rescreen_win2<0>(pool + (u == 0 ? wv : 1) * WIN_SLOT, lane, qf, twoR, e0, e1);
-                            take(lrow[u] + lane, e0);
-                            take(lrow[u] + lane + 64, e1);
-                        }
-                    }
-                }
+            // stage j of each 512-row step to wave j, its window copied into LDS by DMA: one
+            // round trip per step (more than one candidate segment per query is rare); wave 1
+            // copies its first window before the coherence gathers and waits for that alone
+            char *wb = pool + wv * WIN_SLOT;
+            long k0 = 128L * wv, lr = 0;
+            if (k0 < nrs) {
+                lr = stage_row(k0);
+                win_dma(a.im, lr, lane, wb);
+            }
+            if (wv == 1) {
+                asm volatile("" ::: "memory");   // the window's copies are issued first
+                coh_issue();
+                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XW_COH_DMA) : "memory");
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                win_dma_wait();
+            }
+            if (wv == 0) wstamp(11);
+            while (k0 < nrs) {
+                float e0, e1;
+                rescreen_win2(wb, lane, qf, twoR, e0, e1);
+                take(lr + lane, e0);
+                take(lr + lane + 64, e1);
+                k0 += 512;
+                if (k0 >= nrs) break;
+                wave_lds_sync();   // every lane is done reading the slot
+                lr = stage_row(k0);
+                win_dma(a.im, lr, lane, wb);
+                win_dma_wait();
             }
         } else {
-            // row form: one row per thread per step (224-B split rows), waves 0, 2, 3
+            // row form: one row per thread per step (224-B split rows), waves 0, 2, 3 (wave 1's
+            // in-order loads would wait behind its coherence gathers)
+            if (wv == 1) coh_issue();
             const int rt = (wv == 0 ? 0 : wv - 1) * 64 + lane;
             for (long k = rt; wv != 1 && k < nrs; k += 192) {
-                const long seg = full ? k / a.seg_rows : slist[k / a.seg_rows];
-                const long lr = seg_lrow(a.smap, seg, a.seg_rows, k % a.seg_rows);
+                const long seg = full ? (k >> lseg) : slist[k >> lseg];
+                const long lr = seg_lrow(a.smap, seg, a.seg_rows, k & (a.seg_rows - 1));
                 half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
                 load_row16(reinterpret_cast<const half8 *>(a.db), lr < a.nrows ? lr : 0, g0, g1);
                 take(lr, rescreen16(g0, g1, qf, twoR));
@@ -356,47 +368,47 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
         stamp(4);
 
         // ---- 3. fp64 rescore of the listed rows (waves 2, 3, 0 in turn, XW_RPW rows per
-        // batch: lane k gathers feature k, the squares go through LDS, lane j sums row j in
-        // numpy's order) | wave 1: the coherence pick
+        // batch: lane k copies feature k of each row into LDS by DMA, the squares go through
+        // LDS, lane j sums row j in numpy's order) | wave 1: the coherence pick
         const int nl = rcount < XW_ROWCAP ? rcount : XW_ROWCAP;
         XRec b = ob;
         if (wv != 1) {
             const int rk = wv == 2 ? 0 : (wv == 3 ? 1 : 2);
             double *rx = reinterpret_cast<double *>(pool) + (size_t)wv * XW_RPW * IA_DP * 2;
+            unsigned *rw = reinterpret_cast<unsigned *>(pool + XW_STAGE_B) + wv * XW_RPW * 128;
             for (int base = rk * XW_RPW; base < nl; base += 3 * XW_RPW) {
-                // lane j < XW_RPW locates row base + j once; every lane then gathers
+                // lane j < XW_RPW locates row base + j once
                 int li = 0, lr_ = 0, lc = 0;
                 long lg = 0;
                 if (lane < XW_RPW && base + lane < nl) {
                     lg = a.row0 + rlist[base + lane];
-                    const long img = lg / src.hw, rem = lg - img * src.hw;
-                    li = (int)img;
-                    lr_ = (int)(rem / src.A.w);
-                    lc = (int)(rem - (long)lr_ * src.A.w);
+                    row_pos(lg, src.hw, src.A.w, li, lr_, lc);
                 }
-                double g[XW_RPW];
-#pragma unroll
-                for (int j = 0; j < XW_RPW; ++j) {
+                wave_lds_sync();   // the previous batch is done with rx and rw
+#pragma unroll 1
+                for (int j = 0; j < XW_RPW && base + j < nl; ++j) {
                     const int ri = __shfl(li, j), rr = __shfl(lr_, j), rc = __shfl(lc, j);
                     const long rg = __shfl(lg, j);
-                    g[j] = 0.0;
-                    if (base + j < nl) {
-                        if (lane < IA_D) g[j] = db_feat(src, ri, rr, rc, lane);
-                        else if (lane == IA_D) g[j] = src.Ap.lg[rg];
-                    }
+                    ImgPair ap = src.Ap;
+                    ap.sm += (long)ri * src.hws;
+                    ap.lg += (long)ri * src.hw;
+                    int r2, c2;
+                    const double *fp = feat_addr(src.A, ap, rr, rc, lane < IA_D ? lane : 0, r2, c2);
+                    dma_f64(lane == IA_D ? src.Ap.lg + rg : fp, true, rw + j * 128, rw + j * 128 + 64);
                 }
-                wave_lds_sync();   // the previous batch's sums are done with rx
-#pragma unroll
-                for (int j = 0; j < XW_RPW; ++j) {
-                    if (base + j < nl) {
-                        if (lane < IA_D) {
-                            const double xx = g[j] - qs[lane];
-                            const double xw = xx * wts[lane];
-                            rx[j * IA_DP + lane] = xx * xx;
-                            rx[(XW_RPW + j) * IA_DP + lane] = xw * xw;
-                        } else if (lane == IA_D) {
-                            rx[j * IA_DP + IA_D] = g[j];   // the row's A' value (slot 55)
-                        }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                wave_lds_sync();
+                const double ql = lane < IA_D ? qs[lane] : 0.0, wl = lane < IA_D ? wts[lane] : 0.0;
+#pragma unroll 1
+                for (int j = 0; j < XW_RPW && base + j < nl; ++j) {
+                    const double g = lds_f64(rw + j * 128, rw + j * 128 + 64, lane);
+                    if (lane < IA_D) {
+                        const double xx = g - ql;
+                        const double xw = xx * wl;
+                        rx[j * IA_DP + lane] = xx * xx;
+                        rx[(XW_RPW + j) * IA_DP + lane] = xw * xw;
+                    } else if (lane == IA_D) {
+                        rx[j * IA_DP + IA_D] = g;   // the row's A' value (slot 55)
                     }
                 }
                 wave_lds_sync();
@@ -408,24 +420,23 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
             }
         } else {
             // best_coherence_match (algorithms.py:92-130) + the winner's compute_distance
-            // (:133-135): the candidates' features, copied in before the re-screen
+            // (:133-135): the candidates' features, copied in before the re-screen; squares
+            // written over the words from the last candidate down (candidate c's squares
+            // only cover the words of candidates >= c, already read)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_lds_sync();
-            double g[XW_NCOH];
-            {
-                const unsigned *clo = reinterpret_cast<const unsigned *>(&cx[0][0]);
-                const unsigned *chi = reinterpret_cast<const unsigned *>(&cw[0][0]);
-#pragma unroll
-                for (int c = 0; c < XW_NCOH; ++c) g[c] = lds_f64(clo + c * 64, chi + c * 64, lane);
-            }
-            wave_lds_sync();   // every lane has its words before the squares overwrite them
             const long long cix = lane < XW_NCOH ? ccix[lane] : -1;
             const double cvl = cix >= 0 ? lds_f64(cvw[0], cvw[1], lane) : 0.0;
-#pragma unroll
-            for (int c = 0; c < XW_NCOH; ++c) {
-                if (ccix[c] >= 0 && lane < IA_D) {
-                    const double xx = g[c] - qs[lane];
-                    const double xw = xx * wts[lane];
+            const double ql = lane < IA_D ? qs[lane] : 0.0, wl = lane < IA_D ? wts[lane] : 0.0;
+            const unsigned *clo = reinterpret_cast<const unsigned *>(&cx[0][0]);
+            const unsigned *chi = reinterpret_cast<const unsigned *>(&cw[0][0]);
+#pragma unroll 1
+            for (int c = XW_NCOH - 1; c >= 0; --c) {
+                const double g = lds_f64(clo + c * 64, chi + c * 64, lane);
+                wave_lds_sync();   // every lane has candidate c's words
+                if (lane < IA_D) {
+                    const double xx = g - ql;
+                    const double xw = xx * wl;
                     cx[c][lane] = xx * xx;
                     cw[c][lane] = xw * xw;
                 }
@@ -488,11 +499,9 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
         // ---- kappa test and update (image_analogies.py:200-220; finish_apply's rules)
         const CohSel c = cs;
         const long long app = (gb.i < 0 || gb.i >= f.N_total) ? 0 : gb.i;
-        const long hw = src.hw;
-        const int Aw = src.A.w;
-        long img = app / hw;
-        const long rem = app - img * hw;
-        const int ar = (int)(rem / Aw), ac = (int)(rem - (long)(rem / Aw) * Aw);
+        int im0, ar, ac;
+        row_pos(app, src.hw, src.A.w, im0, ar, ac);
+        long img = im0;
         int pr = ar, pc = ac;
         double val = gb.val;
         if (c.valid && c.dcoh <= gb.wd * f.kappa_factor) {
