@@ -49,17 +49,46 @@ F16_MFMA_PEAK_TFLOPS = 4096 * 256 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 # HBM traffic of one launch of the dominant screen instance (k_screen16<11>, the c4 finest
 # level's plateau waves: 321-342 queries x 4,194,304 rows), from rocprofv3 PMC passes of
-# bench.py itself (tools/pmc_bench.sh: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
-# MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process)
-SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r02_final_screen_traffic_bench_pmc.json')
+# bench.py itself (tools/gpu.sh traffic: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
+# MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process).
+# The file records a hash of the screen's sources; a file from other sources is stale and
+# the bench then reports traffic null.
+SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r03_screen_traffic_bench_pmc.json')
+SCREEN_SRCS = ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h')
+
+
+def screen_src_sha1():
+    import hashlib
+    h = hashlib.sha1()
+    for f in SCREEN_SRCS:
+        h.update(open(os.path.join(ROOT, 'image-analogies-python_amd', 'csrc', f), 'rb').read())
+    return h.hexdigest()
 
 
 def screen_pmc():
     if not os.path.exists(SCREEN_PMC_FILE):
         return None
     d = json.load(open(SCREEN_PMC_FILE))
+    if d.get('screen_src_sha1') != screen_src_sha1():
+        return None
     return {'bytes': d['traffic_bytes'], 'kernel': d['kernel'], 'dispatches': d['dispatches'],
             'source': os.path.relpath(SCREEN_PMC_FILE, ROOT)}
+
+SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r03_screen_sq_pmc.json')
+
+
+def screen_sq():
+    """MFMA-busy fraction, held clock and wait share of the dominant screen instance
+    (tools/pmc_sq.py over a PMC pass of bench.py), if the file matches the screen's sources."""
+    if not os.path.exists(SCREEN_SQ_FILE):
+        return None
+    d = json.load(open(SCREEN_SQ_FILE))
+    if d.get('screen_src_sha1') != screen_src_sha1():
+        return None
+    return {k: d[k] for k in ('mfma_busy', 'clock_ghz', 'wait_inst_share',
+                              'lds_bank_conflict_share', 'mean_us')} | {
+        'source': os.path.relpath(SCREEN_SQ_FILE, ROOT)}
+
 
 CONFIGS = {
     'c1': dict(A=(180, 117), B=(180, 117), k=0.5, levels=None, name='shore-crop 180x117 filter analogy, brute force'),
@@ -636,6 +665,10 @@ def main():
                                 'the DB read once (image form: 59 MB of split pixel pairs and '
                                 'norm slots; row form: 939.5 MB) + 11 MB of segment minima'
                                 % (pmc['dispatches'], pmc['kernel'], pmc['source']))
+        sq = screen_sq()
+        if sq is not None:
+            # the same kernel's SQ/GRBM pass: why frac is what it is
+            roof['pmc'] = sq
     if lsh is not None:
         # k_lsh_query is a gather: each examined row costs its 55 fp64 features (440 B)
         examined = sum(p['rows_rescored'] for p in prof if p['timed_screens'])

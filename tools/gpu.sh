@@ -10,7 +10,11 @@
 #   tools/gpu.sh trace TAG -- CMD...          rocprofv3 kernel trace + stats of CMD
 #                                             -> gpurun_out/TAG/ (trace csv removed, stats kept)
 #   tools/gpu.sh pmc TAG COUNTERS -- CMD...   one rocprofv3 --pmc pass (counters space-separated
-#                                             in one argument; respect the per-block limits)
+#                                             in one argument; respect the per-block limits),
+#                                             summarised per kernel (PMC_REGEX filters kernels)
+#   tools/gpu.sh traffic TAG -- CMD...        FETCH_SIZE + WRITE_SIZE passes of the screen
+#                                             -> gpurun_out/traffic_TAG.json (bench.py reads it
+#                                             from profiles/)
 #   tools/gpu.sh abknob TAG VAR A B -- CMD... A/B/A/B of an environment knob (CMD prints one line)
 #   tools/gpu.sh ablib TAG LIB -- CMD...      A/B/A/B of libia.so against another build (IA_LIB_PATH)
 #
@@ -70,12 +74,35 @@ trace)
     head -16 gpurun_out/$tag/run_kernel_stats.csv | cut -d, -f1-6
     rm -f gpurun_out/$tag/run_kernel_trace.csv ;;
 pmc)
+    # counters summarised per kernel on the box (mean per dispatch); the raw csv is dropped
+    # unless KEEP_CSV=1.  PMC_REGEX restricts collection to matching kernels.
     tag=$1; counters=$2; shift 2
     cmd=$(split_cmd "$@")
-    timeout -s KILL 600 rocprofv3 --pmc $counters --output-format csv \
+    rx=(); [ -n "$PMC_REGEX" ] && rx=(--kernel-include-regex "$PMC_REGEX")
+    timeout -s KILL 600 rocprofv3 --pmc $counters "${rx[@]}" --output-format csv \
         -d "$PWD/gpurun_out/$tag" -o run -- $cmd > gpurun_out/$tag.log 2>&1 \
         || { tail -20 gpurun_out/$tag.log; exit 1; }
-    ls gpurun_out/$tag ;;
+    python3 tools/pmc_summary.py gpurun_out/$tag/run_counter_collection.csv > gpurun_out/$tag/summary.txt
+    [ "$KEEP_CSV" = 1 ] || rm -f gpurun_out/$tag/run_counter_collection.csv
+    grep -A12 k_screen16i gpurun_out/$tag/summary.txt | head -40
+    if grep -q k_screen16iILi11E gpurun_out/$tag/summary.txt && grep -q SQ_VALU_MFMA_BUSY gpurun_out/$tag/summary.txt; then
+        python3 tools/pmc_sq.py gpurun_out/$tag/summary.txt > gpurun_out/sq_$tag.json
+    fi ;;
+traffic)
+    # HBM bytes per launch of the dominant screen instance on the bench process: separate
+    # FETCH_SIZE and WRITE_SIZE passes (MI355X_MICROARCH.md HBM section), a stream sync every
+    # 64 waves so the profiler keeps up -> gpurun_out/traffic_TAG.json
+    tag=$1; shift
+    cmd=$(split_cmd "$@")
+    for c in FETCH_SIZE WRITE_SIZE; do
+        IA_SYNC_EVERY=64 timeout -s KILL 600 rocprofv3 --pmc $c --kernel-include-regex k_screen16 \
+            --output-format csv -d "$PWD/gpurun_out/tr_$tag/$c" -o run -- $cmd \
+            > gpurun_out/tr_${tag}_$c.log 2>&1 || { tail -20 gpurun_out/tr_${tag}_$c.log; exit 1; }
+    done
+    python3 tools/pmc_traffic.py gpurun_out/tr_$tag/FETCH_SIZE/run_counter_collection.csv \
+        gpurun_out/tr_$tag/WRITE_SIZE/run_counter_collection.csv > gpurun_out/traffic_$tag.json
+    rm -rf gpurun_out/tr_$tag
+    cat gpurun_out/traffic_$tag.json ;;
 abknob)
     tag=$1; var=$2; va=$3; vb=$4; shift 4
     cmd=$(split_cmd "$@")
