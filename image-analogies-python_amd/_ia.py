@@ -207,9 +207,10 @@ def graph_mode(mode=-1):
 
 
 def xwave(on=-1):
-    """The fused per-wave kernel for this process (1: one launch per wave after the screen
-    runs the exact stage, the device-side exchange, the per-pixel tail and the next wave's
-    query rows [default, IA_XWAVE]; 0: the separate kernels); returns the previous value."""
+    """The fused per-wave kernel for this process (2 [default, IA_XWAVE]: one launch per wave
+    after the screen runs the exact stage, the device-side exchange, the per-pixel tail and
+    the next wave's query rows, in its strip form k_xstrip on strip-order image-form levels;
+    1: k_xwave everywhere; 0: the separate kernels); returns the previous value."""
     return lib().ia_diag_set_xwave(int(on))
 
 

@@ -216,8 +216,8 @@ __device__ __forceinline__ void segmin_load(const float4 *sq4, long n4, float4 (
         v[j] = i < lim ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
     }
 }
-__device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
-                                             float *redf) {
+// this wave's share of e* (valid in every lane), no barrier
+__device__ __forceinline__ float segmin_wave_min(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG]) {
     const int tid = threadIdx.x;
     const long lim = tid < 256 ? n4 : 0;
     float emin = FLT_MAX;
@@ -229,6 +229,12 @@ __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const f
         emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
     }
     for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
+    return emin;
+}
+__device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
+                                             float *redf) {
+    const int tid = threadIdx.x;
+    const float emin = segmin_wave_min(sq4, n4, v);
     if ((tid & 63) == 0 && tid < 256) redf[tid >> 6] = emin;
     __syncthreads();
     return fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));

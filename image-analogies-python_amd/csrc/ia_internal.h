@@ -258,7 +258,11 @@ struct XArgs {
 // k_xwave phase stamps (IA_XW_TRACE=<level tag>, ia_diag_xwave_trace): s_memrealtime (100
 // MHz) at XW_TRACE_N points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T
 constexpr int XW_TRACE_N = 16, XW_TRACE_PX = 8, XW_TRACE_T = 4096;
-int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st, int njobs = 1);
+// form: XW_ROWS (split-f16 rows), XW_IMG (image-form windows, fp32 re-screen), XW_STRIP
+// (strip-order image form: k_xstrip, fp64 windows; xstrip_applies)
+constexpr int XW_ROWS = 0, XW_IMG = 1, XW_STRIP = 2;
+bool xstrip_applies(const DbSrc &src);
+int launch_xwave(const XArgs &a, int nblocks, int form, hipStream_t st, int njobs = 1);
 
 // matcher statistics (profiling only): per-query counters are spread over STATS_SLOTS
 // cache lines so that the atomics of a wave's M queries do not serialise on one address;

@@ -315,8 +315,9 @@ static int shard_tail() {
 
 // the fused per-wave kernel (k_xwave, ia_xwave.hip): after each screen ONE launch runs the
 // exact stage, the device-side exchange, the per-pixel tail and the next wave's query rows
-// (IA_XWAVE / ia_diag_set_xwave: 1 [default] wherever it applies, 0 the separate kernels)
-static std::atomic<int> g_xwave{env_int("IA_XWAVE", 1)};
+// (IA_XWAVE / ia_diag_set_xwave: 2 [default] wherever it applies, with k_xstrip on
+// strip-order image-form levels; 1 k_xwave only; 0 the separate kernels)
+static std::atomic<int> g_xwave{env_int("IA_XWAVE", 2)};
 static int xwave_on() { return g_xwave.load(std::memory_order_relaxed); }
 
 // diagnostic: k_xwave phase stamps of the level tagged IA_XW_TRACE (one process-wide buffer)
@@ -605,7 +606,9 @@ struct LevelRun {
         x.jobs = jt;
         x.trace = xw_trace(a->tag);
         const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
-        if ((rc = launch_xwave(x, R, im, sq, K))) return rc;
+        const int form = !im ? XW_ROWS
+                       : (xwave_on() == 2 && sm.W > 0 && xstrip_applies(src)) ? XW_STRIP : XW_IMG;
+        if ((rc = launch_xwave(x, R, form, sq, K))) return rc;
         ++nscreen;
         pairs += (double)M * (double)a->nrows * K;
         if (prof) Ms.push_back(M);
@@ -724,7 +727,7 @@ int ia_diag_xwave_trace(unsigned long long *out) {
 
 int ia_diag_set_xwave(int on) {
     const int prev = xwave_on();
-    if (on == 0 || on == 1) g_xwave.store(on);
+    if (on >= 0 && on <= 2) g_xwave.store(on);
     return prev;
 }
 

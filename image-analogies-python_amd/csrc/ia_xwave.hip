@@ -139,6 +139,129 @@ __device__ __forceinline__ void xjob_apply(XArgs &a, const XJob &J, int b) {
     a.f.s = J.s; a.f.im = J.im; a.f.dbg_px = J.dbg_px; a.f.dbg_dist = J.dbg_dist;
 }
 
+// ---- the wave's tail, shared by k_xwave and k_xstrip ------------------------------------
+// phase stamp k of a traced pixel (thread 0)
+__device__ __forceinline__ void xw_stamp(unsigned long long *trace, int k) {
+    if (trace && threadIdx.x == 0) trace[k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// step 4 (wave 0, every lane): lb is this rank's winner for pixel (y, x) (ticket i); a
+// sharded DB publishes it and collects every rank's; then the kappa test against the
+// coherence pick c (A' value cval) and the B'/s/im (+ debug) update, and the decision
+// granules for the lower neighbour's next query.  Returns the pixel's new B' value.
+__device__ __forceinline__ double xw_finish(const XArgs &a, int i, int y, int x, int lane, const XRec &lb,
+                                            const CohSel &c, double cval, unsigned int nresc, int ns,
+                                            bool full, unsigned long long *trace) {
+    const FinishArgs &f = a.f;
+    const DbSrc &src = a.src;
+    const int t = f.t, W = f.W;
+    XRec gb = lb;
+    unsigned long long waited = 0;
+    if (f.px.nranks > 0) {
+        peer_publish_rec(f.px, i, lb, lane);
+        const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+        if (!peer_collect_rec(f.px, i, lane, gb)) gb = lb;
+        waited = __builtin_amdgcn_s_memrealtime() - w0;
+    }
+    xw_stamp(trace, 7);
+    if (a.stats && lane == 0) {
+        unsigned long long *sl = stats_slot(a.stats, i);
+        atomicAdd(&sl[0], (unsigned long long)nresc);
+        atomicAdd(&sl[1], (unsigned long long)ns);
+        atomicAdd(&sl[2], full ? 1ULL : 0ULL);
+        atomicAdd(&sl[3], waited);
+    }
+    // ---- kappa test and update (image_analogies.py:200-220; finish_apply's rules)
+    const long long app = (gb.i < 0 || gb.i >= f.N_total) ? 0 : gb.i;
+    int im0, ar, ac;
+    row_pos(app, src.hw, src.A.w, im0, ar, ac);
+    long img = im0;
+    int pr = ar, pc = ac;
+    double val = gb.val;
+    if (c.valid && c.dcoh <= gb.wd * f.kappa_factor) {
+        pr = c.wr; pc = c.wc; img = c.wim;
+        val = cval;
+    }
+    if (lane == 0) {
+        const long q = (long)y * W + x;
+        if (f.dbg_px) {
+            int32_t *o = f.dbg_px + 7 * q;
+            o[0] = ar; o[1] = ac;
+            o[2] = c.valid ? c.wr : 0;
+            o[3] = c.valid ? c.wc : 0;
+            o[4] = c.valid ? c.rr : 0;
+            o[5] = c.valid ? c.rc : 0;
+            o[6] = c.valid;
+            f.dbg_dist[2 * q] = c.valid ? gb.wd : 0.0;
+            f.dbg_dist[2 * q + 1] = c.valid ? c.dcoh : 0.0;
+        }
+        f.Bp_lg[q] = val;
+        f.s[2 * q] = pr;
+        f.s[2 * q + 1] = pc;
+        f.im[q] = (int32_t)img;
+        // the decision for the lower neighbour's next query (step 5)
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(val);
+        unsigned long long *d = a.dbox + 2 * (long)y;
+        __hip_atomic_store(d, dgran(t + 1, (unsigned int)bits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, dgran(t + 1, (unsigned int)(bits >> 32)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return val;
+}
+
+// step 5 (wave 0): the query row of (y, x + 1) for wave t + 1 (k_query_wave's arithmetic):
+// the prefetched features (nxw, LDS-DMA words), this pixel's new value own (dep 1) or the
+// upper neighbour's decision (dep 2, ticket i - 1 of this launch)
+__device__ __forceinline__ void xw_next_query(const XArgs &a, int i, int y, int x, int lane, int dep, double own,
+                                              float amx, const unsigned (*nxw)[64],
+                                              unsigned long long *trace) {
+    const int t = a.f.t;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the prefetched words have landed
+    wave_lds_sync();
+    const double pv = lane < IA_D ? lds_f64(nxw[0], nxw[1], lane) : 0.0;
+    const double pc0 = lane < IA_D ? lds_f64(nxw[2], nxw[3], lane) : 0.0;
+    double nb = 0.0;
+    if (__any(dep == 2)) {   // the upper neighbour (ticket i - 1) decided (y - 1, x + 3)
+        const unsigned long long *d = a.dbox + 2 * (long)(y - 1);
+        unsigned long long g0 = 0, g1 = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        auto waited = [&]() {
+            if (a.stats && lane == 0)
+                atomicAdd(&stats_slot(a.stats, i)[4], __builtin_amdgcn_s_memrealtime() - t0);
+        };
+        for (;;) {
+            g0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(g0 >> 32) == (unsigned)(t + 1) && (unsigned)(g1 >> 32) == (unsigned)(t + 1)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
+                if (lane == 0) atomicOr(a.err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        waited();
+        nb = __longlong_as_double((long long)(((g1 & 0xffffffffULL) << 32) | (g0 & 0xffffffffULL)));
+    }
+    xw_stamp(trace, 9);
+    const double vq = dep == 1 ? own : (dep == 2 ? nb : pv);
+    const double ncen = pc0;
+    const int m = y - a.y_lo_n;
+    double d = 0.0;
+    if (lane < IA_D) {
+        a.q64n[(long)m * IA_DP + lane] = vq;
+        d = vq - ncen;
+        a.qpn[(long)m * IA_DP + perm56(lane)] = -2.0f * (float)d;
+    } else if (lane == IA_D) {
+        a.q64n[(long)m * IA_DP + IA_D] = 0.0;
+        a.qpn[(long)m * IA_DP + perm56(IA_D)] = 1.0f;
+    }
+    double d2 = d * d;
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
+    if (lane == 0) a.nqn[m] = d2;
+    split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, amx);
+    xw_stamp(trace, 10);
+}
+
 // BATCH: a0.jobs holds a batch's pointers; the block copies the launch arguments into LDS
 // once and overrides them with its job's (a private copy of the arguments would live in
 // scratch memory), then reads them from there
@@ -476,124 +599,484 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
         stamp(6);
         if (wv != 0) return;
 
-        // ---- 4. this rank's winner; sharded DB: publish it, collect every rank's
+        // ---- 4. this rank's winner; sharded DB: publish it, collect every rank's; tail
         XRec lb = wbest[0];
 #pragma unroll
         for (int w = 1; w < 4; ++w) xrec_take(lb, wbest[w]);
-        XRec gb = lb;
-        unsigned long long waited = 0;
-        if (f.px.nranks > 0) {
-            peer_publish_rec(f.px, i, lb, lane);
-            const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
-            if (!peer_collect_rec(f.px, i, lane, gb)) gb = lb;
-            waited = __builtin_amdgcn_s_memrealtime() - w0;
-        }
-        stamp(7);
-        if (a.stats && lane == 0) {
-            unsigned long long *sl = stats_slot(a.stats, i);
-            atomicAdd(&sl[0], (unsigned long long)nresc);
-            atomicAdd(&sl[1], (unsigned long long)ns);
-            atomicAdd(&sl[2], full ? 1ULL : 0ULL);
-            atomicAdd(&sl[3], waited);
-        }
-        // ---- kappa test and update (image_analogies.py:200-220; finish_apply's rules)
-        const CohSel c = cs;
-        const long long app = (gb.i < 0 || gb.i >= f.N_total) ? 0 : gb.i;
-        int im0, ar, ac;
-        row_pos(app, src.hw, src.A.w, im0, ar, ac);
-        long img = im0;
-        int pr = ar, pc = ac;
-        double val = gb.val;
-        if (c.valid && c.dcoh <= gb.wd * f.kappa_factor) {
-            pr = c.wr; pc = c.wc; img = c.wim;
-            val = csval;
-        }
-        own = val;
-        if (lane == 0) {
-            const long q = (long)y * W + x;
-            if (f.dbg_px) {
-                int32_t *o = f.dbg_px + 7 * q;
-                o[0] = ar; o[1] = ac;
-                o[2] = c.valid ? c.wr : 0;
-                o[3] = c.valid ? c.wc : 0;
-                o[4] = c.valid ? c.rr : 0;
-                o[5] = c.valid ? c.rc : 0;
-                o[6] = c.valid;
-                f.dbg_dist[2 * q] = c.valid ? gb.wd : 0.0;
-                f.dbg_dist[2 * q + 1] = c.valid ? c.dcoh : 0.0;
-            }
-            f.Bp_lg[q] = val;
-            f.s[2 * q] = pr;
-            f.s[2 * q + 1] = pc;
-            f.im[q] = (int32_t)img;
-            // the decision for the lower neighbour's next query (step 5)
-            const unsigned long long bits = (unsigned long long)__double_as_longlong(val);
-            unsigned long long *d = a.dbox + 2 * (long)y;
-            __hip_atomic_store(d, dgran(t + 1, (unsigned int)bits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(d + 1, dgran(t + 1, (unsigned int)(bits >> 32)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        own = xw_finish(a, i, y, x, lane, lb, cs, csval, nresc, ns, full, trace);
     }
     stamp(8);
     if (wv != 0 || !nxt) return;
-
-    // ---- 5. the query row of (y, x + 1) for wave t + 1 (k_query_wave's arithmetic)
-    const int dep = pdep;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the prefetched words have landed
-    wave_lds_sync();
-    const double pv = lane < IA_D ? lds_f64(nxw[0], nxw[1], lane) : 0.0;
-    const double pc0 = lane < IA_D ? lds_f64(nxw[2], nxw[3], lane) : 0.0;
-    double nb = 0.0;
-    if (__any(dep == 2)) {   // the upper neighbour (ticket i - 1) decided (y - 1, x + 3)
-        const unsigned long long *d = a.dbox + 2 * (long)(y - 1);
-        unsigned long long g0 = 0, g1 = 0;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        auto waited = [&]() {
-            if (a.stats && lane == 0)
-                atomicAdd(&stats_slot(a.stats, i)[4], __builtin_amdgcn_s_memrealtime() - t0);
-        };
-        for (;;) {
-            g0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            g1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(g0 >> 32) == (unsigned)(t + 1) && (unsigned)(g1 >> 32) == (unsigned)(t + 1)) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
-                if (lane == 0) atomicOr(a.err, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        waited();
-        nb = __longlong_as_double((long long)(((g1 & 0xffffffffULL) << 32) | (g0 & 0xffffffffULL)));
-    }
-    stamp(9);
-    const double vq = dep == 1 ? own : (dep == 2 ? nb : pv);
-    const double ncen = pc0;
-    const int m = y - a.y_lo_n;
-    double d = 0.0;
-    if (lane < IA_D) {
-        a.q64n[(long)m * IA_DP + lane] = vq;
-        d = vq - ncen;
-        a.qpn[(long)m * IA_DP + perm56(lane)] = -2.0f * (float)d;
-    } else if (lane == IA_D) {
-        a.q64n[(long)m * IA_DP + IA_D] = 0.0;
-        a.qpn[(long)m * IA_DP + perm56(IA_D)] = 1.0f;
-    }
-    double d2 = d * d;
-    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
-    if (lane == 0) a.nqn[m] = d2;
-    split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, amx);
-    stamp(10);
+    // ---- 5. the query row of (y, x + 1) for wave t + 1
+    xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace);
 }
 
-int launch_xwave(const XArgs &a, int nblocks, bool img, hipStream_t st, int njobs) {
+// ---- strip-order image-form levels: the exact stage from fp64 windows (k_xstrip) ---------
+// A candidate segment of a strip-order level (StageMap W > 0, ia_internal.h) is nst =
+// seg_rows / 128 consecutive scanlines y0 .. y0 + nst - 1 of one 128-pixel column strip
+// [x0, x0 + 128) of one A' image.  Every fp64 sample its rows' features read
+// (algorithms.py:11-47) lies in four windows of the level's pyramids, held in LDS as the
+// REFLECTED images (symi2 applied when they are filled), so that pixel (y, x)'s 55 samples
+// sit at compile-time offsets from two per-pixel bases:
+//   A fine    rows y0 - 2 .. y0 + 5, cols x0 - 4 .. x0 + 131   (8 x 136)
+//   A' fine   rows y0 - 2 .. y0 + 3, the same cols             (6 x 136)
+//   A, A' coarse rows y0/2 - 1 .. y0/2 + 2, cols x0/2 - 2 .. x0/2 + 65   (4 x 68 each)
+// 19.6 KB, copied by DMA as 16-B pieces in ONE round trip; a piece with a column outside
+// the image (strips at the image's left / right edge) is copied from a clamped address and
+// rewritten by its own thread, after the wait, with its two reflected values (loaded in the
+// same round trip).  Every row of the segment is then rescored in fp64 from LDS in the
+// oracle's operation order (row_dist2), two rows per thread: no fp32 re-screen and no
+// per-row gathers.  The exact minimum over every row of the candidate segments is the
+// oracle's winner (the segments hold every row whose screen value is within Tseg, DESIGN.md
+// §4b).  The winner's weighted distance and A' value come from the same windows; the
+// coherence pick (wave 1) computes from its own LDS-DMA gathers while the first windows are
+// in flight.
+constexpr int XS_FW = 136, XS_CW = 68;                       // window columns (doubles)
+constexpr int XS_FA = 0, XS_FP = XS_FA + 8 * XS_FW;          // window offsets (doubles)
+constexpr int XS_CA = XS_FP + 6 * XS_FW, XS_CP = XS_CA + 4 * XS_CW;
+constexpr int XS_DBL = XS_CP + 4 * XS_CW;                    // 2448 doubles, 19584 B
+constexpr int XS_PIECES = XS_DBL / 2;                        // 16-B pieces
+constexpr int XS_DMA = (XS_PIECES + 191) / 192;              // 7 copies per thread of waves 0, 2, 3
+constexpr int XS_LDS_B = XS_DMA * 192 * 16;                  // 21504 B (the tail: dummy copies)
+constexpr int XS_CST = 65;                                   // coherence words per candidate (banks)
+
+bool xstrip_applies(const DbSrc &src) {
+    return src.A.w >= 128 && src.A.w % 2 == 0 && src.A.ws * 2 == src.A.w && src.A.h >= 1 && src.A.hs >= 1;
+}
+
+struct XsWin {
+    const double *fa, *fp, *ca, *cp;   // A and the segment's A' image, fine and coarse
+    long g0;                           // global row of the segment's first pixel (y0, x0)
+    int y0, x0, nst;
+};
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ XsWin xs_window(const XArgs &a, long seg) {
+    const DbSrc &src = a.src;
+    XsWin w;
+    w.g0 = a.row0 + seg_lrow(a.smap, seg, a.seg_rows, 0);
+    int img;
+    row_pos(w.g0, src.hw, src.A.w, img, w.y0, w.x0);
+    w.nst = a.seg_rows >> 7;
+    w.fa = src.A.lg;
+    w.ca = src.A.sm;
+    w.fp = src.Ap.lg + (long)img * src.hw;
+    w.cp = src.Ap.sm + (long)img * src.hws;
+    return w;
+}
+// window bases of pixel (y, x) (fine, coarse); its feature k sits at base + xs_koff(k)
+__device__ __forceinline__ int xs_fbase(const XsWin &w, int y, int x) { return (y - w.y0 + 2) * XS_FW + (x - w.x0 + 4); }
+__device__ __forceinline__ int xs_cbase(const XsWin &w, int y, int x) {
+    return ((y >> 1) - (w.y0 >> 1) + 1) * XS_CW + ((x >> 1) - (w.x0 >> 1) + 2);
+}
+__host__ __device__ constexpr bool xs_coarse(int k) { return k < 9 || (k >= 34 && k < 43); }
+__host__ __device__ constexpr int xs_koff(int k) {
+    return k < 9 ? XS_CA + (k / 3 - 1) * XS_CW + (k % 3 - 1)
+         : k < 34 ? XS_FA + ((k - 9) / 5 - 2) * XS_FW + ((k - 9) % 5 - 2)
+         : k < 43 ? XS_CP + ((k - 34) / 3 - 1) * XS_CW + ((k - 34) % 3 - 1)
+         : XS_FP + ((k - 43) / 5 - 2) * XS_FW + ((k - 43) % 5 - 2);
+}
+
+// thread t = 64 r + lane of DMA wave r (waves 0, 2, 3: wave 1 computes the coherence pick
+// meanwhile) copies pieces p = 192 j + t to byte 16 p of win: the source row of
+// window row r (reflected; rows no pixel of a shorter segment reads are clamped to one that
+// exists) and the piece's first column C (clamped for the copy; edge pieces also load their
+// two reflected values into fx for xs_fix)
+struct XsFix {
+    double v[XS_DMA][2];
+    unsigned mask;
+};
+__device__ __forceinline__ void xs_dma(const XsWin &w, const ImgPair &A, char *win, int dr, int lane, XsFix &fx) {
+    asm volatile("" : "+v"(lane));   // the piece addresses are computed here, not hoisted
+    constexpr int FP = XS_FW / 2, CP = XS_CW / 2;   // pieces per window row
+    fx.mask = 0;
+#pragma unroll
+    for (int j = 0; j < XS_DMA; ++j) {
+        int p = 192 * j + 64 * dr + lane;
+        const double *img = w.fa;
+        int iw = A.w, sr = 0, C = 0;
+        if (p < 8 * FP) {
+            const int r = p / FP;
+            sr = symi2(min(w.y0 - 2 + r, w.y0 + w.nst + 1), A.h);
+            C = w.x0 - 4 + 2 * (p - r * FP);
+        } else if ((p -= 8 * FP) < 6 * FP) {
+            const int r = p / FP;
+            img = w.fp;
+            sr = symi2(min(w.y0 - 2 + r, w.y0 + w.nst - 1), A.h);
+            C = w.x0 - 4 + 2 * (p - r * FP);
+        } else if ((p -= 6 * FP) < 8 * CP) {
+            const int r = p / CP;
+            img = r < 4 ? w.ca : w.cp;
+            iw = A.ws;
+            sr = symi2(min((w.y0 >> 1) - 1 + (r & 3), ((w.y0 + w.nst - 1) >> 1) + 1), A.hs);
+            C = (w.x0 >> 1) - 2 + 2 * (p - r * CP);
+        }
+        const double *row = img + (long)sr * iw;
+        __builtin_amdgcn_global_load_lds((const void *)(row + clampi(C, 0, iw - 2)),
+                                         (void *)(win + (192 * j + 64 * dr) * 16), 16, 0, 0);
+        if (C < 0 || C + 1 >= iw) {
+            fx.mask |= 1u << j;
+            fx.v[j][0] = row[symi2(clampi(C, -2, iw + 1), iw)];
+            fx.v[j][1] = row[symi2(clampi(C + 1, -2, iw + 1), iw)];
+        }
+    }
+}
+// after this thread's copies landed: its edge pieces get their reflected values
+__device__ __forceinline__ void xs_fix(const XsFix &fx, char *win, int t) {
+#pragma unroll
+    for (int j = 0; j < XS_DMA; ++j)
+        if (fx.mask & (1u << j)) {
+            double *d = reinterpret_cast<double *>(win + (192 * j + t) * 16);
+            d[0] = fx.v[j][0];
+            d[1] = fx.v[j][1];
+        }
+}
+template <int K0, int K1, typename F>
+__device__ __forceinline__ void xs_for(F &&f) {
+    if constexpr (K0 < K1) {
+        f(std::integral_constant<int, K0>{});
+        xs_for<K0 + 1, K1>(f);
+    }
+}
+// row_dist2 of two pixels (window bases f*, c*) from the windows: numpy's pairwise order,
+// the query from LDS; groups of 11 features in flight (z carried through asm: every load
+// of a group follows the previous group's)
+__device__ __forceinline__ void xs_dist2(const double *win, int f0, int c0, int f1, int c1, const double *qs,
+                                         double &d0, double &d1) {
+    Pw55 a, b;
+    // the bases pass through asm (integers: the LDS address space stays known), so no
+    // address is hoisted out of the caller's loop
+    asm volatile("" : "+v"(f0), "+v"(c0), "+v"(f1), "+v"(c1));
+    xs_for<0, IA_D>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int o = xs_koff(k);
+        const int b0 = xs_coarse(k) ? c0 : f0, b1 = xs_coarse(k) ? c1 : f1;
+        const double q = qs[k];
+        const double x0 = win[b0 + o] - q, x1 = win[b1 + o] - q;
+        a.feed(k, x0 * x0);
+        b.feed(k, x1 * x1);
+    });
+    d0 = a.res;
+    d1 = b.res;
+    // the sums are finished HERE: sunk past the caller's barrier, every loaded value would
+    // stay live across it (the next window's copies overwrite the LDS they came from)
+    asm volatile("" :: "v"(d0), "v"(d1));
+}
+
+// numpy's pairwise sum (Pw55's order) of term k held by lane k (k < 55), every lane
+__device__ __forceinline__ double pw55_lanes(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = (int)b, hi = (int)(b >> 32);
+    auto at = [&](int k) {
+        return __longlong_as_double((long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(hi, k) << 32) |
+                                                (unsigned)__builtin_amdgcn_readlane(lo, k)));
+    };
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = at(j);
+#pragma unroll
+    for (int k = 8; k < 48; k += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += at(k + j);
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int k = 48; k < IA_D; ++k) res += at(k);
+    return res;
+}
+
+template <bool BATCH>
+__global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
+    __shared__ __attribute__((aligned(16))) char sa_raw[BATCH ? sizeof(XArgs) : 16];
+    XArgs &sa = *reinterpret_cast<XArgs *>(sa_raw);
+    if constexpr (BATCH) {
+        const unsigned long long *w0 = reinterpret_cast<const unsigned long long *>(&a0);
+        unsigned long long *w1 = reinterpret_cast<unsigned long long *>(&sa);
+        for (int w = threadIdx.x; w < (int)(sizeof(XArgs) / 8); w += 256) w1[w] = w0[w];
+        __syncthreads();
+        if (threadIdx.x == 0) xjob_apply(sa, a0.jobs[blockIdx.y], a0.f.t & 1);
+        __syncthreads();
+    }
+    const XArgs &a = BATCH ? sa : a0;
+    __shared__ __attribute__((aligned(16))) char win[XS_LDS_B];
+    __shared__ unsigned clo[XW_NCOH * XS_CST], chi[XW_NCOH * XS_CST];
+    __shared__ unsigned cvw[2][64];
+    __shared__ double qs[IA_DP], wts[IA_DP];
+    __shared__ double cwt[2 * IA_DP];   // the coherence lanes' factors: 1 (distance), weights
+    __shared__ int slist[RESCORE_SEGCAP];
+    __shared__ int tk, scount;
+    __shared__ float redf[4];
+    __shared__ double bds[4];
+    __shared__ long long bis[4];
+    __shared__ CohSel cs;
+    __shared__ double csval;
+    __shared__ long long ccix[XW_NCOH];
+    __shared__ int cpos[XW_NCOH][3];
+    __shared__ unsigned nxw[4][64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const FinishArgs &f = a.f;
+    const DbSrc &src = a.src;
+    const int t = f.t, W = f.W;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
+    __syncthreads();
+    const int i = tk;
+    unsigned long long *trace =
+        (a.trace && i < XW_TRACE_PX && t < XW_TRACE_T) ? a.trace + ((long)t * XW_TRACE_PX + i) * XW_TRACE_N : nullptr;
+    auto wstamp = [&](int k) {   // lane 0 of any wave
+        if (trace && lane == 0) trace[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    if (trace && tid == 0) trace[0] = t_start;
+    xw_stamp(trace, 1);
+    if (i == 0 && tid == 0) __hip_atomic_store(&a.tickets[(t + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int y = f.y_lo + i, x = t - 3 * y;
+    const bool cur = i < a.M;
+    const bool nxt = y >= a.y_lo_n && y < a.y_lo_n + a.M_n;
+
+    // wave 0: the next query's features that do not depend on wave t (as k_xwave)
+    const float amx = a.amax[vidx(0)];
+    int pdep = 0;
+    if (wv == 0 && nxt) {
+        int rr = 0, cc = 0;
+        const double *p = feat_addr(a.B, a.Bp, y, x + 1, lane < IA_D ? lane : 0, rr, cc);
+        pdep = lane < 43 || lane >= IA_D ? 0 : (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
+        dma_f64(p, lane < IA_D && pdep == 0, nxw[0], nxw[1]);
+        dma_f64(a.center + (lane < IA_D ? lane : 0), lane < IA_D, nxw[2], nxw[3]);
+    }
+
+    double own = 0.0;
+    if (cur) {
+        // ---- 1. one round trip: query, weights, norm, bound, segment minima, coherence s / im
+        double qsv = 0.0, wk = 0.0;
+        if (tid < IA_DP) {
+            qsv = a.q64[(long)i * IA_DP + tid];
+            wk = tid < IA_D ? f.weights[tid] : 0.0;
+        }
+        const double nqq = a.nq[vidx(i)];
+        const float am = amx;
+        const long n4 = a.nseg / 4;
+        const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
+        float4 v[RESCORE_REG];
+        segmin_load(sq4, n4, v);
+        const int rr0 = y - 2 + lane / 5, rc0 = x - 2 + lane % 5;
+        const bool cpos_ok = wv == 1 && lane < XW_NCOH && rr0 >= 0 && rc0 >= 0 && rc0 < W &&
+                             (rr0 < y || rc0 < x);
+        int s_r = 0, s_c = 0, s_i = 0;
+        if (cpos_ok) {
+            const long sidx = (long)rr0 * W + rc0;
+            s_r = f.s[2 * sidx];
+            s_c = f.s[2 * sidx + 1];
+            s_i = f.im[sidx];
+        }
+        if (tid == 0) scount = 0;
+        const float ewv = segmin_wave_min(sq4, n4, v);
+        if (lane == 0) redf[wv] = ewv;
+        if (tid < IA_DP) {
+            qs[tid] = qsv;
+            wts[tid] = wk;
+            cwt[tid] = 1.0;
+            cwt[IA_DP + tid] = wk;
+        }
+        // ---- wave 1: the coherence candidates (best_coherence_match, algorithms.py:92-130:
+        // p_r = s(r) + q - r inside A') and their features requested by LDS DMA now, computed
+        // while the first window is in flight: EXACTLY 2 + 2 XW_NCOH copies per lane
+        if (wv == 1) {
+            // candidate c = lane c's (row, col, image): broadcast by readlane, not through LDS
+            int sr = 0, sc = 0, si = 0;
+            bool ok = false;
+            if (lane < XW_NCOH) {
+                sr = s_r + y - rr0;
+                sc = s_c + x - rc0;
+                ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
+                sr = ok ? sr : 0;
+                sc = ok ? sc : 0;
+                si = ok ? s_i : 0;
+                ccix[lane] = ok ? ((long)src.A.h * si + sr) * src.A.w + sc : -1;
+                cpos[lane][0] = sr; cpos[lane][1] = sc; cpos[lane][2] = si;
+            }
+            dma_f64(src.Ap.lg + ((long)src.A.h * si + sr) * src.A.w + sc, true, cvw[0], cvw[1]);
+            // lane k's feature (emit_feature's order): offsets, image and plane, once
+            const int k = lane < IA_D ? lane : 0;
+            const bool yk = k >= 34;
+            const int kk = yk ? k - 34 : k;
+            const bool co = kk < 9;
+            const int t = co ? kk : kk - 9;
+            const int dy = co ? t / 3 - 1 : t / 5 - 2, dx = co ? t % 3 - 1 : t % 5 - 2;
+            const int ih = co ? src.A.hs : src.A.h, iw = co ? src.A.ws : src.A.w;
+            const double *ib = yk ? (co ? src.Ap.sm : src.Ap.lg) : (co ? src.A.sm : src.A.lg);
+            const long istr = yk ? (co ? src.hws : src.hw) : 0;
+#pragma unroll 1
+            for (int c = 0; c < XW_NCOH; ++c) {
+                const int r = __builtin_amdgcn_readlane(sr, c), cc = __builtin_amdgcn_readlane(sc, c);
+                const int im = __builtin_amdgcn_readlane(si, c);
+                const int rr = symi2((co ? (r >> 1) : r) + dy, ih), c2 = symi2((co ? (cc >> 1) : cc) + dx, iw);
+                dma_f64(ib + im * istr + (long)rr * iw + c2, true, clo + c * XS_CST, chi + c * XS_CST);
+            }
+            wstamp(13);
+        }
+        __syncthreads();
+        const float emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
+        xw_stamp(trace, 2);
+        double Tseg, Trow;
+        bool force_full;
+        rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+        segmin_select(sq4, n4, v, Tseg, slist, &scount);
+        __syncthreads();
+        xw_stamp(trace, 3);
+        const int ns = scount;
+        const bool full = ns > RESCORE_SEGCAP || force_full;
+        const long nscan = full ? a.nseg : ns;
+
+        // wave 1: the coherence pick from its copies (lanes c < 15: candidate c's distance,
+        // lanes 32 + c: its weighted distance; (v - q) * 1 == v - q exactly)
+        auto coherence = [&]() {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the gathers landed
+            wave_lds_sync();
+            const int c = (lane & 31) < XW_NCOH ? (lane & 31) : XW_NCOH - 1;
+            const bool wl = lane >= 32;
+            // groups of 11 features in flight (as xs_dist2); the factor from a table, not a
+            // per-lane select (which spilled)
+            int co = c * XS_CST, qo = 0, wo = wl ? IA_DP : 0;
+            asm volatile("" : "+v"(co), "+v"(qo), "+v"(wo));
+            Pw55 pw;
+#pragma unroll
+            for (int k = 0; k < IA_D; ++k) {
+                const double v = __longlong_as_double((long long)(((unsigned long long)chi[co + k] << 32) | clo[co + k]));
+                const double xx = (v - qs[qo + k]) * cwt[wo + k];
+                pw.feed(k, xx * xx);
+                if (k % 11 == 10) asm volatile("" : "+v"(co), "+v"(qo), "+v"(wo) : "v"(xx));
+            }
+            const double r = sqrt(pw.res);
+            asm volatile("" :: "v"(r));   // computed here, not sunk past the caller's barrier
+            const bool valid = (lane & 31) < XW_NCOH && ccix[c] >= 0;
+            double bd = valid && !wl ? r : INFINITY;
+            long long bl = valid && !wl ? c : LLONG_MAX;
+            const double cwd = r * r;
+            for (int o = 32; o > 0; o >>= 1) {
+                const double od = __shfl_xor(bd, o);
+                const long long ol = __shfl_xor(bl, o);
+                fin_best(bd, bl, od, ol);
+            }
+            const int wn = bl == LLONG_MAX ? 0 : (int)bl;
+            const double wd = __shfl(cwd, 32 + wn);
+            const double wval = lds_f64(cvw[0], cvw[1], wn);
+            wstamp(15);
+            if (lane == 0) {
+                cs = bl == LLONG_MAX ? CohSel{0, 0, 0, 0, 0, 0, 0, 0.0}
+                                     : CohSel{ccix[wn], cpos[wn][0], cpos[wn][1], cpos[wn][2],
+                                              y - 2 + wn / 5, x - 2 + wn % 5, 1, wd};
+                csval = wval;
+            }
+        };
+
+        // ---- 2. every row of the candidate segments, rescored in fp64 from the windows
+        double bd = INFINITY;
+        long long bi = LLONG_MAX;
+        XsWin w{};
+        const int Aw = src.A.w;
+        // the first segment's windows are requested before wave 1 computes the coherence
+        // pick (its gathers landed meanwhile)
+        XsFix fx;
+        const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
+        if (nscan > 0) w = xs_window(a, full ? 0 : slist[0]);
+        if (wv == 1) coherence();
+        else if (nscan > 0) xs_dma(w, src.A, win, dr, lane, fx);
+        for (long si = 0; si < nscan; ++si) {
+            if (si > 0) {
+                __syncthreads();   // every row of the last segment is read before the copies
+                w = xs_window(a, full ? si : slist[si]);
+                if (wv != 1) xs_dma(w, src.A, win, dr, lane, fx);
+            }
+            if (wv != 1) {
+                win_dma_wait();
+                xs_fix(fx, win, 64 * dr + lane);
+            }
+            __syncthreads();   // the windows are complete
+            if (si == 0) {
+                xw_stamp(trace, 4);
+                if (wv == 0) wstamp(11);
+            }
+            // rows k = tid, tid + 256 of the segment (k & (seg_rows - 1): the rows past a
+            // shorter segment recompute a real row and are not taken)
+            const int k0 = tid & (a.seg_rows - 1), k1 = (tid + 256) & (a.seg_rows - 1);
+            const int y0 = w.y0 + (k0 >> 7), x0 = w.x0 + (k0 & 127);
+            const int y1 = w.y0 + (k1 >> 7), x1 = w.x0 + (k1 & 127);
+            double d0, d1;
+            xs_dist2(reinterpret_cast<const double *>(win), xs_fbase(w, y0, x0), xs_cbase(w, y0, x0),
+                     xs_fbase(w, y1, x1), xs_cbase(w, y1, x1), qs, d0, d1);
+            if (tid < a.seg_rows) fin_best(bd, bi, d0, w.g0 + (long)(k0 >> 7) * Aw + (k0 & 127));
+            if (tid + 256 < a.seg_rows) fin_best(bd, bi, d1, w.g0 + (long)(k1 >> 7) * Aw + (k1 & 127));
+            if (si == 0 && wv == 0) wstamp(12);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o);
+            const long long oi = __shfl_xor(bi, o);
+            fin_best(bd, bi, od, oi);
+        }
+        if (lane == 0) { bds[wv] = bd; bis[wv] = bi; }
+        __syncthreads();   // the block's winner; the coherence pick is in cs
+        xw_stamp(trace, 5);
+        if (wv != 0) return;
+
+        // ---- 3. the winner's weighted distance (algorithms.py:133-135) and A' value: from
+        // the windows when it is a row of the last segment (always with one candidate
+        // segment), else gathered (row_rec)
+        XRec lb{INFINITY, LLONG_MAX, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xrec_take(lb, XRec{bds[k], bis[k], 0.0, 0.0});
+        const long rel = lb.i - w.g0;
+        const long ry = rel >= 0 ? rel / Aw : -1, rx = rel - ry * Aw;
+        if (nscan > 0 && rel >= 0 && ry < w.nst && rx < 128) {
+            const int py = w.y0 + (int)ry, px = w.x0 + (int)rx;
+            const int fb = xs_fbase(w, py, px), cb = xs_cbase(w, py, px);
+            const double *wdb = reinterpret_cast<const double *>(win);
+            double sq = 0.0;
+            if (lane < IA_D) {
+                const double xw = (wdb[(xs_coarse(lane) ? cb : fb) + xs_koff(lane)] - qs[lane]) * wts[lane];
+                sq = xw * xw;
+            }
+            const double s = sqrt(pw55_lanes(sq));
+            lb.wd = s * s;
+            lb.val = wdb[XS_FP + fb];
+        } else if (lb.i != LLONG_MAX) {
+            // a winner from an earlier window: its samples gathered (lane k: feature k)
+            ImgPair ap;
+            int r, c;
+            src.locate(lb.i, ap, r, c);
+            int rr, cc;
+            const double *fp = feat_addr(src.A, ap, r, c, lane < IA_D ? lane : 0, rr, cc);
+            double sq = 0.0;
+            if (lane < IA_D) {
+                const double xw = (*fp - qs[lane]) * wts[lane];
+                sq = xw * xw;
+            }
+            const double s = sqrt(pw55_lanes(sq));
+            lb.wd = s * s;
+            lb.val = src.Ap.lg[lb.i];
+        }
+        xw_stamp(trace, 6);
+        own = xw_finish(a, i, y, x, lane, lb, cs, csval, (unsigned int)(nscan * a.seg_rows), ns, full, trace);
+    }
+    xw_stamp(trace, 8);
+    if (wv != 0 || !nxt) return;
+    xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace);
+}
+
+int launch_xwave(const XArgs &a, int nblocks, int form, hipStream_t st, int njobs) {
     if (nblocks <= 0) return IA_OK;
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || a.jobs), "launch_xwave: bad batch");
+    IA_ARG(form != XW_STRIP || (a.smap.W > 0 && xstrip_applies(a.src) && a.seg_rows >= 128 && a.seg_rows <= 512),
+           "launch_xwave: the strip form needs a strip-order image-form level");
     const dim3 grid((unsigned)nblocks, (unsigned)njobs);
-    if (njobs > 1) {
-        if (img) k_xwave<true, true><<<grid, 256, 0, st>>>(a);
-        else k_xwave<false, true><<<grid, 256, 0, st>>>(a);
+    const bool b = njobs > 1;
+    if (form == XW_STRIP) {
+        if (b) k_xstrip<true><<<grid, 256, 0, st>>>(a);
+        else k_xstrip<false><<<grid, 256, 0, st>>>(a);
+    } else if (form == XW_IMG) {
+        if (b) k_xwave<true, true><<<grid, 256, 0, st>>>(a);
+        else k_xwave<true, false><<<grid, 256, 0, st>>>(a);
     } else {
-        if (img) k_xwave<true, false><<<grid, 256, 0, st>>>(a);
+        if (b) k_xwave<false, true><<<grid, 256, 0, st>>>(a);
         else k_xwave<false, false><<<grid, 256, 0, st>>>(a);
     }
     IA_LAUNCH_CHECK("k_xwave");

@@ -55,9 +55,10 @@ int ia_diag_set_pyr_form(int stream, int oh);
  * returns the previous value */
 int ia_diag_set_graph_mode(int mode);
 /* the fused per-wave kernel (k_xwave: exact stage, device-side exchange, per-pixel tail and
- * the next wave's query rows in one launch) for this process: 1 [default, IA_XWAVE] wherever
- * it applies, 0 the separate kernels (k_query_wave, k_rescore / work list, k_peer_finish);
- * other values leave it; returns the previous value */
+ * the next wave's query rows in one launch) for this process: 2 [default, IA_XWAVE] wherever
+ * it applies, with its strip form k_xstrip (fp64 windows) on strip-order image-form levels;
+ * 1 k_xwave only; 0 the separate kernels (k_query_wave, k_rescore / work list,
+ * k_peer_finish); other values leave it; returns the previous value */
 int ia_diag_set_xwave(int on);
 /* with IA_XW_TRACE=<level tag>: the fused kernel's phase stamps of that level (100 MHz
  * s_memrealtime) for waves < 4096 and the first 8 pixels of each, 12 stamps per pixel:

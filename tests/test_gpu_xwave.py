@@ -51,17 +51,64 @@ def test_fused_and_separate_kernels_match_oracle(gpu, xw):
         _ia.xwave(prev)
 
 
-def test_fused_kernel_image_form_level(gpu):
-    """A finest level whose DB runs in its image form (width 256: the fused kernel's exact
-    stage re-screens windows copied into LDS by DMA), flat regions for exact ties."""
+@pytest.mark.parametrize('xw', [2, 1])
+def test_fused_kernel_image_form_level(gpu, xw):
+    """A finest level whose DB runs in its image form (width 256), flat regions for exact
+    ties (many candidate segments per query): the strip form k_xstrip (xw 2: every row of
+    the candidate segments rescored in fp64 from LDS windows, 128-row segments) and k_xwave
+    (xw 1: fp32 re-screen of DMA'd split windows), both bit-exact vs the oracle."""
+    import _ia
     import image_analogies as ia
     (A_pyr, Ap_list, B_pyr, Bp_pyr, L, w), ref = oracle_case(62, (256, 256), (40, 52), 1, 0.5,
                                                              flat=True, cap=3)
     assert A_pyr[-1].shape == (256, 256)       # the finest level's DB is 65,536 rows wide 256
+    prev = _ia.xwave(xw)
+    try:
+        Bp_dev = [dev(b) for b in Bp_pyr]
+        out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                                [dev(p) for p in B_pyr], Bp_dev, L, 0.5, w)
+        assert_equal_oracle(out, Bp_dev, ref)
+    finally:
+        _ia.xwave(prev)
+
+
+def test_strip_kernel_512_two_images_matches_oracle(gpu):
+    """k_xstrip on 512-row segments (4 scanlines of a 128-pixel strip: A 512 x 512, two A'
+    images, 524,288 rows) and 256-row segments (the 256 x 256 level): the reflected LDS
+    windows at the images' four edges, segments in both A' images, vs the oracle."""
+    import image_analogies as ia
+    (A_pyr, Ap_list, B_pyr, Bp_pyr, L, w), ref = oracle_case(63, (512, 512), (40, 32), 2, 2.0, cap=3)
+    assert A_pyr[-1].shape == (512, 512)
     Bp_dev = [dev(b) for b in Bp_pyr]
     out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
-                            [dev(p) for p in B_pyr], Bp_dev, L, 0.5, w)
+                            [dev(p) for p in B_pyr], Bp_dev, L, 2.0, w)
     assert_equal_oracle(out, Bp_dev, ref)
+
+
+def test_strip_kernel_equals_xwave_large(gpu):
+    """A 1024 x 1024 (1,048,576 rows, 512-row segments), B 96 x 128: B', s, im and every
+    debug record of the strip form equal k_xwave's (itself pinned to the oracle above)."""
+    import _ia
+    import image_analogies as ia
+    A, Aps, B = analogy_inputs(64, (1024, 1024), (96, 128), 1)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=64, cap=2)
+    w = o.compute_weights(3, 5, 12, 1)
+    res = {}
+    for xw in (2, 1):
+        prev = _ia.xwave(xw)
+        try:
+            Bp_dev = [dev(b) for b in Bp_pyr]
+            out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                                    [dev(p) for p in B_pyr], Bp_dev, L, 1.0, w, debug=True)
+            res[xw] = (out, Bp_dev)
+        finally:
+            _ia.xwave(prev)
+    (o2, b2), (o1, b1) = res[2], res[1]
+    for l in o1:
+        assert torch.equal(b2[l], b1[l]), l
+        assert torch.equal(o2[l][0], o1[l][0]) and torch.equal(o2[l][1], o1[l][1]), l
+        for x, y in zip(o2[l][2], o1[l][2]):
+            assert torch.equal(x, y), l
 
 
 @pytest.mark.parametrize('A_shape,B_shape,cap', [((36, 44), (30, 41), None), ((256, 256), (33, 47), 3)])
