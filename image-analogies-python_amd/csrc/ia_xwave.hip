@@ -139,6 +139,15 @@ __device__ __forceinline__ void xjob_apply(XArgs &a, const XJob &J, int b) {
     a.f.s = J.s; a.f.im = J.im; a.f.dbg_px = J.dbg_px; a.f.dbg_dist = J.dbg_dist;
 }
 
+// a workgroup barrier that orders LDS only: __syncthreads() also waits for every global load
+// the wave has in flight (its release fence), which would make a barrier wait for a wave's
+// prefetches
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // ---- the wave's tail, shared by k_xwave and k_xstrip ------------------------------------
 // phase stamp k of a traced pixel (thread 0)
 __device__ __forceinline__ void xw_stamp(unsigned long long *trace, int k) {
@@ -638,7 +647,7 @@ constexpr int XS_DBL = XS_CP + 4 * XS_CW;                    // 2448 doubles, 19
 constexpr int XS_PIECES = XS_DBL / 2;                        // 16-B pieces
 constexpr int XS_DMA = (XS_PIECES + 191) / 192;              // 7 copies per thread of waves 0, 2, 3
 constexpr int XS_LDS_B = XS_DMA * 192 * 16;                  // 21504 B (the tail: dummy copies)
-constexpr int XS_CST = 65;                                   // coherence words per candidate (banks)
+constexpr int XS_CST = 65;                                   // coherence samples per candidate (banks)
 
 bool xstrip_applies(const DbSrc &src) {
     return src.A.w >= 128 && src.A.w % 2 == 0 && src.A.ws * 2 == src.A.w && src.A.h >= 1 && src.A.hs >= 1;
@@ -762,6 +771,33 @@ __device__ __forceinline__ void xs_dist2(const double *win, int f0, int c0, int 
     asm volatile("" :: "v"(d0), "v"(d1));
 }
 
+// row_dist2 of the vertically adjacent pixels (y, x) and (y + 1, x), y - y0 even (window bases
+// fb, cb of (y, x)): the coarse samples of both are the same (y / 2 == (y + 1) / 2) and
+// pixel (y + 1)'s fine rows are pixel y's shifted by one, so the shared loads are done once
+// (65 window loads for the two rows instead of 110)
+__device__ __forceinline__ void xs_dist_pair(const double *win, int fb, int cb, const double *qs,
+                                             double &d0, double &d1) {
+    Pw55 a, b;
+    asm volatile("" : "+v"(fb), "+v"(cb));
+    xs_for<0, IA_D>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int o = xs_koff(k);
+        const double q = qs[k];
+        if constexpr (xs_coarse(k)) {
+            const double x = win[cb + o] - q;
+            a.feed(k, x * x);
+            b.feed(k, x * x);
+        } else {
+            const double x0 = win[fb + o] - q, x1 = win[fb + XS_FW + o] - q;
+            a.feed(k, x0 * x0);
+            b.feed(k, x1 * x1);
+        }
+    });
+    d0 = a.res;
+    d1 = b.res;
+    asm volatile("" :: "v"(d0), "v"(d1));   // finished here (as xs_dist2)
+}
+
 // numpy's pairwise sum (Pw55's order) of term k held by lane k (k < 55), every lane
 __device__ __forceinline__ double pw55_lanes(double v) {
     const long long b = __double_as_longlong(v);
@@ -798,8 +834,8 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     }
     const XArgs &a = BATCH ? sa : a0;
     __shared__ __attribute__((aligned(16))) char win[XS_LDS_B];
-    __shared__ unsigned clo[XW_NCOH * XS_CST], chi[XW_NCOH * XS_CST];
-    __shared__ unsigned cvw[2][64];
+    __shared__ double cxd[XW_NCOH * XS_CST];   // candidate c's samples at c * XS_CST
+    __shared__ double cval[XW_NCOH];
     __shared__ double qs[IA_DP], wts[IA_DP];
     __shared__ double cwt[2 * IA_DP];   // the coherence lanes' factors: 1 (distance), weights
     __shared__ int slist[RESCORE_SEGCAP];
@@ -868,34 +904,36 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             s_c = f.s[2 * sidx + 1];
             s_i = f.im[sidx];
         }
+        // the loads above stay in this round trip (not sunk to their first use, after the
+        // segment minima's wait: one more round trip on wave 1's path)
+        asm volatile("" ::: "memory");
         if (tid == 0) scount = 0;
         const float ewv = segmin_wave_min(sq4, n4, v);
         if (lane == 0) redf[wv] = ewv;
-        if (tid < IA_DP) {
-            qs[tid] = qsv;
-            wts[tid] = wk;
-            cwt[tid] = 1.0;
-            cwt[IA_DP + tid] = wk;
-        }
+        if (wv == 1) wstamp(14);
         // ---- wave 1: the coherence candidates (best_coherence_match, algorithms.py:92-130:
-        // p_r = s(r) + q - r inside A') and their features requested by LDS DMA now, computed
-        // while the first window is in flight: EXACTLY 2 + 2 XW_NCOH copies per lane
+        // p_r = s(r) + q - r inside A'): lane k loads sample k of each into registers now
+        // (plain loads: cheap to issue, so the e* barrier does not wait for them); they are
+        // transposed through LDS and picked after the selection, while waves 0, 2, 3 copy
+        // the first windows
+        double cv[XW_NCOH], cvl = 0.0;
         if (wv == 1) {
-            // candidate c = lane c's (row, col, image): broadcast by readlane, not through LDS
             int sr = 0, sc = 0, si = 0;
-            bool ok = false;
             if (lane < XW_NCOH) {
                 sr = s_r + y - rr0;
                 sc = s_c + x - rc0;
-                ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
+                const bool ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
                 sr = ok ? sr : 0;
                 sc = ok ? sc : 0;
                 si = ok ? s_i : 0;
-                ccix[lane] = ok ? ((long)src.A.h * si + sr) * src.A.w + sc : -1;
+                const long cix = ((long)src.A.h * si + sr) * src.A.w + sc;
+                ccix[lane] = ok ? cix : -1;
                 cpos[lane][0] = sr; cpos[lane][1] = sc; cpos[lane][2] = si;
+                cvl = src.Ap.lg[cix];   // stored to LDS after the selection (no wait here)
             }
-            dma_f64(src.Ap.lg + ((long)src.A.h * si + sr) * src.A.w + sc, true, cvw[0], cvw[1]);
-            // lane k's feature (emit_feature's order): offsets, image and plane, once
+            // lane k's feature (emit_feature's order): its plane (A / A', fine / coarse) as a
+            // base pointer, image stride, row stride and coordinate shift, and its offset from
+            // the candidate's pixel in that plane, once; per candidate a few integer ops
             const int k = lane < IA_D ? lane : 0;
             const bool yk = k >= 34;
             const int kk = yk ? k - 34 : k;
@@ -903,34 +941,47 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             const int t = co ? kk : kk - 9;
             const int dy = co ? t / 3 - 1 : t / 5 - 2, dx = co ? t % 3 - 1 : t % 5 - 2;
             const int ih = co ? src.A.hs : src.A.h, iw = co ? src.A.ws : src.A.w;
-            const double *ib = yk ? (co ? src.Ap.sm : src.Ap.lg) : (co ? src.A.sm : src.A.lg);
-            const long istr = yk ? (co ? src.hws : src.hw) : 0;
-#pragma unroll 1
+            const int sh = co ? 1 : 0;
+            const int istr = yk ? (int)(co ? src.hws : src.hw) : 0;   // < 2^31 (image sizes)
+            const double *lb0 = yk ? (co ? src.Ap.sm : src.Ap.lg) : (co ? src.A.sm : src.A.lg);
+            const int offk = dy * iw + dx;
+#pragma unroll
             for (int c = 0; c < XW_NCOH; ++c) {
                 const int r = __builtin_amdgcn_readlane(sr, c), cc = __builtin_amdgcn_readlane(sc, c);
                 const int im = __builtin_amdgcn_readlane(si, c);
-                const int rr = symi2((co ? (r >> 1) : r) + dy, ih), c2 = symi2((co ? (cc >> 1) : cc) + dx, iw);
-                dma_f64(ib + im * istr + (long)rr * iw + c2, true, clo + c * XS_CST, chi + c * XS_CST);
+                const int rs = r >> sh, cs2 = cc >> sh;
+                int off = rs * iw + cs2 + offk;
+                // fewer than 2 pixels from an edge of the fine image (uniform test): the
+                // reflected sample instead
+                if (!(r >= 2 && r + 2 < src.A.h && cc >= 2 && cc + 2 < src.A.w))
+                    off = symi2(rs + dy, ih) * iw + symi2(cs2 + dx, iw);
+                cv[c] = lb0[(long)im * istr + off];
             }
             wstamp(13);
         }
-        __syncthreads();
+        if (tid < IA_DP) {
+            qs[tid] = qsv;
+            wts[tid] = wk;
+            cwt[tid] = 1.0;
+            cwt[IA_DP + tid] = wk;
+        }
+        lds_barrier();   // not waiting for wave 1's coherence gathers
         const float emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
         xw_stamp(trace, 2);
         double Tseg, Trow;
         bool force_full;
         rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
         segmin_select(sq4, n4, v, Tseg, slist, &scount);
-        __syncthreads();
+        lds_barrier();
         xw_stamp(trace, 3);
         const int ns = scount;
         const bool full = ns > RESCORE_SEGCAP || force_full;
         const long nscan = full ? a.nseg : ns;
 
-        // wave 1: the coherence pick from its copies (lanes c < 15: candidate c's distance,
-        // lanes 32 + c: its weighted distance; (v - q) * 1 == v - q exactly)
         auto coherence = [&]() {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the gathers landed
+#pragma unroll
+            for (int c = 0; c < XW_NCOH; ++c) cxd[c * XS_CST + lane] = cv[c];
+            if (lane < XW_NCOH) cval[lane] = cvl;
             wave_lds_sync();
             const int c = (lane & 31) < XW_NCOH ? (lane & 31) : XW_NCOH - 1;
             const bool wl = lane >= 32;
@@ -941,8 +992,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             Pw55 pw;
 #pragma unroll
             for (int k = 0; k < IA_D; ++k) {
-                const double v = __longlong_as_double((long long)(((unsigned long long)chi[co + k] << 32) | clo[co + k]));
-                const double xx = (v - qs[qo + k]) * cwt[wo + k];
+                const double xx = (cxd[co + k] - qs[qo + k]) * cwt[wo + k];
                 pw.feed(k, xx * xx);
                 if (k % 11 == 10) asm volatile("" : "+v"(co), "+v"(qo), "+v"(wo) : "v"(xx));
             }
@@ -959,7 +1009,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             }
             const int wn = bl == LLONG_MAX ? 0 : (int)bl;
             const double wd = __shfl(cwd, 32 + wn);
-            const double wval = lds_f64(cvw[0], cvw[1], wn);
+            const double wval = cval[wn];
             wstamp(15);
             if (lane == 0) {
                 cs = bl == LLONG_MAX ? CohSel{0, 0, 0, 0, 0, 0, 0, 0.0}
@@ -979,8 +1029,11 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         XsFix fx;
         const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
         if (nscan > 0) w = xs_window(a, full ? 0 : slist[0]);
-        if (wv == 1) coherence();
-        else if (nscan > 0) xs_dma(w, src.A, win, dr, lane, fx);
+        if (wv == 1) {
+            coherence();
+        } else if (nscan > 0) {
+            xs_dma(w, src.A, win, dr, lane, fx);
+        }
         for (long si = 0; si < nscan; ++si) {
             if (si > 0) {
                 __syncthreads();   // every row of the last segment is read before the copies
@@ -996,16 +1049,28 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
                 xw_stamp(trace, 4);
                 if (wv == 0) wstamp(11);
             }
-            // rows k = tid, tid + 256 of the segment (k & (seg_rows - 1): the rows past a
-            // shorter segment recompute a real row and are not taken)
-            const int k0 = tid & (a.seg_rows - 1), k1 = (tid + 256) & (a.seg_rows - 1);
-            const int y0 = w.y0 + (k0 >> 7), x0 = w.x0 + (k0 & 127);
-            const int y1 = w.y0 + (k1 >> 7), x1 = w.x0 + (k1 & 127);
-            double d0, d1;
-            xs_dist2(reinterpret_cast<const double *>(win), xs_fbase(w, y0, x0), xs_cbase(w, y0, x0),
-                     xs_fbase(w, y1, x1), xs_cbase(w, y1, x1), qs, d0, d1);
-            if (tid < a.seg_rows) fin_best(bd, bi, d0, w.g0 + (long)(k0 >> 7) * Aw + (k0 & 127));
-            if (tid + 256 < a.seg_rows) fin_best(bd, bi, d1, w.g0 + (long)(k1 >> 7) * Aw + (k1 & 127));
+            const double *wdb = reinterpret_cast<const double *>(win);
+            if (w.nst == 4) {
+                // 512 rows: thread tid takes pixels (y0 + 2p, x) and (y0 + 2p + 1, x),
+                // x = x0 + (tid & 127), p = tid >> 7
+                const int px = w.x0 + (tid & 127), py = w.y0 + 2 * (tid >> 7);
+                double d0, d1;
+                xs_dist_pair(wdb, xs_fbase(w, py, px), xs_cbase(w, py, px), qs, d0, d1);
+                const long g = w.g0 + (long)(2 * (tid >> 7)) * Aw + (tid & 127);
+                fin_best(bd, bi, d0, g);
+                fin_best(bd, bi, d1, g + Aw);
+            } else {
+                // rows k = tid, tid + 256 of the segment (k & (seg_rows - 1): the rows past a
+                // shorter segment recompute a real row and are not taken)
+                const int k0 = tid & (a.seg_rows - 1), k1 = (tid + 256) & (a.seg_rows - 1);
+                const int y0 = w.y0 + (k0 >> 7), x0 = w.x0 + (k0 & 127);
+                const int y1 = w.y0 + (k1 >> 7), x1 = w.x0 + (k1 & 127);
+                double d0, d1;
+                xs_dist2(wdb, xs_fbase(w, y0, x0), xs_cbase(w, y0, x0), xs_fbase(w, y1, x1), xs_cbase(w, y1, x1),
+                         qs, d0, d1);
+                if (tid < a.seg_rows) fin_best(bd, bi, d0, w.g0 + (long)(k0 >> 7) * Aw + (k0 & 127));
+                if (tid + 256 < a.seg_rows) fin_best(bd, bi, d1, w.g0 + (long)(k1 >> 7) * Aw + (k1 & 127));
+            }
             if (si == 0 && wv == 0) wstamp(12);
         }
         for (int o = 32; o > 0; o >>= 1) {

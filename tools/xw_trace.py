@@ -62,6 +62,8 @@ def main():
     print('   candidates->w0 window landed %.2f, ->w0 re-screen done %.2f, ->w1 coherence issued %.2f, '
           'B3->w2 rescore done %.2f, B3->w1 coherence done %.2f, ->B3 %.2f, ->B4 %.2f' % (
               med(3, 11), med(3, 12), med(3, 13), med(4, 14), med(4, 15), med(3, 4), med(4, 6)))
+    print('   stamps 11-15 after the ticket (p50, us): ' + ' '.join(
+        '%d:%.2f' % (k, med(1, k)) for k in range(11, 16)))
     for cm in comm or []:
         _ia.lib().ia_comm_destroy(cm)
 
