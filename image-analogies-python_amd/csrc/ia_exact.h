@@ -231,6 +231,35 @@ __device__ __forceinline__ float segmin_wave_min(const float4 *sq4, long n4, con
     for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
     return emin;
 }
+// the same with a segment holding the wave's minimum (the lowest such index): arg
+__device__ __forceinline__ float segmin_wave_argmin(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
+                                                    long &arg) {
+    const int tid = threadIdx.x;
+    const long lim = tid < 256 ? n4 : 0;
+    float m = FLT_MAX;
+    long a = LONG_MAX;
+    auto take = [&](float x, long i) {
+        if (x < m || (x == m && i < a)) { m = x; a = i; }
+    };
+#pragma unroll
+    for (int j = 0; j < RESCORE_REG; ++j) {
+        const long i = 4 * (tid + (long)j * 256);
+        if (tid + (long)j * 256 < lim) {
+            take(v[j].x, i); take(v[j].y, i + 1); take(v[j].z, i + 2); take(v[j].w, i + 3);
+        }
+    }
+    for (long i = tid + (long)RESCORE_REG * 256; i < lim; i += 256) {
+        const float4 x = sq4[i];
+        take(x.x, 4 * i); take(x.y, 4 * i + 1); take(x.z, 4 * i + 2); take(x.w, 4 * i + 3);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float om = __shfl_xor(m, o);
+        const long oa = __shfl_xor(a, o);
+        take(om, oa);
+    }
+    arg = a;
+    return m;
+}
 __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
                                              float *redf) {
     const int tid = threadIdx.x;

@@ -841,6 +841,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ int slist[RESCORE_SEGCAP];
     __shared__ int tk, scount;
     __shared__ float redf[4];
+    __shared__ long redi[4];
     __shared__ double bds[4];
     __shared__ long long bis[4];
     __shared__ CohSel cs;
@@ -908,8 +909,9 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         // segment minima's wait: one more round trip on wave 1's path)
         asm volatile("" ::: "memory");
         if (tid == 0) scount = 0;
-        const float ewv = segmin_wave_min(sq4, n4, v);
-        if (lane == 0) redf[wv] = ewv;
+        long earg;
+        const float ewv = segmin_wave_argmin(sq4, n4, v, earg);
+        if (lane == 0) { redf[wv] = ewv; redi[wv] = earg; }
         if (wv == 1) wstamp(14);
         // ---- wave 1: the coherence candidates (best_coherence_match, algorithms.py:92-130:
         // p_r = s(r) + q - r inside A'): lane k loads sample k of each into registers now
@@ -966,8 +968,22 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             cwt[IA_DP + tid] = wk;
         }
         lds_barrier();   // not waiting for wave 1's coherence gathers
-        const float emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
+        // e* and a segment holding it (always a candidate): its windows are requested now,
+        // in flight during the selection
+        float emin = redf[0];
+        long aseg = redi[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+            if (redf[k] < emin || (redf[k] == emin && redi[k] < aseg)) { emin = redf[k]; aseg = redi[k]; }
         xw_stamp(trace, 2);
+        XsWin w{};
+        XsFix fx;
+        const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
+        const bool pre = aseg >= 0 && aseg < a.nseg;
+        if (pre) {
+            w = xs_window(a, aseg);
+            if (wv != 1) xs_dma(w, src.A, win, dr, lane, fx);
+        }
         double Tseg, Trow;
         bool force_full;
         rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
@@ -1022,22 +1038,22 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         // ---- 2. every row of the candidate segments, rescored in fp64 from the windows
         double bd = INFINITY;
         long long bi = LLONG_MAX;
-        XsWin w{};
         const int Aw = src.A.w;
         // the first segment's windows are requested before wave 1 computes the coherence
         // pick (its gathers landed meanwhile)
-        XsFix fx;
-        const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
-        if (nscan > 0) w = xs_window(a, full ? 0 : slist[0]);
-        if (wv == 1) {
-            coherence();
-        } else if (nscan > 0) {
-            xs_dma(w, src.A, win, dr, lane, fx);
-        }
-        for (long si = 0; si < nscan; ++si) {
+        if (wv == 1) coherence();
+        // the listed segments: aseg first (its windows are in flight), then the others
+        const long nit = pre ? nscan : 0;
+        long li = 0;
+        for (long si = 0; si < nit; ++si) {
             if (si > 0) {
+                long seg;
+                do {   // the next listed segment other than aseg (uniform)
+                    seg = full ? li : slist[li];
+                    ++li;
+                } while (seg == aseg);
                 __syncthreads();   // every row of the last segment is read before the copies
-                w = xs_window(a, full ? si : slist[si]);
+                w = xs_window(a, seg);
                 if (wv != 1) xs_dma(w, src.A, win, dr, lane, fx);
             }
             if (wv != 1) {
@@ -1073,6 +1089,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             }
             if (si == 0 && wv == 0) wstamp(12);
         }
+        if (pre && nit == 0 && wv != 1) win_dma_wait();   // no segment listed (never): drain
         for (int o = 32; o > 0; o >>= 1) {
             const double od = __shfl_xor(bd, o);
             const long long oi = __shfl_xor(bi, o);
@@ -1091,7 +1108,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         for (int k = 0; k < 4; ++k) xrec_take(lb, XRec{bds[k], bis[k], 0.0, 0.0});
         const long rel = lb.i - w.g0;
         const long ry = rel >= 0 ? rel / Aw : -1, rx = rel - ry * Aw;
-        if (nscan > 0 && rel >= 0 && ry < w.nst && rx < 128) {
+        if (nit > 0 && rel >= 0 && ry < w.nst && rx < 128) {
             const int py = w.y0 + (int)ry, px = w.x0 + (int)rx;
             const int fb = xs_fbase(w, py, px), cb = xs_cbase(w, py, px);
             const double *wdb = reinterpret_cast<const double *>(win);
