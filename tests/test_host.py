@@ -361,3 +361,46 @@ def test_peer_exchange_setup_falls_back_to_rccl_on_every_rank(bad, where):
             assert log[2:] == ['destroy'] + rccl(r)
         else:
             assert log == ['peer_create', 'peer_connect', 'peer_check', 'peer_stress', 'destroy'] + rccl(r)
+
+
+def _symi2(i, n):
+    i = -1 - i if i < 0 else i
+    i = 2 * n - 1 - i if i >= n else i
+    return -1 - i if i < 0 else i
+
+
+@pytest.mark.parametrize('h,w', [(8, 128), (9, 256), (64, 384), (2048, 2048)])
+def test_strip_windows_hold_every_reflected_sample(h, w):
+    """k_xstrip's LDS windows (ia_xwave.hip): for every candidate segment position (nst
+    scanlines of a 128-pixel strip, edges included) every sample of every pixel's 55
+    features sits in the window at base + fixed offset, holding the reflected image value
+    (rows reflected when filled, edge pieces rewritten with symi2 of their columns)."""
+    hs, ws = (h + 1) // 2, (w + 1) // 2
+    for nst in (1, 2, 4):
+        ys = sorted({0, nst, h - nst - (h % nst), h // 2 // nst * nst} - {-1})
+        for y0 in [y for y in ys if 0 <= y <= h - nst]:
+            for x0 in range(0, w, 128):
+                # what each window slot holds: (image row, image col) of its plane
+                def fine(r, c, nrows, clamp_row):
+                    assert 0 <= r < nrows and 0 <= c < 136
+                    R, C = y0 - 2 + r, x0 - 4 + c
+                    return _symi2(min(R, clamp_row), h), _symi2(min(max(C, -2), w + 1), w)
+
+                def coarse(r, c):
+                    assert 0 <= r < 4 and 0 <= c < 68
+                    R, C = (y0 >> 1) - 1 + r, (x0 >> 1) - 2 + c
+                    return (_symi2(min(R, ((y0 + nst - 1) >> 1) + 1), hs),
+                            _symi2(min(max(C, -2), ws + 1), ws))
+                for y in range(y0, y0 + nst):
+                    for x in range(x0, x0 + 128, 17):
+                        for dy in range(-2, 3):
+                            for dx in range(-2, 3):
+                                want = (_symi2(y + dy, h), _symi2(x + dx, w))
+                                assert fine(y - y0 + 2 + dy, x - x0 + 4 + dx, 8, y0 + nst + 1) == want
+                                if dy < 0 or (dy == 0 and dx <= 0):   # A' fine half + the pixel
+                                    assert fine(y - y0 + 2 + dy, x - x0 + 4 + dx, 6, y0 + nst - 1) == want
+                        for dy in range(-1, 2):
+                            for dx in range(-1, 2):
+                                want = (_symi2((y >> 1) + dy, hs), _symi2((x >> 1) + dx, ws))
+                                assert coarse((y >> 1) - (y0 >> 1) + 1 + dy,
+                                              (x >> 1) - (x0 >> 1) + 2 + dx) == want
