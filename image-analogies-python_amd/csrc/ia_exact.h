@@ -252,13 +252,25 @@ __device__ __forceinline__ float segmin_wave_argmin(const float4 *sq4, long n4, 
         const float4 x = sq4[i];
         take(x.x, 4 * i); take(x.y, 4 * i + 1); take(x.z, 4 * i + 2); take(x.w, 4 * i + 3);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const float om = __shfl_xor(m, o);
-        const long oa = __shfl_xor(a, o);
-        take(om, oa);
-    }
-    arg = a;
-    return m;
+    // wave minimum by DPP (row shifts, then row broadcasts: lane 63 ends with it), then the
+    // lane-local argmin of the lowest lane that holds it (any segment holding e* will do)
+    float r = m;
+#define IA_DPP_MIN(CTRL, ROWS) \
+    r = fminf(r, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(r), __float_as_int(r), CTRL, ROWS, 0xf, false)))
+    IA_DPP_MIN(0x111, 0xf);   // row_shr:1
+    IA_DPP_MIN(0x112, 0xf);   // row_shr:2
+    IA_DPP_MIN(0x114, 0xf);   // row_shr:4
+    IA_DPP_MIN(0x118, 0xf);   // row_shr:8
+    IA_DPP_MIN(0x142, 0xa);   // row_bcast:15 (rows 1, 3)
+    IA_DPP_MIN(0x143, 0xc);   // row_bcast:31 (rows 2, 3)
+#undef IA_DPP_MIN
+    const float wm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 63));
+    const unsigned long long hit = __ballot(m == wm);
+    const int src = hit ? __builtin_ctzll(hit) : 0;
+    const long long aa = (long long)a;
+    arg = (long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(aa >> 32), src) << 32) |
+                 (unsigned)__builtin_amdgcn_readlane((int)aa, src));
+    return wm;
 }
 __device__ __forceinline__ float segmin_scan(const float4 *sq4, long n4, const float4 (&v)[RESCORE_REG],
                                              float *redf) {

@@ -842,7 +842,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ int tk, scount;
     __shared__ float redf[4];
     __shared__ long redi[4];
-    __shared__ double bds[4];
+    __shared__ double bds[4], bwd[4], bvl[4];
     __shared__ long long bis[4];
     __shared__ CohSel cs;
     __shared__ double csval;
@@ -1095,47 +1095,45 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             const long long oi = __shfl_xor(bi, o);
             fin_best(bd, bi, od, oi);
         }
-        if (lane == 0) { bds[wv] = bd; bis[wv] = bi; }
+        // ---- 3. each wave's best row: its weighted distance (algorithms.py:133-135) and A'
+        // value, from the windows when it is a row of the last segment (always with one
+        // candidate segment), else gathered; the four waves in parallel, before the barrier
+        XRec wb{bd, bi, 0.0, 0.0};
+        if (bi != LLONG_MAX) {
+            const long rel = bi - w.g0;
+            const long ry = rel >= 0 ? rel / Aw : -1, rx = rel - ry * Aw;
+            double sq = 0.0;
+            if (rel >= 0 && ry < w.nst && rx < 128) {
+                const int py = w.y0 + (int)ry, px = w.x0 + (int)rx;
+                const int fb = xs_fbase(w, py, px), cb = xs_cbase(w, py, px);
+                const double *wdb = reinterpret_cast<const double *>(win);
+                if (lane < IA_D) {
+                    const double xw = (wdb[(xs_coarse(lane) ? cb : fb) + xs_koff(lane)] - qs[lane]) * wts[lane];
+                    sq = xw * xw;
+                }
+                wb.val = wdb[XS_FP + fb];
+            } else {
+                ImgPair ap;
+                int r, c;
+                src.locate(bi, ap, r, c);
+                int rr, cc;
+                const double *fp = feat_addr(src.A, ap, r, c, lane < IA_D ? lane : 0, rr, cc);
+                if (lane < IA_D) {
+                    const double xw = (*fp - qs[lane]) * wts[lane];
+                    sq = xw * xw;
+                }
+                wb.val = src.Ap.lg[bi];
+            }
+            const double sw = sqrt(pw55_lanes(sq));
+            wb.wd = sw * sw;
+        }
+        if (lane == 0) { bds[wv] = wb.d; bis[wv] = wb.i; bwd[wv] = wb.wd; bvl[wv] = wb.val; }
         __syncthreads();   // the block's winner; the coherence pick is in cs
         xw_stamp(trace, 5);
         if (wv != 0) return;
-
-        // ---- 3. the winner's weighted distance (algorithms.py:133-135) and A' value: from
-        // the windows when it is a row of the last segment (always with one candidate
-        // segment), else gathered (row_rec)
         XRec lb{INFINITY, LLONG_MAX, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) xrec_take(lb, XRec{bds[k], bis[k], 0.0, 0.0});
-        const long rel = lb.i - w.g0;
-        const long ry = rel >= 0 ? rel / Aw : -1, rx = rel - ry * Aw;
-        if (nit > 0 && rel >= 0 && ry < w.nst && rx < 128) {
-            const int py = w.y0 + (int)ry, px = w.x0 + (int)rx;
-            const int fb = xs_fbase(w, py, px), cb = xs_cbase(w, py, px);
-            const double *wdb = reinterpret_cast<const double *>(win);
-            double sq = 0.0;
-            if (lane < IA_D) {
-                const double xw = (wdb[(xs_coarse(lane) ? cb : fb) + xs_koff(lane)] - qs[lane]) * wts[lane];
-                sq = xw * xw;
-            }
-            const double s = sqrt(pw55_lanes(sq));
-            lb.wd = s * s;
-            lb.val = wdb[XS_FP + fb];
-        } else if (lb.i != LLONG_MAX) {
-            // a winner from an earlier window: its samples gathered (lane k: feature k)
-            ImgPair ap;
-            int r, c;
-            src.locate(lb.i, ap, r, c);
-            int rr, cc;
-            const double *fp = feat_addr(src.A, ap, r, c, lane < IA_D ? lane : 0, rr, cc);
-            double sq = 0.0;
-            if (lane < IA_D) {
-                const double xw = (*fp - qs[lane]) * wts[lane];
-                sq = xw * xw;
-            }
-            const double s = sqrt(pw55_lanes(sq));
-            lb.wd = s * s;
-            lb.val = src.Ap.lg[lb.i];
-        }
+        for (int k = 0; k < 4; ++k) xrec_take(lb, XRec{bds[k], bis[k], bwd[k], bvl[k]});
         xw_stamp(trace, 6);
         own = xw_finish(a, i, y, x, lane, lb, cs, csval, (unsigned int)(nscan * a.seg_rows), ns, full, trace);
     }
