@@ -210,10 +210,14 @@ __device__ __forceinline__ int vidx(int i) {
 __device__ __forceinline__ void segmin_load(const float4 *sq4, long n4, float4 (&v)[RESCORE_REG]) {
     const int tid = threadIdx.x;
     const long lim = tid < 256 ? n4 : 0;
+    // every load unconditional (a valid index past the end; the value replaced after): a
+    // load inside a divergent branch makes the join wait for it, before the caller's next
+    // loads are issued
 #pragma unroll
     for (int j = 0; j < RESCORE_REG; ++j) {
         const long i = tid + (long)j * 256;
-        v[j] = i < lim ? sq4[i] : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+        const float4 x = sq4[i < n4 ? i : 0];
+        v[j] = i < lim ? x : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
     }
 }
 // this wave's share of e* (valid in every lane), no barrier

@@ -72,12 +72,13 @@ __device__ __forceinline__ void row_pos(long g, long hw, int w, int &img, int &r
 
 // lane's double at p into the wave's LDS words lo[lane], hi[lane] by two 4-byte DMA copies
 // (global_load_lds: the gather is in flight without holding registers; the wave waits with
-// s_waitcnt vmcnt(0) before reading the words).  lo / hi must be wave-uniform.
+// s_waitcnt vmcnt(0) before reading the words).  lo / hi must be wave-uniform.  Every lane
+// copies (p must be valid in every lane; `on` only documents which words are used): a copy
+// inside a divergent branch makes the join wait for it, so each copy would cost a round trip
 __device__ __forceinline__ void dma_f64(const double *p, bool on, unsigned *lo, unsigned *hi) {
-    if (on) {
-        __builtin_amdgcn_global_load_lds((const void *)p, (void *)lo, 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const char *>(p) + 4), (void *)hi, 4, 0, 0);
-    }
+    (void)on;
+    __builtin_amdgcn_global_load_lds((const void *)p, (void *)lo, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const char *>(p) + 4), (void *)hi, 4, 0, 0);
 }
 __device__ __forceinline__ double lds_f64(const unsigned *lo, const unsigned *hi, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi[l] << 32) | lo[l]));
@@ -841,7 +842,6 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ int slist[RESCORE_SEGCAP];
     __shared__ int tk, scount;
     __shared__ float redf[4];
-    __shared__ long redi[4];
     __shared__ double bds[4], bwd[4], bvl[4];
     __shared__ long long bis[4];
     __shared__ CohSel cs;
@@ -884,11 +884,11 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     double own = 0.0;
     if (cur) {
         // ---- 1. one round trip: query, weights, norm, bound, segment minima, coherence s / im
-        double qsv = 0.0, wk = 0.0;
-        if (tid < IA_DP) {
-            qsv = a.q64[(long)i * IA_DP + tid];
-            wk = tid < IA_D ? f.weights[tid] : 0.0;
-        }
+        // (unconditional loads, as segmin_load)
+        const int qt = tid < IA_D ? tid : 0;
+        const double qsv = a.q64[(long)i * IA_DP + (tid < IA_DP ? tid : 0)];
+        const double wk0 = f.weights[qt];
+        const double wk = tid < IA_D ? wk0 : 0.0;
         const double nqq = a.nq[vidx(i)];
         const float am = amx;
         const long n4 = a.nseg / 4;
@@ -898,20 +898,16 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         const int rr0 = y - 2 + lane / 5, rc0 = x - 2 + lane % 5;
         const bool cpos_ok = wv == 1 && lane < XW_NCOH && rr0 >= 0 && rc0 >= 0 && rc0 < W &&
                              (rr0 < y || rc0 < x);
-        int s_r = 0, s_c = 0, s_i = 0;
-        if (cpos_ok) {
-            const long sidx = (long)rr0 * W + rc0;
-            s_r = f.s[2 * sidx];
-            s_c = f.s[2 * sidx + 1];
-            s_i = f.im[sidx];
-        }
+        // unconditional loads (a valid index for the other lanes): a load inside a divergent
+        // branch joins through a copy that waits for it
+        const long sidx = cpos_ok ? (long)rr0 * W + rc0 : 0;
+        const int s_r = f.s[2 * sidx], s_c = f.s[2 * sidx + 1], s_i = f.im[sidx];
         // the loads above stay in this round trip (not sunk to their first use, after the
         // segment minima's wait: one more round trip on wave 1's path)
         asm volatile("" ::: "memory");
         if (tid == 0) scount = 0;
-        long earg;
-        const float ewv = segmin_wave_argmin(sq4, n4, v, earg);
-        if (lane == 0) { redf[wv] = ewv; redi[wv] = earg; }
+        const float ewv = segmin_wave_min(sq4, n4, v);
+        if (lane == 0) redf[wv] = ewv;
         if (wv == 1) wstamp(14);
         // ---- wave 1: the coherence candidates (best_coherence_match, algorithms.py:92-130:
         // p_r = s(r) + q - r inside A'): lane k loads sample k of each into registers now
@@ -920,18 +916,16 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         // the first windows
         double cv[XW_NCOH], cvl = 0.0;
         if (wv == 1) {
-            int sr = 0, sc = 0, si = 0;
+            int sr = s_r + y - rr0, sc = s_c + x - rc0;
+            const bool ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
+            sr = ok ? sr : 0;
+            sc = ok ? sc : 0;
+            const int si = ok ? s_i : 0;
+            const long cix = ((long)src.A.h * si + sr) * src.A.w + sc;
+            cvl = src.Ap.lg[cix];   // every lane (valid index); stored to LDS after the selection
             if (lane < XW_NCOH) {
-                sr = s_r + y - rr0;
-                sc = s_c + x - rc0;
-                const bool ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
-                sr = ok ? sr : 0;
-                sc = ok ? sc : 0;
-                si = ok ? s_i : 0;
-                const long cix = ((long)src.A.h * si + sr) * src.A.w + sc;
                 ccix[lane] = ok ? cix : -1;
                 cpos[lane][0] = sr; cpos[lane][1] = sc; cpos[lane][2] = si;
-                cvl = src.Ap.lg[cix];   // stored to LDS after the selection (no wait here)
             }
             // lane k's feature (emit_feature's order): its plane (A / A', fine / coarse) as a
             // base pointer, image stride, row stride and coordinate shift, and its offset from
@@ -968,22 +962,8 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             cwt[IA_DP + tid] = wk;
         }
         lds_barrier();   // not waiting for wave 1's coherence gathers
-        // e* and a segment holding it (always a candidate): its windows are requested now,
-        // in flight during the selection
-        float emin = redf[0];
-        long aseg = redi[0];
-#pragma unroll
-        for (int k = 1; k < 4; ++k)
-            if (redf[k] < emin || (redf[k] == emin && redi[k] < aseg)) { emin = redf[k]; aseg = redi[k]; }
+        const float emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
         xw_stamp(trace, 2);
-        XsWin w{};
-        XsFix fx;
-        const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
-        const bool pre = aseg >= 0 && aseg < a.nseg;
-        if (pre) {
-            w = xs_window(a, aseg);
-            if (wv != 1) xs_dma(w, src.A, win, dr, lane, fx);
-        }
         double Tseg, Trow;
         bool force_full;
         rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
@@ -1041,19 +1021,19 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         const int Aw = src.A.w;
         // the first segment's windows are requested before wave 1 computes the coherence
         // pick (its gathers landed meanwhile)
+        // the first listed segment's windows are requested while wave 1 picks the coherence
+        // candidate
+        XsWin w{};
+        XsFix fx;
+        const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
+        const long nit = nscan;
+        if (nit > 0) w = xs_window(a, full ? 0 : slist[0]);
         if (wv == 1) coherence();
-        // the listed segments: aseg first (its windows are in flight), then the others
-        const long nit = pre ? nscan : 0;
-        long li = 0;
+        else if (nit > 0) xs_dma(w, src.A, win, dr, lane, fx);
         for (long si = 0; si < nit; ++si) {
             if (si > 0) {
-                long seg;
-                do {   // the next listed segment other than aseg (uniform)
-                    seg = full ? li : slist[li];
-                    ++li;
-                } while (seg == aseg);
                 __syncthreads();   // every row of the last segment is read before the copies
-                w = xs_window(a, seg);
+                w = xs_window(a, full ? si : slist[si]);
                 if (wv != 1) xs_dma(w, src.A, win, dr, lane, fx);
             }
             if (wv != 1) {
@@ -1089,7 +1069,6 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             }
             if (si == 0 && wv == 0) wstamp(12);
         }
-        if (pre && nit == 0 && wv != 1) win_dma_wait();   // no segment listed (never): drain
         for (int o = 32; o > 0; o >>= 1) {
             const double od = __shfl_xor(bd, o);
             const long long oi = __shfl_xor(bi, o);
