@@ -936,10 +936,18 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             const bool co = kk < 9;
             const int t = co ? kk : kk - 9;
             const int dy = co ? t / 3 - 1 : t / 5 - 2, dx = co ? t % 3 - 1 : t % 5 - 2;
-            const int ih = co ? src.A.hs : src.A.h, iw = co ? src.A.ws : src.A.w;
+            // the fields as VALUES first (through asm): a per-lane select between struct
+            // fields became a per-lane address into the kernel arguments, i.e. a vector load
+            // and one more round trip
+            int Ah = src.A.h, Ahs = src.A.hs, Aw2 = src.A.w, Aws = src.A.ws;
+            int hw = (int)src.hw, hws = (int)src.hws;   // < 2^31 (image sizes)
+            const double *pAl = src.A.lg, *pAs = src.A.sm, *pPl = src.Ap.lg, *pPs = src.Ap.sm;
+            asm volatile("" : "+v"(Ah), "+v"(Ahs), "+v"(Aw2), "+v"(Aws), "+v"(hw), "+v"(hws));
+            asm volatile("" : "+v"(pAl), "+v"(pAs), "+v"(pPl), "+v"(pPs));
+            const int ih = co ? Ahs : Ah, iw = co ? Aws : Aw2;
             const int sh = co ? 1 : 0;
-            const int istr = yk ? (int)(co ? src.hws : src.hw) : 0;   // < 2^31 (image sizes)
-            const double *lb0 = yk ? (co ? src.Ap.sm : src.Ap.lg) : (co ? src.A.sm : src.A.lg);
+            const int istr = yk ? (co ? hws : hw) : 0;
+            const double *lb0 = yk ? (co ? pPs : pPl) : (co ? pAs : pAl);
             const int offk = dy * iw + dx;
 #pragma unroll
             for (int c = 0; c < XW_NCOH; ++c) {
