@@ -959,7 +959,10 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
                 // reflected sample instead
                 if (!(r >= 2 && r + 2 < src.A.h && cc >= 2 && cc + 2 < src.A.w))
                     off = symi2(rs + dy, ih) * iw + symi2(cs2 + dx, iw);
-                cv[c] = lb0[(long)im * istr + off];
+                // a global load (the laundered pointer lost its address space: a flat load
+                // would also count in lgkmcnt, so every LDS wait would wait for it)
+                typedef const __attribute__((address_space(1))) double gdouble;
+                cv[c] = *(gdouble *)(lb0 + ((long)im * istr + off));
             }
             wstamp(13);
         }
