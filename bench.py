@@ -119,6 +119,7 @@ class Job:
 
     def __init__(self, conf, seed, dev, lsh=None):
         A, Ap, B = make_inputs(conf, seed)
+        self.seed = seed
         self.lsh = lsh
         self.A, self.Ap, self.B = (torch.as_tensor(x).to(dev) for x in (A, Ap, B))
         self.k, self.levels = conf['k'], conf['levels']
@@ -136,7 +137,7 @@ class Job:
         self.pixels = sum(s[0] * s[1] for s in shapes[1:self.max_levels])
         self.waves = sum(_ia.waves(*s) for s in shapes[1:self.max_levels])
 
-    def step(self, comm=None, rank=0, nranks=1, prof=False, eager=False):
+    def step(self, comm=None, rank=0, nranks=1, prof=False, eager=False, check=True):
         A_pyr = ip.gaussian_pyramid_dev(self.A, cfg.n_sm, self.levels)
         Ap_pyr = ip.gaussian_pyramid_dev(self.Ap, cfg.n_sm, self.levels)
         B_pyr = ip.gaussian_pyramid_dev(self.B, cfg.n_sm, self.levels)
@@ -145,7 +146,7 @@ class Job:
             dst.copy_(src)
         return ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, self.Bp, self.max_levels, self.k,
                                  self.weights, comm=comm, rank=rank, nranks=nranks, prof=prof,
-                                 lsh=self.lsh, eager=eager)
+                                 lsh=self.lsh, eager=eager, check=check)
 
     def prepare(self):
         """Pyramids and the B' reset of one step (the batch path's per-job part)."""
@@ -493,19 +494,28 @@ def main():
             main.wait_stream(st)
         return [r for part in res for r in part]
 
-    def run_batches(prof=False):
+    def run_batches(prof=False, check=True):
         outs = []
         for b0 in range(0, len(jobs), batch):
             part = jobs[b0:b0 + batch]
             ins = [jb.prepare() for jb in part]
             outs += ia.synthesize_batch_dev(ins, part[0].max_levels, [jb.k for jb in part],
-                                            part[0].weights, prof=prof)
+                                            part[0].weights, prof=prof, check=check)
         return outs
 
     def run_step(prof=False):
+        # no per-step ia_synth_status (a host sync per step): every level folds its error
+        # word into the device's sticky word, checked once after each timed pass
         if batch > 1:
-            return run_batches(prof)
-        run_jobs(lambda jb: jb.step(comm, rank, world, prof))
+            return run_batches(prof, check=False)
+        run_jobs(lambda jb: jb.step(comm, rank, world, prof, check=False))
+
+    def pass_status():
+        """After a pass: raise ScheduleFault (a neighbour-decision wait timed out, a fault of
+        the fused kernel) or ExchangeTimeout (another rank's records never came)."""
+        _ia.sched_status()
+        for cm in comm or []:
+            _ia.exchange_status(cm)
 
     def timed_pass(prof):
         """K steps between two barrier + synchronize brackets; prof: HIP events around
@@ -531,20 +541,24 @@ def main():
         for _ in range(args.warmup):
             run_step(True)
         _ia.prof_end()
+        pass_status()
         # `value`: the product path alone; then the same K steps with the HIP events of the
         # roofline (their cost is reported as events_overhead)
         plain, _ = timed_pass(False)
+        pass_status()
         evented, prof = timed_pass(True)
+        pass_status()
         return plain, evented, prof
 
     exchange_fallback = None
     try:
         elapsed, elapsed_ev, prof = measure()
-    except RuntimeError as e:
-        # a wait inside the device schedule timed out (synthesize_dev raises through
-        # ia_synth_status): with the device-side exchange, every rank agrees, takes the RCCL
-        # exchange and measures again from scratch (every step rebuilds pyramids, DBs, B')
-        if not (comm and _ia.exchange_kind() == 'peer' and 'timed out' in str(e)) or args.strict_exchange:
+    except _ia.ExchangeTimeout as e:
+        # another rank's records never came over the device-side exchange: every rank
+        # agrees, takes the RCCL exchange and measures again from scratch (every step
+        # rebuilds pyramids, DBs, B').  A ScheduleFault (a neighbour-decision wait inside
+        # the fused kernel) is a bug of the kernel, not of the exchange: it propagates.
+        if not (comm and _ia.exchange_kind() == 'peer') or args.strict_exchange:
             raise
         exchange_fallback = 'device-side exchange wait timed out: %s' % e
     if comm and exchange_fallback is None and _ia.exchange_kind() == 'peer':
@@ -563,6 +577,7 @@ def main():
         elapsed, elapsed_ev, prof = measure()
     for cm in comm or []:
         _ia.exchange_status(cm)     # raises if a device-side exchange wait timed out
+    own_elapsed = elapsed
     t = torch.tensor([elapsed, elapsed_ev], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -571,15 +586,20 @@ def main():
     # consistency of the result (outside the timed region): B' == A'[im][s] per level and
     # identical replicas across ranks
     batch_ok = None
+
+    def job_sum(jb, out):
+        return sum(float(jb.Bp[l].sum().item()) + float(s_.double().sum().item())
+                   for l, (s_, _) in out.items())
+    job_sums = None
     if batch > 1:
         # every job of a batch equals its own one-job synthesis (same inputs, same B' init)
-        def job_sum(jb, out):
-            return sum(float(jb.Bp[l].sum().item()) + float(s_.double().sum().item())
-                       for l, (s_, _) in out.items())
         outs = run_batches()
         torch.cuda.synchronize()
         bsums = [job_sum(jb, o) for jb, o in zip(jobs, outs)]
         batch_ok = all(b == job_sum(jb, jb.step()) for b, jb in zip(bsums, jobs))
+        job_sums = {str(jb.seed): b for jb, b in zip(jobs, bsums)}
+    elif args.config == 'c5':
+        job_sums = {str(jb.seed): job_sum(jb, jb.step()) for jb in jobs}
     out = jobs[0].step(comm, rank, world)
     chk = 0.0
     consistent = True
@@ -591,10 +611,6 @@ def main():
     ct = torch.tensor([chk], dtype=torch.float64)
     concurrent_ok = None
     if pool is not None:   # every job's result: concurrent streams == one stream, in order
-
-        def job_sum(jb, out):
-            return sum(float(jb.Bp[l].sum().item()) + float(s_.double().sum().item())
-                       for l, (s_, _) in out.items())
         outs = run_jobs(lambda jb: jb.step(comm, rank, world))
         torch.cuda.synchronize()
         order = [j for i in range(nstreams) for j in jobs[i::nstreams]]
@@ -613,7 +629,12 @@ def main():
     # roofline of the dominant kernel: the screen instance k_screen16<G> (G = query tiles
     # per block) with the most time over the timed steps, from the HIP events on its
     # stream around each of its launches; also the whole finest level and all levels
-    per_pair = 3 * 2 * 55      # split-f16: 3 f16 products x 2 flop x 55 features per pair
+    # 2*D = 110 algorithmic flop per (query, row) pair; the split-f16 screen
+    # issues 3 f16 products per feature (a_h q_h + a_h q_l + a_l q_h), 330 flop per pair, so
+    # its algorithmic fraction of the f16 dense peak is capped at 1/3; the
+    # MFMA pipe's utilisation is reported beside it as pipe_frac
+    per_pair = 2 * 55
+    pipe_per_pair = 3 * 2 * 55
     inst = {}
     lv = {}
     for p in prof:
@@ -644,8 +665,12 @@ def main():
             'achieved': achieved,
             'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
             'frac': achieved / F16_MFMA_PEAK_TFLOPS, 'traffic': traffic,
-            'algorithmic': '%d f16 flop per (query,row) pair; %d launches, %.4g pairs (mean M '
-                           '%.1f queries)' % (per_pair, i_n, i_pairs, i_q / max(i_n, 1)),
+            'algorithmic': '%d flop per (query,row) pair (2 x D, D = 55; SURVEY 8(d)); %d launches, '
+                           '%.4g pairs (mean M %.1f queries)' % (per_pair, i_n, i_pairs,
+                                                                 i_q / max(i_n, 1)),
+            'pipe_frac': achieved * pipe_per_pair / per_pair / F16_MFMA_PEAK_TFLOPS,
+            'pipe_note': 'f16 MFMA pipe utilisation: the split issues %d f16 flop per pair '
+                         '(3 products x 2 x 55), so frac <= pipe_frac / 3' % pipe_per_pair,
             'screen_avg_us': i_ms * 1e3 / max(i_n, 1),
             'source': 'HIP events around every launch of this kernel in the timed steps',
             'fp32_equivalent_tflops': fp32eq,
@@ -653,7 +678,9 @@ def main():
             'finest_level': {'level': fin, 'rows': f_rows, 'launches': f_n,
                              'screen_avg_us': f_ms * 1e3 / max(f_n, 1),
                              'frac': (per_pair * f_pairs / (f_ms * 1e-3) / 1e12 /
-                                      F16_MFMA_PEAK_TFLOPS) if f_ms else 0.0},
+                                      F16_MFMA_PEAK_TFLOPS) if f_ms else 0.0,
+                             'pipe_frac': (pipe_per_pair * f_pairs / (f_ms * 1e-3) / 1e12 /
+                                           F16_MFMA_PEAK_TFLOPS) if f_ms else 0.0},
             'all_levels': {'launches': screens, 'pairs': pairs,
                            'screen_avg_us': screen_ms * 1e3 / max(screens, 1),
                            'screen_ms_per_step': screen_ms / args.steps,
@@ -732,8 +759,25 @@ def main():
                    **({'concurrent_streams': nstreams, 'concurrent_identical': concurrent_ok}
                       if concurrent_ok is not None else {}),
                    **({'batch_jobs': batch, 'batch_identical': batch_ok}
-                      if batch_ok is not None else {})},
+                      if batch_ok is not None else {}),
+                   # c5: every job's checksum by its seed (1000 + 3 (rank + world j)), so that
+                   # any job can be compared with the same seed's run at another world size
+                   **({'job_sums': job_sums} if job_sums is not None and world == 1 else {})},
     }
+    if world > 1:
+        # per-rank facts, so that the first run across GPUs explains itself
+        rq = pixels_per_step * args.steps // (world if args.config == 'c5' else 1)
+        mine = {'rank': rank, 'local_rank': local, 'device': torch.cuda.get_device_name(dev),
+                'ms_per_step': own_elapsed / args.steps * 1e3,
+                'jobs': len(jobs), 'pixels_per_step': sum(jb.pixels for jb in jobs),
+                'exchanges': list(_ia.EXCHANGE_INFO),
+                'exchange_fallback': list(_ia._EXCHANGE_FALLBACK),
+                'peer_wait_us_per_pixel': sum(p['peer_wait_us'] for p in prof) / max(1, rq),
+                'neighbour_wait_us_per_pixel': sum(p['neighbour_wait_us'] for p in prof) / max(1, rq),
+                'checksum': chk, **({'job_sums': job_sums} if job_sums is not None else {})}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        result['ranks'] = allr
     if lsh is not None:
         result['lsh_quality'] = jobs[0].lsh_quality()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

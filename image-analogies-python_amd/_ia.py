@@ -18,7 +18,7 @@ import numpy as np
 import torch  # noqa: F401  (must precede libia.so, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# IA_LIB_PATH: another build of the same library (A/B of build variants, tools/ab_lib.sh)
+# IA_LIB_PATH: another build of the same library (A/B of build variants, `tools/gpu.sh ablib`)
 LIB_PATH = os.environ.get('IA_LIB_PATH') or os.path.join(_HERE, 'libia.so')
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'ia.h')
 
@@ -113,6 +113,7 @@ _SIGS = {
                                               ctypes.c_int, ctypes.c_int, _dp, _dp]),
     'ia_synth_levels': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_synth_status': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
+    'ia_sched_status': (ctypes.c_int, [ctypes.c_int]),
     'ia_synth_levels_batch': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, ctypes.c_int,
                                              _dp]),
     'ia_lsh_bytes': (ctypes.c_size_t, [ctypes.c_long, ctypes.c_int]),
@@ -272,9 +273,29 @@ def prof_end():
     return out
 
 
+IA_E_TIMEOUT = -5      # include/ia.h: a device-side exchange wait for another rank
+IA_E_SCHED = -6        # include/ia.h: a neighbour-decision wait inside the fused kernel
+
+
+class ExchangeTimeout(RuntimeError):
+    """Another rank's records never reached this rank's receive box (IA_E_TIMEOUT)."""
+
+
+class ScheduleFault(RuntimeError):
+    """A wait for a neighbouring pixel's decision timed out inside the fused per-wave kernel
+    (IA_E_SCHED): a fault of the device schedule itself, never an exchange problem."""
+
+
 def check(rc, what):
     if rc != 0:
-        raise RuntimeError('%s failed (%d): %s' % (what, rc, lib().ia_last_error().decode()))
+        msg = '%s failed (%d): %s' % (what, rc, lib().ia_last_error().decode())
+        raise {IA_E_TIMEOUT: ExchangeTimeout, IA_E_SCHED: ScheduleFault}.get(rc, RuntimeError)(msg)
+
+
+def sched_status(clear=True):
+    """Raise ScheduleFault if any fused level run on this device since the last clear had a
+    neighbour-decision wait time out (ia_sched_status; synchronises the device)."""
+    check(lib().ia_sched_status(1 if clear else 0), 'ia_sched_status')
 
 
 def require_device():
@@ -349,6 +370,12 @@ def _all_ok(ok, world):
     return bool(t.item())
 
 
+# what each exchange() of this process ended up as (bench.py reports it per rank at N > 1)
+EXCHANGE_INFO = []
+PEER_MEM_KINDS = {0: 'uncached device memory', 1: 'fine-grained device memory',
+                  2: 'plain device memory'}
+
+
 def exchange(rank, world, kind=None, mcap=4096):
     """One exchange object (the IaSynthArgs.comm of one sharded level) over the initialised
     torch.distributed process group: every rank calls it at the same point.  'rccl': an
@@ -372,6 +399,7 @@ def exchange(rank, world, kind=None, mcap=4096):
             dist.broadcast(uid, 0)
         check(lib().ia_comm_init(uid.numpy().tobytes(), world, rank, ctypes.byref(h)),
               'ia_comm_init')
+        EXCHANGE_INFO.append({'kind': 'rccl'})
         return h
     if world > PEER_MAX:
         _EXCHANGE_FALLBACK.append('%d ranks > the device-side exchange\'s %d' % (world, PEER_MAX))
@@ -407,7 +435,12 @@ def exchange(rank, world, kind=None, mcap=4096):
                 why = 'rank %d: %s' % (rank, lib().ia_last_error().decode())
             elif bad.value:
                 why = 'rank %d: %d of 16 x %d stress records wrong' % (rank, bad.value, min(mcap, 256))
+            stress = 'ok: 16 waves x %d records' % min(mcap, 256) if why is None else why
         if _all_ok(why is None, world):
+            EXCHANGE_INFO.append({'kind': 'peer', 'peer_mem_kind': int(lib().ia_peer_mem_kind(h)),
+                                  'peer_mem': PEER_MEM_KINDS.get(int(lib().ia_peer_mem_kind(h))),
+                                  'handshake': 'ok',
+                                  'stress': stress if world > 1 else 'skipped (1 rank)'})
             return h
     # some rank could not map or reach the others' boxes: every rank drops its peer
     # exchange and takes the RCCL one

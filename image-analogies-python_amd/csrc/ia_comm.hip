@@ -265,7 +265,7 @@ int ia_peer_status(void *comm) {
     IA_HIP(hipMemcpy(&e, c->peer->v.err, sizeof(e), hipMemcpyDeviceToHost));
     if (e) {
         set_error("peer exchange: a wait for another rank's records timed out");
-        return IA_E_COMM;
+        return IA_E_TIMEOUT;
     }
     return IA_OK;
 }

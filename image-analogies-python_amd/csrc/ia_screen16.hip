@@ -214,7 +214,7 @@ __device__ __forceinline__ void expand_groups(const char *wb, half8 *E, int lane
 // buffers, one operand buffer: 63.7 KB of LDS, 2 blocks per CU, which overlap one block's
 // expansion with the other's MFMAs).  Measured against a pipelined form (two operand
 // buffers, the next stage expanded before this one's MFMAs, one barrier per stage, 81.8 KB):
-// c4 1615-1635 vs 1650-1656 ms/step (tools/gpu_img_check.sh, profiles/r02_image_form_ab.txt).
+// c4 1615-1635 vs 1650-1656 ms/step (`tools/gpu.sh ablib`, profiles/r02_image_form_ab.txt).
 template <int G, int W>
 __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, int *smin,
                                          const StageMap &sm, long chunk, int nstage, int tps,

@@ -29,6 +29,20 @@
 
 namespace ia {
 
+// Sticky schedule-error word of this device: every level's done() folds its fused kernel's
+// error word (a neighbour-decision wait that timed out) into it on the level's stream, so
+// callers that skip the per-call ia_synth_status (bench.py's timed steps) check once at the
+// end with ia_sched_status.  Vector stores only.
+__device__ unsigned int g_sched_err;
+
+__global__ __launch_bounds__(64) void k_err_sticky(const unsigned int *__restrict__ ctl,
+                                                   const XJob *__restrict__ jt, int K) {
+    for (int k = threadIdx.x; k < K; k += 64) {
+        const unsigned int e = jt ? jt[k].ctl[2] : ctl[2];
+        if (e) g_sched_err = 1u;
+    }
+}
+
 // Sharded DB, after the cross-rank exchange: one wave per query pixel takes the
 // lexicographic (distance, row) minimum over the ranks' ShardRec (lane g = rank g), whose
 // weighted distance the owning rank already computed, and finishes the pixel with the
@@ -306,7 +320,7 @@ int comm_peer_mcap(void *comm);
 // sharded tail form (IA_SHARD_TAIL): 0 [default] the exchange carries (distance, row) and
 // k_finish_gather does the coherence pick and the weighting after it; 1 the exact stage
 // prepares the tail (ShardRec, CohSel) and k_finish only reduces.  Measured on the
-// simulated G = 8 rank (tools/ab_shard.sh, one box): finest level 335 vs 361 ms, pipelined
+// simulated G = 8 rank (`tools/gpu.sh abknob ... -- python tools/shard_sim.py 8`, one box): finest level 335 vs 361 ms, pipelined
 // step 415 vs 450 ms, so 0
 static int shard_tail() {
     static const int v = env_int("IA_SHARD_TAIL", 0);
@@ -523,6 +537,10 @@ struct LevelRun {
         if (rc || nj == 1) return rc;
         IA_ARG(nj <= IA_BATCH_MAX, "ia_synth_levels_batch: too many jobs in one batch");
         IA_ARG(xw, "ia_synth_levels_batch: batches run the exact matcher on one GPU (fused kernel)");
+        // XJob carries no exchange view: K jobs would publish into one box (cells indexed by
+        // query only) and advance its epoch once per wave for K jobs
+        IA_ARG(!a->comm && !a->lsh,
+               "ia_synth_levels_batch: a batch of K > 1 jobs takes neither a comm nor an LSH index");
         K = nj;
         part.resize(K - 1);
         for (int k = 1; k < K; ++k) {
@@ -641,6 +659,10 @@ struct LevelRun {
     }
 
     int done(hipStream_t st) {
+        if (xw) {
+            k_err_sticky<<<1, 64, 0, st>>>(ws.ctl, K > 1 ? ws.jtab : nullptr, K);
+            IA_HIP(hipGetLastError());
+        }
         if (prof) {   // read back by ia_prof_end (no synchronisation here)
             IA_HIP(hipMemcpyAsync(hstats, ws.stats, STATS_BYTES, hipMemcpyDeviceToHost, st));
             prof_push(ProfRec{a->tag, K, a->nrows, pairs, ev0, nscreen, timed ? 1 : 0, hstats,
@@ -742,13 +764,30 @@ int ia_synth_status(const IaSynthArgs *levels, int n, void *stream) {
         unsigned int e = 0;
         IA_HIP(hipMemcpy(&e, w.ctl + XW_CTL_ERR, sizeof(e), hipMemcpyDeviceToHost));
         if (e) {
-            set_error("ia_synth_status: a wait for a neighbouring pixel's decision timed out");
-            return IA_E_COMM;
+            set_error("ia_synth_status: a wait for a neighbouring pixel's decision timed out "
+                      "(device schedule fault)");
+            return IA_E_SCHED;
         }
         if (comm_peer_mcap(a.comm) > 0) {
             const int rc = ia_peer_status(a.comm);
             if (rc) return rc;
         }
+    }
+    return IA_OK;
+}
+
+int ia_sched_status(int clear) {
+    IA_HIP(hipDeviceSynchronize());
+    unsigned int e = 0;
+    IA_HIP(hipMemcpyFromSymbol(&e, HIP_SYMBOL(g_sched_err), sizeof(e), 0, hipMemcpyDeviceToHost));
+    if (clear && e) {
+        const unsigned int z = 0;
+        IA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sched_err), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+    }
+    if (e) {
+        set_error("ia_sched_status: a wait for a neighbouring pixel's decision timed out in some "
+                  "level since the last clear (device schedule fault)");
+        return IA_E_SCHED;
     }
     return IA_OK;
 }
@@ -915,7 +954,7 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
     hipStream_t st = S(stream);
     // one stream per level; coarser levels at high priority (IA_PIPE_PRIO, default 1) so
     // that they run ahead of the finest level instead of time-sharing with it.  Measured
-    // (c4, one box, tools/ab_pipeline.sh): one level at a time 1706-1713 ms/step; pipelined
+    // (c4, one box, `tools/gpu.sh abknob`): one level at a time 1706-1713 ms/step; pipelined
     // with the coarse levels enqueued whole first at high priority 1641-1643 ms (the finest
     // level's plateau screens undisturbed: k_screen16<11> 400 vs 396 us); enqueued just
     // ahead of their need 1619-1621 ms but the plateau screens contended (414 us)

@@ -30,6 +30,9 @@ extern "C" {
 #define IA_E_HIP (-2)       /* HIP runtime error                         */
 #define IA_E_COMM (-3)      /* RCCL error                                */
 #define IA_E_UNSUPPORTED (-4)
+#define IA_E_TIMEOUT (-5)   /* device-side exchange: another rank's records never came */
+#define IA_E_SCHED (-6)     /* device schedule fault: a neighbouring pixel's decision wait
+                               timed out inside the fused per-wave kernel (never a peer) */
 
 #define IA_D 55             /* feature length, 1 channel: 9 + 25 + 9 + 12          */
 #define IA_DP 56            /* padded row: 55 features + squared norm slot         */
@@ -241,12 +244,16 @@ int ia_synth_levels(const IaSynthArgs *levels, int n, void *stream);
  * about one job's launch latency; results equal K separate ia_synth_levels calls.  Exact
  * matcher on one GPU only (comm and lsh NULL), 1 <= K <= 128. */
 int ia_synth_levels_batch(const IaSynthArgs *levels, int n, int K, void *stream);
-/* after ia_synth_level(s) calls on `stream`: synchronises the stream and returns IA_E_COMM if
- * any wait inside those levels' synthesis timed out (a neighbouring pixel's decision inside
- * the fused per-wave kernel, or another rank's records on a device-side exchange): the
- * results are then wrong.  The reference has no such wait (image_analogies.py:161-220 is one
+/* after ia_synth_level(s) calls on `stream`: synchronises the stream and returns IA_E_SCHED if
+ * a wait for a neighbouring pixel's decision inside the fused per-wave kernel timed out, or
+ * IA_E_TIMEOUT if another rank's records on a device-side exchange never came: the results
+ * are then wrong.  The reference has no such wait (image_analogies.py:161-220 is one
  * thread); this is the device schedule's own integrity check. */
 int ia_synth_status(const IaSynthArgs *levels, int n, void *stream);
+/* the same check for every fused level run on this device since the last clear (the level
+ * workspaces may be gone): synchronises the device; IA_E_SCHED if any neighbour wait timed
+ * out.  clear != 0 resets the sticky word.  Peer timeouts: ia_peer_status. */
+int ia_sched_status(int clear);
 
 /* profiling of ia_synth_level calls flagged IA_SYNTH_PROF (process-wide, thread-safe):
  * ia_prof_begin opens a profile (the caller has synchronised); ia_prof_end synchronises the

@@ -9,8 +9,13 @@ exact brute-force matcher, algorithms.py:73-75 restated):
                   fp64 queries captured from a GPU synthesis (tools/capture_c4_queries.py,
                   committed as c4_queries_in.npz) plus synthetic near-ties, with the
                   oracle's exact 1-NN row and distance over the full database.
+  c4_levels.npz   config c4 (job seed 0) with every level below the finest synthesized
+                  in full by the oracle (levels 1-3: up to 512x512 B' pixels against the
+                  1,048,576-row database): s, im and the SHA-256 of B' per level.
+  c5_job.npz      config c5's first job (512x512, seed 1000 = bench.py's rank 0 job 0),
+                  every level in full (349,184 B' pixels; 262,144 rows at the finest level).
 
-Usage:  python tests/golden/make_config_fixtures.py c3|c4 [threads]
+Usage:  python tests/golden/make_config_fixtures.py c3|c4|c4levels|c5 [threads]
 The inputs are rebuilt from bench.py's workload definitions, so the GPU tests regenerate
 them identically on the box.
 """
@@ -30,32 +35,46 @@ import ia_oracle as o      # noqa: E402
 import ia_oracle_c as oc   # noqa: E402
 
 
-def workload(name):
-    """(A, [A'], B, kappa, levels cap, B' init seed) of a bench.py config, job seed 0."""
+def workload(name, job_seed=0):
+    """(A, [A'], B, kappa, levels cap, B' init seed) of a bench.py config (bench.Job)."""
     import bench
     conf = bench.CONFIGS[name]
-    A, Ap, B = bench.make_inputs(conf, 0)
-    return A, [Ap], B, conf['k'], conf['levels'], 2
+    A, Ap, B = bench.make_inputs(conf, job_seed)
+    return A, [Ap], B, conf['k'], conf['levels'], job_seed + 2
 
 
 def bp_hash(x):
     return hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest()
 
 
-def make_c3():
-    A, Aps, B, k, cap, seed = workload('c3')
+def full_run(name, fname, job_seed=0, skip_finest=False):
+    """The oracle's scanline run of a config's levels -> per-level s, im, B' hash."""
+    A, Aps, B, k, cap, seed = workload(name, job_seed)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, cap=cap, seed=seed)
     w = o.compute_weights(3, 5, 12, 1)
+    levels = range(1, L - 1) if skip_finest else None
     t0 = time.time()
-    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w)
-    print('c3 oracle: %d levels in %.1f s' % (len(out), time.time() - t0))
-    rec = {'max_levels': np.int32(L)}
+    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w, levels=levels)
+    print('%s oracle: %d levels in %.1f s' % (name, len(out), time.time() - t0))
+    rec = {'max_levels': np.int32(L), 'job_seed': np.int32(job_seed)}
     for l, (bp, s, im) in out.items():
         rec['s%d' % l] = s.astype(np.int16)
         rec['im%d' % l] = im.astype(np.uint8)
         rec['bp_sha%d' % l] = np.array(bp_hash(bp))
         rec['bp_sum%d' % l] = np.float64(bp.sum())
-    np.savez_compressed(os.path.join(HERE, 'c3_oracle.npz'), **rec)
+    np.savez_compressed(os.path.join(HERE, fname), **rec)
+
+
+def make_c3():
+    full_run('c3', 'c3_oracle.npz')
+
+
+def make_c4levels():
+    full_run('c4', 'c4_levels.npz', skip_finest=True)
+
+
+def make_c5():
+    full_run('c5', 'c5_job.npz', job_seed=1000)
 
 
 def make_c4():
@@ -83,4 +102,4 @@ def make_c4():
 if __name__ == '__main__':
     if len(sys.argv) > 2:
         oc.set_threads(int(sys.argv[2]))
-    {'c3': make_c3, 'c4': make_c4}[sys.argv[1]]()
+    {'c3': make_c3, 'c4': make_c4, 'c4levels': make_c4levels, 'c5': make_c5}[sys.argv[1]]()

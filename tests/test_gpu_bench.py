@@ -103,3 +103,41 @@ def test_bench_c4_two_ranks_sharing_the_gpu_equal_one_rank(gpu):
     assert two['config']['exchange'].startswith('peer') and 'exchange_fallback' not in two['checks']
     assert two['checks']['replicas_identical'] is True and two['checks']['bp_equals_ap_at_s'] is True
     assert two['checks']['checksum'] == one['checks']['checksum']
+    for r in two['ranks']:       # each rank explains its exchange
+        assert r['exchanges'] and all(e['kind'] == 'peer' for e in r['exchanges'])
+        assert all(e['stress'].startswith('ok') for e in r['exchanges'])
+        assert r['checksum'] == one['checks']['checksum'] and r['peer_wait_us_per_pixel'] >= 0
+
+
+@pytest.mark.gpu
+def test_bench_c5_two_ranks_sharing_the_gpu(gpu):
+    """c5 (the multi_script batch, multi_script.py:13-32) as the driver's 2-GPU run starts
+    it, both ranks on the box's one GPU: n_gpus 2, parallelism jobs2, the pixel accounting
+    of the whole job (2 ranks x 3 jobs x 349,184 B' pixels), per-rank fields, and every
+    rank's jobs (seeds 1000 + 3 (rank + 2 j)) equal to the same seeds' one-rank run."""
+    one = run_bench('--config', 'c5', '--jobs', '6', '--steps', '1', '--warmup', '0',
+                    '--no-cpu-baseline')
+    env = dict(os.environ, IA_SHARE_GPU='1')
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--config', 'c5', '--jobs', '3', '--steps', '1', '--warmup', '0',
+                        '--no-cpu-baseline'],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, p.stdout[-2000:]
+    two = json.loads(lines[0])
+    assert two['n_gpus'] == 2 and two['config']['parallelism'] == 'jobs2'
+    assert two['scaling'] == 'weak'
+    assert two['config']['pixels_per_step'] == 2 * 3 * 349184
+    assert abs(two['value'] - 2 * 3 * 349184 / (two['ms_per_step'] * 1e-3)) < 1e-6 * two['value']
+    ranks = two['ranks']
+    assert [r['rank'] for r in ranks] == [0, 1]
+    ref = one['checks']['job_sums']
+    assert len(ref) == 6
+    seen = {}
+    for r in ranks:
+        assert r['jobs'] == 3 and r['pixels_per_step'] == 3 * 349184
+        for seed, v in r['job_sums'].items():
+            assert (int(seed) - 1000) // 3 % 2 == r['rank'], (seed, r['rank'])
+            seen[seed] = v
+    assert seen == ref

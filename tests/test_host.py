@@ -307,6 +307,9 @@ class _FakeLib:
         self.log.append('destroy')
         return 0
 
+    def ia_peer_mem_kind(self, h):
+        return 0
+
     def ia_last_error(self):
         return b'hipIpcOpenMemHandle: invalid argument'
 

@@ -1,5 +1,5 @@
 """Debug: one rank of a 2-rank peer-exchange synthesis on one GPU vs the same synthesis
-unsharded in-process (debug records compared pixel by pixel).  Run by tools/exchange_debug.sh."""
+unsharded in-process (debug records compared pixel by pixel).  Run as `python tools/exchange_debug.py` on the GPU box."""
 import os
 import sys
 

@@ -1,5 +1,5 @@
 """Run bench.hbm_kernels once (the bandwidth-bound kernels: YIQ, pyramid reduce, DB build)
-as a short process for rocprofv3 kernel traces / PMC passes (tools/prof_hbm.sh)."""
+as a short process for rocprofv3 kernel traces / PMC passes (`tools/gpu.sh trace TAG -- python tools/hbm_probe.py`)."""
 import json
 import os
 import sys

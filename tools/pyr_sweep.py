@@ -1,5 +1,5 @@
 """ia_pyr_reduce_f64 at 2048^2 -> 1024^2 (the c4 A level): HIP-event time of the C entry
-per form / streaming block height, median of 50 (diagnostic; tools/pyr_sweep.sh)."""
+per form / streaming block height, median of 50 (diagnostic; `python tools/pyr_sweep.py` on the GPU box)."""
 import ctypes
 import os
 import sys
