@@ -201,8 +201,10 @@ int ia_peer_create(int nranks, int rank, int mcap, void **comm, uint8_t handle[6
     if (e == hipSuccess) e = hipMemset(err, 0, 256);
     if (e == hipSuccess) e = hipMemset(p->mine, 0, p->bytes);   // epochs start at 1
     if (e == hipSuccess && env_int("IA_PEER_TRACE", 0)) {
-        e = hipMalloc(&p->v.trace, 1024 * 8 * 12 * sizeof(double));
-        if (e == hipSuccess) e = hipMemset(p->v.trace, 0, 1024 * 8 * 12 * sizeof(double));
+        double *tr = nullptr;
+        e = hipMalloc(&tr, 1024 * 8 * 12 * sizeof(double));
+        p->v.trace = tr;
+        if (e == hipSuccess) e = hipMemset(tr, 0, 1024 * 8 * 12 * sizeof(double));
     }
     hipIpcMemHandle_t h;
     if (e == hipSuccess) e = hipIpcGetMemHandle(&h, p->mine);

@@ -35,6 +35,30 @@ int hip_fail(hipError_t e, const char *what);
         if (!(cond)) { ::ia::set_error(msg); return IA_E_ARG; }   \
     } while (0)
 
+// A pointer into device (global) memory held in an argument struct.  On the device its
+// value is typed addrspace(1), so every access through it compiles to a global load or
+// store even when the struct itself was read from LDS or from a job table in memory
+// (pointers loaded from memory are generic otherwise: FLAT accesses, which also count in
+// lgkmcnt, so every LDS wait of the wave would wait for them too).  Same size and bits as
+// T* on the host, where it is a plain pointer.
+template <class T>
+struct gptr {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __attribute__((address_space(1))) T *p;
+#else
+    T *p;
+#endif
+    gptr() = default;
+    __host__ __device__ gptr(T *q) : p((decltype(p))q) {}
+    template <class U, class = decltype(static_cast<T *>((U *)nullptr))>
+    __host__ __device__ gptr(const gptr<U> &o) : p((decltype(p))o.get()) {}
+    __host__ __device__ operator T *() const { return (T *)p; }
+    __host__ __device__ T *get() const { return (T *)p; }
+    __host__ __device__ gptr &operator+=(long d) { p += d; return *this; }
+    __host__ __device__ gptr &operator-=(long d) { p -= d; return *this; }
+};
+static_assert(sizeof(gptr<double>) == sizeof(double *), "gptr is a plain pointer");
+
 static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -79,7 +103,7 @@ __device__ __forceinline__ long mirrori(long c, long n) {
 // Emits the 55 values in feature order through f(k, v).
 // ---------------------------------------------------------------------------------
 struct ImgPair {          // one image at levels l-1 (sm) and l (lg)
-    const double *sm, *lg;
+    gptr<const double> sm, lg;
     int hs, ws, h, w;
 };
 

@@ -203,7 +203,7 @@ __device__ __forceinline__ DbWinCtx db_stage(const DbSrc &src, long row0, long n
     double vf[8][2], vc[6];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        const double *row = (r < 5 ? A.lg : Apl) + (long)symi2(y - 2 + (r < 5 ? r : r - 5), A.h) * A.w;
+        const double *row = (r < 5 ? A.lg.get() : Apl) + (long)symi2(y - 2 + (r < 5 ? r : r - 5), A.h) * A.w;
         vf[r][0] = row[fc0];
         vf[r][1] = row[fc1];
     }
@@ -562,11 +562,11 @@ int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double
     IA_LAUNCH_CHECK("k_img_pad");
     if (db) {
         k_img_norm<<<(unsigned)((nrows + 255) / 256), 256, 0, st>>>(reinterpret_cast<const half8 *>(db), nrows,
-                                                                   const_cast<uint32_t *>(v.norm));
+                                                                   const_cast<uint32_t *>(v.norm.get()));
         IA_LAUNCH_CHECK("k_img_norm");
     } else {     // nrows is a multiple of 512 here (whole chunks, ia_internal.h)
         k_db_build_t<true><<<(unsigned)(nrows / 256), 256, 0, st>>>(d, row0, nrows, center, amax, nullptr,
-                                                                    const_cast<uint32_t *>(v.norm));
+                                                                    const_cast<uint32_t *>(v.norm.get()));
         IA_LAUNCH_CHECK("k_db_build_t<norm>");
     }
     return IA_OK;

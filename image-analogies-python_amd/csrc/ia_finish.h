@@ -134,7 +134,7 @@ __device__ __forceinline__ unsigned long long *peer_cell(unsigned long long *box
 __device__ __forceinline__ unsigned long long *peer_box(const PeerView &p, int g) {
     unsigned long long *box = p.box[0];
 #pragma unroll
-    for (int k = 1; k < IA_PEER_MAX; ++k) box = g == k ? p.box[k] : box;
+    for (int k = 1; k < IA_PEER_MAX; ++k) box = g == k ? p.box[k].get() : box;
     return box;
 }
 // lanes g < nranks of one wave: this rank's winner of query q into rank g's box (system-
@@ -163,7 +163,7 @@ __device__ __forceinline__ bool peer_collect(const PeerView &p, int q, int lane,
     const bool mine = lane < p.nranks;
     const unsigned long long *src = peer_cell(peer_box(p, p.rank), p, mine ? lane : 0, q);
     unsigned long long g0 = 0, g1 = 0, g2 = 0;
-    bool dead = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    bool dead = __hip_atomic_load(p.err.get(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok;
     for (;;) {
@@ -177,7 +177,7 @@ __device__ __forceinline__ bool peer_collect(const PeerView &p, int q, int lane,
         }
         if (__all(ok) || dead) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
-            if (lane == 0) __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) __hip_atomic_fetch_or(p.err.get(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             dead = true;
             break;
         }
@@ -249,7 +249,7 @@ __device__ __forceinline__ bool peer_collect_rec(const PeerView &p, int q, int l
     const bool mine = lane < p.nranks;
     const unsigned long long *src = peer_cell(peer_box(p, p.rank), p, mine ? lane : 0, q);
     unsigned long long g0 = 0, g1 = 0, g2 = 0, g3 = 0, g4 = 0, g5 = 0, g6 = 0;
-    bool dead = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    bool dead = __hip_atomic_load(p.err.get(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     auto ld = [&](int k) { return __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
     auto tagged = [&](unsigned long long v) { return (unsigned)(v >> 32) == p.epoch; };
@@ -262,7 +262,7 @@ __device__ __forceinline__ bool peer_collect_rec(const PeerView &p, int q, int l
         }
         if (__all(ok) || dead) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT_TICKS) {
-            if (lane == 0) __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) __hip_atomic_fetch_or(p.err.get(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             dead = true;
             break;
         }

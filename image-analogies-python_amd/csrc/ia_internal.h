@@ -80,7 +80,7 @@ static inline bool db_strips_enabled() {
 // the rows fill whole chunks (no padding rows): see img_db_applies.
 constexpr int IMG_PX = 4, IMG_PY = 2;
 struct ImgDb {
-    const uint32_t *fa, *ca, *norm, *ap;   // ap: A' image 0's fine section
+    gptr<const uint32_t> fa, ca, norm, ap;   // ap: A' image 0's fine section
     int W, Wp, Wcp;                         // width, padded fine / coarse widths
     long fsz, csz, apstride, apc;           // padded image sizes (u32), A' image stride,
                                             // offset of an A' image's coarse section
@@ -169,9 +169,9 @@ static inline int qrows_alloc(int Mmax) {
 // record first).
 constexpr int IA_PEER_MAX = 16;
 struct PeerView {
-    unsigned long long *box[IA_PEER_MAX];   // box[g]: rank g's receive box (box[rank]: own)
-    unsigned int *err;                      // this rank's timeout word (0: fine)
-    double *trace;                          // diagnostic (nullable): ia_diag_peer_trace
+    gptr<unsigned long long> box[IA_PEER_MAX];   // box[g]: rank g's receive box (box[rank]: own)
+    gptr<unsigned int> err;                      // this rank's timeout word (0: fine)
+    gptr<double> trace;                          // diagnostic (nullable): ia_diag_peer_trace
     int nranks, rank, mcap;                 // nranks 0: not a peer exchange
     unsigned int epoch;                     // this wave's tag (>= 1, one per wave)
 };
@@ -185,16 +185,16 @@ static inline size_t peer_box_words(int nranks, int mcap) { return (size_t)2 * n
 struct FinishArgs {
     int t, y_lo, W;
     long N_total;
-    const double *weights;
+    gptr<const double> weights;
     double kappa_factor;
-    double *Bp_lg;
-    int32_t *s, *im;
-    int32_t *dbg_px;     // nullable: 7 int32 per pixel (ia.h IaSynthArgs)
-    double *dbg_dist;    // nullable: 2 doubles per pixel
+    gptr<double> Bp_lg;
+    gptr<int32_t> s, im;
+    gptr<int32_t> dbg_px;     // nullable: 7 int32 per pixel (ia.h IaSynthArgs)
+    gptr<double> dbg_dist;    // nullable: 2 doubles per pixel
     // sharded DB (nullable otherwise): the exact stage writes each query's ShardRec and
     // its coherence pick (CohSel, ia_finish.h) here instead of finishing the pixel
-    ShardRec *shard_out;
-    void *coh_out;
+    gptr<ShardRec> shard_out;
+    gptr<void> coh_out;
     // sharded DB with the device-side exchange (px.nranks > 0): the exact stage publishes
     // its shard's winner, collects every rank's, and finishes the pixel in the same kernel
     PeerView px{};
@@ -205,24 +205,24 @@ struct FinishArgs {
 // outputs and control words; the screen and k_xwave take job blockIdx.y's pointers from a
 // device table of these
 struct XJob {
-    const double *A_sm, *A_lg, *Ap_sm, *Ap_lg;   // DbSrc images
-    const uint32_t *fa, *ca, *norm, *ap;          // image-form DB sections (ImgDb)
-    const void *db;                               // split-f16 rows
-    float *segmin;
-    double *q64[2];
-    float *qp[2];
-    double *nq[2];
-    _Float16 *q16[2];
-    const float *amax;
-    const double *center;
-    const double *B_sm, *B_lg, *Bp_sm;
-    double *Bp_lg;
-    const double *weights;
+    gptr<const double> A_sm, A_lg, Ap_sm, Ap_lg;   // DbSrc images
+    gptr<const uint32_t> fa, ca, norm, ap;          // image-form DB sections (ImgDb)
+    gptr<const void> db;                            // split-f16 rows
+    gptr<float> segmin;
+    gptr<double> q64[2];
+    gptr<float> qp[2];
+    gptr<double> nq[2];
+    gptr<_Float16> q16[2];
+    gptr<const float> amax;
+    gptr<const double> center;
+    gptr<const double> B_sm, B_lg, Bp_sm;
+    gptr<double> Bp_lg;
+    gptr<const double> weights;
     double kappa_factor;
-    int32_t *s, *im, *dbg_px;
-    double *dbg_dist;
-    unsigned long long *dbox;
-    unsigned int *ctl;                            // tickets[2], error word
+    gptr<int32_t> s, im, dbg_px;
+    gptr<double> dbg_dist;
+    gptr<unsigned long long> dbox;
+    gptr<unsigned int> ctl;                         // tickets[2], error word
 };
 constexpr int IA_BATCH_MAX = 128;
 
@@ -231,29 +231,29 @@ constexpr int IA_BATCH_MAX = 128;
 struct XArgs {
     DbSrc src;
     ImgDb im;                     // image-form DB (IMG) ...
-    const void *db;               // ... or the split-f16 rows (half8)
+    gptr<const void> db;          // ... or the split-f16 rows (half8)
     long row0, nrows, nseg;
     int seg_rows;
     StageMap smap;                // segment -> rows
-    const float *segmin;          // [M][nseg], this wave's screen
-    const double *q64;            // this wave's query rows (M)
-    const float *qp;
-    const double *nq;
-    const float *amax;
-    const double *center;
-    double *q64n;                 // wave t + 1's query rows (M_n), written here
-    float *qpn;
-    double *nqn;
-    _Float16 *q16n;
+    gptr<const float> segmin;     // [M][nseg], this wave's screen
+    gptr<const double> q64;       // this wave's query rows (M)
+    gptr<const float> qp;
+    gptr<const double> nq;
+    gptr<const float> amax;
+    gptr<const double> center;
+    gptr<double> q64n;            // wave t + 1's query rows (M_n), written here
+    gptr<float> qpn;
+    gptr<double> nqn;
+    gptr<_Float16> q16n;
     ImgPair B, Bp;                // B / B' at levels l - 1, l (the query's features)
     int H, M, y_lo_n, M_n;        // wave t: M pixels from f.y_lo; wave t + 1: M_n from y_lo_n
-    unsigned long long *dbox;     // decision granules, 2 per row
-    unsigned int *tickets;        // [2]: this launch uses tickets[t & 1]
-    unsigned int *err;            // set when a wait for a neighbour's decision times out
-    unsigned long long *stats;    // nullable: rows rescored, candidate segments, full scans
+    gptr<unsigned long long> dbox;  // decision granules, 2 per row
+    gptr<unsigned int> tickets;   // [2]: this launch uses tickets[t & 1]
+    gptr<unsigned int> err;       // set when a wait for a neighbour's decision times out
+    gptr<unsigned long long> stats;  // nullable: rows rescored, candidate segments, full scans
     FinishArgs f;                 // t, y_lo, W, ..., px (sharded DB: the device-side exchange)
-    const XJob *jobs;             // nullable: a batch, job blockIdx.y's pointers override these
-    unsigned long long *trace;    // diagnostic (nullable): phase stamps, XW_TRACE_* below
+    gptr<const XJob> jobs;        // nullable: a batch, job blockIdx.y's pointers override these
+    gptr<unsigned long long> trace;  // diagnostic (nullable): phase stamps, XW_TRACE_* below
 };
 // k_xwave phase stamps (IA_XW_TRACE=<level tag>, ia_diag_xwave_trace): s_memrealtime (100
 // MHz) at XW_TRACE_N points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T

@@ -69,7 +69,7 @@ __device__ __forceinline__ void exact_tail(const DbSrc &src, int q, long long wi
         if (!have_cs) __syncthreads();
         if (wv == 0 && lane == 0) {
             fa.shard_out[q] = ShardRec{bd, win, d_app, 0.0};
-            reinterpret_cast<CohSel *>(fa.coh_out)[q] = *cs;
+            reinterpret_cast<CohSel *>(fa.coh_out.get())[q] = *cs;
         }
     }
 }

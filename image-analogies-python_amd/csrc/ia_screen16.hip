@@ -28,6 +28,7 @@
 #include "ia_imgwin.h"
 #include "ia_split16.h"
 
+#include <atomic>
 #include <float.h>
 #include <stdint.h>
 #include <type_traits>
@@ -103,6 +104,90 @@ __device__ __forceinline__ void stage_mfma(const half8 *sb, const half8 (&bq)[NS
     });
 }
 
+// ---- chain-major stage (IA_SCREEN_SCHED=1) -------------------------------------------
+// The same chains as stage_mfma, but each (query tile, stage tile) chain runs its 11 MFMAs
+// back to back into one of two ping-pong accumulators (a single accumulation chain of
+// v_mfma_f32_32x32x16 issues at the full rate), its running-minimum fold is issued after the
+// NEXT chain's first MFMA (the VALU overlaps that chain's MFMAs instead of waiting on the
+// last result behind an s_nop), and the next stage tile's 7 operand reads are issued at the
+// start of the current tile's last chain (two operand register sets), so no tile boundary
+// waits on an LDS round trip.  Same products, same per-accumulator order, same minima.
+template <int G, int W>
+__host__ __device__ constexpr int ch_count() {
+    int n = 0;
+    for (int u = 0; u < STAGE_TILES; ++u)
+        for (int k = 0; k < bal_ns(G, W); ++k) n += bal_on(G, W, k, u) ? 1 : 0;
+    return n;
+}
+// (stage tile, chain slot) of wave W's c-th chain in tile-major order
+template <int G, int W>
+__host__ __device__ constexpr int ch_u(int c) {
+    for (int u = 0; u < STAGE_TILES; ++u)
+        for (int k = 0; k < bal_ns(G, W); ++k)
+            if (bal_on(G, W, k, u) && c-- == 0) return u;
+    return -1;
+}
+template <int G, int W>
+__host__ __device__ constexpr int ch_k(int c) {
+    for (int u = 0; u < STAGE_TILES; ++u)
+        for (int k = 0; k < bal_ns(G, W); ++k)
+            if (bal_on(G, W, k, u) && c-- == 0) return k;
+    return -1;
+}
+// ordinal of chain c's stage tile among the wave's distinct tiles (its operand set parity)
+template <int G, int W>
+__host__ __device__ constexpr int ch_uo(int c) {
+    int o = 0;
+    for (int i = 1; i <= c; ++i) o += ch_u<G, W>(i) != ch_u<G, W>(i - 1) ? 1 : 0;
+    return o;
+}
+
+__device__ __forceinline__ void fold_min(const floatx16 &x, float &mn) {
+    const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+    const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+    const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+    const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+    mn = fminf(fminf(mn, u0), u1);
+}
+
+template <int G, int W, int NS>
+__device__ __forceinline__ void stage_mfma_cm(const half8 *sb, const half8 (&bq)[NS][Q16_GROUPS],
+                                              float (&mn)[NS], int lane) {
+    constexpr int NC = ch_count<G, W>();
+    const floatx16 zero = {};
+    half8 a[2][DB16_GROUPS];
+    floatx16 acc[2];
+    {
+        const half8 *p = sb + ch_u<G, W>(0) * TILE_H8 + lane;
+#pragma unroll
+        for (int g = 0; g < DB16_GROUPS; ++g) a[0][g] = p[g * 64];
+    }
+    static_for<0, NC>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        constexpr int k = ch_k<G, W>(c), ab = ch_uo<G, W>(c) & 1, cb = c & 1;
+        if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c)) {
+            // the next tile's operand, into the set no issued chain still reads
+            const half8 *p = sb + ch_u<G, W>(c + 1) * TILE_H8 + lane;
+#pragma unroll
+            for (int g = 0; g < DB16_GROUPS; ++g) a[ab ^ 1][g] = p[g * 64];
+        }
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
+        if constexpr (c > 0) fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
+#pragma unroll
+        for (int m = 1; m < MFMA16; ++m)
+            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][mfma_a(m)], bq[k][mfma_b(m)], acc[cb],
+                                                             0, 0, 0);
+    });
+    fold_min(acc[(NC - 1) & 1], mn[ch_k<G, W>(NC - 1)]);
+}
+
+template <int SCHED, int G, int W, int NS>
+__device__ __forceinline__ void stage_run(const half8 *sb, const half8 (&bq)[NS][Q16_GROUPS],
+                                          float (&mn)[NS], int lane) {
+    if constexpr (SCHED == 1) stage_mfma_cm<G, W, NS>(sb, bq, mn, lane);
+    else stage_mfma<G, W, NS>(sb, bq, mn, lane);
+}
+
 // after stage s: when it closes a segment, fold the wave's minima into smin[seg][G * 32]
 template <int G, int W, int NS>
 __device__ __forceinline__ void stage_close(int s, int tps, int *smin, float (&mn)[NS], int lane) {
@@ -142,7 +227,7 @@ __device__ __forceinline__ void copies_barrier() {
 }
 
 // row form: wave W's share of one chunk, the DB rows streamed into LDS stage by stage
-template <int G, int W>
+template <int SCHED, int G, int W>
 __device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
                                            const StageMap &sm, long chunk, int nstage, int tps,
                                            const half8 *__restrict__ q16) {
@@ -166,7 +251,7 @@ __device__ __forceinline__ void chain_body(const half8 *__restrict__ db16, half8
     copies_barrier();
     for (int s = 0; s < nstage; ++s) {
         if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
-        stage_mfma<G, W, NS>(sbuf + (s & 1) * STAGE_H8, bq, mn, lane);
+        stage_run<SCHED, G, W, NS>(sbuf + (s & 1) * STAGE_H8, bq, mn, lane);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
         copies_barrier();   // stage s+1 landed and stage s is free again
     }
@@ -215,7 +300,7 @@ __device__ __forceinline__ void expand_groups(const char *wb, half8 *E, int lane
 // expansion with the other's MFMAs).  Measured against a pipelined form (two operand
 // buffers, the next stage expanded before this one's MFMAs, one barrier per stage, 81.8 KB):
 // c4 1615-1635 vs 1650-1656 ms/step (`tools/gpu.sh ablib`, profiles/r02_image_form_ab.txt).
-template <int G, int W>
+template <int SCHED, int G, int W>
 __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, int *smin,
                                          const StageMap &sm, long chunk, int nstage, int tps,
                                          const half8 *__restrict__ q16) {
@@ -245,7 +330,7 @@ __device__ __forceinline__ void img_body(const ImgDb &im, half8 *E, char *wbuf, 
         if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
         expand_groups<W, 0, DB16_GROUPS>(wbuf + (s & 1) * WIN_B, E, lane);
         __syncthreads();   // the stage operand is complete
-        stage_mfma<G, W, NS>(E, bq, mn, lane);
+        stage_run<SCHED, G, W, NS>(E, bq, mn, lane);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
         copies_barrier();   // the operand is consumed and window s + 1 has landed
     }
@@ -316,7 +401,7 @@ __device__ __forceinline__ void expand_ring(const char *ring, int y, int ns, hal
     });
 }
 
-template <int G, int W>
+template <int SCHED, int G, int W>
 __device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring, int *smin,
                                            const StageMap &sm, long chunk, int nstage, int tps,
                                            const half8 *__restrict__ q16) {
@@ -354,7 +439,7 @@ __device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring
         }
         expand_ring<W>(ring, y, s & 1, E, lane);
         __syncthreads();   // the stage operand is complete
-        stage_mfma<G, W, NS>(E, bq, mn, lane);
+        stage_run<SCHED, G, W, NS>(E, bq, mn, lane);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
         copies_barrier();  // the operand is consumed and stage s + 1's rows have landed
     }
@@ -363,7 +448,7 @@ __device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring
 // grid: (nchunks rounded up to 8) x groups, XCD-aware: all groups of a chunk share
 // blockIdx % 8 (one XCD under round-robin dispatch), so the chunk is fetched from HBM once
 // per launch.  Group g holds query tiles [g G, g G + G).
-template <int G>
+template <int G, int SCHED>
 __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ db16, int nchunks,
                                                      int ch, int seg_rows, StageMap sm,
                                                      const half8 *__restrict__ q16, int M,
@@ -372,8 +457,8 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     __shared__ half8 sbuf[2 * STAGE_H8];
     if (jobs) {   // batch: this job's DB, query rows and minima
         const XJob &J = jobs[blockIdx.y];
-        db16 = reinterpret_cast<const half8 *>(J.db);
-        q16 = reinterpret_cast<const half8 *>(J.q16[parity]);
+        db16 = reinterpret_cast<const half8 *>(J.db.get());
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity].get());
         segmin = J.segmin;
     }
     __shared__ int smin[SPC_MAX * G * 32];
@@ -388,10 +473,10 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     const int tps = seg_rows >> 5;
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv == 0) chain_body<G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    else if (wv == 1) chain_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    else if (wv == 2) chain_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    else chain_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    if (wv == 0) chain_body<SCHED, G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else if (wv == 1) chain_body<SCHED, G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else if (wv == 2) chain_body<SCHED, G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else chain_body<SCHED, G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
     __syncthreads();
     // the chunk's minima, spc consecutive segments per query
     const long seg0 = (long)chunk * spc;
@@ -402,7 +487,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     }
 }
 
-template <int G>
+template <int G, int SCHED>
 __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int ch, int seg_rows,
                                                       StageMap sm,
                                                       const half8 *__restrict__ q16, int M,
@@ -412,7 +497,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
     if (jobs) {   // batch: this job's image-form sections, query rows and minima
         const XJob &J = jobs[blockIdx.y];
         im.fa = J.fa; im.ca = J.ca; im.norm = J.norm; im.ap = J.ap;
-        q16 = reinterpret_cast<const half8 *>(J.q16[parity]);
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity].get());
         segmin = J.segmin;
     }
     static_assert(RW_B <= 2 * WIN_B, "the rings fit the window buffers");
@@ -430,15 +515,15 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (sm.W > 0) {   // strips: the rolling window (wbuf holds the rings)
-        if (wv == 0) strip_body<G, 0>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
-        else if (wv == 1) strip_body<G, 1>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
-        else if (wv == 2) strip_body<G, 2>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
-        else strip_body<G, 3>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        if (wv == 0) strip_body<SCHED, G, 0>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 1) strip_body<SCHED, G, 1>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 2) strip_body<SCHED, G, 2>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else strip_body<SCHED, G, 3>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
     } else {
-        if (wv == 0) img_body<G, 0>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
-        else if (wv == 1) img_body<G, 1>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
-        else if (wv == 2) img_body<G, 2>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
-        else img_body<G, 3>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        if (wv == 0) img_body<SCHED, G, 0>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 1) img_body<SCHED, G, 1>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else if (wv == 2) img_body<SCHED, G, 2>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
+        else img_body<SCHED, G, 3>(im, E, wbuf, smin, sm, chunk, nstage, tps, qg);
     }
     __syncthreads();
     // the chunk's minima, spc consecutive segments per query (as k_screen16)
@@ -452,6 +537,18 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
 
 // query tiles per launch group: T tiles in ceil(T / 11) equal groups
 static inline int screen_groups(int T) { return (T + MAX_G - 1) / MAX_G; }
+
+// the stage's MFMA schedule (IA_SCREEN_SCHED / ia_diag_set_screen_sched): 0 tile-major (one
+// accumulator per chain of the tile, folds after the tile), 1 chain-major pipelined
+static std::atomic<int> g_screen_sched{-1};
+static int screen_sched() {
+    int v = g_screen_sched.load();
+    if (v < 0) {
+        v = env_int("IA_SCREEN_SCHED", 0) ? 1 : 0;
+        g_screen_sched.store(v);
+    }
+    return v;
+}
 
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st, const XJob *jobs,
@@ -474,14 +571,17 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
     IA_ARG(nb < (1L << 31), "screen grid too large");
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || jobs), "launch_screen16: bad batch");
     const dim3 grid((unsigned)nb, (unsigned)njobs);
+    const int sched = screen_sched();
+#define IA_SCREEN16_SCHED(GG, SS)                                                               \
+    if (img)                                                                                    \
+        k_screen16i<GG, SS><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
+                                                  groups, segmin, nseg, jobs, parity);          \
+    else                                                                                        \
+        k_screen16<GG, SS><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,   \
+                                                 groups, segmin, nseg, jobs, parity);
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
-        if (img)                                                                                \
-            k_screen16i<GG><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
-                                                  groups, segmin, nseg, jobs, parity);          \
-        else                                                                                    \
-            k_screen16<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,   \
-                                                 groups, segmin, nseg, jobs, parity);           \
+        if (sched) { IA_SCREEN16_SCHED(GG, 1) } else { IA_SCREEN16_SCHED(GG, 0) }               \
         break;
     switch (G) {
         IA_SCREEN16_CASE(1)
@@ -498,8 +598,19 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
         default: set_error("launch_screen16: bad query split"); return IA_E_ARG;
     }
 #undef IA_SCREEN16_CASE
+#undef IA_SCREEN16_SCHED
     IA_LAUNCH_CHECK("k_screen16");
     return IA_OK;
 }
+
+}  // namespace ia
+
+extern "C" int ia_diag_set_screen_sched(int sched) {
+    const int prev = ia::screen_sched();
+    if (sched >= 0 && sched <= 1) ia::g_screen_sched.store(sched);
+    return prev;
+}
+
+namespace ia {
 
 }  // namespace ia

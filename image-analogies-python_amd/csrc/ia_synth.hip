@@ -130,7 +130,7 @@ __global__ __launch_bounds__(128) void k_peer_finish(DbSrc src, const Best *__re
         if (lane == 0) cs = c;
     } else {
         const bool tron = f.px.trace && m < 8 && f.px.epoch < 1024;
-        unsigned long long *tr = tron ? reinterpret_cast<unsigned long long *>(f.px.trace) +
+        unsigned long long *tr = tron ? reinterpret_cast<unsigned long long *>(f.px.trace.get()) +
                                             ((long)f.px.epoch * 8 + m) * 12
                                       : nullptr;
         peer_collect(f.px, m, lane, gd, gw, tr ? tr + 4 : nullptr);

@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
                 const long seg = full ? (k >> lseg) : slist[k >> lseg];
                 const long lr = seg_lrow(a.smap, seg, a.seg_rows, k & (a.seg_rows - 1));
                 half8 g0[DB16_GROUPS], g1[DB16_GROUPS];
-                load_row16(reinterpret_cast<const half8 *>(a.db), lr < a.nrows ? lr : 0, g0, g1);
+                load_row16(reinterpret_cast<const half8 *>(a.db.get()), lr < a.nrows ? lr : 0, g0, g1);
                 take(lr, rescreen16(g0, g1, qf, twoR));
             }
         }

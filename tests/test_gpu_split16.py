@@ -146,12 +146,22 @@ def test_split16_segment_minima_within_bound(gpu, scale):
     assert worst < 1.0
 
 
-def test_split16_screen_every_query_split(gpu):
+@pytest.mark.parametrize('sched', [0, 1])
+def test_split16_screen_every_query_split(gpu, sched):
     """k_screen16 at query counts that hit every block shape (G = 1..11 query tiles, and
     launches of more than 11 tiles split into equal groups) on a 1M-row level (8192-row
     chunks: 16 segments per chunk, many stages): every segment minimum within eps16 of
     the fp64 value, and the image-form stream (k_screen16i) gives the same minima bit for
-    bit."""
+    bit; for both stage schedules (ia_diag_set_screen_sched: tile-major, chain-major)."""
+    import _ia
+    prev = _ia.lib().ia_diag_set_screen_sched(sched)
+    try:
+        _every_query_split()
+    finally:
+        _ia.lib().ia_diag_set_screen_sched(prev)
+
+
+def _every_query_split():
     import algorithms
     A, Aps, _ = analogy_inputs(45, (1024, 1024), (8, 8), n_ap=1)
     A_pyr = o.compute_gaussian_pyramid(A, 3, cap=2)

@@ -1,0 +1,95 @@
+"""Image-form screen timing on c4's finest level (the product's dominant kernel,
+k_screen16i<G> in strip order over the 4,194,304-row DB) for each stage schedule
+(ia_diag_set_screen_sched), at M queries taken from tests/golden/c4_queries.npz; checks
+that every schedule gives the same segment minima bit for bit.
+
+  python tools/screen_img_bench.py [--M 342,256,128] [--reps 20] [--sched 0,1]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'image-analogies-python_amd'))
+sys.path.insert(0, ROOT)
+
+import _ia            # noqa: E402
+import algorithms     # noqa: E402
+import bench          # noqa: E402
+import config as cfg  # noqa: E402
+import img_preprocess as ip  # noqa: E402
+
+F16_PEAK = 4096.0 * 256 * 2.4e9 / 1e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--M', default='342,256,128')
+    ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--sched', default='0,1')
+    args = ap.parse_args()
+    Ms = [int(x) for x in args.M.split(',')]
+    scheds = [int(x) for x in args.sched.split(',')]
+    dev = torch.device('cuda', 0)
+    job = bench.Job(bench.CONFIGS['c4'], 0, dev)
+    A_pyr = ip.gaussian_pyramid_dev(job.A, cfg.n_sm, job.levels)
+    Ap_pyr = ip.gaussian_pyramid_dev(job.Ap, cfg.n_sm, job.levels)
+    level = job.max_levels - 1
+    idx = algorithms.level_index(A_pyr, [Ap_pyr], level)
+    assert idx.dbi is not None
+    lib = _ia.lib()
+    N = idx.nrows
+    g = np.load(os.path.join(ROOT, 'tests', 'golden', 'c4_queries.npz'))
+    Mmax = max(Ms)
+    Q = np.asarray(g['q'][:Mmax], dtype=np.float64)
+    qrows = lib.ia_diag_qp_rows(Mmax)
+    q64 = torch.zeros((Mmax, _ia.IA_DP), dtype=torch.float64, device=dev)
+    q64[:, :55] = torch.as_tensor(Q).to(dev)
+    qp = torch.zeros((qrows, _ia.IA_DP), dtype=torch.float32, device=dev)
+    q16 = torch.zeros((qrows, 256), dtype=torch.float16, device=dev)
+    nq = torch.zeros(qrows, dtype=torch.float64, device=dev)
+    st = _ia.stream()
+    _ia.check(lib.ia_diag_query_rows16(_ia.ptr(q64), Mmax, _ia.ptr(idx.center), _ia.ptr(idx.amax),
+                                       _ia.ptr(qp), _ia.ptr(q16), _ia.ptr(nq), st), 'query rows')
+    nseg = lib.ia_db_rows_padded(N) // min(lib.ia_db_chunk_rows(N), 512)
+    ref = {}
+    prev = lib.ia_diag_set_screen_sched(-1)
+    for M in Ms:
+        for sc in scheds:
+            lib.ia_diag_set_screen_sched(sc)
+            segmin = torch.full((qrows, nseg), float('nan'), dtype=torch.float32, device=dev)
+
+            def run():
+                _ia.check(lib.ia_diag_screen16_image(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.dbi),
+                                                     _ia.ptr(q16), M, _ia.ptr(segmin), st), 'screen')
+            run()
+            torch.cuda.synchronize()
+            key = segmin[:M].view(torch.int32).clone()
+            same = None
+            if M in ref:
+                same = bool(torch.equal(ref[M], key))
+            else:
+                ref[M] = key
+            ts = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                run()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3)
+            ts.sort()
+            med = ts[len(ts) // 2]
+            pairs = float(M) * N
+            print('M %3d sched %d: median %7.1f us  min %7.1f us  pipe_frac %.3f  frac %.3f  same_minima %s'
+                  % (M, sc, med, ts[0], 330 * pairs / (med * 1e-6) / 1e12 / F16_PEAK,
+                     110 * pairs / (med * 1e-6) / 1e12 / F16_PEAK, same), flush=True)
+    lib.ia_diag_set_screen_sched(prev)
+
+
+if __name__ == '__main__':
+    main()
