@@ -142,6 +142,7 @@ _SIGS = {
     'ia_diag_set_graph_mode': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_xwave': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_sched': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_screen_pc': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_xwave_trace': (ctypes.c_int, [_dp]),
     'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_pyr_form': (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),

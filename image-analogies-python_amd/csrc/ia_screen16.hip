@@ -219,6 +219,13 @@ __device__ __forceinline__ void load_queries(const half8 *__restrict__ q16, half
     }
 }
 
+// a workgroup barrier ordering LDS only (no wait for global loads in flight)
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // every wave's copies of the next stage retired, then the barrier (the compiler's own wait
 // before __syncthreads() does not cover global_load_lds)
 __device__ __forceinline__ void copies_barrier() {
@@ -445,6 +452,131 @@ __device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring
     }
 }
 
+// ---- strips, producer / consumer (IA_SCREEN_PC=1): k_screen16p -----------------------
+// One 8-wave workgroup per CU.  Waves 0-3 (one per SIMD) only run MFMA stages: the same
+// chains as strip_body (chain-major, the next stage tile's operand prefetched).  Waves 4-7
+// (the other wave of each SIMD) expand stage s + 1's operand from the rings into the second
+// operand buffer and copy stage s + 2's window rows into the rings while the MFMA waves run
+// stage s, so the matrix pipe never waits on an expansion: one barrier per stage hands the
+// operand buffers over.  Rings as strip_body's with a third norm slot (rows two stages
+// ahead: A fine needs 6 of its 8 slots, A' fine 4 of 4, coarse 4 of 4 each).
+constexpr int RP_NM = RW_NM, RP_B = RW_NM + 3 * 512;
+
+// stage s + 2's new rows (stage s + 1 -> s + 2 is one scanline down), wave X of the
+// expanders; nslot = (s + 2) % 3
+__device__ __forceinline__ void rp_rows(const ImgDb &im, const WinSrc &w1, const WinSrc &w2, char *ring,
+                                        int nslot, int X, int lane) {
+    const bool cnew = (w2.y >> 1) != (w1.y >> 1);
+    if (X == 0) rw_load(im, w2, ring, 0, w2.y + 4, 0, lane);
+    else if (X == 1) rw_load(im, w2, ring, 1, w2.y + 2, 0, lane);
+    else if (X == 2) {
+        // norm slots: rw_load's kind 4 writes slot nslot of RW_NM..; three slots here
+        if (lane < 32)
+            __builtin_amdgcn_global_load_lds((const void *)(im.norm.get() + w2.lrow + 4 * lane),
+                                             (void *)(ring + RP_NM + nslot * 512), 16, 0, 2);
+    } else if (cnew) {
+        rw_load(im, w2, ring, 2, (w2.y >> 1) + 3, 0, lane);
+        rw_load(im, w2, ring, 3, (w2.y >> 1) + 3, 0, lane);
+    }
+}
+
+template <int G, int W>
+__device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps,
+                                        const half8 *__restrict__ q16) {
+    constexpr int NS = bal_ns(G, W);
+    const int lane = threadIdx.x & 63;
+    half8 bq[NS][Q16_GROUPS];
+    load_queries<G, W, NS>(q16, bq, lane);
+    float mn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    lds_sync();       // the expanders' first window landed (their first barrier)
+    for (int s = 0; s < nstage; ++s) {
+        lds_sync();   // barrier s: operand s is complete (and operand s - 1 free for s + 1)
+        stage_mfma_cm<G, W, NS>(E + (s & 1) * STAGE_H8, bq, mn, lane);
+        stage_close<G, W, NS>(s, tps, smin, mn, lane);
+    }
+    lds_sync();       // the last stage's operand reads done (pairs with the expanders' last)
+}
+
+template <int X>
+__device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring, const StageMap &sm,
+                                          long chunk, int nstage) {
+    const int lane = threadIdx.x & 63;
+    // stage 0's whole window and stage 1's new rows, then operand 0
+    WinSrc w0 = win_src(im, stage_lrow(sm, chunk, 0));
+    for (int j = X; j < 15; j += 4) {
+        const int kind = j < 5 ? 0 : j < 8 ? 1 : j < 11 ? 2 : j < 14 ? 3 : 4;
+        const int r = j < 5 ? w0.y + j : j < 8 ? w0.y + j - 5 : j < 11 ? (w0.y >> 1) + 1 + j - 8
+                                                                      : (w0.y >> 1) + 1 + j - 11;
+        rw_load(im, w0, ring, kind, r, 0, lane);
+    }
+    WinSrc w1 = nstage > 1 ? win_src(im, stage_lrow(sm, chunk, 1)) : w0;
+    if (nstage > 1) rp_rows(im, w0, w1, ring, 1, X, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_sync();   // every expander's copies landed
+    expand_ring<X>(ring, w0.y, 0, E, lane);
+    for (int s = 0; s < nstage; ++s) {
+        // barrier s: operand s complete, stage s + 1's rows landed, operand (s + 1) & 1 free
+        lds_sync();
+        if (s + 1 < nstage) {
+            if (s + 2 < nstage) {
+                const WinSrc w2 = win_src(im, stage_lrow(sm, chunk, s + 2));
+                rp_rows(im, w1, w2, ring, (s + 2) % 3, X, lane);
+                expand_ring<X>(ring, w1.y, (s + 1) % 3, E + ((s + 1) & 1) * STAGE_H8, lane);
+                w1 = w2;
+            } else {
+                expand_ring<X>(ring, w1.y, (s + 1) % 3, E + ((s + 1) & 1) * STAGE_H8, lane);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    lds_sync();
+}
+
+template <int G>
+__global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int ch, int seg_rows,
+                                                      StageMap sm, const half8 *__restrict__ q16,
+                                                      int M, int groups, float *__restrict__ segmin,
+                                                      long nseg, const XJob *jobs, int parity) {
+    __shared__ half8 E[2 * STAGE_H8];
+    if (jobs) {   // batch: this job's image-form sections, query rows and minima
+        const XJob &J = jobs[blockIdx.y];
+        im.fa = J.fa; im.ca = J.ca; im.norm = J.norm; im.ap = J.ap;
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity].get());
+        segmin = J.segmin;
+    }
+    __shared__ __attribute__((aligned(16))) char ring[RP_B];
+    __shared__ int smin[SPC_MAX * G * 32];
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;   // uniform over the block, before any barrier
+    const int spc = ch / seg_rows;
+    for (int i = threadIdx.x; i < spc * G * 32; i += 512) smin[i] = 0x7fffffff;
+    const int nstage = ch / (STAGE_TILES * 32);
+    const int tps = seg_rows >> 5;
+    const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // waves 0-3 and 4-7 pair up on the SIMDs (wave w and w + 4 share SIMD w % 4)
+    if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg);
+    else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg);
+    else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg);
+    else if (wv == 3) pc_mfma<G, 3>(E, smin, nstage, tps, qg);
+    else if (wv == 4) pc_expand<0>(im, E, ring, sm, chunk, nstage);
+    else if (wv == 5) pc_expand<1>(im, E, ring, sm, chunk, nstage);
+    else if (wv == 6) pc_expand<2>(im, E, ring, sm, chunk, nstage);
+    else pc_expand<3>(im, E, ring, sm, chunk, nstage);
+    __syncthreads();
+    const long seg0 = (long)chunk * spc;
+    const int q0 = group * G * 32;
+    for (int i = threadIdx.x; i < G * 32 * spc; i += 512) {
+        const int ql = i / spc, sg = i - ql * spc;
+        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
+    }
+}
+
 // grid: (nchunks rounded up to 8) x groups, XCD-aware: all groups of a chunk share
 // blockIdx % 8 (one XCD under round-robin dispatch), so the chunk is fetched from HBM once
 // per launch.  Group g holds query tiles [g G, g G + G).
@@ -549,6 +681,17 @@ static int screen_sched() {
     }
     return v;
 }
+// strip-order image-form levels: the producer / consumer kernel k_screen16p (IA_SCREEN_PC /
+// ia_diag_set_screen_pc: 1) or k_screen16i's 4-wave body (0)
+static std::atomic<int> g_screen_pc{-1};
+static int screen_pc() {
+    int v = g_screen_pc.load();
+    if (v < 0) {
+        v = env_int("IA_SCREEN_PC", 0) ? 1 : 0;
+        g_screen_pc.store(v);
+    }
+    return v;
+}
 
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st, const XJob *jobs,
@@ -572,6 +715,7 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || jobs), "launch_screen16: bad batch");
     const dim3 grid((unsigned)nb, (unsigned)njobs);
     const int sched = screen_sched();
+    const bool pc = img && sm.W > 0 && screen_pc();
 #define IA_SCREEN16_SCHED(GG, SS)                                                               \
     if (img)                                                                                    \
         k_screen16i<GG, SS><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
@@ -581,7 +725,10 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
                                                  groups, segmin, nseg, jobs, parity);
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
-        if (sched) { IA_SCREEN16_SCHED(GG, 1) } else { IA_SCREEN16_SCHED(GG, 0) }               \
+        if (pc)                                                                                 \
+            k_screen16p<GG><<<grid, 512, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
+                                                  groups, segmin, nseg, jobs, parity);          \
+        else if (sched) { IA_SCREEN16_SCHED(GG, 1) } else { IA_SCREEN16_SCHED(GG, 0) }          \
         break;
     switch (G) {
         IA_SCREEN16_CASE(1)
@@ -608,6 +755,12 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
 extern "C" int ia_diag_set_screen_sched(int sched) {
     const int prev = ia::screen_sched();
     if (sched >= 0 && sched <= 1) ia::g_screen_sched.store(sched);
+    return prev;
+}
+
+extern "C" int ia_diag_set_screen_pc(int on) {
+    const int prev = ia::screen_pc();
+    if (on >= 0 && on <= 1) ia::g_screen_pc.store(on);
     return prev;
 }
 

@@ -53,10 +53,17 @@ def decide(As, A_shape, q, app_row, s, im, y, x, W, weights, kappa_factor):
     return pr, pc, pimg
 
 
-def sample_pixels(H, W, rng, n_rand=256):
-    """Border, corner and interior pixels of an H x W level (deterministic given rng)."""
+def sample_pixels(H, W, rng, n_rand=256, full_rows=(), border_step=0):
+    """Border, corner and interior pixels of an H x W level (deterministic given rng);
+    full_rows: whole scanlines added; border_step > 0: every border_step-th pixel of the
+    four borders (plus the two pixels next to each corner) added."""
     rows = sorted({0, 1, 2, 3, H // 2, H - 3, H - 2, H - 1})
     cols = sorted({0, 1, 2, 3, W // 3, W // 2, W - 3, W - 2, W - 1})
     px = [(y, x) for y in rows for x in cols if 0 <= y < H and 0 <= x < W]
     px += [(int(y), int(x)) for y, x in zip(rng.randint(0, H, n_rand), rng.randint(0, W, n_rand))]
+    for y in full_rows:
+        px += [(y, x) for x in range(W)]
+    if border_step:
+        px += [(y, x) for y in (0, H - 1) for x in list(range(0, W, border_step)) + [1, W - 2]]
+        px += [(y, x) for x in (0, W - 1) for y in list(range(0, H, border_step)) + [1, H - 2]]
     return sorted(set(px))

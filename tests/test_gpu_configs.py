@@ -4,10 +4,13 @@
       oracle's full scanline run (tests/golden/c3_oracle.npz, make_config_fixtures.py c3)
   c4  A = A' 2048x2048 x B 1024x1024: (1) the matcher over the 4,194,304-row finest
       database against the oracle's exact 1-NN of 500+ queries captured from a GPU
-      synthesis plus near-ties (tests/golden/c4_queries.npz); (2) the whole synthesis,
-      spot-checked: at hundreds of border / interior pixels of the two largest levels the
-      reference's decision is re-derived from the run's own state with the oracle
-      (tests/spotcheck.py) and must equal what the GPU wrote; B' == A'[im][s] everywhere
+      synthesis plus near-ties (tests/golden/c4_queries.npz); (2) the whole synthesis:
+      every level below the finest bit-exact against the oracle's full run
+      (tests/golden/c4_levels.npz), the finest level re-derived by the oracle from the
+      run's own state at > 2,000 pixels incl. two whole scanlines and the borders
+      (tests/spotcheck.py); B' == A'[im][s] everywhere
+  c5  one whole 512x512 job (seed 1000), alone and inside a batch, bit-exact against the
+      oracle's full run (tests/golden/c5_job.npz)
   c2  180x117, kappa 5, LSH matcher: every level bit-exact against the oracle's scanline
       loop driven by the same LSH tables (oracle LshIndex)
 """
@@ -108,7 +111,7 @@ def test_c4_matcher_sharded_reduction_vs_oracle_fixture(gpu, G):
     assert len(bad) == 0, (len(bad), bad[:10])
 
 
-def _spot_check(job, out, level, n_rand, seed):
+def _spot_check(job, out, level, n_rand, seed, full_rows=(), border_step=0):
     import config as cfg
     A_pyr = [p.cpu().numpy() for p in _pyr(job, job.A)]
     Ap_pyr = [p.cpu().numpy() for p in _pyr(job, job.Ap)]
@@ -118,7 +121,7 @@ def _spot_check(job, out, level, n_rand, seed):
     s = out[level][0].cpu().numpy()
     im = out[level][1].cpu().numpy()
     H, W = B_pyr[level].shape
-    px = spotcheck.sample_pixels(H, W, np.random.RandomState(seed), n_rand)
+    px = spotcheck.sample_pixels(H, W, np.random.RandomState(seed), n_rand, full_rows, border_step)
     Q = spotcheck.queries(B_pyr, Bp, init, level, px)
     db = oc.LevelDB(level, A_pyr, [Ap_pyr])
     try:
@@ -138,18 +141,73 @@ def _spot_check(job, out, level, n_rand, seed):
     return len(px), wrong
 
 
-def test_c4_full_synthesis_spot_check(gpu):
+@pytest.mark.timeout(600)
+def test_c4_full_synthesis_vs_oracle(gpu):
+    """c4 whole (job seed 0): every level below the finest bit-exact against the oracle's
+    full scanline run (s, im, B' hash; tests/golden/c4_levels.npz: up to 512 x 512 pixels
+    against the 1,048,576-row database), and the finest level (1024 x 1024 pixels against
+    4,194,304 rows, beyond a full oracle run) re-derived by the oracle at > 2,000 pixels:
+    two whole scanlines, the four borders every 8 pixels, corners and 1,000 random pixels
+    (tests/spotcheck.py); B' == A'[im][s] at every pixel of every level."""
+    g = golden('c4_levels.npz')
     job = _job('c4')
     out = job.step()
     torch.cuda.synchronize()
+    assert job.max_levels == int(g['max_levels'])
     Ap_pyr = _pyr(job, job.Ap)
     for l, (s, im) in out.items():     # B' == A'[im][s] at every pixel of every level
         src = Ap_pyr[l]
         assert torch.equal(job.Bp[l].flatten(), src[s[:, 0].long(), s[:, 1].long()]), l
         assert int(im.max().item()) == 0 and int(im.min().item()) == 0
-    for level, n_rand, seed in ((job.max_levels - 1, 240, 7), (job.max_levels - 2, 120, 8)):
-        n, wrong = _spot_check(job, out, level, n_rand, seed)
-        assert not wrong, (level, n, wrong[:5])
+    for l in range(1, job.max_levels - 1):
+        s, im = out[l]
+        assert np.array_equal(s.cpu().numpy(), g['s%d' % l].astype(np.int32)), l
+        assert np.array_equal(im.cpu().numpy(), g['im%d' % l].astype(np.int32)), l
+        bp = job.Bp[l].cpu().numpy()
+        assert hashlib.sha256(np.ascontiguousarray(bp).tobytes()).hexdigest() == str(g['bp_sha%d' % l]), l
+    fin = job.max_levels - 1
+    H = job.Bp[fin].shape[0]
+    n, wrong = _spot_check(job, out, fin, 1000, 7, full_rows=(1, H // 2 + 1), border_step=8)
+    assert n >= 2000
+    assert not wrong, (fin, n, wrong[:5])
+
+
+def _c5_check(g, out, Bp):
+    assert sorted(out) == list(range(1, int(g['max_levels'])))
+    for l, r in out.items():
+        s, im = r[0], r[1]
+        assert np.array_equal(s.cpu().numpy(), g['s%d' % l].astype(np.int32)), l
+        assert np.array_equal(im.cpu().numpy(), g['im%d' % l].astype(np.int32)), l
+        bp = Bp[l].cpu().numpy()
+        assert hashlib.sha256(np.ascontiguousarray(bp).tobytes()).hexdigest() == str(g['bp_sha%d' % l]), l
+
+
+def test_c5_job_full_size_bit_exact_vs_oracle(gpu):
+    """c5's first job (512 x 512, seed 1000 = bench.py's rank 0 job 0, 349,184 B' pixels)
+    synthesised alone: every level's s / im / B' bit-exact against the oracle's whole
+    scanline run (tests/golden/c5_job.npz)."""
+    bench = _bench()
+    g = golden('c5_job.npz')
+    job = bench.Job(bench.CONFIGS['c5'], int(g['job_seed']), torch.device('cuda', 0))
+    assert job.max_levels == int(g['max_levels'])
+    out = job.step()
+    torch.cuda.synchronize()
+    _c5_check(g, out, job.Bp)
+
+
+def test_c5_job_in_a_batch_bit_exact_vs_oracle(gpu):
+    """The same job as the first of a 3-job batch (ia_synth_levels_batch: one screen and one
+    fused launch per wave serve all three, bench.py's c5 form): bit-exact against the
+    oracle's whole run."""
+    import image_analogies as ia
+    bench = _bench()
+    g = golden('c5_job.npz')
+    dev = torch.device('cuda', 0)
+    jobs = [bench.Job(bench.CONFIGS['c5'], int(g['job_seed']) + 3 * j, dev) for j in range(3)]
+    ins = [jb.prepare() for jb in jobs]
+    outs = ia.synthesize_batch_dev(ins, jobs[0].max_levels, [jb.k for jb in jobs], jobs[0].weights)
+    torch.cuda.synchronize()
+    _c5_check(g, outs[0], jobs[0].Bp)
 
 
 def test_c2_lsh_full_size_vs_oracle(gpu):

@@ -146,19 +146,22 @@ def test_split16_segment_minima_within_bound(gpu, scale):
     assert worst < 1.0
 
 
-@pytest.mark.parametrize('sched', [0, 1])
-def test_split16_screen_every_query_split(gpu, sched):
+@pytest.mark.parametrize('sched,pc', [(0, 0), (1, 0), (0, 1)])
+def test_split16_screen_every_query_split(gpu, sched, pc):
     """k_screen16 at query counts that hit every block shape (G = 1..11 query tiles, and
     launches of more than 11 tiles split into equal groups) on a 1M-row level (8192-row
     chunks: 16 segments per chunk, many stages): every segment minimum within eps16 of
     the fp64 value, and the image-form stream (k_screen16i) gives the same minima bit for
-    bit; for both stage schedules (ia_diag_set_screen_sched: tile-major, chain-major)."""
+    bit; for both stage schedules (ia_diag_set_screen_sched: tile-major, chain-major) and
+    the producer / consumer strip kernel (ia_diag_set_screen_pc)."""
     import _ia
     prev = _ia.lib().ia_diag_set_screen_sched(sched)
+    prev_pc = _ia.lib().ia_diag_set_screen_pc(pc)
     try:
         _every_query_split()
     finally:
         _ia.lib().ia_diag_set_screen_sched(prev)
+        _ia.lib().ia_diag_set_screen_pc(prev_pc)
 
 
 def _every_query_split():

@@ -3,7 +3,8 @@ k_screen16i<G> in strip order over the 4,194,304-row DB) for each stage schedule
 (ia_diag_set_screen_sched), at M queries taken from tests/golden/c4_queries.npz; checks
 that every schedule gives the same segment minima bit for bit.
 
-  python tools/screen_img_bench.py [--M 342,256,128] [--reps 20] [--sched 0,1]
+  python tools/screen_img_bench.py [--M 342,256,128] [--reps 20] [--forms s0,s1,pc]
+  (s0 / s1: k_screen16i with the tile-major / chain-major stage; pc: k_screen16p)
 """
 import argparse
 import ctypes
@@ -30,10 +31,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--M', default='342,256,128')
     ap.add_argument('--reps', type=int, default=20)
-    ap.add_argument('--sched', default='0,1')
+    ap.add_argument('--forms', default='s0,s1,pc')
     args = ap.parse_args()
     Ms = [int(x) for x in args.M.split(',')]
-    scheds = [int(x) for x in args.sched.split(',')]
+    forms = args.forms.split(',')
     dev = torch.device('cuda', 0)
     job = bench.Job(bench.CONFIGS['c4'], 0, dev)
     A_pyr = ip.gaussian_pyramid_dev(job.A, cfg.n_sm, job.levels)
@@ -58,9 +59,11 @@ def main():
     nseg = lib.ia_db_rows_padded(N) // min(lib.ia_db_chunk_rows(N), 512)
     ref = {}
     prev = lib.ia_diag_set_screen_sched(-1)
+    prev_pc = lib.ia_diag_set_screen_pc(-1)
     for M in Ms:
-        for sc in scheds:
-            lib.ia_diag_set_screen_sched(sc)
+        for sc in forms:
+            lib.ia_diag_set_screen_sched(1 if sc == 's1' else 0)
+            lib.ia_diag_set_screen_pc(1 if sc == 'pc' else 0)
             segmin = torch.full((qrows, nseg), float('nan'), dtype=torch.float32, device=dev)
 
             def run():
@@ -85,10 +88,11 @@ def main():
             ts.sort()
             med = ts[len(ts) // 2]
             pairs = float(M) * N
-            print('M %3d sched %d: median %7.1f us  min %7.1f us  pipe_frac %.3f  frac %.3f  same_minima %s'
+            print('M %3d %s: median %7.1f us  min %7.1f us  pipe_frac %.3f  frac %.3f  same_minima %s'
                   % (M, sc, med, ts[0], 330 * pairs / (med * 1e-6) / 1e12 / F16_PEAK,
                      110 * pairs / (med * 1e-6) / 1e12 / F16_PEAK, same), flush=True)
     lib.ia_diag_set_screen_sched(prev)
+    lib.ia_diag_set_screen_pc(prev_pc)
 
 
 if __name__ == '__main__':
