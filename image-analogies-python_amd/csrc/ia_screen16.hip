@@ -150,7 +150,7 @@ __device__ __forceinline__ void fold_min(const floatx16 &x, float &mn) {
     mn = fminf(fminf(mn, u0), u1);
 }
 
-template <int G, int W, int NS>
+template <int G, int W, int NS, bool CM_PIN = false>
 __device__ __forceinline__ void stage_mfma_cm(const half8 *sb, const half8 (&bq)[NS][Q16_GROUPS],
                                               float (&mn)[NS], int lane) {
     constexpr int NC = ch_count<G, W>();
@@ -177,6 +177,24 @@ __device__ __forceinline__ void stage_mfma_cm(const half8 *sb, const half8 (&bq)
         for (int m = 1; m < MFMA16; ++m)
             acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][mfma_a(m)], bq[k][mfma_b(m)], acc[cb],
                                                              0, 0, 0);
+        if constexpr (CM_PIN) {
+            // this chain's region: [operand reads,] MFMA, then the previous chain's fold two
+            // VALU at a time between the next MFMAs (each pair well inside an MFMA's 32
+            // cycles), then the rest of the chain
+            if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c))
+                __builtin_amdgcn_sched_group_barrier(0x100, DB16_GROUPS, 0);   // DS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if constexpr (c > 0) {
+                static_for<0, 4>([&](auto) {
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                });
+                __builtin_amdgcn_sched_group_barrier(0x008, MFMA16 - 5, 0);
+            } else {
+                __builtin_amdgcn_sched_group_barrier(0x008, MFMA16 - 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
     });
     fold_min(acc[(NC - 1) & 1], mn[ch_k<G, W>(NC - 1)]);
 }
@@ -456,28 +474,90 @@ __device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring
 // One 8-wave workgroup per CU.  Waves 0-3 (one per SIMD) only run MFMA stages: the same
 // chains as strip_body (chain-major, the next stage tile's operand prefetched).  Waves 4-7
 // (the other wave of each SIMD) expand stage s + 1's operand from the rings into the second
-// operand buffer and copy stage s + 2's window rows into the rings while the MFMA waves run
-// stage s, so the matrix pipe never waits on an expansion: one barrier per stage hands the
-// operand buffers over.  Rings as strip_body's with a third norm slot (rows two stages
-// ahead: A fine needs 6 of its 8 slots, A' fine 4 of 4, coarse 4 of 4 each).
-constexpr int RP_NM = RW_NM, RP_B = RW_NM + 3 * 512;
+// operand buffer while the MFMA waves run stage s, so the matrix pipe never waits on an
+// expansion: one barrier per stage hands the operand buffers over.  Window rows are copied
+// three stages ahead and waited one stage later (a copy has a whole MFMA stage to land):
+// rings of 8 slots per image (rows in use: 5 + 2 in flight for A fine, 3 + 2 for the others)
+// and 4 norm slots.
+#ifndef IA_PC_PIN
+#define IA_PC_PIN 0
+#endif
+constexpr bool PC_PIN = IA_PC_PIN;   // k_screen16p pins its MFMA stage's schedule (CM_PIN)
+#ifndef IA_PC_AHEAD
+#define IA_PC_AHEAD 3
+#endif
+constexpr int PC_AHEAD = IA_PC_AHEAD;   // stages ahead the expanders request window rows (2, 3)
+static_assert(PC_AHEAD == 2 || PC_AHEAD == 3, "ring depth");
+constexpr int RP_FA = 0, RP_FP = RP_FA + 8 * FROW_B, RP_CA = RP_FP + 8 * FROW_B;
+constexpr int RP_CP = RP_CA + 8 * CROW_B, RP_NM = RP_CP + 8 * CROW_B, RP_B = RP_NM + 4 * 512;
 
-// stage s + 2's new rows (stage s + 1 -> s + 2 is one scanline down), wave X of the
-// expanders; nslot = (s + 2) % 3
+// one window row job into the 8-slot rings (as rw_load): kind 0 A fine, 1 A' fine, 2 A
+// coarse, 3 A' coarse (padded image row r), 4 norms (slot nslot)
+__device__ __forceinline__ void rp_load(const ImgDb &im, const WinSrc &w, char *ring, int kind, int r,
+                                        int nslot, int lane) {
+    const uint32_t *src;
+    char *dst;
+    int n;
+    if (kind == 0) { src = im.fa + (long)r * im.Wp + w.x0; dst = ring + RP_FA + (r & 7) * FROW_B; n = WF_PC; }
+    else if (kind == 1) { src = w.fp + (long)r * im.Wp + w.x0; dst = ring + RP_FP + (r & 7) * FROW_B; n = WF_PC; }
+    else if (kind == 2) { src = im.ca + (long)r * im.Wcp + (w.x0 >> 1); dst = ring + RP_CA + (r & 7) * CROW_B; n = WC_PC; }
+    else if (kind == 3) { src = w.cp + (long)r * im.Wcp + (w.x0 >> 1); dst = ring + RP_CP + (r & 7) * CROW_B; n = WC_PC; }
+    else { src = im.norm + w.lrow; dst = ring + RP_NM + nslot * 512; n = 32; }
+    if (lane < n) __builtin_amdgcn_global_load_lds((const void *)(src + 4 * lane), (void *)dst, 16, 0, 2);
+}
+
+// the rows stage w2 adds to stage w1 (one scanline down), expander X: exactly RP_N(X) copies
+// (X 3 re-copies the current coarse rows when w2 starts none: identical bytes into the
+// slots they already hold, so that every iteration waits on a fixed count)
+__host__ __device__ constexpr int rp_n(int X) { return X == 3 ? 2 : 1; }
+template <int X>
 __device__ __forceinline__ void rp_rows(const ImgDb &im, const WinSrc &w1, const WinSrc &w2, char *ring,
-                                        int nslot, int X, int lane) {
-    const bool cnew = (w2.y >> 1) != (w1.y >> 1);
-    if (X == 0) rw_load(im, w2, ring, 0, w2.y + 4, 0, lane);
-    else if (X == 1) rw_load(im, w2, ring, 1, w2.y + 2, 0, lane);
-    else if (X == 2) {
-        // norm slots: rw_load's kind 4 writes slot nslot of RW_NM..; three slots here
-        if (lane < 32)
-            __builtin_amdgcn_global_load_lds((const void *)(im.norm.get() + w2.lrow + 4 * lane),
-                                             (void *)(ring + RP_NM + nslot * 512), 16, 0, 2);
-    } else if (cnew) {
-        rw_load(im, w2, ring, 2, (w2.y >> 1) + 3, 0, lane);
-        rw_load(im, w2, ring, 3, (w2.y >> 1) + 3, 0, lane);
+                                        int nslot, int lane) {
+    (void)w1;
+    if constexpr (X == 0) rp_load(im, w2, ring, 0, w2.y + 4, 0, lane);
+    else if constexpr (X == 1) rp_load(im, w2, ring, 1, w2.y + 2, 0, lane);
+    else if constexpr (X == 2) rp_load(im, w2, ring, 4, 0, nslot, lane);
+    else {
+        rp_load(im, w2, ring, 2, (w2.y >> 1) + 3, 0, lane);
+        rp_load(im, w2, ring, 3, (w2.y >> 1) + 3, 0, lane);
     }
+}
+
+// expand_ring over the 8-slot rings
+template <int W>
+__device__ __forceinline__ void rp_expand(const char *ring, int y, int ns, half8 *E, int lane) {
+    constexpr int H = W & 1;
+    const int tile = 2 * (W >> 1) + (lane >> 5), j = lane & 31;
+    const int px = 32 * tile + j;
+    const int c1 = (y >> 1) + 1;
+    const char *fa[5], *fp[3], *ca[3], *cp[3];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) fa[r] = ring + RP_FA + ((y + r) & 7) * FROW_B + px * 4;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        fp[r] = ring + RP_FP + ((y + r) & 7) * FROW_B + px * 4;
+        ca[r] = ring + RP_CA + ((c1 + r) & 7) * CROW_B + (px >> 1) * 4;
+        cp[r] = ring + RP_CP + ((c1 + r) & 7) * CROW_B + (px >> 1) * 4;
+    }
+    const char *nm = ring + RP_NM + ns * 512 + px * 4;
+    half8 *e = E + tile * TILE_H8 + H * 32 + j;
+    static_for<0, DB16_GROUPS>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        constexpr int k0 = grp_k0(H, g);
+        constexpr int hb = grp_hi(H, g) ? 0 : 2;
+        half8 o;
+        static_for<0, 8>([&](auto ec) {
+            constexpr int k = k0 + decltype(ec)::value;
+            const char *b;
+            if constexpr (k < 9) b = ca[k / 3] + (k % 3 + 3) * 4;
+            else if constexpr (k < 34) b = fa[(k - 9) / 5] + ((k - 9) % 5 + 2) * 4;
+            else if constexpr (k < 43) b = cp[(k - 34) / 3] + ((k - 34) % 3 + 3) * 4;
+            else if constexpr (k < 55) b = fp[(k - 43) / 5] + ((k - 43) % 5 + 2) * 4;
+            else b = nm;
+            o[decltype(ec)::value] = *reinterpret_cast<const _Float16 *>(b + hb);
+        });
+        e[g * 64] = o;
+    });
 }
 
 template <int G, int W>
@@ -490,10 +570,10 @@ __device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps
     float mn[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
-    lds_sync();       // the expanders' first window landed (their first barrier)
+    lds_sync();       // the expanders' first windows landed (their first barrier)
     for (int s = 0; s < nstage; ++s) {
         lds_sync();   // barrier s: operand s is complete (and operand s - 1 free for s + 1)
-        stage_mfma_cm<G, W, NS>(E + (s & 1) * STAGE_H8, bq, mn, lane);
+        stage_mfma_cm<G, W, NS, PC_PIN>(E + (s & 1) * STAGE_H8, bq, mn, lane);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
     }
     lds_sync();       // the last stage's operand reads done (pairs with the expanders' last)
@@ -503,33 +583,43 @@ template <int X>
 __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring, const StageMap &sm,
                                           long chunk, int nstage) {
     const int lane = threadIdx.x & 63;
-    // stage 0's whole window and stage 1's new rows, then operand 0
-    WinSrc w0 = win_src(im, stage_lrow(sm, chunk, 0));
+    // stage 0's whole window, stages 1 and 2's new rows; wait for stages 0 and 1; operand 0
+    const WinSrc w0 = win_src(im, stage_lrow(sm, chunk, 0));
     for (int j = X; j < 15; j += 4) {
         const int kind = j < 5 ? 0 : j < 8 ? 1 : j < 11 ? 2 : j < 14 ? 3 : 4;
         const int r = j < 5 ? w0.y + j : j < 8 ? w0.y + j - 5 : j < 11 ? (w0.y >> 1) + 1 + j - 8
                                                                       : (w0.y >> 1) + 1 + j - 11;
-        rw_load(im, w0, ring, kind, r, 0, lane);
+        rp_load(im, w0, ring, kind, r, 0, lane);
     }
-    WinSrc w1 = nstage > 1 ? win_src(im, stage_lrow(sm, chunk, 1)) : w0;
-    if (nstage > 1) rp_rows(im, w0, w1, ring, 1, X, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_sync();   // every expander's copies landed
-    expand_ring<X>(ring, w0.y, 0, E, lane);
+    WinSrc wl = w0;                      // the last stage whose rows were requested
+    int req = 0;
+    for (int k = 1; k < PC_AHEAD && k < nstage; ++k) {
+        const WinSrc wk = win_src(im, stage_lrow(sm, chunk, k));
+        rp_rows<X>(im, wl, wk, ring, k & 3, lane);
+        wl = wk;
+        req = k;
+    }
+    if (PC_AHEAD == 3 && req == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_n(X)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_sync();   // every expander's copies of stages 0 and 1 landed
+    rp_expand<X>(ring, w0.y, 0, E, lane);
+    WinSrc wn = nstage > 1 ? win_src(im, stage_lrow(sm, chunk, 1)) : w0;   // the next to expand
     for (int s = 0; s < nstage; ++s) {
         // barrier s: operand s complete, stage s + 1's rows landed, operand (s + 1) & 1 free
         lds_sync();
-        if (s + 1 < nstage) {
-            if (s + 2 < nstage) {
-                const WinSrc w2 = win_src(im, stage_lrow(sm, chunk, s + 2));
-                rp_rows(im, w1, w2, ring, (s + 2) % 3, X, lane);
-                expand_ring<X>(ring, w1.y, (s + 1) % 3, E + ((s + 1) & 1) * STAGE_H8, lane);
-                w1 = w2;
-            } else {
-                expand_ring<X>(ring, w1.y, (s + 1) % 3, E + ((s + 1) & 1) * STAGE_H8, lane);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool more = s + PC_AHEAD < nstage;
+        if (more) {
+            const WinSrc w3 = win_src(im, stage_lrow(sm, chunk, s + PC_AHEAD));
+            rp_rows<X>(im, wl, w3, ring, (s + PC_AHEAD) & 3, lane);
+            wl = w3;
         }
+        if (s + 1 < nstage) {
+            rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
+            if (s + 2 < nstage) wn = win_src(im, stage_lrow(sm, chunk, s + 2));
+        }
+        // stage s + 2's rows (requested one iteration ago) land before barrier s + 1
+        if (PC_AHEAD == 3 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_n(X)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_sync();
 }
