@@ -53,7 +53,7 @@ HBM_PEAK_GBS = 8000.0
 # MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process).
 # The file records a hash of the screen's sources; a file from other sources is stale and
 # the bench then reports traffic null.
-SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r03_screen_traffic_bench_pmc.json')
+SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r04_screen_traffic_bench_pmc.json')
 SCREEN_SRCS = ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h')
 
 
@@ -74,7 +74,7 @@ def screen_pmc():
     return {'bytes': d['traffic_bytes'], 'kernel': d['kernel'], 'dispatches': d['dispatches'],
             'source': os.path.relpath(SCREEN_PMC_FILE, ROOT)}
 
-SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r03_screen_sq_pmc.json')
+SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r04_screen_sq_pmc.json')
 
 
 def screen_sq():
@@ -659,9 +659,12 @@ def main():
     traffic, pmc = None, screen_pmc()
     if pmc and args.config == 'c4' and world == 1 and domG == 11 and lsh is None:
         traffic = pmc['bytes']
-    # the finest level's screen streams the DB's image form when it applies (k_screen16i)
+    # the finest level's screen streams the DB's image form when it applies (k_screen16i;
+    # k_screen16p, the producer / consumer form, on strip-order levels: every c4 / c5 level)
     img_form = _ia.db_image_enabled() and jobs[0].A.shape[1] % 128 == 0 and lsh is None
-    roof = {'bound': 'mfma', 'kernel': ('k_screen16i<%s>' if img_form else 'k_screen16<%s>') % domG,
+    kname = ('k_screen16p<%s>' if _ia.lib().ia_diag_set_screen_pc(-1) else 'k_screen16i<%s>') \
+        if img_form else 'k_screen16<%s>'
+    roof = {'bound': 'mfma', 'kernel': kname % domG,
             'achieved': achieved,
             'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
             'frac': achieved / F16_MFMA_PEAK_TFLOPS, 'traffic': traffic,

@@ -777,7 +777,7 @@ static std::atomic<int> g_screen_pc{-1};
 static int screen_pc() {
     int v = g_screen_pc.load();
     if (v < 0) {
-        v = env_int("IA_SCREEN_PC", 0) ? 1 : 0;
+        v = env_int("IA_SCREEN_PC", 1) ? 1 : 0;
         g_screen_pc.store(v);
     }
     return v;

@@ -63,8 +63,8 @@ int ia_diag_set_xwave(int on);
 /* the split-f16 screen's stage schedule for this process (IA_SCREEN_SCHED): 0 tile-major,
  * 1 chain-major pipelined (same minima); returns the previous value, -1 leaves it */
 int ia_diag_set_screen_sched(int sched);
-/* strip-order image-form levels: the producer / consumer screen k_screen16p (1; IA_SCREEN_PC)
- * or k_screen16i (0); same minima; returns the previous value, -1 leaves it */
+/* strip-order image-form levels: the producer / consumer screen k_screen16p (1, default;
+ * IA_SCREEN_PC) or k_screen16i (0); same minima; returns the previous value, -1 leaves it */
 int ia_diag_set_screen_pc(int on);
 /* with IA_XW_TRACE=<level tag>: the fused kernel's phase stamps of that level (100 MHz
  * s_memrealtime) for waves < 4096 and the first 8 pixels of each, 12 stamps per pixel:

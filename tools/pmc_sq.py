@@ -24,9 +24,10 @@ def parse(path):
     return blocks
 
 
-def main(path, sub='k_screen16iILi11E'):
+def main(path, sub=None):
     b = parse(path)
-    name = next(k for k in b if sub in k)
+    subs = [sub] if sub else ['k_screen16pILi11E', 'k_screen16iILi11E']
+    name = next(k for s in subs for k in b if s in k)
     d = b[name]
     cyc = d['GRBM_GUI_ACTIVE'] / 8
     out = {'kernel': name, 'dispatches': d['dispatches'], 'mean_us': d['us'],
