@@ -203,6 +203,21 @@ class Job:
         return sum(bl[l][0] * bl[l][1] * al[l][0] * al[l][1] for l in range(1, self.max_levels))
 
 
+def wave_spacing(prof, level):
+    """Mean / median per-wave spacing of one level from the events pass (us)."""
+    recs = [p for p in prof if p['level'] == level and len(p.get('tail_ms', [])) > 1]
+    if not recs:
+        return None
+    scr = np.concatenate([p['launch_ms'] for p in recs]) * 1e3
+    tail = np.concatenate([p['tail_ms'] for p in recs]) * 1e3
+    gap = np.concatenate([p['gap_ms'][:-1] for p in recs]) * 1e3
+    return {'waves': int(len(scr)),
+            'screen_mean': float(scr.mean()), 'screen_p50': float(np.median(scr)),
+            'fused_tail_mean': float(tail.mean()), 'fused_tail_p50': float(np.median(tail)),
+            'gap_to_next_screen_mean': float(gap.mean()), 'gap_to_next_screen_p50': float(np.median(gap)),
+            'period_mean': float((scr.sum() + tail.sum() + gap.sum()) / len(scr))}
+
+
 def cpu_threads():
     """Host threads of the all-cores CPU baseline: OMP_NUM_THREADS when set (the GPU box
     sets it to the box's CPU share), else every CPU of this process's affinity mask."""
@@ -536,7 +551,7 @@ def main():
 
     def measure():
         # warm-up steps run profiled too; the event pool is created before any timed region
-        nev = 2 * args.steps * sum(jb.waves for jb in jobs)
+        nev = 3 * args.steps * sum(jb.waves for jb in jobs)
         _ia.prof_begin(nev)
         for _ in range(args.warmup):
             run_step(True)
@@ -752,6 +767,10 @@ def main():
                         max(1, pixels_per_step * args.steps // (world if args.config == 'c5' else 1))},
         'events_pass': {'ms_per_step': elapsed_ev / args.steps * 1e3,
                         'overhead': (elapsed_ev - elapsed) / elapsed,
+                        # the finest level's wave spacing on its stream (HIP events, no
+                        # profiler): screen, end of screen -> end of the fused kernel, and
+                        # end of the fused kernel -> start of the next screen
+                        'finest_wave_us': wave_spacing(prof, fin),
                         'note': 'the same K steps again with HIP events around every screen '
                                 'launch and the matcher statistics (the roofline\'s source); '
                                 '`value` is the pass without them'},

@@ -133,6 +133,8 @@ _SIGS = {
     'ia_peer_mem_kind': (ctypes.c_int, [_dp]),
     'ia_prof_begin': (ctypes.c_int, []),
     'ia_prof_prepare': (ctypes.c_int, [ctypes.c_long]),
+    'ia_prof_waves': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                     ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     'ia_prof_end': (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     'ia_prof_launches': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                         ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
@@ -143,6 +145,7 @@ _SIGS = {
     'ia_diag_set_xwave': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_sched': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_pc': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_screen_trace': (ctypes.c_int, [_dp]),
     'ia_diag_xwave_trace': (ctypes.c_int, [_dp]),
     'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_pyr_form': (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
@@ -271,6 +274,13 @@ def prof_end():
             check(got, 'ia_prof_launches')
         rec['launch_ms'] = np.array(ms[:got], dtype=np.float64)
         rec['launch_M'] = np.array(Ms[:got], dtype=np.int64)
+        tl = (ctypes.c_float * max(nl, 1))()
+        gp = (ctypes.c_float * max(nl, 1))()
+        got = lib().ia_prof_waves(r, tl, gp, nl)
+        if got < 0:
+            check(got, 'ia_prof_waves')
+        rec['tail_ms'] = np.array(tl[:got], dtype=np.float64)
+        rec['gap_ms'] = np.array(gp[:got], dtype=np.float64)
         out.append(rec)
     return out
 

@@ -560,9 +560,17 @@ __device__ __forceinline__ void rp_expand(const char *ring, int y, int ns, half8
     });
 }
 
+// stage timing of k_screen16p (ia_diag_screen_trace): blocks 0 and 300, every wave, per stage
+// (< 64) four s_memtime stamps: MFMA waves {barrier arrival, departure, MFMAs issued, close
+// done}; expanders {arrival, departure, copies issued + operand written, copies landed}
+__device__ unsigned long long *g_pc_trace;
+__device__ __forceinline__ void pc_stamp(unsigned long long *tr, int s, int k) {
+    if (tr && (threadIdx.x & 63) == 0 && s < 64) tr[s * 4 + k] = __builtin_readcyclecounter();
+}
+
 template <int G, int W>
 __device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps,
-                                        const half8 *__restrict__ q16) {
+                                        const half8 *__restrict__ q16, unsigned long long *tr) {
     constexpr int NS = bal_ns(G, W);
     const int lane = threadIdx.x & 63;
     half8 bq[NS][Q16_GROUPS];
@@ -572,16 +580,20 @@ __device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps
     for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
     lds_sync();       // the expanders' first windows landed (their first barrier)
     for (int s = 0; s < nstage; ++s) {
+        pc_stamp(tr, s, 0);
         lds_sync();   // barrier s: operand s is complete (and operand s - 1 free for s + 1)
+        pc_stamp(tr, s, 1);
         stage_mfma_cm<G, W, NS, PC_PIN>(E + (s & 1) * STAGE_H8, bq, mn, lane);
+        pc_stamp(tr, s, 2);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
+        pc_stamp(tr, s, 3);
     }
     lds_sync();       // the last stage's operand reads done (pairs with the expanders' last)
 }
 
 template <int X>
 __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring, const StageMap &sm,
-                                          long chunk, int nstage) {
+                                          long chunk, int nstage, unsigned long long *tr) {
     const int lane = threadIdx.x & 63;
     // stage 0's whole window, stages 1 and 2's new rows; wait for stages 0 and 1; operand 0
     const WinSrc w0 = win_src(im, stage_lrow(sm, chunk, 0));
@@ -606,7 +618,9 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
     WinSrc wn = nstage > 1 ? win_src(im, stage_lrow(sm, chunk, 1)) : w0;   // the next to expand
     for (int s = 0; s < nstage; ++s) {
         // barrier s: operand s complete, stage s + 1's rows landed, operand (s + 1) & 1 free
+        pc_stamp(tr, s, 0);
         lds_sync();
+        pc_stamp(tr, s, 1);
         const bool more = s + PC_AHEAD < nstage;
         if (more) {
             const WinSrc w3 = win_src(im, stage_lrow(sm, chunk, s + PC_AHEAD));
@@ -617,9 +631,11 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
             rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
             if (s + 2 < nstage) wn = win_src(im, stage_lrow(sm, chunk, s + 2));
         }
+        pc_stamp(tr, s, 2);
         // stage s + 2's rows (requested one iteration ago) land before barrier s + 1
         if (PC_AHEAD == 3 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_n(X)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        pc_stamp(tr, s, 3);
     }
     lds_sync();
 }
@@ -650,14 +666,16 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // waves 0-3 and 4-7 pair up on the SIMDs (wave w and w + 4 share SIMD w % 4)
-    if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg);
-    else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg);
-    else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg);
-    else if (wv == 3) pc_mfma<G, 3>(E, smin, nstage, tps, qg);
-    else if (wv == 4) pc_expand<0>(im, E, ring, sm, chunk, nstage);
-    else if (wv == 5) pc_expand<1>(im, E, ring, sm, chunk, nstage);
-    else if (wv == 6) pc_expand<2>(im, E, ring, sm, chunk, nstage);
-    else pc_expand<3>(im, E, ring, sm, chunk, nstage);
+    unsigned long long *tr = g_pc_trace;
+    tr = tr && (b == 0 || b == 300) ? tr + ((b == 0 ? 0 : 8) + wv) * 256 : nullptr;
+    if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 3) pc_mfma<G, 3>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 4) pc_expand<0>(im, E, ring, sm, chunk, nstage, tr);
+    else if (wv == 5) pc_expand<1>(im, E, ring, sm, chunk, nstage, tr);
+    else if (wv == 6) pc_expand<2>(im, E, ring, sm, chunk, nstage, tr);
+    else pc_expand<3>(im, E, ring, sm, chunk, nstage, tr);
     __syncthreads();
     const long seg0 = (long)chunk * spc;
     const int q0 = group * G * 32;
@@ -846,6 +864,12 @@ extern "C" int ia_diag_set_screen_sched(int sched) {
     const int prev = ia::screen_sched();
     if (sched >= 0 && sched <= 1) ia::g_screen_sched.store(sched);
     return prev;
+}
+
+extern "C" int ia_diag_screen_trace(void *buf) {
+    unsigned long long *p = reinterpret_cast<unsigned long long *>(buf);
+    IA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ia::g_pc_trace), &p, sizeof(p), 0, hipMemcpyHostToDevice));
+    return IA_OK;
 }
 
 extern "C" int ia_diag_set_screen_pc(int on) {

@@ -406,7 +406,7 @@ struct LevelRun {
         Bp = ImgPair{a->Bp_sm, a->Bp_lg, a->B_hs, a->B_ws, H, W};
         prof = !member && (a->flags & IA_SYNTH_PROF) && prof_active();
         timed = prof;
-        if (prof && (rc = prof_reserve(2 * (size_t)nw, &ev0, &hstats))) return rc;
+        if (prof && (rc = prof_reserve(3 * (size_t)nw, &ev0, &hstats))) return rc;
         // fused tail (one launch + one round trip less per wave): on a single shard the exact
         // stage's last kernel (k_rescore, or k_gather of the work list) runs the pixel tail;
         // on a sharded DB it prepares the tail (coherence pick, the winner's weighted
@@ -450,8 +450,8 @@ struct LevelRun {
         if ((rc = launch_query_wave(B, Bp, t, y_lo, M, a->center, ws.q64, ws.qp, ws.nq, a->amax,
                                     ws.q16, sq)))
             return rc;
-        hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
-        hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
+        hipEvent_t e0 = timed ? prof_event(ev0 + 3 * nscreen) : nullptr;
+        hipEvent_t e1 = timed ? prof_event(ev0 + 3 * nscreen + 1) : nullptr;
         FinishArgs fa{t, y_lo, W, a->N_total, a->weights, a->kappa_factor, a->Bp_lg, a->s,
                       a->im, a->dbg_px, a->dbg_dist,
                       a->comm && !peer && shard_tail() ? ws.rec_local : nullptr,
@@ -476,6 +476,8 @@ struct LevelRun {
         // dispatches in flight (rocprofv3 --pmc runs of the whole bench crash otherwise)
         static const int sync_every = env_int("IA_SYNC_EVERY", 0);
         if (sync_every > 0 && t % sync_every == sync_every - 1) IA_HIP(hipStreamSynchronize(sq));
+        // e2 of this wave: right after the exact stage (the unfused tails are not bracketed)
+        if (timed) IA_HIP(hipEventRecord(prof_event(ev0 + 3 * (nscreen - 1) + 2), sq));
         if (fused) return IA_OK;   // the exact stage already ran the per-pixel tail
         if (peer) {                // collect the ranks' winners, finish the pixel
             k_peer_finish<<<M, 128, 0, sq>>>(src, ws.best_local, fa, ws.q64);
@@ -588,8 +590,8 @@ struct LevelRun {
                "ia_synth_level: an image-form DB for a level it does not apply to");
         IA_ARG(im || a->db, "ia_synth_level: no DB (row form or image form)");
         float *segmin = match_segmin(ws.scratch);
-        hipEvent_t e0 = timed ? prof_event(ev0 + 2 * nscreen) : nullptr;
-        hipEvent_t e1 = timed ? prof_event(ev0 + 2 * nscreen + 1) : nullptr;
+        hipEvent_t e0 = timed ? prof_event(ev0 + 3 * nscreen) : nullptr;
+        hipEvent_t e1 = timed ? prof_event(ev0 + 3 * nscreen + 1) : nullptr;
         if (e0) IA_HIP(hipEventRecord(e0, sq));
         const StageMap sm = db_stage_map(a->row0, a->nrows, src.A.w, src.A.h);
         if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b)))
@@ -627,6 +629,7 @@ struct LevelRun {
         const int form = !im ? XW_ROWS
                        : (xwave_on() == 2 && sm.W > 0 && xstrip_applies(src)) ? XW_STRIP : XW_IMG;
         if ((rc = launch_xwave(x, R, form, sq, K))) return rc;
+        if (timed) IA_HIP(hipEventRecord(prof_event(ev0 + 3 * nscreen + 2), sq));
         ++nscreen;
         pairs += (double)M * (double)a->nrows * K;
         if (prof) Ms.push_back(M);
@@ -842,8 +845,24 @@ int ia_prof_launches(int rec, float *ms, int *M, int max) {
     const ProfRec &p = g_prof->recs[rec];
     const int n = p.timed ? p.nscreen : 0;
     for (int i = 0; i < n && i < max; ++i) {
-        if (ms) IA_HIP(hipEventElapsedTime(&ms[i], g_prof->ev[p.ev0 + 2 * i], g_prof->ev[p.ev0 + 2 * i + 1]));
+        if (ms) IA_HIP(hipEventElapsedTime(&ms[i], g_prof->ev[p.ev0 + 3 * i], g_prof->ev[p.ev0 + 3 * i + 1]));
         if (M) M[i] = p.M[i];
+    }
+    return n;
+}
+
+int ia_prof_waves(int rec, float *tail_ms, float *gap_ms, int max) {
+    std::lock_guard<std::mutex> l(g_prof->mu);
+    IA_ARG(rec >= 0 && rec < (int)g_prof->recs.size(), "ia_prof_waves: no such record");
+    const ProfRec &p = g_prof->recs[rec];
+    const int n = p.timed ? p.nscreen : 0;
+    for (int i = 0; i < n && i < max; ++i) {
+        const size_t e = p.ev0 + 3 * i;
+        if (tail_ms) IA_HIP(hipEventElapsedTime(&tail_ms[i], g_prof->ev[e + 1], g_prof->ev[e + 2]));
+        if (gap_ms) {
+            gap_ms[i] = 0.f;
+            if (i + 1 < n) IA_HIP(hipEventElapsedTime(&gap_ms[i], g_prof->ev[e + 2], g_prof->ev[e + 3]));
+        }
     }
     return n;
 }
@@ -858,7 +877,7 @@ int ia_prof_end(double *out, int maxrec) {
         double ms = 0.0;
         for (int i = 0; p.timed && i < p.nscreen; ++i) {
             float e = 0.f;
-            IA_HIP(hipEventElapsedTime(&e, g_prof->ev[p.ev0 + 2 * i], g_prof->ev[p.ev0 + 2 * i + 1]));
+            IA_HIP(hipEventElapsedTime(&e, g_prof->ev[p.ev0 + 3 * i], g_prof->ev[p.ev0 + 3 * i + 1]));
             ms += e;
         }
         unsigned long long st[STATS_LINE] = {};

@@ -273,6 +273,10 @@ int ia_prof_end(double *out, int maxrec);
 /* after ia_prof_end: record rec's screen launches one by one (ms from the HIP events, M
  * the launch's query count); returns the number of timed launches */
 int ia_prof_launches(int rec, float *ms, int *M, int max);
+/* the same record's per-wave spacing from a third event after each wave's exact stage:
+ * tail_ms[i] = end of screen i -> end of its exact-stage / fused kernel, gap_ms[i] = that
+ * -> the start of screen i + 1 on the level's stream (0 for the last wave) */
+int ia_prof_waves(int rec, float *tail_ms, float *gap_ms, int max);
 /* destroy the calling host thread's graph-capture stream and last executable graph */
 int ia_release_thread_resources(void);
 

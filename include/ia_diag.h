@@ -66,6 +66,9 @@ int ia_diag_set_screen_sched(int sched);
 /* strip-order image-form levels: the producer / consumer screen k_screen16p (1, default;
  * IA_SCREEN_PC) or k_screen16i (0); same minima; returns the previous value, -1 leaves it */
 int ia_diag_set_screen_pc(int on);
+/* k_screen16p stage stamps into buf (device, 16 waves x 256 u64: blocks 0 and 300, per
+ * stage < 64 four s_memtime values; see ia_screen16.hip pc_stamp), NULL turns them off */
+int ia_diag_screen_trace(void *buf);
 /* with IA_XW_TRACE=<level tag>: the fused kernel's phase stamps of that level (100 MHz
  * s_memrealtime) for waves < 4096 and the first 8 pixels of each, 12 stamps per pixel:
  * {start, ticket, e*, candidates, re-screen, rescore | coherence, winner, exchange,

@@ -32,6 +32,9 @@ def main():
     ap.add_argument('--M', default='342,256,128')
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--forms', default='s0,s1,pc')
+    ap.add_argument('--trace', action='store_true',
+                    help='k_screen16p stage stamps (ia_diag_screen_trace) for the last M: per-stage '
+                         'phase medians of blocks 0 and 300 in shader cycles')
     args = ap.parse_args()
     Ms = [int(x) for x in args.M.split(',')]
     forms = args.forms.split(',')
@@ -91,6 +94,46 @@ def main():
             print('M %3d %s: median %7.1f us  min %7.1f us  pipe_frac %.3f  frac %.3f  same_minima %s'
                   % (M, sc, med, ts[0], 330 * pairs / (med * 1e-6) / 1e12 / F16_PEAK,
                      110 * pairs / (med * 1e-6) / 1e12 / F16_PEAK, same), flush=True)
+    if args.trace:
+        lib.ia_diag_set_screen_sched(0)
+        lib.ia_diag_set_screen_pc(1)
+        tr = torch.zeros(16 * 256, dtype=torch.int64, device=dev)
+        _ia.check(lib.ia_diag_screen_trace(_ia.ptr(tr)), 'trace on')
+        for M in Ms:
+            segmin = torch.empty((qrows, nseg), dtype=torch.float32, device=dev)
+            for _ in range(3):
+                tr.zero_()
+                _ia.check(lib.ia_diag_screen16_image(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.dbi),
+                                                     _ia.ptr(q16), M, _ia.ptr(segmin), st), 'screen')
+                torch.cuda.synchronize()
+            t = tr.view(2, 8, 64, 4).cpu().numpy().astype(np.float64)
+            for blk in range(2):
+                mf, ex = t[blk, :4], t[blk, 4:]
+                ok = (mf[:, 1:63, 0] > 0).all() and (ex[:, 1:62, 0] > 0).all()
+                if not ok:
+                    print('trace block %d: incomplete' % blk)
+                    continue
+                s_ = slice(4, 60)
+                wait_m = np.median(mf[:, s_, 1] - mf[:, s_, 0])        # MFMA waves at the barrier
+                mfma = np.median(mf[:, s_, 2] - mf[:, s_, 1])          # MFMAs issued
+                close = np.median(mf[:, s_, 3] - mf[:, s_, 2])
+                period = np.median(np.diff(mf[:, 4:61, 1], axis=1))    # stage period
+                wait_x = np.median(ex[:, s_, 1] - ex[:, s_, 0])
+                work_x = np.median(ex[:, s_, 2] - ex[:, s_, 1])
+                vm_x = np.median(ex[:, s_, 3] - ex[:, s_, 2])
+                print('M %3d block %d (cycles, median over stages 4-59): period %.0f | MFMA waves: '
+                      'barrier wait %.0f, MFMAs %.0f, close %.0f | expanders: barrier wait %.0f, '
+                      'copies+operand %.0f, copy wait %.0f' % (M, 300 * blk, period, wait_m, mfma, close,
+                                                              wait_x, work_x, vm_x), flush=True)
+                for w in range(4):
+                    print('   MFMA wave %d: wait %.0f mfma %.0f close %.0f | expander %d: wait %.0f work %.0f '
+                          'copy wait %.0f' % (w, np.median(mf[w, s_, 1] - mf[w, s_, 0]),
+                                              np.median(mf[w, s_, 2] - mf[w, s_, 1]),
+                                              np.median(mf[w, s_, 3] - mf[w, s_, 2]), w,
+                                              np.median(ex[w, s_, 1] - ex[w, s_, 0]),
+                                              np.median(ex[w, s_, 2] - ex[w, s_, 1]),
+                                              np.median(ex[w, s_, 3] - ex[w, s_, 2])), flush=True)
+        _ia.check(lib.ia_diag_screen_trace(None), 'trace off')
     lib.ia_diag_set_screen_sched(prev)
     lib.ia_diag_set_screen_pc(prev_pc)
 
