@@ -564,9 +564,12 @@ __device__ __forceinline__ void rp_expand(const char *ring, int y, int ns, half8
 // (< 64) four s_memtime stamps: MFMA waves {barrier arrival, departure, MFMAs issued, close
 // done}; expanders {arrival, departure, copies issued + operand written, copies landed}
 __device__ unsigned long long *g_pc_trace;
+// (the stamps go to LDS, a wave-uniform address, and are copied out at the end: a global
+// pointer held across the stage loop pushed G = 11 into spills)
 __device__ __forceinline__ void pc_stamp(unsigned long long *tr, int s, int k) {
-    if (tr && (threadIdx.x & 63) == 0 && s < 64) tr[s * 4 + k] = __builtin_readcyclecounter();
+    if (tr && s < 64) tr[s * 4 + k] = __builtin_readcyclecounter();
 }
+static std::atomic<bool> g_pc_trace_on{false};   // host side: launch the TRACE instantiation
 
 template <int G, int W>
 __device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps,
@@ -584,9 +587,8 @@ __device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps
         lds_sync();   // barrier s: operand s is complete (and operand s - 1 free for s + 1)
         pc_stamp(tr, s, 1);
         stage_mfma_cm<G, W, NS, PC_PIN>(E + (s & 1) * STAGE_H8, bq, mn, lane);
-        pc_stamp(tr, s, 2);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
-        pc_stamp(tr, s, 3);
+        pc_stamp(tr, s, 3);   // (no stamp between: the last fold's accumulator is live there)
     }
     lds_sync();       // the last stage's operand reads done (pairs with the expanders' last)
 }
@@ -640,7 +642,7 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
     lds_sync();
 }
 
-template <int G>
+template <int G, bool TRACE = false>
 __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int ch, int seg_rows,
                                                       StageMap sm, const half8 *__restrict__ q16,
                                                       int M, int groups, float *__restrict__ segmin,
@@ -666,8 +668,9 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // waves 0-3 and 4-7 pair up on the SIMDs (wave w and w + 4 share SIMD w % 4)
-    unsigned long long *tr = g_pc_trace;
-    tr = tr && (b == 0 || b == 300) ? tr + ((b == 0 ? 0 : 8) + wv) * 256 : nullptr;
+    // stage stamps (TRACE instantiation only): per wave 256 u64 in LDS, copied out below
+    __shared__ unsigned long long trs[TRACE ? 8 * 256 : 1];
+    unsigned long long *tr = TRACE && (b == 0 || b == 300) ? trs + wv * 256 : nullptr;
     if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg, tr);
     else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg, tr);
     else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg, tr);
@@ -677,6 +680,8 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     else if (wv == 6) pc_expand<2>(im, E, ring, sm, chunk, nstage, tr);
     else pc_expand<3>(im, E, ring, sm, chunk, nstage, tr);
     __syncthreads();
+    if (TRACE && (b == 0 || b == 300) && g_pc_trace)
+        for (int i = threadIdx.x; i < 8 * 256; i += 512) g_pc_trace[(b == 0 ? 0 : 8 * 256) + i] = trs[i];
     const long seg0 = (long)chunk * spc;
     const int q0 = group * G * 32;
     for (int i = threadIdx.x; i < G * 32 * spc; i += 512) {
@@ -833,7 +838,10 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
                                                  groups, segmin, nseg, jobs, parity);
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
-        if (pc)                                                                                 \
+        if (pc && (GG == 11 || GG == 4) && g_pc_trace_on.load())                                \
+            k_screen16p<GG, (GG == 11 || GG == 4)><<<grid, 512, 0, st>>>(                       \
+                *img, (int)nchunks, ch, seg_rows, sm, q, M, groups, segmin, nseg, jobs, parity);\
+        else if (pc)                                                                            \
             k_screen16p<GG><<<grid, 512, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
                                                   groups, segmin, nseg, jobs, parity);          \
         else if (sched) { IA_SCREEN16_SCHED(GG, 1) } else { IA_SCREEN16_SCHED(GG, 0) }          \
@@ -869,6 +877,7 @@ extern "C" int ia_diag_set_screen_sched(int sched) {
 extern "C" int ia_diag_screen_trace(void *buf) {
     unsigned long long *p = reinterpret_cast<unsigned long long *>(buf);
     IA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ia::g_pc_trace), &p, sizeof(p), 0, hipMemcpyHostToDevice));
+    ia::g_pc_trace_on.store(p != nullptr);
     return IA_OK;
 }
 

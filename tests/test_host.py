@@ -407,3 +407,31 @@ def test_strip_windows_hold_every_reflected_sample(h, w):
                                 want = (_symi2((y >> 1) + dy, hs), _symi2((x >> 1) + dx, ws))
                                 assert coarse((y >> 1) - (y0 >> 1) + 1 + dy,
                                               (x >> 1) - (x0 >> 1) + 2 + dx) == want
+
+
+def test_hot_kernels_do_not_spill():
+    """The build's kernel resource reports (csrc/_build/*.res, -Rpass-analysis=kernel-
+    resource-usage): the hot path's kernels (screens, the fused strip kernel, pyramid, YIQ,
+    DB build) use no scratch memory: a spill there (e.g. G = 11 of the screen at 249 of
+    256 VGPRs) costs 2.5x silently."""
+    import glob
+    import re
+    res = glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'image-analogies-python_amd', 'csrc', '_build', '*.res'))
+    if not res:
+        pytest.skip('no resource reports (build with make -C image-analogies-python_amd/csrc)')
+    hot = ('k_screen16', 'k_xstrip', 'k_pyr_wave', 'k_db_build_t', 'k_rgb_to_yiq', 'k_img_pad')
+    seen, bad = 0, []
+    for f in res:
+        name = None
+        for line in open(f):
+            m = re.search(r'Function Name: (\S+)', line)
+            if m:
+                name = m.group(1)
+                continue
+            m = re.search(r'ScratchSize \[bytes/lane\]: (\d+)', line)
+            if m and name and any(h in name for h in hot):
+                seen += 1
+                if int(m.group(1)) != 0:
+                    bad.append((name, int(m.group(1))))
+    assert seen > 20, seen
+    assert not bad, bad

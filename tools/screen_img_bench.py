@@ -115,8 +115,8 @@ def main():
                     continue
                 s_ = slice(4, 60)
                 wait_m = np.median(mf[:, s_, 1] - mf[:, s_, 0])        # MFMA waves at the barrier
-                mfma = np.median(mf[:, s_, 2] - mf[:, s_, 1])          # MFMAs issued
-                close = np.median(mf[:, s_, 3] - mf[:, s_, 2])
+                mfma = np.median(mf[:, s_, 3] - mf[:, s_, 1])          # MFMAs + folds + close
+                close = 0.0
                 period = np.median(np.diff(mf[:, 4:61, 1], axis=1))    # stage period
                 wait_x = np.median(ex[:, s_, 1] - ex[:, s_, 0])
                 work_x = np.median(ex[:, s_, 2] - ex[:, s_, 1])
@@ -126,10 +126,9 @@ def main():
                       'copies+operand %.0f, copy wait %.0f' % (M, 300 * blk, period, wait_m, mfma, close,
                                                               wait_x, work_x, vm_x), flush=True)
                 for w in range(4):
-                    print('   MFMA wave %d: wait %.0f mfma %.0f close %.0f | expander %d: wait %.0f work %.0f '
+                    print('   MFMA wave %d: wait %.0f mfma+close %.0f | expander %d: wait %.0f work %.0f '
                           'copy wait %.0f' % (w, np.median(mf[w, s_, 1] - mf[w, s_, 0]),
-                                              np.median(mf[w, s_, 2] - mf[w, s_, 1]),
-                                              np.median(mf[w, s_, 3] - mf[w, s_, 2]), w,
+                                              np.median(mf[w, s_, 3] - mf[w, s_, 1]), w,
                                               np.median(ex[w, s_, 1] - ex[w, s_, 0]),
                                               np.median(ex[w, s_, 2] - ex[w, s_, 1]),
                                               np.median(ex[w, s_, 3] - ex[w, s_, 2])), flush=True)
