@@ -296,10 +296,13 @@ int launch_query_rows(const double *qin, int M, const double *center, float *qp,
 // img (nullable): the DB's image form (ImgDb, whole chunks) streamed instead of the rows
 // (same minima, bit for bit)
 // jobs (nullable): a batch of njobs identical-shape jobs in one launch (grid y = job; each
-// job's DB sections, q16[parity] and segmin from its table entry)
+// job's DB sections, q16[parity] and segmin from its table entry).  sharded: a level whose
+// fused kernels wait for other ranks: never the producer / consumer screen there (its
+// one-per-CU blocks need ~94 KB of a CU's LDS, which waiting workgroups can hold for as long
+// as another rank needs: measured, 2 ranks sharing one GPU timed out on c4)
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st,
-                    const XJob *jobs = nullptr, int njobs = 1, int parity = 0);
+                    const XJob *jobs = nullptr, int njobs = 1, int parity = 0, bool sharded = false);
 // the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
 // stats (nullable): rows rescored, candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);

@@ -465,7 +465,11 @@ int launch_match(const DbSrc &src, long row0, long nrows, const void *dbv, const
     const SegWs ws = seg_ws(scratch, M, nrows);
     if (ev0) IA_HIP(hipEventRecord(ev0, st));
     const StageMap sm = db_stage_map(row0, nrows, src.A.w, src.A.h);
-    if ((rc = launch_screen16(db, dbi ? &img : nullptr, nrows, sm, q16, M, ws.segmin, st))) return rc;
+    // (the unfused matcher also serves sharded levels whose tails wait for other ranks: the
+    // 4-wave screen here, never the one-block-per-CU producer / consumer form)
+    if ((rc = launch_screen16(db, dbi ? &img : nullptr, nrows, sm, q16, M, ws.segmin, st, nullptr, 1, 0,
+                              true)))
+        return rc;
     if (ev1) IA_HIP(hipEventRecord(ev1, st));
     const FinishArgs fa = fin ? *fin : FinishArgs{};
     const int rm = rescore_mode();

@@ -808,7 +808,7 @@ static int screen_pc() {
 
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st, const XJob *jobs,
-                    int njobs, int parity) {
+                    int njobs, int parity, bool sharded) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -828,7 +828,7 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || jobs), "launch_screen16: bad batch");
     const dim3 grid((unsigned)nb, (unsigned)njobs);
     const int sched = screen_sched();
-    const bool pc = img && sm.W > 0 && screen_pc();
+    const bool pc = img && sm.W > 0 && !sharded && screen_pc();
 #define IA_SCREEN16_SCHED(GG, SS)                                                               \
     if (img)                                                                                    \
         k_screen16i<GG, SS><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \

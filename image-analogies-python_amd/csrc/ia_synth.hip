@@ -594,7 +594,8 @@ struct LevelRun {
         hipEvent_t e1 = timed ? prof_event(ev0 + 3 * nscreen + 1) : nullptr;
         if (e0) IA_HIP(hipEventRecord(e0, sq));
         const StageMap sm = db_stage_map(a->row0, a->nrows, src.A.w, src.A.h);
-        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b)))
+        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b,
+                                  a->comm != nullptr)))
             return rc;
         if (e1) IA_HIP(hipEventRecord(e1, sq));
         int y_lo_n = 0, M_n = 0;
