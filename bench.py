@@ -288,8 +288,8 @@ def hbm_kernels(dev, reps=20):
                  fp64 pyramids read once (A, A' fine: 8 B per row each; coarse: 8 B per 4
                  rows each)
       db_image   ia_db_build_image without a row form (what the product builds where the
-                 image form applies: k_db_range + k_db_bound + k_img_pad + the tiled norm
-                 pass), same level: the fp64 pyramids read once (20 B per row) + the padded
+                 image form applies: the range pass k_db_range_at + the one-pass build
+                 k_img_build), same level: the fp64 pyramids read once (20 B per row) + the padded
                  u32 split pairs (A, A' fine: 4 B per row each; coarse: 4 B per 4 rows each)
                  and the norm slots (4 B per row) written once: 34 B per row
     """
@@ -358,8 +358,8 @@ def hbm_kernels(dev, reps=20):
                                             None, _ia.ptr(ix.amax), _ia.ptr(ix.dbi), _ia.stream()),
                       'ia_db_build_image')
         put('db_image', timed(build_image), N * 34,
-            'ia_db_build_image without rows (k_db_range + k_db_bound + k_img_pad + tiled norm '
-            'pass), 4,194,304 rows')
+            'ia_db_build_image without rows (k_db_range_at + one-pass k_img_build: pads, norm '
+            'slots and the bound), 4,194,304 rows')
     return out
 
 

@@ -145,6 +145,7 @@ _SIGS = {
     'ia_diag_set_xwave': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_sched': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_pc': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_img_fused': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_screen_trace': (ctypes.c_int, [_dp]),
     'ia_diag_xwave_trace': (ctypes.c_int, [_dp]),
     'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),

@@ -110,6 +110,23 @@ __global__ __launch_bounds__(256) void k_db_range(DbSpans sp, double *__restrict
     }
 }
 
+// the split scale's bound from the four value ranges fin[2g] (lo), fin[2g + 1] (hi) of the
+// images g (0 coarse A, 1 fine A, 2 coarse A', 3 fine A'): fl32 rounded up of sqrt(sum over
+// features of the larger squared deviation of its image's range from the centre); the
+// terms are summed in feature order by one thread (the same value in every caller)
+__device__ __forceinline__ float db_bound_f(const double *fin, const double *__restrict__ center) {
+    double b2 = 0.0;
+    for (int k = 0; k < 55; ++k) {
+        const int g = k < 9 ? 0 : (k < 34 ? 1 : (k < 43 ? 2 : 3));
+        const double dl = fin[2 * g] - center[k], dh = fin[2 * g + 1] - center[k];
+        b2 += fmax(dl * dl, dh * dh);
+    }
+    const double a = sqrt(b2 * (1.0 + 1e-12));
+    float f = (float)a;
+    if ((double)f < a) f = nextafterf(f, INFINITY);
+    return f;
+}
+
 // one block of DBB_BLOCKS threads, one partial each: reduce, then amax = max(amax, fl32
 // rounded up of sqrt(bound))
 __global__ __launch_bounds__(1024) void k_db_bound(const double *__restrict__ part, int nb,
@@ -128,7 +145,7 @@ __global__ __launch_bounds__(1024) void k_db_bound(const double *__restrict__ pa
 #pragma unroll
         for (int i = 0; i < 8; ++i) red[wv][i] = v[i];
     __syncthreads();
-    __shared__ double fin[8], term[64];
+    __shared__ double fin[8];
     if (threadIdx.x < 8) {
         const int i = threadIdx.x;
         double x = red[0][i];
@@ -136,21 +153,7 @@ __global__ __launch_bounds__(1024) void k_db_bound(const double *__restrict__ pa
         fin[i] = x;
     }
     __syncthreads();
-    if (threadIdx.x < 55) {   // feature k's term: the larger squared deviation of its image's range
-        const int k = threadIdx.x;
-        const int g = k < 9 ? 0 : (k < 34 ? 1 : (k < 43 ? 2 : 3));
-        const double dl = fin[2 * g] - center[k], dh = fin[2 * g + 1] - center[k];
-        term[k] = fmax(dl * dl, dh * dh);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double b2 = 0.0;
-        for (int k = 0; k < 55; ++k) b2 += term[k];
-        const double a = sqrt(b2 * (1.0 + 1e-12));
-        float f = (float)a;
-        if ((double)f < a) f = nextafterf(f, INFINITY);
-        amax[0] = fmaxf(amax[0], f);
-    }
+    if (threadIdx.x == 0) amax[0] = fmaxf(amax[0], db_bound_f(fin, center));
 }
 
 // ---- tiled form (A width % 32 == 0, row0 % 32 == 0: every 32-row DB tile is 32 pixels of
@@ -360,6 +363,301 @@ __global__ __launch_bounds__(256) void k_img_pad(const double *__restrict__ img,
     out[i] = (uint32_t)__builtin_bit_cast(uint16_t, xh) | ((uint32_t)__builtin_bit_cast(uint16_t, xl) << 16);
 }
 
+// ---- the image form in one pass over the images (IA_IMG_FUSED, default 1) -------------
+// (1) k_db_range_at: the four value ranges as order-preserving keys, atomic-min'd into 8
+//     words of the image form's scratch (lo, and hi negated; one memset of 0xff first).
+// (2) k_img_build: every block first derives the split scale's bound from those 8 words
+//     (db_bound_f, the same value k_db_bound computes) and amax = max(amax, bound) (block 0
+//     stores it; every block uses the same value); then each thread walks one column of
+//     IB_R scanlines of one A' image with the features' windows in registers (5 x 5 fine A,
+//     3 x 5 fine A', 3 x 3 coarse of each; one new row per step), and writes
+//       - the padded split pairs of its fine pixel of A (image 0 only) and of A', and of the
+//         coarse pixel when its fine coordinates are even,
+//       - the row's norm slot (the tiled build's fp64 sum in feature order, split: the same
+//         bits as k_db_build_t<true>).
+//     The pad margins (reflections outside the images) come from extra blocks, one thread
+//     per margin pixel (k_img_pad's gather).
+// One read of the images for the range, one for everything else (the two-read floor: the
+// split scale needs the global bound before any value is split).
+__device__ __forceinline__ unsigned long long okey(double x) {   // order-preserving key
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double okey_inv(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k));
+}
+
+__global__ __launch_bounds__(256) void k_db_range_at(DbSpans sp, unsigned long long *__restrict__ rng) {
+    __shared__ double red[4][2];
+    int g = 0;
+    while (g < 3 && (int)blockIdx.x >= sp.first[g + 1]) ++g;
+    const int nb = sp.first[g + 1] - sp.first[g], lb = blockIdx.x - sp.first[g];
+    const double *x = sp.x[g];
+    const long n = sp.n[g];
+    double lo = INFINITY, hi = -INFINITY;
+    const long stride = (long)nb * 256;
+    const double2 *x2 = reinterpret_cast<const double2 *>(x);
+    const long n2 = reinterpret_cast<uintptr_t>(x) % 16 == 0 ? n / 2 : 0;
+    long i = (long)lb * 256 + threadIdx.x;
+    for (; i + 7 * stride < n2; i += 8 * stride) {
+        double2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = x2[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            lo = fmin(lo, fmin(v[k].x, v[k].y));
+            hi = fmax(hi, fmax(v[k].x, v[k].y));
+        }
+    }
+    for (; i < n2; i += stride) {
+        const double2 v = x2[i];
+        lo = fmin(lo, fmin(v.x, v.y));
+        hi = fmax(hi, fmax(v.x, v.y));
+    }
+    for (long j = 2 * n2 + (long)lb * 256 + threadIdx.x; j < n; j += stride) {
+        lo = fmin(lo, x[j]);
+        hi = fmax(hi, x[j]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o));
+        hi = fmax(hi, __shfl_xor(hi, o));
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[wv][0] = lo; red[wv][1] = hi; }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        double v = red[0][threadIdx.x];
+        for (int w = 1; w < 4; ++w) v = threadIdx.x ? fmax(v, red[w][1]) : fmin(v, red[w][0]);
+        atomicMin(&rng[2 * g + threadIdx.x], okey(threadIdx.x ? -v : v));
+    }
+}
+
+constexpr int IB_R = 16;    // scanlines per thread
+constexpr int IB_T = 128;   // threads (columns) per block
+
+struct ImgBuild {
+    const double *A_lg, *A_sm, *Ap_lg, *Ap_sm;   // A' image 0; image i at i * hw / hws
+    int H, W, hs, ws, nAp;
+    long hw, hws;
+    ImgDb v;                                     // the output sections
+    long row0, nrows;
+    int tiles_x, tiles_y, main_blocks;           // main blocks: tiles_x * tiles_y * nAp
+    long mf, mc;                                 // margin pixels per fine / coarse image
+};
+
+__device__ __forceinline__ uint32_t split_pair(double d, int ea) {
+    _Float16 xh, xl;
+    split16f(ldexpf((float)d, ea), xh, xl);
+    return (uint32_t)__builtin_bit_cast(uint16_t, xh) | ((uint32_t)__builtin_bit_cast(uint16_t, xl) << 16);
+}
+
+// margin pixel m of a padded image (hh x ww source, wp padded width): its padded position
+__device__ __forceinline__ void margin_pos(long m, int hh, int ww, int wp, int &r, int &q) {
+    const long top = (long)IMG_PY * wp;
+    if (m < top) { r = (int)(m / wp); q = (int)(m - (long)r * wp); return; }
+    m -= top;
+    if (m < top) { const int rr = (int)(m / wp); r = IMG_PY + hh + rr; q = (int)(m - (long)rr * wp); return; }
+    m -= top;
+    const int side = 2 * IMG_PX;   // per source row: PX left, PX right
+    const int rr = (int)(m / side), c = (int)(m - (long)rr * side);
+    r = IMG_PY + rr;
+    q = c < IMG_PX ? c : ww + c;   // c - PX + PX + ww
+}
+
+// one main block's tile of k_img_build: column x of IB_R scanlines of A' image img.
+// SQ (every centre of A's features equal, and of A''s: the product's centres): the windows
+// hold the squared deviations, each computed once when its sample enters (the centre
+// column's deviations kept for the pads); the norm sums them in the same order, so the bits
+// equal the general form's (d = v - c_k; n2 += d * d per feature)
+template <bool SQ>
+__device__ __forceinline__ void img_tile(const ImgBuild &b, int blk, const double *cs, const Split16Db &sc) {
+    const int img = blk / (b.tiles_x * b.tiles_y);
+    const int t2 = blk - img * b.tiles_x * b.tiles_y;
+    const int ty = t2 / b.tiles_x, tx = t2 - ty * b.tiles_x;
+    const int x = tx * IB_T + threadIdx.x;
+    const int y0 = ty * IB_R;
+    const int H = b.H, W = b.W;
+    const double *A = b.A_lg, *As = b.A_sm;
+    const double *P = b.Ap_lg + (long)img * b.hw, *Ps = b.Ap_sm + (long)img * b.hws;
+    uint32_t *fa = const_cast<uint32_t *>(b.v.fa.get()), *ca = const_cast<uint32_t *>(b.v.ca.get());
+    uint32_t *fp = const_cast<uint32_t *>(b.v.ap.get()) + (long)img * b.v.apstride;
+    uint32_t *cp = fp + b.v.apc;
+    uint32_t *nm = const_cast<uint32_t *>(b.v.norm.get());
+    const double cA = cs[0], cP = cs[34];
+    int col[5], ccol[3];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) col[d] = symi2(x + d - 2, W);
+    const int cx = x >> 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) ccol[d] = symi2(cx + d - 1, b.ws);
+    // windows: fine A rows y-2..y+2, fine A' rows y-2..y, coarse rows cy-1..cy+1 (raw samples,
+    // or with SQ their squared deviations); dv*: the centre column's deviations (SQ)
+    double wa[5][5], wp[3][5], wca[3][3], wcp[3][3];
+    double dva[5], dvp[3], dvca[3], dvcp[3];
+    auto ldrow5 = [&](const double *im, int r, double c, double (&o)[5], double &dc) {
+        const double *row = im + (long)symi2(r, H) * W;
+#pragma unroll
+        for (int d = 0; d < 5; ++d) {
+            const double v = row[col[d]];
+            if constexpr (SQ) {
+                const double dd = v - c;
+                o[d] = dd * dd;
+                if (d == 2) dc = dd;
+            } else {
+                o[d] = v;
+            }
+        }
+    };
+    auto ldrow3 = [&](const double *im, int r, double c, double (&o)[3], double &dc) {
+        const double *row = im + (long)symi2(r, b.hs) * b.ws;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double v = row[ccol[d]];
+            if constexpr (SQ) {
+                const double dd = v - c;
+                o[d] = dd * dd;
+                if (d == 1) dc = dd;
+            } else {
+                o[d] = v;
+            }
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < 5; ++r) ldrow5(A, y0 - 2 + r, cA, wa[r], dva[r]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) ldrow5(P, y0 - 2 + r, cP, wp[r], dvp[r]);
+    int cy = y0 >> 1;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        ldrow3(As, cy - 1 + r, cA, wca[r], dvca[r]);
+        ldrow3(Ps, cy - 1 + r, cP, wcp[r], dvcp[r]);
+    }
+#pragma unroll
+    for (int s = 0; s < IB_R; ++s) {
+        const int y = y0 + s;
+        if (s > 0) {   // slide one scanline down
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int d = 0; d < 5; ++d) wa[r][d] = wa[r + 1][d];
+                dva[r] = dva[r + 1];
+            }
+            ldrow5(A, y + 2, cA, wa[4], dva[4]);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+#pragma unroll
+                for (int d = 0; d < 5; ++d) wp[r][d] = wp[r + 1][d];
+                dvp[r] = dvp[r + 1];
+            }
+            ldrow5(P, y, cP, wp[2], dvp[2]);
+            if ((y >> 1) != cy) {
+                cy = y >> 1;
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) { wca[r][d] = wca[r + 1][d]; wcp[r][d] = wcp[r + 1][d]; }
+                    dvca[r] = dvca[r + 1];
+                    dvcp[r] = dvcp[r + 1];
+                }
+                ldrow3(As, cy + 1, cA, wca[2], dvca[2]);
+                ldrow3(Ps, cy + 1, cP, wcp[2], dvcp[2]);
+            }
+        }
+        if (y >= H) break;
+        // the norm slot: the tiled build's sum in feature order (db_win_features)
+        double n2 = 0.0;
+        auto term = [&](double w, int k) {
+            if constexpr (SQ) {
+                n2 += w;
+            } else {
+                const double d = w - cs[k];
+                n2 += d * d;
+            }
+        };
+#pragma unroll
+        for (int t = 0; t < 9; ++t) term(wca[t / 3][t % 3], t);
+#pragma unroll
+        for (int t = 0; t < 25; ++t) term(wa[t / 5][t % 5], 9 + t);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) term(wcp[t / 3][t % 3], 34 + t);
+#pragma unroll
+        for (int t = 0; t < 12; ++t) term(wp[t / 5][t % 5], 43 + t);
+        const long g = (long)img * b.hw + (long)y * W + x;
+        if (g >= b.row0 && g < b.row0 + b.nrows) {
+            _Float16 h, l;
+            split16f(ldexpf((float)n2, sc.ea - sc.R), h, l);
+            nm[g - b.row0] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+        }
+        // padded pixels: fine A (image 0), fine A', and the coarse ones at even coordinates
+        const double da = SQ ? dva[2] : wa[2][2] - cA, dp = SQ ? dvp[2] : wp[2][2] - cP;
+        const long pf = (long)(y + IMG_PY) * b.v.Wp + x + IMG_PX;
+        if (img == 0) fa[pf] = split_pair(da, sc.ea);
+        fp[pf] = split_pair(dp, sc.ea);
+        if (!(y & 1) && !(x & 1)) {
+            const double dca = SQ ? dvca[1] : wca[1][1] - cA, dcp = SQ ? dvcp[1] : wcp[1][1] - cP;
+            const long pc = (long)(cy + IMG_PY) * b.v.Wcp + cx + IMG_PX;
+            if (img == 0) ca[pc] = split_pair(dca, sc.ea);
+            cp[pc] = split_pair(dcp, sc.ea);
+        }
+    }
+}
+
+__global__ __launch_bounds__(IB_T) void k_img_build(ImgBuild b, const double *__restrict__ center,
+                                                    float *amax, const unsigned long long *__restrict__ rng) {
+    __shared__ double cs[56];
+    __shared__ float amx;
+    __shared__ int uni_s;
+    if (threadIdx.x < IA_D) cs[threadIdx.x] = center[threadIdx.x];
+    if (threadIdx.x == 0) {
+        int u = 1;
+        for (int k = 1; k < IA_D; ++k) u &= center[k] == center[k < 34 ? 0 : 34];
+        uni_s = u;
+        double fin[8];
+        for (int i = 0; i < 8; ++i) fin[i] = (i & 1) ? -okey_inv(rng[i]) : okey_inv(rng[i]);
+        const float a = fmaxf(amax[0], db_bound_f(fin, center));
+        amx = a;
+        if (blockIdx.x == 0) amax[0] = a;
+    }
+    __syncthreads();
+    const Split16Db sc = split16_db_scale(amx);
+    const bool uni = uni_s != 0;
+    const int blk = blockIdx.x;
+    if (blk >= b.main_blocks) {   // margins: one thread per margin pixel of one padded image
+        const long m = (long)(blk - b.main_blocks) * IB_T + threadIdx.x;
+        // images: A fine, A coarse, then per A' image fine, coarse
+        const long per = b.mf + b.mc;
+        const long img = m / per;
+        if (img > b.nAp) return;
+        long mm = m - img * per;
+        const bool coarse = mm >= b.mf;
+        if (coarse) mm -= b.mf;
+        const int hh = coarse ? b.hs : b.H, ww = coarse ? b.ws : b.W, wp = coarse ? b.v.Wcp : b.v.Wp;
+        int r, q;
+        margin_pos(mm, hh, ww, wp, r, q);
+        const double *src = img == 0 ? (coarse ? b.A_sm : b.A_lg)
+                                     : (coarse ? b.Ap_sm + (img - 1) * b.hws : b.Ap_lg + (img - 1) * b.hw);
+        const uint32_t *o0 = img == 0 ? (coarse ? b.v.ca.get() : b.v.fa.get())
+                                      : b.v.ap.get() + (img - 1) * b.v.apstride + (coarse ? b.v.apc : 0);
+        uint32_t *out = const_cast<uint32_t *>(o0);
+        const double v = src[(long)symi(r - IMG_PY, hh) * ww + symi(q - IMG_PX, ww)];
+        const double c = cs[img == 0 ? 0 : 34];
+        out[(long)r * wp + q] = split_pair(v - c, sc.ea);
+        return;
+    }
+    if (uni) img_tile<true>(b, blk, cs, sc);
+    else img_tile<false>(b, blk, cs, sc);
+}
+
+static std::atomic<int> g_img_fused{-1};
+static int img_fused() {
+    int v = g_img_fused.load();
+    if (v < 0) {
+        v = env_int("IA_IMG_FUSED", 1) ? 1 : 0;
+        g_img_fused.store(v);
+    }
+    return v;
+}
+
 // the rows' norm-slot pairs, read back from the row form (feature 55: hi in lane half 1's
 // group 2, lo in its group 6, element 7; ia_split16.h)
 __global__ __launch_bounds__(256) void k_img_norm(const half8 *__restrict__ db16, long nrows,
@@ -477,6 +775,12 @@ long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
 size_t ia_db_bytes(long nrows) { return db_bytes(nrows); }
 
 static int g_db_tiled = 1;   // ia_diag_set_db_build_form
+int ia_diag_set_img_fused(int on) {
+    const int prev = img_fused();
+    if (on == 0 || on == 1) g_img_fused.store(on);
+    return prev;
+}
+
 int ia_diag_set_db_build_form(int tiled) {
     const int prev = g_db_tiled;
     if (tiled == 0 || tiled == 1) g_db_tiled = tiled;
@@ -542,6 +846,41 @@ int ia_db_build_image(const IaSrcLevel *src, long row0, long nrows, const double
            "ia_db_build_image: the image form needs width and row0 multiples of 128 and whole chunks");
     hipStream_t st = S(stream);
     const DbSrc d = make_dbsrc(*src);
+    if (!db && img_fused() && src->A_ws * 2 == src->Aw && src->A_hs == (src->Ah + 1) / 2) {
+        // one pass for the ranges, one for the pads and the norm slots (k_img_build)
+        unsigned long long *rng = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(dbi) + v.scr);
+        IA_HIP(hipMemsetAsync(rng, 0xff, 8 * sizeof(unsigned long long), st));
+        DbSpans sp;
+        sp.x[0] = src->A_sm; sp.n[0] = d.hws;
+        sp.x[1] = src->A_lg; sp.n[1] = d.hw;
+        sp.x[2] = src->Ap_sm; sp.n[2] = (long)src->nAp * d.hws;
+        sp.x[3] = src->Ap_lg; sp.n[3] = (long)src->nAp * d.hw;
+        const long tot = sp.n[0] + sp.n[1] + sp.n[2] + sp.n[3];
+        sp.first[0] = 0;
+        for (int g = 0; g < 4; ++g) {
+            const long want = std::max<long>(1, (long)((double)(DBB_BLOCKS - 4) * sp.n[g] / tot));
+            sp.first[g + 1] = sp.first[g] + (int)want;
+        }
+        k_db_range_at<<<sp.first[4], 256, 0, st>>>(sp, rng);
+        IA_LAUNCH_CHECK("k_db_range_at");
+        ImgBuild bb;
+        bb.A_lg = src->A_lg; bb.A_sm = src->A_sm; bb.Ap_lg = src->Ap_lg; bb.Ap_sm = src->Ap_sm;
+        bb.H = src->Ah; bb.W = src->Aw; bb.hs = src->A_hs; bb.ws = src->A_ws; bb.nAp = src->nAp;
+        bb.hw = d.hw; bb.hws = d.hws;
+        bb.v = v;
+        bb.row0 = row0; bb.nrows = nrows;
+        bb.tiles_x = src->Aw / IB_T;
+        bb.tiles_y = (src->Ah + IB_R - 1) / IB_R;
+        bb.main_blocks = bb.tiles_x * bb.tiles_y * src->nAp;
+        bb.mf = 2L * IMG_PY * v.Wp + 2L * IMG_PX * src->Ah;
+        bb.mc = 2L * IMG_PY * v.Wcp + 2L * IMG_PX * src->A_hs;
+        const long mblocks = ((1 + src->nAp) * (bb.mf + bb.mc) + IB_T - 1) / IB_T;
+        IA_ARG(src->Aw % IB_T == 0 && (long)bb.main_blocks + mblocks < (1L << 31),
+               "ia_db_build_image: fused build shape");
+        k_img_build<<<(unsigned)(bb.main_blocks + mblocks), IB_T, 0, st>>>(bb, center, amax, rng);
+        IA_LAUNCH_CHECK("k_img_build");
+        return IA_OK;
+    }
     if (!db) {   // no row form: amax here, from the scratch section's partials
         const int rc = launch_db_amax(src, d, center, amax,
                                       reinterpret_cast<double *>(reinterpret_cast<char *>(dbi) + v.scr), st);

@@ -66,6 +66,9 @@ int ia_diag_set_screen_sched(int sched);
 /* strip-order image-form levels: the producer / consumer screen k_screen16p (1, default;
  * IA_SCREEN_PC) or k_screen16i (0); same minima; returns the previous value, -1 leaves it */
 int ia_diag_set_screen_pc(int on);
+/* ia_db_build_image without rows: the fused one-pass build k_img_build (1, default;
+ * IA_IMG_FUSED) or the range + bound + pad + norm-pass kernels (0); same bytes and amax */
+int ia_diag_set_img_fused(int on);
 /* k_screen16p stage stamps into buf (device, 16 waves x 256 u64: blocks 0 and 300, per
  * stage < 64 four s_memtime values; see ia_screen16.hip pc_stamp), NULL turns them off */
 int ia_diag_screen_trace(void *buf);

@@ -330,3 +330,46 @@ def test_image_form_alone_equals_image_form_from_rows(gpu):
             dd = np.add.reduce((As - q) ** 2, axis=1)
             j = int(np.argmin(dd))
             assert (d[qi], i[qi]) == (dd[j], j), (mode, qi)
+
+
+@pytest.mark.parametrize('shape,n_ap,shards,jitter', [((256, 384), 2, 1, False), ((129, 256), 1, 1, False),
+                                                      ((130, 128), 3, 3, False), ((64, 512), 1, 2, False),
+                                                      ((129, 256), 2, 1, True)])
+def test_image_form_fused_build_equals_kernel_chain(gpu, shape, n_ap, shards, jitter):
+    """ia_db_build_image's one-pass build (k_db_range_at + k_img_build: windows in registers,
+    pads, norm slots and the bound in one sweep) writes the same bytes (pads of every image,
+    the shard's norm slots) and the same amax as the range / bound / pad / norm-pass chain,
+    for odd heights, several A' images and row shards; jitter: a centre whose features differ
+    within A's and A''s groups (the build's general path instead of its squared windows)."""
+    import _ia
+    import algorithms
+    import image_analogies as ia
+    A, Aps, _ = analogy_inputs(51, shape, (8, 8), n_ap=n_ap)
+    A_pyr = o.compute_gaussian_pyramid(A, 3, cap=2)
+    Ap_pyr = [o.compute_gaussian_pyramid(x, 3, cap=2) for x in Aps]
+    L = len(A_pyr)
+    Ad, Apd = [dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_pyr]
+    lib = _ia.lib()
+    for r in range(shards):
+        idx = algorithms.level_index(Ad, Apd, L - 1, (lambda lv, N: ia.shard_rows(N, r, shards))
+                                     if shards > 1 else None)
+        if idx.dbi is None:
+            continue
+        if jitter:
+            idx.center += torch.arange(idx.center.numel(), device='cuda', dtype=idx.center.dtype) * 1e-3
+        n = lib.ia_db_image_bytes(ctypes.byref(idx.src), idx.row0, idx.nrows) - 65536
+        outs = []
+        for fused in (0, 1):
+            prev = lib.ia_diag_set_img_fused(fused)
+            try:
+                z = torch.zeros_like(idx.dbi)
+                amax = torch.zeros(1, dtype=torch.float32, device='cuda')
+                _ia.check(lib.ia_db_build_image(ctypes.byref(idx.src), idx.row0, idx.nrows,
+                                                _ia.ptr(idx.center), None, _ia.ptr(amax), _ia.ptr(z),
+                                                _ia.stream()), 'ia_db_build_image')
+                torch.cuda.synchronize()
+                outs.append((z[:n].clone(), float(amax.item())))
+            finally:
+                lib.ia_diag_set_img_fused(prev)
+        assert outs[0][1] == outs[1][1] > 0, (r, outs[0][1], outs[1][1])
+        assert torch.equal(outs[0][0], outs[1][0]), r
