@@ -821,6 +821,75 @@ __device__ __forceinline__ double pw55_lanes(double v) {
     return res;
 }
 
+// ---- k_xstrip's segment-minima phase on waves 0, 2, 3 only (192 threads; wave 1 picks the
+// coherence candidate meanwhile and never waits for this phase): thread t3 holds the float4s
+// t3 + 192 j of the query's minima in registers (XS_REG of them: c4's 8192 segments on one
+// GPU), the rest are streamed.  Same e* and candidate set as segmin_* over 256 threads.
+constexpr int XS_REG = 11;
+__device__ __forceinline__ void seg3_load(const float4 *sq4, long n4, int t3, float4 (&v)[XS_REG]) {
+#pragma unroll
+    for (int j = 0; j < XS_REG; ++j) {
+        const long i = t3 + (long)j * 192;
+        const float4 x = sq4[i < n4 ? i : 0];   // unconditional (a valid index past the end)
+        v[j] = i < n4 ? x : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+    }
+}
+__device__ __forceinline__ float seg3_wave_min(const float4 *sq4, long n4, int t3, const float4 (&v)[XS_REG]) {
+    float emin = FLT_MAX;
+#pragma unroll
+    for (int j = 0; j < XS_REG; ++j) emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
+    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+        const float4 x = sq4[i];
+        emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
+    }
+    for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
+    return emin;
+}
+__device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, const float4 (&v)[XS_REG],
+                                            double Tseg, int *slist, int *scount) {
+    static_assert(XS_REG * 4 <= 64, "one 64-bit mask");
+    unsigned long long m = 0;
+#pragma unroll
+    for (int j = 0; j < XS_REG; ++j) {
+        m |= (unsigned long long)((double)v[j].x <= Tseg) << (4 * j);
+        m |= (unsigned long long)((double)v[j].y <= Tseg) << (4 * j + 1);
+        m |= (unsigned long long)((double)v[j].z <= Tseg) << (4 * j + 2);
+        m |= (unsigned long long)((double)v[j].w <= Tseg) << (4 * j + 3);
+    }
+    if (m) {
+        int pos = atomicAdd(scount, __builtin_popcountll(m));
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            if (pos < RESCORE_SEGCAP) slist[pos] = 4 * (t3 + (b >> 2) * 192) + (b & 3);
+            ++pos;
+        }
+    }
+    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+        const float4 x = sq4[i];
+        unsigned mt = ((double)x.x <= Tseg ? 1u : 0u) | ((double)x.y <= Tseg ? 2u : 0u) |
+                      ((double)x.z <= Tseg ? 4u : 0u) | ((double)x.w <= Tseg ? 8u : 0u);
+        if (mt) {
+            int pos = atomicAdd(scount, __builtin_popcount(mt));
+            while (mt) {
+                const int b = __builtin_ctz(mt);
+                mt &= mt - 1;
+                if (pos < RESCORE_SEGCAP) slist[pos] = (int)(4 * i + b);
+                ++pos;
+            }
+        }
+    }
+}
+// a barrier of waves 0, 2 and 3 only (an LDS counter; wave 1 never takes part): generation g
+// releases when all three have arrived for the g-th time
+__device__ __forceinline__ void sync3(unsigned *cnt, unsigned g, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3u * g)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
 template <bool BATCH>
 __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ __attribute__((aligned(16))) char sa_raw[BATCH ? sizeof(XArgs) : 16];
@@ -840,7 +909,8 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ double qs[IA_DP], wts[IA_DP];
     __shared__ double cwt[2 * IA_DP];   // the coherence lanes' factors: 1 (distance), weights
     __shared__ int slist[RESCORE_SEGCAP];
-    __shared__ int tk, scount;
+    __shared__ int tk, scount, sfull;
+    __shared__ unsigned bar3;
     __shared__ float redf[4];
     __shared__ double bds[4], bwd[4], bvl[4];
     __shared__ long long bis[4];
@@ -855,7 +925,11 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     const DbSrc &src = a.src;
     const int t = f.t, W = f.W;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
+    if (tid == 0) {
+        tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
+        bar3 = 0;
+        scount = 0;
+    }
     __syncthreads();
     const int i = tk;
     unsigned long long *trace =
@@ -883,18 +957,21 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
 
     double own = 0.0;
     if (cur) {
-        // ---- 1. one round trip: query, weights, norm, bound, segment minima, coherence s / im
-        // (unconditional loads, as segmin_load)
-        const int qt = tid < IA_D ? tid : 0;
-        const double qsv = a.q64[(long)i * IA_DP + (tid < IA_DP ? tid : 0)];
-        const double wk0 = f.weights[qt];
-        const double wk = tid < IA_D ? wk0 : 0.0;
+        // ---- 1. one round trip each: waves 0, 2, 3 the query norm, bound and segment minima
+        // (e* and the candidate segments among themselves, sync3); wave 1 the query, weights
+        // and the coherence window's s / im, then the coherence gathers and pick, without
+        // waiting for the others until the first windows have landed
+        const int t3 = (wv == 0 ? 0 : wv - 1) * 64 + lane;   // waves 0, 2, 3
+        const int ql = lane < IA_DP ? lane : 0;
+        const double qsv = a.q64[(long)i * IA_DP + ql];
+        const double wk0 = f.weights[lane < IA_D ? lane : 0];
+        const double wk = lane < IA_D ? wk0 : 0.0;
         const double nqq = a.nq[vidx(i)];
         const float am = amx;
         const long n4 = a.nseg / 4;
         const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
-        float4 v[RESCORE_REG];
-        segmin_load(sq4, n4, v);
+        float4 v[XS_REG];
+        if (wv != 1) seg3_load(sq4, n4, t3, v);
         const int rr0 = y - 2 + lane / 5, rc0 = x - 2 + lane % 5;
         const bool cpos_ok = wv == 1 && lane < XW_NCOH && rr0 >= 0 && rc0 >= 0 && rc0 < W &&
                              (rr0 < y || rc0 < x);
@@ -905,9 +982,10 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         // the loads above stay in this round trip (not sunk to their first use, after the
         // segment minima's wait: one more round trip on wave 1's path)
         asm volatile("" ::: "memory");
-        if (tid == 0) scount = 0;
-        const float ewv = segmin_wave_min(sq4, n4, v);
-        if (lane == 0) redf[wv] = ewv;
+        if (wv != 1) {
+            const float ewv = seg3_wave_min(sq4, n4, t3, v);
+            if (lane == 0) redf[wv] = ewv;
+        }
         if (wv == 1) wstamp(14);
         // ---- wave 1: the coherence candidates (best_coherence_match, algorithms.py:92-130:
         // p_r = s(r) + q - r inside A'): lane k loads sample k of each into registers now
@@ -966,24 +1044,28 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             }
             wstamp(13);
         }
-        if (tid < IA_DP) {
-            qs[tid] = qsv;
-            wts[tid] = wk;
-            cwt[tid] = 1.0;
-            cwt[IA_DP + tid] = wk;
+        if (wv == 1 && lane < IA_DP) {   // read by the others after the first full barrier
+            qs[lane] = qsv;
+            wts[lane] = wk;
+            cwt[lane] = 1.0;
+            cwt[IA_DP + lane] = wk;
         }
-        lds_barrier();   // not waiting for wave 1's coherence gathers
-        const float emin = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
-        xw_stamp(trace, 2);
-        double Tseg, Trow;
-        bool force_full;
-        rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
-        segmin_select(sq4, n4, v, Tseg, slist, &scount);
-        lds_barrier();
-        xw_stamp(trace, 3);
-        const int ns = scount;
-        const bool full = ns > RESCORE_SEGCAP || force_full;
-        const long nscan = full ? a.nseg : ns;
+        int ns = 0;
+        bool full = false;
+        if (wv != 1) {
+            sync3(&bar3, 1, lane);   // e* (waves 0, 2, 3)
+            const float emin = fminf(redf[0], fminf(redf[2], redf[3]));
+            xw_stamp(trace, 2);
+            double Tseg, Trow;
+            bool force_full;
+            rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+            seg3_select(sq4, n4, t3, v, Tseg, slist, &scount);
+            sync3(&bar3, 2, lane);
+            xw_stamp(trace, 3);
+            ns = scount;
+            full = ns > RESCORE_SEGCAP || force_full;
+            if (tid == 0) sfull = full ? 1 : 0;
+        }
 
         auto coherence = [&]() {
 #pragma unroll
@@ -1037,21 +1119,36 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         XsWin w{};
         XsFix fx;
         const int dr = wv == 0 ? 0 : wv - 1;   // DMA rank of waves 0, 2, 3
-        const long nit = nscan;
-        if (nit > 0) w = xs_window(a, full ? 0 : slist[0]);
-        if (wv == 1) coherence();
-        else if (nit > 0) xs_dma(w, src.A, win, dr, lane, fx);
+        long nit = full ? a.nseg : ns;          // (wave 1: after the barrier below)
+        if (wv != 1 && nit > 0) {
+            w = xs_window(a, full ? 0 : slist[0]);
+            xs_dma(w, src.A, win, dr, lane, fx);
+        }
+        if (wv == 1) {
+            coherence();
+        } else if (nit > 0) {
+            win_dma_wait();
+            xs_fix(fx, win, 64 * dr + lane);
+        }
+        __syncthreads();   // the first windows complete; the selection visible to wave 1
+        if (wv == 1) {
+            ns = scount;
+            full = sfull != 0;
+            nit = full ? a.nseg : ns;
+            if (nit > 0) w = xs_window(a, full ? 0 : slist[0]);
+        }
+        const long nscan = nit;
         for (long si = 0; si < nit; ++si) {
             if (si > 0) {
                 __syncthreads();   // every row of the last segment is read before the copies
                 w = xs_window(a, full ? si : slist[si]);
-                if (wv != 1) xs_dma(w, src.A, win, dr, lane, fx);
+                if (wv != 1) {
+                    xs_dma(w, src.A, win, dr, lane, fx);
+                    win_dma_wait();
+                    xs_fix(fx, win, 64 * dr + lane);
+                }
+                __syncthreads();   // the windows are complete
             }
-            if (wv != 1) {
-                win_dma_wait();
-                xs_fix(fx, win, 64 * dr + lane);
-            }
-            __syncthreads();   // the windows are complete
             if (si == 0) {
                 xw_stamp(trace, 4);
                 if (wv == 0) wstamp(11);
