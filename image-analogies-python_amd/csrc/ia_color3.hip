@@ -41,6 +41,27 @@ struct Pw165 {
     __device__ __forceinline__ double result() const { return h1 + h2; }
 };
 
+// Pw165's sum of t[0..164] (the same accumulator order, the accumulators in registers: the
+// struct's runtime-indexed r[] lives in scratch when its feeding loop is not unrolled)
+__device__ __forceinline__ double pw165_sum(const double *t) {
+    double h[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const double *u = t + 80 * half;
+        double r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = u[j];
+#pragma unroll 1
+        for (int i = 8; i < 80; i += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] += u[i + j];
+        h[half] = Pw165::tree(r);
+    }
+#pragma unroll
+    for (int k = 160; k < D3; ++k) h[1] += t[k];
+    return h[0] + h[1];
+}
+
 struct Img3 {            // a channel-interleaved image (h x w x 3, fp64)
     const double *p;
     int h, w;
@@ -281,6 +302,128 @@ __global__ __launch_bounds__(64) void k_finish3(Fin3 f) {
     }
 }
 
+// The per-pixel tail with the per-query reduction of k_match3's partials folded in, one
+// 256-thread workgroup per pixel (k_finish3 took one wave and summed each distance serially
+// from global memory).  The 15 coherence candidates' and the exact winner's rows are read
+// once, lane-parallel over (row, feature); their plain and weighted squared terms go to LDS,
+// and 31 threads sum one row each in numpy's pairwise order (Pw165): the same values as
+// row3_dist.  The reduction of the partials is a lexicographic minimum, so its order does
+// not matter.
+__global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict__ part, int nb) {
+    __shared__ double qs[D3P], wsh[D3P];
+    __shared__ double tp[15][D3], tw[16][D3];   // plain terms (candidates), weighted (+ winner)
+    __shared__ double sump[15], sumw[16];
+    __shared__ long long rix[16];               // rows: candidates 0..14, winner 15 (-1: none)
+    __shared__ int rpos[15][3];
+    __shared__ double rd[4];
+    __shared__ long long ri[4];
+    const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int y = f.y_lo + m, x = f.t - 3 * y;
+    const int W = f.W, Ah = f.Ah, Aw = f.Aw;
+    const long hw = (long)Ah * Aw;
+    const bool first = y == 0 && x == 0;
+    // the query, the weights, the partials' minimum and the candidates' rows: one round trip
+    if (tid < D3P) {
+        qs[tid] = f.q3[(long)m * D3P + tid];
+        wsh[tid] = tid < D3 ? f.weights[tid] : 0.0;
+    }
+    double bd = INFINITY;
+    long long bi = 0x7fffffffffffffffLL;
+    for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o);
+        const long long oi = __shfl_xor(bi, o);
+        best3(bd, bi, od, oi);
+    }
+    if (lane == 0) { rd[wv] = bd; ri[wv] = bi; }
+    if (tid < 15) {
+        long long cix = -1;
+        int cr = 0, cc = 0, cim = 0;
+        if (!first) {
+            const int rr = y - 2 + tid / 5, rc = x - 2 + tid % 5;
+            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
+                const long sidx = (long)rr * W + rc;
+                const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
+                if (sr >= 0 && sr < Ah && sc >= 0 && sc < Aw) {
+                    const int simg = f.im[sidx];
+                    cix = ((long)Ah * simg + sr) * Aw + sc;
+                    cr = sr; cc = sc; cim = simg;
+                }
+            }
+        }
+        rix[tid] = cix;
+        rpos[tid][0] = cr; rpos[tid][1] = cc; rpos[tid][2] = cim;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w) best3(rd[0], ri[0], rd[w], ri[w]);
+        rix[15] = ri[0];
+    }
+    __syncthreads();
+    const long long app = rix[15];
+    // the terms: (row j, feature k) pairs spread over the block, each row read once
+    for (int e = tid; e < 16 * D3; e += 256) {
+        const int j = e / D3, k = e - j * D3;
+        const long long ix = rix[j];
+        if (ix < 0) continue;
+        const double d = f.db3[ix * D3P + k] - qs[k];
+        const double dw = d * wsh[k];
+        if (j < 15) tp[j][k] = d * d;
+        tw[j][k] = dw * dw;
+    }
+    __syncthreads();
+    if (tid < 31) {   // one row per thread, numpy's pairwise order
+        const bool pl = tid < 15;
+        const int j = pl ? tid : tid - 15;
+        const double *t = pl ? tp[j] : tw[j];
+        if (rix[j] >= 0) {
+            const double sq = sqrt(pw165_sum(t));
+            if (pl) sump[j] = sq; else sumw[j] = sq * sq;
+        } else {
+            if (pl) sump[j] = INFINITY; else sumw[j] = 0.0;
+        }
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    // coherence: the first minimum of the plain distances in (row, col) candidate order
+    double cd = lane < 15 && rix[lane] >= 0 ? sump[lane] : INFINITY;
+    long long cl = lane < 15 && rix[lane] >= 0 ? lane : 0x7fffffffffffffffLL;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(cd, o);
+        const long long ol = __shfl_xor(cl, o);
+        best3(cd, cl, od, ol);
+    }
+    const bool valid = cl != 0x7fffffffffffffffLL;
+    const int win = valid ? (int)cl : 0;
+    const int wr = rpos[win][0], wc = rpos[win][1], wim = rpos[win][2];
+    const double d_app = valid ? sumw[15] : 0.0, d_coh = valid ? sumw[win] : 0.0;
+    long img = app / hw;
+    long rem = app - img * hw;
+    const int ar = (int)(rem / Aw), ac = (int)(rem - (long)(rem / Aw) * Aw);
+    int pr = ar, pc = ac;
+    if (valid && d_coh <= d_app * f.kappa_factor) { pr = wr; pc = wc; img = wim; }
+    const long qpx = (long)y * W + x;
+    if (lane < 3)
+        f.Bp_lg[qpx * 3 + lane] = f.Ap_lg[((img * hw) + (long)pr * Aw + pc) * 3 + lane];
+    if (lane == 0) {
+        f.s[2 * qpx] = pr;
+        f.s[2 * qpx + 1] = pc;
+        f.im[qpx] = (int32_t)img;
+        if (f.dbg_px) {
+            int32_t *o = f.dbg_px + 7 * qpx;
+            o[0] = ar;
+            o[1] = ac;
+            o[2] = valid ? wr : 0;
+            o[3] = valid ? wc : 0;
+            o[4] = valid ? y - 2 + win / 5 : 0;
+            o[5] = valid ? x - 2 + win % 5 : 0;
+            o[6] = valid;
+            f.dbg_dist[2 * qpx] = valid ? d_app : 0.0;
+            f.dbg_dist[2 * qpx + 1] = valid ? d_coh : 0.0;
+        }
+    }
+}
+
 // per-pixel API helpers (algorithms.py:92-135) for 165-dim rows: the coherence argmin over n
 // candidate rows (first minimum of sqrt(pairwise((a - q)^2))) and weighted distances
 __global__ void k_coherence_pick3(const double *__restrict__ rows, int n, const double *__restrict__ q,
@@ -431,10 +574,9 @@ int ia_synth_level3(const IaSynthArgs *a, void *stream) {
         if (M <= 0) continue;
         k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, q3);
         k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, q3, M, part);
-        k_reduce3<<<M, 256, 0, st>>>(part, nb, best);
         f.t = t;
         f.y_lo = y_lo;
-        k_finish3<<<M, 64, 0, st>>>(f);
+        k_finish3w<<<M, 256, 0, st>>>(f, part, nb);
         IA_LAUNCH_CHECK("ia_synth_level3 wave");
     }
     return IA_OK;
