@@ -147,6 +147,9 @@ _SIGS = {
     'ia_diag_set_screen_pc': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_img_fused': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_screen_trace': (ctypes.c_int, [_dp]),
+    'ia_diag_set_color16': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_color16_stats': (ctypes.c_int, [_dp]),
+    'ia_diag_screen3': (ctypes.c_int, [_dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp, _dp]),
     'ia_diag_xwave_trace': (ctypes.c_int, [_dp]),
     'ia_diag_set_db_build_form': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_pyr_form': (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),

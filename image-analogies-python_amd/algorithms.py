@@ -190,7 +190,8 @@ class LevelIndex:
 
 class LevelIndex3:
     """As[level] for 3-channel images (num_ch = 3): the materialised fp64 rows
-    [A full | A'_i half], 165 values each (ia_db3_build), searched exhaustively in fp64
+    [A full | A'_i half], 165 values each (ia_db3_build, which also builds the split-f16
+    rows of the synthesis screen after them), searched exhaustively in fp64
     (ia_match3_batch) — exact like LevelIndex."""
 
     def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg):
@@ -230,7 +231,7 @@ class LevelIndex3:
 
     def features(self):
         """The full fp64 As[level] matrix (N x 165)."""
-        return self.db3.view(self.N, 168)[:, :165]
+        return self.db3[:self.N * 168].view(self.N, 168)[:, :165]
 
 
 class _LazyAs(list):

@@ -14,8 +14,10 @@
 // update of all three channels) runs one 64-lane wave per pixel.  Single GPU, exact matcher.
 #include "ia_common.h"
 #include "ia_internal.h"
+#include "ia_split16.h"
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 namespace ia {
@@ -128,6 +130,281 @@ __global__ __launch_bounds__(256) void k_query3(Img3 Bsm, Img3 Blg, Img3 Bpsm, I
     if (k < D3_FULL) v = feat3(Bsm, Blg, y, x, k);
     else if (k < D3) v = feat3(Bpsm, Bplg, y, x, k - D3_FULL);
     q3[(long)m * D3P + k] = v;
+}
+
+// ---- the split-f16 screen for 165-dim rows (IA_COLOR16=1) ---------------
+// The screen value of row r and query j is e = |a'|^2 - 2 a'.q' over 166 slots (165
+// centred features + the norm slot), carried as f16 pairs exactly like the luminance screen
+// (ia_split16.h: the same scales sa, 2^R, sq): alpha = [sa a'_k, sa 2^-R |a'|^2], beta =
+// [sq (-2 q'_k), sq 2^R], alpha . beta = sa sq e.  The 176 slots (166 + 10 zeros) are 11
+// chunks of 16, each one v_mfma_f32_32x32x16_f16 per product: the 22 cross-term MFMAs
+// (a_h q_l, a_l q_h) first, then the 11 main ones (a_h q_h, the norm slot in the last): 33
+// per 32x32 tile.  The screen keeps the minimum per (query, 32-row tile); the exact stage
+// (k_finish3w<true>) rescores in fp64 every row of the tiles whose minimum is within 2 eps3
+// of the smallest (the error bound of DESIGN.md §4c).
+constexpr int C16_CH = 11;                 // 16-slot chunks
+constexpr int C16_GRP = 2 * C16_CH;        // half8 groups per lane and tile: (chunk, hi / lo)
+constexpr int C16_TILE = C16_GRP * 64;     // half8 per 32-row (or 32-query) tile
+constexpr int C3_NSLOT = 16 * C16_CH;      // 176
+constexpr int C3_CAND = 64;                // candidate tiles listed per query (more: all)
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// lane (row / query l & 31, half h = l >> 5) of group (chunk c, part p) holds slots
+// 16c + 8h .. +7: half8 index within a tile
+__host__ __device__ constexpr int c16_at(int c, int p, int h, int j) { return (2 * c + p) * 64 + h * 32 + j; }
+
+struct Col16Meta {                         // per database: centre, range keys, bound
+    double center[D3P];
+    unsigned long long rng[2 * D3P];       // order keys of min and of -max per feature
+    unsigned int amax_bits;                // fp32 bits of A >= max row |a'| (atomicMax)
+    unsigned int pad;
+};
+
+struct Db3View {                           // the ia_db3_build buffer: fp64 rows | split | meta
+    double *rows;
+    half8 *db16;
+    Col16Meta *meta;
+    long ntiles;
+};
+static inline size_t db3_rows_bytes(long nrows) { return align_up((size_t)nrows * D3P * sizeof(double), 256); }
+__host__ __device__ inline long db3_tiles(long nrows) { return (nrows + 31) / 32; }
+static inline size_t db3_split_bytes(long nrows) { return (size_t)db3_tiles(nrows) * C16_TILE * sizeof(half8); }
+static inline Db3View db3_view(void *base, long nrows) {
+    char *b = reinterpret_cast<char *>(base);
+    Db3View v;
+    v.rows = reinterpret_cast<double *>(b);
+    v.db16 = reinterpret_cast<half8 *>(b + db3_rows_bytes(nrows));
+    v.meta = reinterpret_cast<Col16Meta *>(b + db3_rows_bytes(nrows) + db3_split_bytes(nrows));
+    v.ntiles = db3_tiles(nrows);
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long c3key(double x) {   // order-preserving key
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double c3key_inv(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k));
+}
+
+// per-feature range of the rows: thread k of a block scans RB rows of feature k
+constexpr int C3_RB = 1024;
+__global__ __launch_bounds__(D3P) void k_db3_range(const double *__restrict__ rows, long nrows,
+                                                   Col16Meta *__restrict__ meta) {
+    const int k = threadIdx.x;
+    if (k >= D3) return;
+    const long r0 = (long)blockIdx.x * C3_RB;
+    const long r1 = r0 + C3_RB < nrows ? r0 + C3_RB : nrows;
+    double lo = INFINITY, hi = -INFINITY;
+    for (long r = r0; r < r1; ++r) {
+        const double v = rows[r * D3P + k];
+        lo = fmin(lo, v);
+        hi = fmax(hi, v);
+    }
+    atomicMin(&meta->rng[2 * k], c3key(lo));
+    atomicMin(&meta->rng[2 * k + 1], c3key(-hi));
+}
+
+// the centre (midrange) into LDS from the range keys
+__device__ __forceinline__ void c3_center(const Col16Meta *meta, double *cs) {
+    for (int k = threadIdx.x; k < D3P; k += blockDim.x)
+        cs[k] = k < D3 ? 0.5 * (c3key_inv(meta->rng[2 * k]) - c3key_inv(meta->rng[2 * k + 1])) : 0.0;
+}
+
+__device__ __forceinline__ double c3_norm(const double *a, const double *cs) {
+    double n = 0.0;
+#pragma unroll 5
+    for (int k = 0; k < D3; ++k) {
+        const double d = a[k] - cs[k];
+        n = fma(d, d, n);
+    }
+    return n;
+}
+
+// A: max over rows of |a'| rounded up to fp32 (one thread per row); block 0 stores the centre
+__global__ __launch_bounds__(256) void k_db3_bound(const double *__restrict__ rows, long nrows,
+                                                   Col16Meta *__restrict__ meta) {
+    __shared__ double cs[D3P];
+    __shared__ float red[4];
+    c3_center(meta, cs);
+    __syncthreads();
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k < D3P; k += 256) meta->center[k] = cs[k];
+    const long r = (long)blockIdx.x * 256 + threadIdx.x;
+    float a = 0.f;
+    if (r < nrows) {
+        const double n = c3_norm(rows + r * D3P, cs);
+        a = (float)sqrt(n);
+        if ((double)a * (double)a < n) a = nextafterf(a, INFINITY);
+        a = nextafterf(a, INFINITY);   // the fp64 norm's own rounding
+    }
+    for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        atomicMax(&meta->amax_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+// the split rows, one thread per row (rows >= nrows repeat the last row): 22 half8 per row,
+// lanes of consecutive rows writing consecutive 16 B
+__global__ __launch_bounds__(256) void k_db3_split(const double *__restrict__ rows, long nrows,
+                                                   const Col16Meta *__restrict__ meta,
+                                                   half8 *__restrict__ db16) {
+    __shared__ double cs[D3P];
+    for (int k = threadIdx.x; k < D3P; k += 256) cs[k] = meta->center[k];
+    __syncthreads();
+    const long r = (long)blockIdx.x * 256 + threadIdx.x;
+    if (r >= db3_tiles(nrows) * 32) return;
+    const double *a = rows + (r < nrows ? r : nrows - 1) * D3P;
+    const float amax = __uint_as_float(meta->amax_bits);
+    const Split16Db sc = split16_db_scale(amax);
+    const double nrm = c3_norm(a, cs);
+    half8 *t = db16 + (r >> 5) * C16_TILE + (r & 31);
+#pragma unroll 1
+    for (int c = 0; c < C16_CH; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            half8 vh, vl;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = 16 * c + 8 * h + e;
+                double x = 0.0;
+                if (k < D3) x = ldexp(a[k] - cs[k], sc.ea);
+                else if (k == D3) x = ldexp((double)(float)nrm, sc.ea - sc.R);
+                _Float16 xh, xl;
+                split16d(x, xh, xl);
+                vh[e] = xh;
+                vl[e] = xl;
+            }
+            t[c16_at(c, 0, h, 0)] = vh;
+            t[c16_at(c, 1, h, 0)] = vl;
+        }
+}
+
+// the split operand of query m (q16) and |q'|^2 (qn) from thread k's feature v (256
+// threads; m >= M: zero columns)
+__device__ __forceinline__ void c3_query_split(int m, int M, int k, double v, const Col16Meta *meta,
+                                               double *qn, _Float16 *q16, double *red) {
+    _Float16 *qt = q16 + (long)(m >> 5) * C16_TILE * 8;
+    const int col = m & 31;
+    auto put = [&](int slot, _Float16 h, _Float16 l) {
+        const int c = slot >> 4, hh = (slot >> 3) & 1, e = slot & 7;
+        qt[c16_at(c, 0, hh, col) * 8 + e] = h;
+        qt[c16_at(c, 1, hh, col) * 8 + e] = l;
+    };
+    if (m >= M) {
+        if (k < C3_NSLOT) put(k, (_Float16)0.f, (_Float16)0.f);
+        return;
+    }
+    const double d = k < D3 ? v - meta->center[k] : 0.0;
+    double n = d * d;
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if ((k & 63) == 0) red[k >> 6] = n;
+    __syncthreads();
+    const double nq = (red[0] + red[1]) + (red[2] + red[3]);
+    if (k == 0) qn[m] = nq;
+    if (k < C3_NSLOT) {
+        const Split16Db sc = split16_db_scale(__uint_as_float(meta->amax_bits));
+        const int eq = split16_q_scale(nq, sc.R);
+        double b = 0.0;
+        if (k < D3) b = ldexp(-2.0 * d, eq);
+        else if (k == D3) b = ldexp(1.0, eq + sc.R);
+        _Float16 h, l;
+        split16d(b, h, l);
+        put(k, h, l);
+    }
+}
+
+// queries of wave t for the split-f16 screen: the fp64 row (q3, as k_query3), |q'|^2 (qn)
+// and the split operand (q16); blocks M .. Mpad-1 zero their query columns
+__global__ __launch_bounds__(256) void k_query3s(Img3 Bsm, Img3 Blg, Img3 Bpsm, Img3 Bplg, int t,
+                                                 int y_lo, int M, const Col16Meta *__restrict__ meta,
+                                                 double *__restrict__ q3, double *__restrict__ qn,
+                                                 _Float16 *__restrict__ q16) {
+    __shared__ double red[4];
+    const int m = blockIdx.x, k = threadIdx.x;
+    double v = 0.0;
+    if (m < M) {
+        const int y = y_lo + m, x = t - 3 * y;
+        if (k < D3_FULL) v = feat3(Bsm, Blg, y, x, k);
+        else if (k < D3) v = feat3(Bpsm, Bplg, y, x, k - D3_FULL);
+        if (k < D3P) q3[(long)m * D3P + k] = v;
+    }
+    c3_query_split(m, M, k, v, meta, qn, q16, red);
+}
+
+// diagnostic: the split operand of given queries (M x 165)
+__global__ __launch_bounds__(256) void k_qsplit3(const double *__restrict__ q165, int M,
+                                                 const Col16Meta *__restrict__ meta,
+                                                 double *__restrict__ qn, _Float16 *__restrict__ q16) {
+    __shared__ double red[4];
+    const int m = blockIdx.x, k = threadIdx.x;
+    const double v = m < M && k < D3 ? q165[(long)m * D3 + k] : 0.0;
+    c3_query_split(m, M, k, v, meta, qn, q16, red);
+}
+
+// diagnostic: the screen's tile minima in unscaled units (e = s / (sa sq)), eps3 per query
+__global__ void k_screen3_unscale(const float *__restrict__ smin, int M, int ntiles,
+                                  const double *__restrict__ qn, const Col16Meta *__restrict__ meta,
+                                  double *__restrict__ e, double *__restrict__ eps) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)M * ntiles) return;
+    const int m = (int)(i / ntiles);
+    const float amax = __uint_as_float(meta->amax_bits);
+    const Split16Db sc = split16_db_scale(amax);
+    const int eq = split16_q_scale(qn[m], sc.R);
+    e[i] = ldexp((double)smin[i], -(sc.ea + eq));
+    if (i % ntiles == 0) {
+        constexpr double U32 = 5.9604644775390625e-08;
+        const double A = (double)amax;
+        eps[m] = U32 * (900.0 * A * sqrt(qn[m]) + 450.0 * A * A);
+    }
+}
+
+// the screen: block (x, query tile y) of 4 waves, each wave a run of tpw row tiles against
+// the query tile held in registers; per (query, row tile) the minimum of the 32 values
+__global__ __launch_bounds__(256) void k_screen3(const half8 *__restrict__ db16, int ntiles,
+                                                 const half8 *__restrict__ q16, int M, int tpw,
+                                                 float *__restrict__ smin) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int qt = blockIdx.y;
+    half8 qh[C16_CH], ql[C16_CH];
+    const half8 *qb = q16 + (long)qt * C16_TILE + lane;
+#pragma unroll
+    for (int c = 0; c < C16_CH; ++c) {
+        qh[c] = qb[(2 * c) * 64];
+        ql[c] = qb[(2 * c + 1) * 64];
+    }
+    const int q = qt * 32 + lane;
+    const bool wr = lane < 32 && q < M;
+    float *out = smin + (long)q * ntiles;
+    const int t0 = (blockIdx.x * 4 + wv) * tpw;
+    const int t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+    const floatx16 zero = {};
+    for (int t = t0; t < t1; ++t) {
+        const half8 *db = db16 + (long)t * C16_TILE + lane;
+        half8 ah[C16_CH], al[C16_CH];
+#pragma unroll
+        for (int c = 0; c < C16_CH; ++c) {
+            ah[c] = db[(2 * c) * 64];
+            al[c] = db[(2 * c + 1) * 64];
+        }
+        floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[0], ql[0], zero, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[0], qh[0], acc, 0, 0, 0);
+#pragma unroll
+        for (int c = 1; c < C16_CH; ++c) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], ql[c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], qh[c], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < C16_CH; ++c)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], qh[c], acc, 0, 0, 0);
+        float mn = acc[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) mn = fminf(mn, acc[i]);
+        mn = fminf(mn, __shfl_xor(mn, 32));
+        if (wr) out[t] = mn;
+    }
 }
 
 // exhaustive fp64 search: a block takes 32 rows (staged in LDS) against every query, 8 at
@@ -302,34 +579,108 @@ __global__ __launch_bounds__(64) void k_finish3(Fin3 f) {
     }
 }
 
-// The per-pixel tail with the per-query reduction of k_match3's partials folded in, one
-// 256-thread workgroup per pixel (k_finish3 took one wave and summed each distance serially
-// from global memory).  The 15 coherence candidates' and the exact winner's rows are read
-// once, lane-parallel over (row, feature); their plain and weighted squared terms go to LDS,
-// and 31 threads sum one row each in numpy's pairwise order (Pw165): the same values as
-// row3_dist.  The reduction of the partials is a lexicographic minimum, so its order does
-// not matter.
-__global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict__ part, int nb) {
+// the exact stage's inputs on the split-f16 screen: per (query, row tile) minima, |q'|^2
+struct Scr3 {
+    const float *smin;       // M x ntiles
+    int ntiles;
+    long nrows;
+    const double *qn;
+    const Col16Meta *meta;
+    unsigned long long *stats;   // [candidate tiles, full scans] (diagnostic, may be null)
+};
+
+// Thresholds of the colour exact stage: Tseg = e* + 2 eps3 in screen units,
+// eps3 = u (900 A|q'| + 450 A^2); full scan when the norm slot nears the f16 floor
+__device__ __forceinline__ double c3_tseg(float emin, float amax0, double nqq, bool &force_full) {
+    constexpr double U32 = 5.9604644775390625e-08;
+    const double A = (double)amax0;
+    const Split16Db sc = split16_db_scale(amax0);
+    const int eq = split16_q_scale(nqq, sc.R);
+    const int e2 = sc.ea + eq;
+    const double em = ldexp((double)emin, -e2);
+    const double eps3 = U32 * (900.0 * A * sqrt(nqq) + 450.0 * A * A);
+    const double slack = 1e-12 * (fabs(em) + nqq + A * A);
+    force_full = eq + sc.R < -10;
+    return ldexp(em + 2.0 * eps3 + slack, e2);
+}
+
+// The per-pixel tail, one 256-thread workgroup per pixel (k_finish3 took one wave and summed
+// each distance serially from global memory).  The winner: SCR = false reduces k_match3's
+// partials (a lexicographic minimum: order free); SCR = true is the exact stage of the
+// split-f16 screen: e* over the query's tile minima, the tiles within the threshold, and
+// every row of those tiles rescored in fp64 (terms lane-parallel into LDS, one thread per
+// row summing them in numpy's pairwise order, Pw165), lexicographic (distance, row) minimum.
+// Then the 15 coherence candidates' and the winner's rows are read once, lane-parallel over
+// (row, feature); their plain and weighted squared terms go to LDS, and 31 threads sum one
+// row each (Pw165): the same values as row3_dist.
+template <bool SCR>
+__global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict__ part, int nb, Scr3 sc) {
     __shared__ double qs[D3P], wsh[D3P];
-    __shared__ double tp[15][D3], tw[16][D3];   // plain terms (candidates), weighted (+ winner)
+    __shared__ double tt[32 * D3];              // exact-stage terms; then tp / tw below
+    double (*tp)[D3] = reinterpret_cast<double (*)[D3]>(tt);            // 15 plain (candidates)
+    double (*tw)[D3] = reinterpret_cast<double (*)[D3]>(tt + 15 * D3);  // 16 weighted (+ winner)
     __shared__ double sump[15], sumw[16];
     __shared__ long long rix[16];               // rows: candidates 0..14, winner 15 (-1: none)
     __shared__ int rpos[15][3];
     __shared__ double rd[4];
     __shared__ long long ri[4];
+    __shared__ float fmn[4];
+    __shared__ int clist[C3_CAND], ccount;
     const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int y = f.y_lo + m, x = f.t - 3 * y;
     const int W = f.W, Ah = f.Ah, Aw = f.Aw;
     const long hw = (long)Ah * Aw;
     const bool first = y == 0 && x == 0;
-    // the query, the weights, the partials' minimum and the candidates' rows: one round trip
+    // the query, the weights, the partials' minimum (or the tile minima's) and the
+    // candidates' rows: one round trip
     if (tid < D3P) {
         qs[tid] = f.q3[(long)m * D3P + tid];
         wsh[tid] = tid < D3 ? f.weights[tid] : 0.0;
     }
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
-    for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
+    if constexpr (!SCR) {
+        for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
+    } else {
+        const float *sm = sc.smin + (long)m * sc.ntiles;
+        float mn = INFINITY;
+        for (int i = tid; i < sc.ntiles; i += 256) mn = fminf(mn, sm[i]);
+        for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o));
+        if (lane == 0) fmn[wv] = mn;
+        if (tid == 0) ccount = 0;
+        __syncthreads();
+        mn = fminf(fminf(fmn[0], fmn[1]), fminf(fmn[2], fmn[3]));
+        bool full;
+        const double Tseg = c3_tseg(mn, __uint_as_float(sc.meta->amax_bits), sc.qn[m], full);
+        if (!full)
+            for (int i = tid; i < sc.ntiles; i += 256)
+                if ((double)sm[i] <= Tseg) {
+                    const int j = atomicAdd(&ccount, 1);
+                    if (j < C3_CAND) clist[j] = i;
+                }
+        __syncthreads();
+        const int nc = ccount;
+        full = full || nc > C3_CAND;
+        const int ntl = full ? sc.ntiles : nc;
+        if (tid == 0 && sc.stats) {
+            atomicAdd(&sc.stats[0], (unsigned long long)ntl);
+            if (full) atomicAdd(&sc.stats[1], 1ull);
+        }
+        for (int b = 0; b < ntl; ++b) {
+            const long r0 = (long)(full ? b : clist[b]) * 32;
+            for (int e = tid; e < 32 * D3; e += 256) {
+                const int j = e / D3, k = e - j * D3;
+                const long r = r0 + j;
+                if (r < sc.nrows) {
+                    const double d = f.db3[r * D3P + k] - qs[k];
+                    tt[e] = d * d;
+                }
+            }
+            __syncthreads();
+            if (tid < 32 && r0 + tid < sc.nrows) best3(bd, bi, pw165_sum(tt + tid * D3), r0 + tid);
+            __syncthreads();
+        }
+    }
     for (int o = 32; o > 0; o >>= 1) {
         const double od = __shfl_xor(bd, o);
         const long long oi = __shfl_xor(bi, o);
@@ -472,22 +823,66 @@ __global__ void k_split_best3(const Best *__restrict__ b, int M, int64_t *idx, d
 static inline int max_wave(int H, int W) { return std::min(H, (W + 2) / 3) + 1; }
 static inline int match3_blocks(long nrows) { return (int)((nrows + M3_ROWS - 1) / M3_ROWS); }
 
+// IA_COLOR16 (ia_diag_set_color16): 1 the split-f16 screen + exact stage, 0 the exhaustive
+// fp64 search (k_match3)
+static std::atomic<int> g_color16{env_int("IA_COLOR16", 1)};
+static unsigned long long *g_c3_stats = nullptr;   // diagnostic counters (ia_diag_color16_stats)
+
+// the synthesis workspace: q3 | best | partials (fp64 search) | q16 | qn | tile minima
+struct Ws3 {
+    double *q3;
+    Best *best, *part;
+    half8 *q16;
+    double *qn;
+    float *smin;
+};
+static inline size_t ws3_layout(int H, int W, long nrows, char *base, Ws3 *w) {
+    const size_t M = (size_t)max_wave(H, W), Mp = (M + 31) / 32 * 32;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { char *p = base ? base + o : nullptr; o += align_up(bytes, 256); return p; };
+    char *q3 = take(Mp * D3P * sizeof(double));
+    char *best = take(M * sizeof(Best));
+    char *part = take(M * (size_t)match3_blocks(nrows) * sizeof(Best));
+    char *q16 = take(Mp / 32 * C16_TILE * sizeof(half8));
+    char *qn = take(Mp * sizeof(double));
+    char *smin = take(M * (size_t)db3_tiles(nrows) * sizeof(float));
+    if (w) {
+        w->q3 = reinterpret_cast<double *>(q3);
+        w->best = reinterpret_cast<Best *>(best);
+        w->part = reinterpret_cast<Best *>(part);
+        w->q16 = reinterpret_cast<half8 *>(q16);
+        w->qn = reinterpret_cast<double *>(qn);
+        w->smin = reinterpret_cast<float *>(smin);
+    }
+    return o;
+}
+
 }  // namespace ia
 
 using namespace ia;
 
 extern "C" {
 
-size_t ia_db3_bytes(long nrows) { return nrows > 0 ? (size_t)nrows * D3P * sizeof(double) : 0; }
+size_t ia_db3_bytes(long nrows) {
+    return nrows > 0 ? db3_rows_bytes(nrows) + db3_split_bytes(nrows) + sizeof(Col16Meta) : 0;
+}
 
 int ia_db3_build(const IaSrcLevel *src, long row0, long nrows, double *db3, void *stream) {
     IA_ARG(src && db3 && nrows > 0 && row0 >= 0, "ia_db3_build: bad args");
     IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db3_build: rows out of range");
     const Img3 Asm{src->A_sm, src->A_hs, src->A_ws}, Alg{src->A_lg, src->Ah, src->Aw};
     const long n = nrows * D3P;
-    k_db3_build<<<(unsigned)((n + 255) / 256), 256, 0, S(stream)>>>(Asm, Alg, src->Ap_sm, src->Ap_lg,
-                                                                   row0, nrows, db3);
-    IA_LAUNCH_CHECK("k_db3_build");
+    hipStream_t st = S(stream);
+    k_db3_build<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(Asm, Alg, src->Ap_sm, src->Ap_lg,
+                                                            row0, nrows, db3);
+    // the split-f16 rows of the screen: range -> centre and bound -> split
+    const Db3View v = db3_view(db3, nrows);
+    IA_HIP(hipMemsetAsync(v.meta->rng, 0xff, sizeof(v.meta->rng), st));
+    IA_HIP(hipMemsetAsync(&v.meta->amax_bits, 0, sizeof(unsigned int), st));
+    k_db3_range<<<(unsigned)((nrows + C3_RB - 1) / C3_RB), D3P, 0, st>>>(v.rows, nrows, v.meta);
+    k_db3_bound<<<(unsigned)((nrows + 255) / 256), 256, 0, st>>>(v.rows, nrows, v.meta);
+    k_db3_split<<<(unsigned)((v.ntiles * 32 + 255) / 256), 256, 0, st>>>(v.rows, nrows, v.meta, v.db16);
+    IA_LAUNCH_CHECK("ia_db3_build");
     return IA_OK;
 }
 
@@ -541,11 +936,7 @@ int ia_match3_batch(const double *db3, long nrows, const double *q165, int M, in
     return IA_OK;
 }
 
-size_t ia_synth3_workspace_bytes(int H, int W, long nrows) {
-    const size_t M = (size_t)max_wave(H, W);
-    return align_up(M * D3P * sizeof(double), 256) + align_up(M * sizeof(Best), 256) +
-           align_up(M * (size_t)match3_blocks(nrows) * sizeof(Best), 256);
-}
+size_t ia_synth3_workspace_bytes(int H, int W, long nrows) { return ws3_layout(H, W, nrows, nullptr, nullptr); }
 
 int ia_synth_level3(const IaSynthArgs *a, void *stream) {
     IA_ARG(a && a->db && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg && a->weights && a->s && a->im &&
@@ -556,29 +947,85 @@ int ia_synth_level3(const IaSynthArgs *a, void *stream) {
     IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level3: debug outputs come in pairs");
     hipStream_t st = S(stream);
     const int H = a->H, W = a->W;
-    const int Mmax = max_wave(H, W);
-    char *ws = reinterpret_cast<char *>(a->workspace);
-    double *q3 = reinterpret_cast<double *>(ws);
-    Best *best = reinterpret_cast<Best *>(ws + align_up((size_t)Mmax * D3P * sizeof(double), 256));
-    Best *part = reinterpret_cast<Best *>(reinterpret_cast<char *>(best) + align_up((size_t)Mmax * sizeof(Best), 256));
+    Ws3 w;
+    ws3_layout(H, W, a->nrows, reinterpret_cast<char *>(a->workspace), &w);
     const int nb = match3_blocks(a->nrows);
     const Img3 Bsm{a->B_sm, a->B_hs, a->B_ws}, Blg{a->B_lg, H, W};
     const Img3 Bpsm{a->Bp_sm, a->B_hs, a->B_ws}, Bplg{a->Bp_lg, H, W};
-    Fin3 f{reinterpret_cast<const double *>(a->db), q3, best, a->src.Ap_lg, a->src.Ah, a->src.Aw,
+    const Db3View v = db3_view(const_cast<void *>(a->db), a->nrows);
+    Fin3 f{v.rows, w.q3, w.best, a->src.Ap_lg, a->src.Ah, a->src.Aw,
            0, 0, W, a->weights, a->kappa_factor, a->Bp_lg, a->s, a->im, a->dbg_px, a->dbg_dist};
+    const bool split = g_color16.load(std::memory_order_relaxed) != 0;
+    const int ntiles = (int)v.ntiles;
+    const Scr3 sc{w.smin, ntiles, a->nrows, w.qn, v.meta, g_c3_stats};
     const int nwaves = (W - 1) + 3 * (H - 1) + 1;
     for (int t = 0; t < nwaves; ++t) {
         const int y_lo = std::max(0, (t - (W - 1) + 2) / 3);
         const int y_hi = std::min(H - 1, t / 3);
         const int M = y_hi - y_lo + 1;
         if (M <= 0) continue;
-        k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, q3);
-        k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, q3, M, part);
         f.t = t;
         f.y_lo = y_lo;
-        k_finish3w<<<M, 256, 0, st>>>(f, part, nb);
+        if (split) {
+            const int QT = (M + 31) / 32;
+            // row tiles per wave: about 2048 waves over the (row tile, query tile) pairs
+            const int tpw = std::max(1, (int)(((long)ntiles * QT + 2047) / 2048));
+            const dim3 grid((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QT);
+            k_query3s<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, w.q3, w.qn,
+                                               reinterpret_cast<_Float16 *>(w.q16));
+            k_screen3<<<grid, 256, 0, st>>>(v.db16, ntiles, w.q16, M, tpw, w.smin);
+            k_finish3w<true><<<M, 256, 0, st>>>(f, nullptr, 0, sc);
+        } else {
+            k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, w.q3);
+            k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, w.q3, M, w.part);
+            k_finish3w<false><<<M, 256, 0, st>>>(f, w.part, nb, sc);
+        }
         IA_LAUNCH_CHECK("ia_synth_level3 wave");
     }
+    return IA_OK;
+}
+
+int ia_diag_screen3(const void *db3, long nrows, const double *q165, int M, double *e, double *eps,
+                    double *qn) {
+    IA_ARG(db3 && q165 && e && eps && qn && nrows > 0 && M > 0, "ia_diag_screen3: bad args");
+    const Db3View v = db3_view(const_cast<void *>(db3), nrows);
+    const int QT = (M + 31) / 32, ntiles = (int)v.ntiles;
+    half8 *q16 = nullptr;
+    float *smin = nullptr;
+    IA_HIP(hipMalloc(&q16, (size_t)QT * C16_TILE * sizeof(half8)));
+    IA_HIP(hipMalloc(&smin, (size_t)M * ntiles * sizeof(float)));
+    k_qsplit3<<<QT * 32, 256>>>(q165, M, v.meta, qn, reinterpret_cast<_Float16 *>(q16));
+    const int tpw = std::max(1, (int)(((long)ntiles * QT + 2047) / 2048));
+    k_screen3<<<dim3((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QT), 256>>>(
+        v.db16, ntiles, q16, M, tpw, smin);
+    const long n = (long)M * ntiles;
+    k_screen3_unscale<<<(unsigned)((n + 255) / 256), 256>>>(smin, M, ntiles, qn, v.meta, e, eps);
+    IA_LAUNCH_CHECK("ia_diag_screen3");
+    IA_HIP(hipDeviceSynchronize());
+    IA_HIP(hipFree(q16));
+    IA_HIP(hipFree(smin));
+    return IA_OK;
+}
+
+int ia_diag_set_color16(int on) {
+    const int prev = g_color16.load();
+    if (on == 0 || on == 1) g_color16.store(on);
+    return prev;
+}
+
+// the colour exact stage's counters since the last call: [candidate tiles rescored, queries
+// that scanned every tile]; the first call allocates them (and returns zeros)
+int ia_diag_color16_stats(unsigned long long *out) {
+    IA_ARG(out, "ia_diag_color16_stats: bad args");
+    if (!g_c3_stats) {
+        IA_HIP(hipMalloc(&g_c3_stats, 2 * sizeof(unsigned long long)));
+        IA_HIP(hipMemset(g_c3_stats, 0, 2 * sizeof(unsigned long long)));
+        out[0] = out[1] = 0;
+        return IA_OK;
+    }
+    IA_HIP(hipDeviceSynchronize());
+    IA_HIP(hipMemcpy(out, g_c3_stats, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    IA_HIP(hipMemset(g_c3_stats, 0, 2 * sizeof(unsigned long long)));
     return IA_OK;
 }
 

@@ -72,6 +72,17 @@ int ia_diag_set_img_fused(int on);
 /* k_screen16p stage stamps into buf (device, 16 waves x 256 u64: blocks 0 and 300, per
  * stage < 64 four s_memtime values; see ia_screen16.hip pc_stamp), NULL turns them off */
 int ia_diag_screen_trace(void *buf);
+
+/* 3-channel matching (ia_color3.hip): IA_COLOR16 (1 the split-f16 screen + exact stage, 0 the
+ * exhaustive fp64 search; returns the previous value), the exact stage's counters since the
+ * last call ([candidate 32-row tiles rescored, queries that scanned every tile]; the first call
+ * starts counting), and the screen of M queries (M x 165) over an ia_db3_build buffer: per
+ * (query, 32-row tile) the minimum screen value unscaled (M x ntiles, ntiles = ceil(nrows /
+ * 32)), eps3 and |q'|^2 per query */
+int ia_diag_set_color16(int on);
+int ia_diag_color16_stats(unsigned long long *out);
+int ia_diag_screen3(const void *db3, long nrows, const double *q165, int M, double *e, double *eps,
+                    double *qn);
 /* with IA_XW_TRACE=<level tag>: the fused kernel's phase stamps of that level (100 MHz
  * s_memrealtime) for waves < 4096 and the first 8 pixels of each, 12 stamps per pixel:
  * {start, ticket, e*, candidates, re-screen, rescore | coherence, winner, exchange,

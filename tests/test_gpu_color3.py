@@ -92,11 +92,65 @@ def test_api3_vs_oracle(gpu):
             assert tuple(np.asarray(got[2]).tolist()) == tuple(np.asarray(ref[2]).tolist())
 
 
+@pytest.fixture
+def color16():
+    """Select the 3-channel matcher (1 split-f16 screen + exact stage, 0 exhaustive fp64)."""
+    import _ia
+    lib = _ia.lib()
+    prev = lib.ia_diag_set_color16(1)
+    yield lib.ia_diag_set_color16
+    lib.ia_diag_set_color16(prev)
+
+
+@pytest.mark.parametrize('scale', [1e-3, 1.0, 1e3])
+def test_screen3_error_bound(gpu, scale):
+    """The colour screen's tile minima (split-f16 MFMA) are within eps3 of
+    the exact min over the tile of |a - q|^2 - |q'|^2, at input scales 1e-3 .. 1e3, for
+    queries near DB rows (small distances) and far from them."""
+    import ctypes
+    import _ia
+    import algorithms
+    A_pyr, Ap_list, _, _, L = inputs(85, (45, 70), (20, 20), n_ap=2)
+    lv = L - 1
+    sc = lambda p: dev(p * scale)  # noqa: E731
+    idx = algorithms.LevelIndex3(sc(A_pyr[lv - 1]), sc(A_pyr[lv]),
+                                 torch.stack([sc(p[lv - 1]) for p in Ap_list]),
+                                 torch.stack([sc(p[lv]) for p in Ap_list]))
+    rows = idx.features().cpu().numpy()
+    N = rows.shape[0]
+    rs = np.random.RandomState(5)
+    Q = np.vstack([rows[rs.randint(0, N, 40)] + rs.randn(40, 165) * 1e-3 * scale,
+                   rs.rand(24, 165) * scale, rows[rs.randint(0, N, 6)]])
+    M = Q.shape[0]
+    nt = (N + 31) // 32
+    e = torch.empty((M, nt), dtype=torch.float64, device='cuda')
+    eps = torch.empty(M, dtype=torch.float64, device='cuda')
+    qn = torch.empty(M, dtype=torch.float64, device='cuda')
+    Qd = dev(Q)
+    _ia.check(_ia.lib().ia_diag_screen3(_ia.ptr(idx.db3), N, _ia.ptr(Qd), M, _ia.ptr(e),
+                                        _ia.ptr(eps), _ia.ptr(qn)), 'ia_diag_screen3')
+    torch.cuda.synchronize()
+    e, eps, qn = e.cpu().numpy(), eps.cpu().numpy(), qn.cpu().numpy()
+    pad = np.vstack([rows, np.repeat(rows[-1:], nt * 32 - N, 0)])
+    worst = 0.0
+    for m in range(M):
+        D = ((pad - Q[m]) ** 2).sum(1) - qn[m]
+        x = D.reshape(nt, 32).min(1)
+        err = np.abs(e[m] - x).max()
+        slack = 1e-12 * (np.abs(x).max() + qn[m])
+        assert err <= eps[m] + slack, (m, err, eps[m])
+        worst = max(worst, err / eps[m])
+    assert worst > 0.0
+
+
+@pytest.mark.parametrize('matcher', [1, 0])
 @pytest.mark.parametrize('n_ap,k', [(1, 1.0), (2, 25.0)])
-def test_synthesis3_vs_oracle(gpu, n_ap, k):
+def test_synthesis3_vs_oracle(gpu, color16, n_ap, k, matcher):
     """Whole-level 3-channel synthesis: B' (all channels), s, im and the debug lists equal
-    the oracle's scanline run (image_analogies.py:130-240 with num_ch = 3)."""
+    the oracle's scanline run (image_analogies.py:130-240 with num_ch = 3), with the
+    split-f16 screen + exact stage (1) and the exhaustive fp64 search (0)."""
     import image_analogies as ia
+    color16(matcher)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = inputs(83 + n_ap, (36, 44), (30, 34), n_ap=n_ap)
     w = o.compute_weights(3, 5, 12, 3)
     As = o.create_index(A_pyr, Ap_list, L)
@@ -121,6 +175,36 @@ def test_synthesis3_vs_oracle(gpu, n_ap, k):
             assert rec[key] == rd[key], (level, key)
         assert np.array_equal(rec['app_dist'], rd['app_dist']), level
         assert np.array_equal(rec['coh_dist'], rd['coh_dist']), level
+
+
+def test_synthesis3_split_larger_vs_oracle(gpu, color16):
+    """A larger 3-channel synthesis on the split-f16 screen (A 72 x 90, two A' images, B
+    60 x 66, every level): s, im and B' equal the oracle's, and the exact stage's work stays
+    small (candidate tiles per query, no query scanning every tile)."""
+    import ctypes
+    import _ia
+    import image_analogies as ia
+    color16(1)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = inputs(88, (72, 90), (60, 66), n_ap=2)
+    w = o.compute_weights(3, 5, 12, 3)
+    As = o.create_index(A_pyr, Ap_list, L)
+    Bp_ref = [b.copy() for b in Bp_pyr]
+    ref = {l: o.synthesize_level(l, L, A_pyr, Ap_list, B_pyr, Bp_ref, As[l], w, 2.0)
+           for l in range(1, L)}
+    st = (ctypes.c_ulonglong * 2)()
+    _ia.check(_ia.lib().ia_diag_color16_stats(st), 'stats')
+    Bp_dev = [dev(b) for b in Bp_pyr]
+    out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                            [dev(p) for p in B_pyr], Bp_dev, L, 2.0, w)
+    _ia.check(_ia.lib().ia_diag_color16_stats(st), 'stats')
+    for level in range(1, L):
+        s, im = out[level]
+        assert np.array_equal(s.cpu().numpy(), ref[level][0]), level
+        assert np.array_equal(im.cpu().numpy(), ref[level][1]), level
+        assert np.array_equal(Bp_dev[level].cpu().numpy(), Bp_ref[level]), level
+    queries = sum(B_pyr[l].shape[0] * B_pyr[l].shape[1] for l in range(1, L))
+    print('candidate tiles per query %.3f, full scans %d' % (st[0] / queries, st[1]))
+    assert st[1] == 0 and st[0] < 8 * queries
 
 
 def test_main_convert_false_colour_vs_oracle(gpu, tmp_path):
