@@ -618,10 +618,10 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
     lds_sync();   // every expander's copies of stages 0 and 1 landed
     rp_expand<X>(ring, w0.y, 0, E, lane);
     WinSrc wn = nstage > 1 ? win_src(im, stage_lrow(sm, chunk, 1)) : w0;   // the next to expand
-    lds_sync();   // barrier 0: operand 0 complete
     for (int s = 0; s < nstage; ++s) {
-        // after barrier s: stage s + 1's rows landed; buffer (s + 1) % 3 is free (operand
-        // s - 2, read by the MFMA waves before they met barrier s)
+        // barrier s: operand s complete, stage s + 1's rows landed, operand (s + 1) & 1 free
+        pc_stamp(tr, s, 0);
+        lds_sync();
         pc_stamp(tr, s, 1);
         const bool more = s + PC_AHEAD < nstage;
         if (more) {
@@ -630,7 +630,7 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
             wl = w3;
         }
         if (s + 1 < nstage) {
-            rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) % 3) * STAGE_H8, lane);
+            rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
             if (s + 2 < nstage) wn = win_src(im, stage_lrow(sm, chunk, s + 2));
         }
         pc_stamp(tr, s, 2);
@@ -638,7 +638,6 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
         if (PC_AHEAD == 3 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_n(X)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         pc_stamp(tr, s, 3);
-        lds_sync();   // barrier s + 1: operand s + 1 complete
     }
     lds_sync();
 }
@@ -648,7 +647,7 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
                                                       StageMap sm, const half8 *__restrict__ q16,
                                                       int M, int groups, float *__restrict__ segmin,
                                                       long nseg, const XJob *jobs, int parity) {
-    __shared__ half8 E[3 * STAGE_H8];
+    __shared__ half8 E[2 * STAGE_H8];
     if (jobs) {   // batch: this job's image-form sections, query rows and minima
         const XJob &J = jobs[blockIdx.y];
         im.fa = J.fa; im.ca = J.ca; im.norm = J.norm; im.ap = J.ap;
