@@ -486,7 +486,16 @@ constexpr bool PC_PIN = IA_PC_PIN;   // k_screen16p pins its MFMA stage's schedu
 #ifndef IA_PC_AHEAD
 #define IA_PC_AHEAD 3
 #endif
-constexpr int PC_AHEAD = IA_PC_AHEAD;   // stages ahead the expanders request window rows (2, 3)
+constexpr int PC_AHEAD = IA_PC_AHEAD;
+// A/B build knobs (diagnostic builds only; the product uses the defaults): IA_PC_PRIO raises
+// the MFMA waves' issue priority (s_setprio); IA_PC_NOEXP=1 makes the expanders skip the
+// operand expansion (wrong minima: the MFMA waves' time without that contention)
+#ifndef IA_PC_PRIO
+#define IA_PC_PRIO 0
+#endif
+#ifndef IA_PC_NOEXP
+#define IA_PC_NOEXP 0
+#endif   // stages ahead the expanders request window rows (2, 3)
 static_assert(PC_AHEAD == 2 || PC_AHEAD == 3, "ring depth");
 constexpr int RP_FA = 0, RP_FP = RP_FA + 8 * FROW_B, RP_CA = RP_FP + 8 * FROW_B;
 constexpr int RP_CP = RP_CA + 8 * CROW_B, RP_NM = RP_CP + 8 * CROW_B, RP_B = RP_NM + 4 * 512;
@@ -630,7 +639,7 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
             wl = w3;
         }
         if (s + 1 < nstage) {
-            rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
+            if (!IA_PC_NOEXP) rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
             if (s + 2 < nstage) wn = win_src(im, stage_lrow(sm, chunk, s + 2));
         }
         pc_stamp(tr, s, 2);
@@ -671,6 +680,7 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     // stage stamps (TRACE instantiation only): per wave 256 u64 in LDS, copied out below
     __shared__ unsigned long long trs[TRACE ? 8 * 256 : 1];
     unsigned long long *tr = TRACE && (b == 0 || b == 300) ? trs + wv * 256 : nullptr;
+    if (IA_PC_PRIO && wv < 4) __builtin_amdgcn_s_setprio(IA_PC_PRIO);
     if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg, tr);
     else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg, tr);
     else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg, tr);
