@@ -64,6 +64,20 @@ __device__ __forceinline__ int fkey(float x) {
 }
 __device__ __forceinline__ float fkey_inv(int b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
 
+// a screen block's chunk minima: per query of its group the minimum over the chunk's spc
+// segment minima (LDS keys) -> cmin[q][nchunks] (the fused per-wave path's e* and candidate
+// chunks, ia_internal.h db_nmins)
+template <int G>
+__device__ __forceinline__ void chunk_mins(const int *smin, int spc, int q0, int M, float *cmin,
+                                           int nchunks, int chunk, int nthr) {
+    for (int ql = threadIdx.x; ql < G * 32; ql += nthr) {
+        if (q0 + ql >= M) continue;
+        int m = smin[ql];
+        for (int sg = 1; sg < spc; ++sg) m = min(m, smin[sg * (G * 32) + ql]);
+        cmin[(long)(q0 + ql) * nchunks + chunk] = fkey_inv(m);
+    }
+}
+
 // wave W's MFMA chains of one 4-tile stage (operand sb in LDS) into its running minima
 template <int G, int W, int NS>
 __device__ __forceinline__ void stage_mfma(const half8 *sb, const half8 (&bq)[NS][Q16_GROUPS],
@@ -682,9 +696,7 @@ __device__ __forceinline__ void stage_pc(const half8 *sb, const half8 *sbn, half
         constexpr int k = ch_k<G, W>(c), ab = (ch_uo<G, W>(c) + P0) & 1, cb = c & 1;
         constexpr bool fol = ch_u<G, W>(c) == LASTU && (c == 0 || ch_u<G, W>(c - 1) != LASTU);
         if constexpr (fol) {
-            pc_stamp(tr, s, 0);
             lds_sync();   // the stage's operand reads done; operand s + 1 complete
-            pc_stamp(tr, s, 1);
             // the next stage's first tile (the last stage re-reads its own: no branch)
             const half8 *p = sbn + ch_u<G, W>(0) * TILE_H8 + lane;
 #pragma unroll
@@ -744,11 +756,17 @@ __device__ __forceinline__ void pc_mfma_eb(half8 *E, int *smin, int nstage, int 
         const half8 *e0 = E + (s & 1) * STAGE_H8, *e1 = E + ((s + 1) & 1) * STAGE_H8;
         stage_pc<G, W, NS, 0, PIN>(e0, s + 1 < nstage ? e1 : e0, a, bq, mn, lane, tr, s);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
+        // (stamps only between stages: one inside the pinned stage pushed G = 11 into spills;
+        // the MFMA waves' barrier wait is not measured in this layout)
+        pc_stamp(tr, s, 0);
+        pc_stamp(tr, s, 1);
         pc_stamp(tr, s, 3);
         if constexpr (ALT) {
             if (s + 1 < nstage) {
                 stage_pc<G, W, NS, 1, PIN>(e1, s + 2 < nstage ? e0 : e1, a, bq, mn, lane, tr, s + 1);
                 stage_close<G, W, NS>(s + 1, tps, smin, mn, lane);
+                pc_stamp(tr, s + 1, 0);
+                pc_stamp(tr, s + 1, 1);
                 pc_stamp(tr, s + 1, 3);
             }
         }
@@ -810,7 +828,8 @@ template <int G, bool TRACE = false>
 __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int ch, int seg_rows,
                                                       StageMap sm, const half8 *__restrict__ q16,
                                                       int M, int groups, float *__restrict__ segmin,
-                                                      long nseg, const XJob *jobs, int parity) {
+                                                      long nseg, const XJob *jobs, int parity,
+                                                      int cmin) {
     __shared__ half8 E[2 * STAGE_H8];
     if (jobs) {   // batch: this job's image-form sections, query rows and minima
         const XJob &J = jobs[blockIdx.y];
@@ -863,7 +882,7 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     for (int i = threadIdx.x; i < G * 32 * spc; i += 512) {
         const int ql = i / spc, sg = i - ql * spc;
         if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
-    }
+    }    if (cmin) chunk_mins<G>(smin, spc, q0, M, segmin + (long)M * nseg, nchunks, chunk, 512);
 }
 
 // grid: (nchunks rounded up to 8) x groups, XCD-aware: all groups of a chunk share
@@ -874,7 +893,8 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
                                                      int ch, int seg_rows, StageMap sm,
                                                      const half8 *__restrict__ q16, int M,
                                                      int groups, float *__restrict__ segmin,
-                                                     long nseg, const XJob *jobs, int parity) {
+                                                     long nseg, const XJob *jobs, int parity,
+                                                      int cmin) {
     __shared__ half8 sbuf[2 * STAGE_H8];
     if (jobs) {   // batch: this job's DB, query rows and minima
         const XJob &J = jobs[blockIdx.y];
@@ -905,7 +925,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
         const int ql = i / spc, s = i - ql * spc;
         if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + s] = fkey_inv(smin[s * (G * 32) + ql]);
-    }
+    }    if (cmin) chunk_mins<G>(smin, spc, q0, M, segmin + (long)M * nseg, nchunks, chunk, 256);
 }
 
 template <int G, int SCHED>
@@ -913,7 +933,8 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
                                                       StageMap sm,
                                                       const half8 *__restrict__ q16, int M,
                                                       int groups, float *__restrict__ segmin,
-                                                      long nseg, const XJob *jobs, int parity) {
+                                                      long nseg, const XJob *jobs, int parity,
+                                                      int cmin) {
     __shared__ half8 E[STAGE_H8];
     if (jobs) {   // batch: this job's image-form sections, query rows and minima
         const XJob &J = jobs[blockIdx.y];
@@ -953,7 +974,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
     for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
         const int ql = i / spc, sg = i - ql * spc;
         if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
-    }
+    }    if (cmin) chunk_mins<G>(smin, spc, q0, M, segmin + (long)M * nseg, nchunks, chunk, 256);
 }
 
 // query tiles per launch group: T tiles in ceil(T / 11) equal groups
@@ -984,7 +1005,7 @@ static int screen_pc() {
 
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st, const XJob *jobs,
-                    int njobs, int parity, bool sharded) {
+                    int njobs, int parity, bool sharded, bool cmin) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -1008,18 +1029,18 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
 #define IA_SCREEN16_SCHED(GG, SS)                                                               \
     if (img)                                                                                    \
         k_screen16i<GG, SS><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
-                                                  groups, segmin, nseg, jobs, parity);          \
+                                                  groups, segmin, nseg, jobs, parity, cmin);          \
     else                                                                                        \
         k_screen16<GG, SS><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,   \
-                                                 groups, segmin, nseg, jobs, parity);
+                                                 groups, segmin, nseg, jobs, parity, cmin);
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
         if (pc && (GG == 11 || GG == 4) && g_pc_trace_on.load())                                \
             k_screen16p<GG, (GG == 11 || GG == 4)><<<grid, 512, 0, st>>>(                       \
-                *img, (int)nchunks, ch, seg_rows, sm, q, M, groups, segmin, nseg, jobs, parity);\
+                *img, (int)nchunks, ch, seg_rows, sm, q, M, groups, segmin, nseg, jobs, parity, cmin);\
         else if (pc)                                                                            \
             k_screen16p<GG><<<grid, 512, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
-                                                  groups, segmin, nseg, jobs, parity);          \
+                                                  groups, segmin, nseg, jobs, parity, cmin);          \
         else if (sched) { IA_SCREEN16_SCHED(GG, 1) } else { IA_SCREEN16_SCHED(GG, 0) }          \
         break;
     switch (G) {
