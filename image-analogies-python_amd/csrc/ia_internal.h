@@ -35,10 +35,6 @@ static inline int db_seg_rows(long nrows) {
     return ch < DB_SEG_MAX ? ch : DB_SEG_MAX;
 }
 static inline long db_nsegs(long nrows) { return db_rows_padded(nrows) / db_seg_rows(nrows); }
-// the screen's minima of a wave of M queries (match_segmin): [M][nseg] segment minima, then
-// (when the launch asks for them, the fused per-wave path) [M][nchunks] chunk minima, the
-// minimum of each chunk's segments (k_xstrip finds e* and the candidate chunks from these)
-static inline long db_nmins(long nrows) { return db_nsegs(nrows) + db_nchunks(nrows); }
 
 // ---- the matcher's order of a DB's rows: chunks, stages, segments -------
 // A screen workgroup owns a chunk of ch rows and walks it in 128-row stages; a segment (one
@@ -236,10 +232,10 @@ struct XArgs {
     DbSrc src;
     ImgDb im;                     // image-form DB (IMG) ...
     gptr<const void> db;          // ... or the split-f16 rows (half8)
-    long row0, nrows, nseg, nchunk;
+    long row0, nrows, nseg;
     int seg_rows;
     StageMap smap;                // segment -> rows
-    gptr<const float> segmin;     // [M][nseg] + [M][nchunk] (chunk minima), this wave's screen
+    gptr<const float> segmin;     // [M][nseg], this wave's screen
     gptr<const double> q64;       // this wave's query rows (M)
     gptr<const float> qp;
     gptr<const double> nq;
@@ -306,8 +302,7 @@ int launch_query_rows(const double *qin, int M, const double *center, float *qp,
 // as another rank needs: measured, 2 ranks sharing one GPU timed out on c4)
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st,
-                    const XJob *jobs = nullptr, int njobs = 1, int parity = 0, bool sharded = false,
-                    bool cmin = false);
+                    const XJob *jobs = nullptr, int njobs = 1, int parity = 0, bool sharded = false);
 // the whole exact matcher (screen + exact stage); scratch of match_scratch_bytes(M, nrows).
 // stats (nullable): rows rescored, candidate segments, full scans.
 size_t match_scratch_bytes(int qrows, long nrows);

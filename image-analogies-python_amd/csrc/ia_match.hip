@@ -440,15 +440,14 @@ static SegWs seg_ws(void *scratch, int M, long nrows) {
     SegWs w;
     w.ctr = reinterpret_cast<int *>(p);
     w.segmin = reinterpret_cast<float *>(p + WL_HEAD);
-    w.items = reinterpret_cast<WItem *>(p + WL_HEAD + align_up((size_t)M * db_nmins(nrows) * sizeof(float), 256));
+    w.items = reinterpret_cast<WItem *>(p + WL_HEAD + align_up(n * sizeof(float), 256));
     w.ibest = reinterpret_cast<Best *>(reinterpret_cast<char *>(w.items) + align_up(n * sizeof(WItem), 256));
     w.sel = reinterpret_cast<QSel *>(reinterpret_cast<char *>(w.ibest) + align_up(n * sizeof(Best), 256));
     return w;
 }
 size_t match_scratch_bytes(int qrows, long nrows) {
     const size_t n = (size_t)qrows * db_nsegs(nrows);
-    return WL_HEAD + align_up((size_t)qrows * db_nmins(nrows) * sizeof(float), 256) +
-           align_up(n * sizeof(WItem), 256) +
+    return WL_HEAD + align_up(n * sizeof(float), 256) + align_up(n * sizeof(WItem), 256) +
            align_up(n * sizeof(Best), 256) + align_up((size_t)qrows * sizeof(QSel), 256);
 }
 

@@ -64,20 +64,6 @@ __device__ __forceinline__ int fkey(float x) {
 }
 __device__ __forceinline__ float fkey_inv(int b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
 
-// a screen block's chunk minima: per query of its group the minimum over the chunk's spc
-// segment minima (LDS keys) -> cmin[q][nchunks] (the fused per-wave path's e* and candidate
-// chunks, ia_internal.h db_nmins)
-template <int G>
-__device__ __forceinline__ void chunk_mins(const int *smin, int spc, int q0, int M, float *cmin,
-                                           int nchunks, int chunk, int nthr) {
-    for (int ql = threadIdx.x; ql < G * 32; ql += nthr) {
-        if (q0 + ql >= M) continue;
-        int m = smin[ql];
-        for (int sg = 1; sg < spc; ++sg) m = min(m, smin[sg * (G * 32) + ql]);
-        cmin[(long)(q0 + ql) * nchunks + chunk] = fkey_inv(m);
-    }
-}
-
 // wave W's MFMA chains of one 4-tile stage (operand sb in LDS) into its running minima
 template <int G, int W, int NS>
 __device__ __forceinline__ void stage_mfma(const half8 *sb, const half8 (&bq)[NS][Q16_GROUPS],
@@ -494,15 +480,9 @@ __device__ __forceinline__ void strip_body(const ImgDb &im, half8 *E, char *ring
 // rings of 8 slots per image (rows in use: 5 + 2 in flight for A fine, 3 + 2 for the others)
 // and 4 norm slots.
 #ifndef IA_PC_PIN
-#define IA_PC_PIN -1
+#define IA_PC_PIN 0
 #endif
-// k_screen16p pins its MFMA stage's schedule (CM_PIN): -1 for G >= 8 (measured at M = 342:
-// 4508 vs 4772 cycles of MFMA-wave time per stage; slower at G = 4, an expander-bound shape)
-template <int G>
-__host__ __device__ constexpr bool pc_pin() { return IA_PC_PIN < 0 ? G >= 8 : IA_PC_PIN != 0; }
-#ifndef IA_PC_EARLY
-#define IA_PC_EARLY 1
-#endif
+constexpr bool PC_PIN = IA_PC_PIN;   // k_screen16p pins its MFMA stage's schedule (CM_PIN)
 #ifndef IA_PC_AHEAD
 #define IA_PC_AHEAD 3
 #endif
@@ -615,7 +595,7 @@ __device__ __forceinline__ void pc_mfma(half8 *E, int *smin, int nstage, int tps
         pc_stamp(tr, s, 0);
         lds_sync();   // barrier s: operand s is complete (and operand s - 1 free for s + 1)
         pc_stamp(tr, s, 1);
-        stage_mfma_cm<G, W, NS, pc_pin<G>()>(E + (s & 1) * STAGE_H8, bq, mn, lane);
+        stage_mfma_cm<G, W, NS, PC_PIN>(E + (s & 1) * STAGE_H8, bq, mn, lane);
         stage_close<G, W, NS>(s, tps, smin, mn, lane);
         pc_stamp(tr, s, 3);   // (no stamp between: the last fold's accumulator is live there)
     }
@@ -671,165 +651,11 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
     lds_sync();
 }
 
-// ---- early stage barrier (IA_PC_EARLY=1) ----------------------------------------------
-// The hand-over barrier of stage s sits inside stage s, right after the MFMA waves' reads of
-// its LAST tile's operand completed (they then hold the rest of the stage in registers):
-// there operand s + 1 must be complete, and the first tile of stage s + 1 is read during
-// the last tile's chains, so no stage starts on an LDS round trip.  The expanders expand
-// operand s + 1 before that barrier and operand s + 2 after it into the buffer operand s
-// just vacated: still two buffers.  The operand register sets persist across stages; P0 is
-// the set holding this stage's first tile (it alternates when a wave's stage has an odd
-// number of tiles).
-template <int G, int W>
-__host__ __device__ constexpr int pc_ntiles() { return ch_uo<G, W>(ch_count<G, W>() - 1) + 1; }
-
-template <int G, int W, int NS, int P0, bool PIN>
-__device__ __forceinline__ void stage_pc(const half8 *sb, const half8 *sbn, half8 (&a)[2][DB16_GROUPS],
-                                         const half8 (&bq)[NS][Q16_GROUPS], float (&mn)[NS], int lane,
-                                         unsigned long long *tr, int s) {
-    constexpr int NC = ch_count<G, W>();
-    constexpr int LASTU = ch_u<G, W>(NC - 1);
-    const floatx16 zero = {};
-    floatx16 acc[2];
-    static_for<0, NC>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        constexpr int k = ch_k<G, W>(c), ab = (ch_uo<G, W>(c) + P0) & 1, cb = c & 1;
-        constexpr bool fol = ch_u<G, W>(c) == LASTU && (c == 0 || ch_u<G, W>(c - 1) != LASTU);
-        if constexpr (fol) {
-            lds_sync();   // the stage's operand reads done; operand s + 1 complete
-            // the next stage's first tile (the last stage re-reads its own: no branch)
-            const half8 *p = sbn + ch_u<G, W>(0) * TILE_H8 + lane;
-#pragma unroll
-            for (int g = 0; g < DB16_GROUPS; ++g) a[ab ^ 1][g] = p[g * 64];
-        }
-        if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c)) {
-            const half8 *p = sb + ch_u<G, W>(c + 1) * TILE_H8 + lane;
-#pragma unroll
-            for (int g = 0; g < DB16_GROUPS; ++g) a[ab ^ 1][g] = p[g * 64];
-        }
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
-        if constexpr (c > 0) fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
-#pragma unroll
-        for (int m = 1; m < MFMA16; ++m)
-            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][mfma_a(m)], bq[k][mfma_b(m)], acc[cb],
-                                                             0, 0, 0);
-        if constexpr (PIN) {
-            if constexpr (fol || (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c)))
-                __builtin_amdgcn_sched_group_barrier(0x100, DB16_GROUPS, 0);   // DS reads
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            if constexpr (c > 0) {
-                static_for<0, 4>([&](auto) {
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                });
-                __builtin_amdgcn_sched_group_barrier(0x008, MFMA16 - 5, 0);
-            } else {
-                __builtin_amdgcn_sched_group_barrier(0x008, MFMA16 - 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    });
-    fold_min(acc[(NC - 1) & 1], mn[ch_k<G, W>(NC - 1)]);
-}
-
-template <int G, int W>
-__device__ __forceinline__ void pc_mfma_eb(half8 *E, int *smin, int nstage, int tps,
-                                           const half8 *__restrict__ q16, unsigned long long *tr) {
-    constexpr int NS = bal_ns(G, W);
-    constexpr bool PIN = pc_pin<G>();
-    constexpr bool ALT = pc_ntiles<G, W>() & 1;
-    const int lane = threadIdx.x & 63;
-    half8 bq[NS][Q16_GROUPS];
-    load_queries<G, W, NS>(q16, bq, lane);
-    float mn[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
-    lds_sync();       // the expanders' first windows landed (their first barrier)
-    lds_sync();       // operand 0 complete
-    half8 a[2][DB16_GROUPS];
-    {
-        const half8 *p = E + ch_u<G, W>(0) * TILE_H8 + lane;
-#pragma unroll
-        for (int g = 0; g < DB16_GROUPS; ++g) a[0][g] = p[g * 64];
-    }
-    for (int s = 0; s < nstage; s += ALT ? 2 : 1) {
-        const half8 *e0 = E + (s & 1) * STAGE_H8, *e1 = E + ((s + 1) & 1) * STAGE_H8;
-        stage_pc<G, W, NS, 0, PIN>(e0, s + 1 < nstage ? e1 : e0, a, bq, mn, lane, tr, s);
-        stage_close<G, W, NS>(s, tps, smin, mn, lane);
-        // (stamps only between stages: one inside the pinned stage pushed G = 11 into spills;
-        // the MFMA waves' barrier wait is not measured in this layout)
-        pc_stamp(tr, s, 0);
-        pc_stamp(tr, s, 1);
-        pc_stamp(tr, s, 3);
-        if constexpr (ALT) {
-            if (s + 1 < nstage) {
-                stage_pc<G, W, NS, 1, PIN>(e1, s + 2 < nstage ? e0 : e1, a, bq, mn, lane, tr, s + 1);
-                stage_close<G, W, NS>(s + 1, tps, smin, mn, lane);
-                pc_stamp(tr, s + 1, 0);
-                pc_stamp(tr, s + 1, 1);
-                pc_stamp(tr, s + 1, 3);
-            }
-        }
-    }
-    lds_sync();       // pairs with the expanders' last
-}
-
-template <int X>
-__device__ __forceinline__ void pc_expand_eb(const ImgDb &im, half8 *E, char *ring, const StageMap &sm,
-                                             long chunk, int nstage, unsigned long long *tr) {
-    const int lane = threadIdx.x & 63;
-    // stage 0's whole window, stages 1 and 2's new rows; wait for stages 0 and 1; operand 0
-    const WinSrc w0 = win_src(im, stage_lrow(sm, chunk, 0));
-    for (int j = X; j < 15; j += 4) {
-        const int kind = j < 5 ? 0 : j < 8 ? 1 : j < 11 ? 2 : j < 14 ? 3 : 4;
-        const int r = j < 5 ? w0.y + j : j < 8 ? w0.y + j - 5 : j < 11 ? (w0.y >> 1) + 1 + j - 8
-                                                                      : (w0.y >> 1) + 1 + j - 11;
-        rp_load(im, w0, ring, kind, r, 0, lane);
-    }
-    WinSrc wl = w0;                      // the last stage whose rows were requested
-    int req = 0;
-    for (int k = 1; k < PC_AHEAD && k < nstage; ++k) {
-        const WinSrc wk = win_src(im, stage_lrow(sm, chunk, k));
-        rp_rows<X>(im, wl, wk, ring, k & 3, lane);
-        wl = wk;
-        req = k;
-    }
-    if (PC_AHEAD == 3 && req == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_n(X)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_sync();   // every expander's copies of stages 0 and 1 landed
-    if (!IA_PC_NOEXP) rp_expand<X>(ring, w0.y, 0, E, lane);
-    WinSrc wn = nstage > 1 ? win_src(im, stage_lrow(sm, chunk, 1)) : w0;   // the next to expand
-    lds_sync();   // operand 0 complete
-    for (int s = 0; s < nstage; ++s) {
-        // after the barrier of stage s - 1: operand s - 1's buffer is free for s + 1
-        const bool more = s + PC_AHEAD < nstage;
-        if (more) {
-            const WinSrc w3 = win_src(im, stage_lrow(sm, chunk, s + PC_AHEAD));
-            rp_rows<X>(im, wl, w3, ring, (s + PC_AHEAD) & 3, lane);
-            wl = w3;
-        }
-        if (s + 1 < nstage) {
-            if (!IA_PC_NOEXP) rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
-            if (s + 2 < nstage) wn = win_src(im, stage_lrow(sm, chunk, s + 2));
-        }
-        pc_stamp(tr, s, 2);
-        // stage s + 2's rows (requested one iteration ago) land before this barrier
-        if (PC_AHEAD == 3 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_n(X)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        pc_stamp(tr, s, 3);
-        pc_stamp(tr, s, 0);
-        lds_sync();   // stage s's barrier: operand s + 1 complete
-        pc_stamp(tr, s, 1);
-    }
-    lds_sync();
-}
-
 template <int G, bool TRACE = false>
 __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int ch, int seg_rows,
                                                       StageMap sm, const half8 *__restrict__ q16,
                                                       int M, int groups, float *__restrict__ segmin,
-                                                      long nseg, const XJob *jobs, int parity,
-                                                      int cmin) {
+                                                      long nseg, const XJob *jobs, int parity) {
     __shared__ half8 E[2 * STAGE_H8];
     if (jobs) {   // batch: this job's image-form sections, query rows and minima
         const XJob &J = jobs[blockIdx.y];
@@ -855,25 +681,14 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     __shared__ unsigned long long trs[TRACE ? 8 * 256 : 1];
     unsigned long long *tr = TRACE && (b == 0 || b == 300) ? trs + wv * 256 : nullptr;
     if (IA_PC_PRIO && wv < 4) __builtin_amdgcn_s_setprio(IA_PC_PRIO);
-    if constexpr (IA_PC_EARLY) {
-        if (wv == 0) pc_mfma_eb<G, 0>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 1) pc_mfma_eb<G, 1>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 2) pc_mfma_eb<G, 2>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 3) pc_mfma_eb<G, 3>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 4) pc_expand_eb<0>(im, E, ring, sm, chunk, nstage, tr);
-        else if (wv == 5) pc_expand_eb<1>(im, E, ring, sm, chunk, nstage, tr);
-        else if (wv == 6) pc_expand_eb<2>(im, E, ring, sm, chunk, nstage, tr);
-        else pc_expand_eb<3>(im, E, ring, sm, chunk, nstage, tr);
-    } else {
-        if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 3) pc_mfma<G, 3>(E, smin, nstage, tps, qg, tr);
-        else if (wv == 4) pc_expand<0>(im, E, ring, sm, chunk, nstage, tr);
-        else if (wv == 5) pc_expand<1>(im, E, ring, sm, chunk, nstage, tr);
-        else if (wv == 6) pc_expand<2>(im, E, ring, sm, chunk, nstage, tr);
-        else pc_expand<3>(im, E, ring, sm, chunk, nstage, tr);
-    }
+    if (wv == 0) pc_mfma<G, 0>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 1) pc_mfma<G, 1>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 2) pc_mfma<G, 2>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 3) pc_mfma<G, 3>(E, smin, nstage, tps, qg, tr);
+    else if (wv == 4) pc_expand<0>(im, E, ring, sm, chunk, nstage, tr);
+    else if (wv == 5) pc_expand<1>(im, E, ring, sm, chunk, nstage, tr);
+    else if (wv == 6) pc_expand<2>(im, E, ring, sm, chunk, nstage, tr);
+    else pc_expand<3>(im, E, ring, sm, chunk, nstage, tr);
     __syncthreads();
     if (TRACE && (b == 0 || b == 300) && g_pc_trace)
         for (int i = threadIdx.x; i < 8 * 256; i += 512) g_pc_trace[(b == 0 ? 0 : 8 * 256) + i] = trs[i];
@@ -882,7 +697,7 @@ __global__ __launch_bounds__(512, 1) void k_screen16p(ImgDb im, int nchunks, int
     for (int i = threadIdx.x; i < G * 32 * spc; i += 512) {
         const int ql = i / spc, sg = i - ql * spc;
         if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
-    }    if (cmin) chunk_mins<G>(smin, spc, q0, M, segmin + (long)M * nseg, nchunks, chunk, 512);
+    }
 }
 
 // grid: (nchunks rounded up to 8) x groups, XCD-aware: all groups of a chunk share
@@ -893,8 +708,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
                                                      int ch, int seg_rows, StageMap sm,
                                                      const half8 *__restrict__ q16, int M,
                                                      int groups, float *__restrict__ segmin,
-                                                     long nseg, const XJob *jobs, int parity,
-                                                      int cmin) {
+                                                     long nseg, const XJob *jobs, int parity) {
     __shared__ half8 sbuf[2 * STAGE_H8];
     if (jobs) {   // batch: this job's DB, query rows and minima
         const XJob &J = jobs[blockIdx.y];
@@ -925,7 +739,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16(const half8 *__restrict__ d
     for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
         const int ql = i / spc, s = i - ql * spc;
         if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + s] = fkey_inv(smin[s * (G * 32) + ql]);
-    }    if (cmin) chunk_mins<G>(smin, spc, q0, M, segmin + (long)M * nseg, nchunks, chunk, 256);
+    }
 }
 
 template <int G, int SCHED>
@@ -933,8 +747,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
                                                       StageMap sm,
                                                       const half8 *__restrict__ q16, int M,
                                                       int groups, float *__restrict__ segmin,
-                                                      long nseg, const XJob *jobs, int parity,
-                                                      int cmin) {
+                                                      long nseg, const XJob *jobs, int parity) {
     __shared__ half8 E[STAGE_H8];
     if (jobs) {   // batch: this job's image-form sections, query rows and minima
         const XJob &J = jobs[blockIdx.y];
@@ -974,7 +787,7 @@ __global__ __launch_bounds__(256, 2) void k_screen16i(ImgDb im, int nchunks, int
     for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
         const int ql = i / spc, sg = i - ql * spc;
         if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + sg] = fkey_inv(smin[sg * (G * 32) + ql]);
-    }    if (cmin) chunk_mins<G>(smin, spc, q0, M, segmin + (long)M * nseg, nchunks, chunk, 256);
+    }
 }
 
 // query tiles per launch group: T tiles in ceil(T / 11) equal groups
@@ -1005,7 +818,7 @@ static int screen_pc() {
 
 int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap &sm,
                     const _Float16 *q16, int M, float *segmin, hipStream_t st, const XJob *jobs,
-                    int njobs, int parity, bool sharded, bool cmin) {
+                    int njobs, int parity, bool sharded) {
     const int ch = db_chunk_rows(nrows);
     const long nchunks = db_nchunks(nrows);
     const int seg_rows = db_seg_rows(nrows);
@@ -1029,18 +842,18 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
 #define IA_SCREEN16_SCHED(GG, SS)                                                               \
     if (img)                                                                                    \
         k_screen16i<GG, SS><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
-                                                  groups, segmin, nseg, jobs, parity, cmin);          \
+                                                  groups, segmin, nseg, jobs, parity);          \
     else                                                                                        \
         k_screen16<GG, SS><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,   \
-                                                 groups, segmin, nseg, jobs, parity, cmin);
+                                                 groups, segmin, nseg, jobs, parity);
 #define IA_SCREEN16_CASE(GG)                                                                    \
     case GG:                                                                                    \
         if (pc && (GG == 11 || GG == 4) && g_pc_trace_on.load())                                \
             k_screen16p<GG, (GG == 11 || GG == 4)><<<grid, 512, 0, st>>>(                       \
-                *img, (int)nchunks, ch, seg_rows, sm, q, M, groups, segmin, nseg, jobs, parity, cmin);\
+                *img, (int)nchunks, ch, seg_rows, sm, q, M, groups, segmin, nseg, jobs, parity);\
         else if (pc)                                                                            \
             k_screen16p<GG><<<grid, 512, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
-                                                  groups, segmin, nseg, jobs, parity, cmin);          \
+                                                  groups, segmin, nseg, jobs, parity);          \
         else if (sched) { IA_SCREEN16_SCHED(GG, 1) } else { IA_SCREEN16_SCHED(GG, 0) }          \
         break;
     switch (G) {

@@ -595,7 +595,7 @@ struct LevelRun {
         if (e0) IA_HIP(hipEventRecord(e0, sq));
         const StageMap sm = db_stage_map(a->row0, a->nrows, src.A.w, src.A.h);
         if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b,
-                                  a->comm != nullptr, true)))
+                                  a->comm != nullptr)))
             return rc;
         if (e1) IA_HIP(hipEventRecord(e1, sq));
         int y_lo_n = 0, M_n = 0;
@@ -607,7 +607,6 @@ struct LevelRun {
         x.row0 = a->row0;
         x.nrows = a->nrows;
         x.nseg = db_nsegs(a->nrows);
-        x.nchunk = db_nchunks(a->nrows);
         x.seg_rows = db_seg_rows(a->nrows);
         x.smap = sm;
         x.segmin = segmin;

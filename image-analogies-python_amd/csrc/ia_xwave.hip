@@ -822,62 +822,64 @@ __device__ __forceinline__ double pw55_lanes(double v) {
 }
 
 // ---- k_xstrip's segment-minima phase on waves 0, 2, 3 only (192 threads; wave 1 picks the
-// coherence candidate meanwhile and never waits for this phase).
-// From the chunk minima (the screen's [M][nchunk] section): e* over the
-// query's chunk minima (c4: 512 per query, 2 KB, instead of 8192 segment minima, 32 KB: the
-// wave's M queries read 0.7 MB instead of 11 MB), the chunks within the threshold, then only
-// their segment minima.  Same e* (the minimum of the chunk minima is the minimum of the
-// segment minima) and the same candidate set (a segment at or under the threshold lies in a
-// chunk whose minimum is).
-constexpr int XC_REG = 1;       // float4s of chunk minima per thread in registers (512 chunks)
-constexpr int XC_CAP = 64;      // candidate chunks listed in LDS (more: scan every segment)
-__device__ __forceinline__ void cmin3_load(const float4 *cq4, long n4, int t3, float4 (&v)[XC_REG]) {
+// coherence candidate meanwhile and never waits for this phase): thread t3 holds the float4s
+// t3 + 192 j of the query's minima in registers (XS_REG of them: c4's 8192 segments on one
+// GPU), the rest are streamed.  Same e* and candidate set as segmin_* over 256 threads.
+constexpr int XS_REG = 11;
+__device__ __forceinline__ void seg3_load(const float4 *sq4, long n4, int t3, float4 (&v)[XS_REG]) {
 #pragma unroll
-    for (int j = 0; j < XC_REG; ++j) {
+    for (int j = 0; j < XS_REG; ++j) {
         const long i = t3 + (long)j * 192;
-        const float4 x = cq4[i < n4 ? i : 0];
+        const float4 x = sq4[i < n4 ? i : 0];   // unconditional (a valid index past the end)
         v[j] = i < n4 ? x : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
     }
 }
-__device__ __forceinline__ float cmin3_wave_min(const float4 *cq4, long n4, int t3, const float4 (&v)[XC_REG]) {
+__device__ __forceinline__ float seg3_wave_min(const float4 *sq4, long n4, int t3, const float4 (&v)[XS_REG]) {
     float emin = FLT_MAX;
 #pragma unroll
-    for (int j = 0; j < XC_REG; ++j) emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
-    for (long i = t3 + (long)XC_REG * 192; i < n4; i += 192) {
-        const float4 x = cq4[i];
+    for (int j = 0; j < XS_REG; ++j) emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
+    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+        const float4 x = sq4[i];
         emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
     }
     for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
     return emin;
 }
-__device__ __forceinline__ void cmin3_chunks(const float4 *cq4, long n4, int t3, const float4 (&v)[XC_REG],
-                                             double Tseg, int *clist, int *ccount) {
-    auto push = [&](float4 x, long i) {
-        const unsigned mt = ((double)x.x <= Tseg ? 1u : 0u) | ((double)x.y <= Tseg ? 2u : 0u) |
-                            ((double)x.z <= Tseg ? 4u : 0u) | ((double)x.w <= Tseg ? 8u : 0u);
-        if (mt) {
-            int pos = atomicAdd(ccount, __builtin_popcount(mt));
-            for (unsigned m = mt; m; m &= m - 1, ++pos)
-                if (pos < XC_CAP) clist[pos] = (int)(4 * i + __builtin_ctz(m));
-        }
-    };
+__device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, const float4 (&v)[XS_REG],
+                                            double Tseg, int *slist, int *scount) {
+    static_assert(XS_REG * 4 <= 64, "one 64-bit mask");
+    unsigned long long m = 0;
 #pragma unroll
-    for (int j = 0; j < XC_REG; ++j) push(v[j], t3 + (long)j * 192);
-    for (long i = t3 + (long)XC_REG * 192; i < n4; i += 192) push(cq4[i], i);
-}
-// the candidate chunks' segment minima (spc per chunk, one round trip) -> slist
-__device__ __forceinline__ void cmin3_segs(const float *sq, int spc, int t3, const int *clist, int nc,
-                                           double Tseg, int *slist, int *scount) {
-    for (int e = t3; e < nc * spc; e += 192) {
-        const int c = e / spc;
-        const int sg = clist[c] * spc + (e - c * spc);
-        if ((double)sq[sg] <= Tseg) {
-            const int pos = atomicAdd(scount, 1);
-            if (pos < RESCORE_SEGCAP) slist[pos] = sg;
+    for (int j = 0; j < XS_REG; ++j) {
+        m |= (unsigned long long)((double)v[j].x <= Tseg) << (4 * j);
+        m |= (unsigned long long)((double)v[j].y <= Tseg) << (4 * j + 1);
+        m |= (unsigned long long)((double)v[j].z <= Tseg) << (4 * j + 2);
+        m |= (unsigned long long)((double)v[j].w <= Tseg) << (4 * j + 3);
+    }
+    if (m) {
+        int pos = atomicAdd(scount, __builtin_popcountll(m));
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            if (pos < RESCORE_SEGCAP) slist[pos] = 4 * (t3 + (b >> 2) * 192) + (b & 3);
+            ++pos;
+        }
+    }
+    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+        const float4 x = sq4[i];
+        unsigned mt = ((double)x.x <= Tseg ? 1u : 0u) | ((double)x.y <= Tseg ? 2u : 0u) |
+                      ((double)x.z <= Tseg ? 4u : 0u) | ((double)x.w <= Tseg ? 8u : 0u);
+        if (mt) {
+            int pos = atomicAdd(scount, __builtin_popcount(mt));
+            while (mt) {
+                const int b = __builtin_ctz(mt);
+                mt &= mt - 1;
+                if (pos < RESCORE_SEGCAP) slist[pos] = (int)(4 * i + b);
+                ++pos;
+            }
         }
     }
 }
-
 // a barrier of waves 0, 2 and 3 only (an LDS counter; wave 1 never takes part): generation g
 // releases when all three have arrived for the g-th time
 __device__ __forceinline__ void sync3(unsigned *cnt, unsigned g, int lane) {
@@ -907,8 +909,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ double qs[IA_DP], wts[IA_DP];
     __shared__ double cwt[2 * IA_DP];   // the coherence lanes' factors: 1 (distance), weights
     __shared__ int slist[RESCORE_SEGCAP];
-    __shared__ int clist[XC_CAP];
-    __shared__ int tk, scount, sfull, ccount;
+    __shared__ int tk, scount, sfull;
     __shared__ unsigned bar3;
     __shared__ float redf[4];
     __shared__ double bds[4], bwd[4], bvl[4];
@@ -928,7 +929,6 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
         bar3 = 0;
         scount = 0;
-        ccount = 0;
     }
     __syncthreads();
     const int i = tk;
@@ -968,12 +968,10 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         const double wk = lane < IA_D ? wk0 : 0.0;
         const double nqq = a.nq[vidx(i)];
         const float am = amx;
-        // e* and the candidates from the chunk minima (cmin3_*)
-        const long nc4 = a.nchunk / 4;
-        const float *sq = a.segmin + (long)i * a.nseg;
-        const float4 *cq4 = reinterpret_cast<const float4 *>(a.segmin + (long)a.M * a.nseg + (long)i * a.nchunk);
-        float4 v[XC_REG];
-        if (wv != 1) cmin3_load(cq4, nc4, t3, v);
+        const long n4 = a.nseg / 4;
+        const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
+        float4 v[XS_REG];
+        if (wv != 1) seg3_load(sq4, n4, t3, v);
         const int rr0 = y - 2 + lane / 5, rc0 = x - 2 + lane % 5;
         const bool cpos_ok = wv == 1 && lane < XW_NCOH && rr0 >= 0 && rc0 >= 0 && rc0 < W &&
                              (rr0 < y || rc0 < x);
@@ -985,7 +983,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         // segment minima's wait: one more round trip on wave 1's path)
         asm volatile("" ::: "memory");
         if (wv != 1) {
-            const float ewv = cmin3_wave_min(cq4, nc4, t3, v);
+            const float ewv = seg3_wave_min(sq4, n4, t3, v);
             if (lane == 0) redf[wv] = ewv;
         }
         if (wv == 1) wstamp(14);
@@ -1061,15 +1059,11 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             double Tseg, Trow;
             bool force_full;
             rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
-            if (!force_full) cmin3_chunks(cq4, nc4, t3, v, Tseg, clist, &ccount);
+            seg3_select(sq4, n4, t3, v, Tseg, slist, &scount);
             sync3(&bar3, 2, lane);
-            const int nc = ccount;
-            if (!force_full && nc <= XC_CAP)
-                cmin3_segs(sq, (int)(a.nseg / a.nchunk), t3, clist, nc, Tseg, slist, &scount);
-            sync3(&bar3, 3, lane);
             xw_stamp(trace, 3);
             ns = scount;
-            full = ns > RESCORE_SEGCAP || nc > XC_CAP || force_full;
+            full = ns > RESCORE_SEGCAP || force_full;
             if (tid == 0) sfull = full ? 1 : 0;
         }
 

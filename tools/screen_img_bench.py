@@ -119,27 +119,18 @@ def main():
                 close = 0.0
                 period = np.median(np.diff(mf[:, 4:61, 1], axis=1))    # stage period
                 wait_x = np.median(ex[:, s_, 1] - ex[:, s_, 0])
-                # early-barrier layout (IA_PC_EARLY): the expanders' stamp 1 is the departure
-                # from stage s's barrier, after the copy wait; their work of stage s starts at
-                # the previous departure
-                eb = np.median(ex[:, s_, 1] - ex[:, s_, 3]) > 0
-                prev1 = ex[:, 3:59, 1] if eb else ex[:, s_, 1]
-                work_x = np.median(ex[:, s_, 2] - prev1)
+                work_x = np.median(ex[:, s_, 2] - ex[:, s_, 1])
                 vm_x = np.median(ex[:, s_, 3] - ex[:, s_, 2])
-                if eb:   # the MFMA waves' barrier sits inside the stage: busy = period - wait
-                    mfma = period - wait_m
                 print('M %3d block %d (cycles, median over stages 4-59): period %.0f | MFMA waves: '
                       'barrier wait %.0f, MFMAs %.0f, close %.0f | expanders: barrier wait %.0f, '
-                      'copies+operand %.0f, copy wait %.0f%s' % (M, 300 * blk, period, wait_m, mfma, close,
-                                                                wait_x, work_x, vm_x,
-                                                                ' (early barrier)' if eb else ''),
-                      flush=True)
+                      'copies+operand %.0f, copy wait %.0f' % (M, 300 * blk, period, wait_m, mfma, close,
+                                                              wait_x, work_x, vm_x), flush=True)
                 for w in range(4):
                     print('   MFMA wave %d: wait %.0f mfma+close %.0f | expander %d: wait %.0f work %.0f '
                           'copy wait %.0f' % (w, np.median(mf[w, s_, 1] - mf[w, s_, 0]),
                                               np.median(mf[w, s_, 3] - mf[w, s_, 1]), w,
                                               np.median(ex[w, s_, 1] - ex[w, s_, 0]),
-                                              np.median(ex[w, s_, 2] - prev1[w]),
+                                              np.median(ex[w, s_, 2] - ex[w, s_, 1]),
                                               np.median(ex[w, s_, 3] - ex[w, s_, 2])), flush=True)
         _ia.check(lib.ia_diag_screen_trace(None), 'trace off')
     lib.ia_diag_set_screen_sched(prev)
