@@ -361,50 +361,75 @@ __global__ void k_screen3_unscale(const float *__restrict__ smin, int M, int nti
     }
 }
 
-// the screen: block (x, query tile y) of 4 waves, each wave a run of tpw row tiles against
-// the query tile held in registers; per (query, row tile) the minimum of the 32 values
-__global__ __launch_bounds__(256) void k_screen3(const half8 *__restrict__ db16, int ntiles,
-                                                 const half8 *__restrict__ q16, int M, int tpw,
-                                                 float *__restrict__ smin) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int qt = blockIdx.y;
-    half8 qh[C16_CH], ql[C16_CH];
-    const half8 *qb = q16 + (long)qt * C16_TILE + lane;
+// the screen: block (x, query group y) of 4 waves.  The group's query tiles (up to S3_QG)
+// are staged in LDS once; each wave then walks row tiles t = (x tpw + i) 4 + wave, holding
+// the tile's 22 operand groups in registers (the next tile's loaded while this one's chains
+// run) against every staged query tile: 33 MFMAs per (row tile, query tile), and per query
+// the minimum over the tile's 32 rows.  Each DB tile is read once per query group (round 4's
+// first form read it once per query tile: 7 times per wave at the c3 size).
+constexpr int S3_QG = 4;                  // query tiles per group (LDS: 4 x 22.5 KB)
+__device__ __forceinline__ void s3_load(const half8 *db16, int t, int lane, half8 (&ah)[C16_CH],
+                                        half8 (&al)[C16_CH]) {
+    const half8 *db = db16 + (long)t * C16_TILE + lane;
 #pragma unroll
     for (int c = 0; c < C16_CH; ++c) {
-        qh[c] = qb[(2 * c) * 64];
-        ql[c] = qb[(2 * c + 1) * 64];
+        ah[c] = db[(2 * c) * 64];
+        al[c] = db[(2 * c + 1) * 64];
     }
-    const int q = qt * 32 + lane;
-    const bool wr = lane < 32 && q < M;
-    float *out = smin + (long)q * ntiles;
-    const int t0 = (blockIdx.x * 4 + wv) * tpw;
-    const int t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+}
+__global__ __launch_bounds__(256, 1) void k_screen3(const half8 *__restrict__ db16, int ntiles,
+                                                    const half8 *__restrict__ q16, int M, int tpw,
+                                                    float *__restrict__ smin) {
+    __shared__ half8 qsh[S3_QG * C16_TILE];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int qt0 = blockIdx.y * S3_QG;
+    const int QT = (M + 31) / 32;
+    const int nq = QT - qt0 < S3_QG ? QT - qt0 : S3_QG;
+    for (int i = threadIdx.x; i < nq * C16_TILE; i += 256) qsh[i] = q16[(long)qt0 * C16_TILE + i];
+    __syncthreads();
     const floatx16 zero = {};
-    for (int t = t0; t < t1; ++t) {
-        const half8 *db = db16 + (long)t * C16_TILE + lane;
-        half8 ah[C16_CH], al[C16_CH];
+    const int tb = blockIdx.x * tpw * 4 + wv;
+    int t = tb;
+    if (t >= ntiles) return;   // (after the only barrier)
+    half8 ah[C16_CH], al[C16_CH], nh[C16_CH], nl[C16_CH];
+    s3_load(db16, t, lane, ah, al);
+    for (int it = 0; it < tpw; ++it, t += 4) {
+        const int tn = t + 4;
+        const bool more = it + 1 < tpw && tn < ntiles;
+        if (more) s3_load(db16, tn, lane, nh, nl);
+        for (int j = 0; j < nq; ++j) {
+            const half8 *qb = qsh + j * C16_TILE + lane;
+            floatx16 acc = zero;
+#pragma unroll
+            for (int c = 0; c < C16_CH; ++c) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], qb[(2 * c + 1) * 64], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], qb[(2 * c) * 64], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < C16_CH; ++c)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], qb[(2 * c) * 64], acc, 0, 0, 0);
+            float mn = acc[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) mn = fminf(mn, acc[i]);
+            mn = fminf(mn, __shfl_xor(mn, 32));
+            const int q = (qt0 + j) * 32 + lane;
+            if (lane < 32 && q < M) smin[(long)q * ntiles + t] = mn;
+        }
+        if (!more) break;
 #pragma unroll
         for (int c = 0; c < C16_CH; ++c) {
-            ah[c] = db[(2 * c) * 64];
-            al[c] = db[(2 * c + 1) * 64];
+            ah[c] = nh[c];
+            al[c] = nl[c];
         }
-        floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[0], ql[0], zero, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[0], qh[0], acc, 0, 0, 0);
-#pragma unroll
-        for (int c = 1; c < C16_CH; ++c) {
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], ql[c], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], qh[c], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int c = 0; c < C16_CH; ++c)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], qh[c], acc, 0, 0, 0);
-        float mn = acc[0];
-#pragma unroll
-        for (int i = 1; i < 16; ++i) mn = fminf(mn, acc[i]);
-        mn = fminf(mn, __shfl_xor(mn, 32));
-        if (wr) out[t] = mn;
     }
+}
+
+// grid of k_screen3: row tiles per wave so that about 512 workgroups cover the
+// (row tile, query group) pairs
+static inline dim3 screen3_grid(int ntiles, int M, int &tpw) {
+    const int QG = ((M + 31) / 32 + S3_QG - 1) / S3_QG;
+    tpw = (int)std::max(1L, ((long)ntiles * QG + 4L * 512 - 1) / (4L * 512));
+    return dim3((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QG);
 }
 
 // exhaustive fp64 search: a block takes 32 rows (staged in LDS) against every query, 8 at
@@ -968,9 +993,8 @@ int ia_synth_level3(const IaSynthArgs *a, void *stream) {
         f.y_lo = y_lo;
         if (split) {
             const int QT = (M + 31) / 32;
-            // row tiles per wave: about 2048 waves over the (row tile, query tile) pairs
-            const int tpw = std::max(1, (int)(((long)ntiles * QT + 2047) / 2048));
-            const dim3 grid((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QT);
+            int tpw;
+            const dim3 grid = screen3_grid(ntiles, M, tpw);
             k_query3s<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, w.q3, w.qn,
                                                reinterpret_cast<_Float16 *>(w.q16));
             k_screen3<<<grid, 256, 0, st>>>(v.db16, ntiles, w.q16, M, tpw, w.smin);
@@ -995,9 +1019,8 @@ int ia_diag_screen3(const void *db3, long nrows, const double *q165, int M, doub
     IA_HIP(hipMalloc(&q16, (size_t)QT * C16_TILE * sizeof(half8)));
     IA_HIP(hipMalloc(&smin, (size_t)M * ntiles * sizeof(float)));
     k_qsplit3<<<QT * 32, 256>>>(q165, M, v.meta, qn, reinterpret_cast<_Float16 *>(q16));
-    const int tpw = std::max(1, (int)(((long)ntiles * QT + 2047) / 2048));
-    k_screen3<<<dim3((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QT), 256>>>(
-        v.db16, ntiles, q16, M, tpw, smin);
+    int tpw;
+    k_screen3<<<screen3_grid(ntiles, M, tpw), 256>>>(v.db16, ntiles, q16, M, tpw, smin);
     const long n = (long)M * ntiles;
     k_screen3_unscale<<<(unsigned)((n + 255) / 256), 256>>>(smin, M, ntiles, qn, v.meta, e, eps);
     IA_LAUNCH_CHECK("ia_diag_screen3");
