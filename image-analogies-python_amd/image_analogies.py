@@ -200,7 +200,10 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     pipelined).  pipeline: run the levels concurrently (ia_synth_levels; default
     pipeline_default()), else one after the other.  check: synchronise at the end and raise
     if a wait inside the device schedule timed out (ia_synth_status: the results would be
-    wrong).  Returns {level: (s, im[, debug])} device tensors."""
+    wrong) -- a blocking call (one stream sync and one small copy per level, every level's
+    workspace kept alive until then); check=False returns as soon as the work is queued,
+    and the caller checks later (_ia.sched_status(), as bench.py does once per timed pass).
+    Returns {level: (s, im[, debug])} device tensors."""
     if B_pyr[-1].dim() == 3:     # 3-channel matching (num_ch = 3)
         if comm is not None or nranks > 1 or lsh is not None:
             raise NotImplementedError('3-channel matching runs on one GPU with the exact matcher')
