@@ -677,7 +677,11 @@ def main():
     # the finest level's screen streams the DB's image form when it applies (k_screen16i;
     # k_screen16p, the producer / consumer form, on strip-order levels: every c4 / c5 level)
     img_form = _ia.db_image_enabled() and jobs[0].A.shape[1] % 128 == 0 and lsh is None
-    kname = ('k_screen16p<%s>' if _ia.lib().ia_diag_set_screen_pc(-1) else 'k_screen16i<%s>') \
+    # (the producer / consumer form runs single-job, unsharded levels: a batch of jobs and a
+    # sharded finest level take the 4-wave k_screen16i)
+    pc_used = (_ia.lib().ia_diag_set_screen_pc(-1) and batch == 1 and
+               comm is None)
+    kname = ('k_screen16p<%s>' if pc_used else 'k_screen16i<%s>') \
         if img_form else 'k_screen16<%s>'
     roof = {'bound': 'mfma', 'kernel': kname % domG,
             'achieved': achieved,

@@ -838,7 +838,9 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || jobs), "launch_screen16: bad batch");
     const dim3 grid((unsigned)nb, (unsigned)njobs);
     const int sched = screen_sched();
-    const bool pc = img && sm.W > 0 && !sharded && screen_pc();
+    // (not for a batch of jobs: its one-per-CU workgroups ran c5 19% slower than the 4-wave
+    // screen, 7.59 vs 9.04 M px/s on one box, profiles/r04_ab_c5_screen_pc.txt)
+    const bool pc = img && sm.W > 0 && !sharded && njobs == 1 && screen_pc();
 #define IA_SCREEN16_SCHED(GG, SS)                                                               \
     if (img)                                                                                    \
         k_screen16i<GG, SS><<<grid, 256, 0, st>>>(*img, (int)nchunks, ch, seg_rows, sm, q, M,  \
