@@ -86,6 +86,7 @@ _SIGS = {
     'ia_db_rows_padded': (ctypes.c_long, [ctypes.c_long]),
     'ia_db_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_db_chunk_rows': (ctypes.c_int, [ctypes.c_long]),
+    'ia_set_chunk_target': (ctypes.c_long, [ctypes.c_long]),
     'ia_db_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
                                    _dp, _dp, _dp, _dp]),
     'ia_db_image_bytes': (ctypes.c_size_t, [ctypes.POINTER(IaSrcLevel), ctypes.c_long,

@@ -13,6 +13,8 @@
 
 namespace ia {
 
+std::atomic<long> g_db_chunk_target{DB_TARGET_CHUNKS};
+
 __global__ void k_level_features(ImgPair p, int full, double *out) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (long)p.h * p.w) return;
@@ -771,6 +773,12 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
 }
 
 int ia_db_chunk_rows(long nrows) { return db_chunk_rows(nrows); }
+
+long ia_set_chunk_target(long chunks) {
+    const long prev = g_db_chunk_target.load();
+    if (chunks >= 4 && chunks <= DB_TARGET_CHUNKS) g_db_chunk_target.store(chunks);
+    return prev;
+}
 long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
 size_t ia_db_bytes(long nrows) { return db_bytes(nrows); }
 

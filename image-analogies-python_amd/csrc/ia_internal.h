@@ -2,6 +2,8 @@
 #pragma once
 #include "ia_common.h"
 
+#include <atomic>
+
 namespace ia {
 
 // ---- database chunking (shared by ia_db_build, the screen and the exact stage) ------
@@ -11,11 +13,15 @@ namespace ia {
 // profiles/r01_screen_bench_shard_sizes.txt, r01_chunks_ab_end.txt).  The chunk count is
 // rounded up to a multiple of 4 (the exact stage reads the segment minima as float4).
 constexpr long DB_TARGET_CHUNKS = 512;
+// the chunk target in force (ia_set_chunk_target): a batch of K DBs screened in one launch
+// asks for fewer, longer chunks per DB (the workgroups of K DBs fill the GPU anyway)
+extern std::atomic<long> g_db_chunk_target;
 constexpr int DB_CHUNK_MAX = 8192;     // 64 tiles
 constexpr int DB_SEG_MAX = 512;        // rows per segment (one minimum per query)
 
 static inline int db_chunk_rows(long nrows) {
-    const long want = (nrows + DB_TARGET_CHUNKS * 128 - 1) / (DB_TARGET_CHUNKS * 128);
+    const long target = g_db_chunk_target.load(std::memory_order_relaxed);
+    const long want = (nrows + target * 128 - 1) / (target * 128);
     long tpw = 1;   // 128-row units, a power of two in [1, 64]
     while (tpw < want && tpw < DB_CHUNK_MAX / 128) tpw <<= 1;
     return (int)(128 * tpw);

@@ -94,6 +94,12 @@ long ia_db_rows_padded(long nrows);
 /* bytes of the db buffer ia_db_build fills: 224 B per padded row */
 size_t ia_db_bytes(long nrows);
 int ia_db_chunk_rows(long nrows);
+/* the chunk target (chunks per database, 4 .. 512; default 512) from which every database's
+ * chunking (ia_db_chunk_rows, the padded row counts, workspace sizes) derives; returns the
+ * previous one (any value outside the range only queries).  Process-wide: a database must be
+ * built, sized and synthesised under the same target.  synthesize_batch_dev uses
+ * max(64, 512 / K) for a batch of K jobs (longer chunks, the same results). */
+long ia_set_chunk_target(long chunks);
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 void *db, float *amax, void *stream);
 /* the DB's image form: each pixel's split-f16 pair once, in images padded by
