@@ -286,7 +286,8 @@ def synthesize_batch_dev(jobs, max_levels, k, weights, prof=False, debug=False, 
     # K databases per launch: fewer, longer chunks per database (the screen's workgroups
     # amortise their prologue; c5: +11% on one box), restored before returning
     lib = _ia.lib()
-    prev = lib.ia_set_chunk_target(max(64, 512 // K))
+    target = int(os.environ.get('IA_BATCH_CHUNKS', 0)) or max(64, 512 // K)
+    prev = lib.ia_set_chunk_target(target)
     try:
         for level in levels:
             for (A_pyr, Ap_list, B_pyr, Bp_pyr), kj in zip(jobs, ks):
