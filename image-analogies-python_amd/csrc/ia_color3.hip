@@ -641,9 +641,8 @@ __device__ __forceinline__ double c3_tseg(float emin, float amax0, double nqq, b
 template <bool SCR>
 __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict__ part, int nb, Scr3 sc) {
     __shared__ double qs[D3P], wsh[D3P];
-    __shared__ double tt[32 * D3];              // exact-stage terms; then tp / tw below
-    double (*tp)[D3] = reinterpret_cast<double (*)[D3]>(tt);            // 15 plain (candidates)
-    double (*tw)[D3] = reinterpret_cast<double (*)[D3]>(tt + 15 * D3);  // 16 weighted (+ winner)
+    __shared__ double tt[32 * D3];              // exact-stage terms
+    __shared__ double tp[15][D3], tw[16][D3];   // coherence rows: plain, weighted (+ winner)
     __shared__ double sump[15], sumw[16];
     __shared__ long long rix[16];               // rows: candidates 0..14, winner 15 (-1: none)
     __shared__ int rpos[15][3];
@@ -662,8 +661,28 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
         qs[tid] = f.q3[(long)m * D3P + tid];
         wsh[tid] = tid < D3 ? f.weights[tid] : 0.0;
     }
+    // the coherence candidates' rows (their s / im in the same round trip as the rest)
+    if (tid < 15) {
+        long long cix = -1;
+        int cr = 0, cc = 0, cim = 0;
+        if (!first) {
+            const int rr = y - 2 + tid / 5, rc = x - 2 + tid % 5;
+            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
+                const long sidx = (long)rr * W + rc;
+                const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
+                if (sr >= 0 && sr < Ah && sc >= 0 && sc < Aw) {
+                    const int simg = f.im[sidx];
+                    cix = ((long)Ah * simg + sr) * Aw + sc;
+                    cr = sr; cc = sc; cim = simg;
+                }
+            }
+        }
+        rix[tid] = cix;
+        rpos[tid][0] = cr; rpos[tid][1] = cc; rpos[tid][2] = cim;
+    }
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
+    bool coh_done = false;   // the coherence rows' sums (SCR: beside the first tile's)
     if constexpr (!SCR) {
         for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
     } else {
@@ -701,10 +720,32 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
                     tt[e] = d * d;
                 }
             }
+            if (b == 0) {   // with the first tile: the coherence rows' terms
+                for (int e = tid; e < 15 * D3; e += 256) {
+                    const int j = e / D3, k = e - j * D3;
+                    const long long ix = rix[j];
+                    if (ix < 0) continue;
+                    const double d = f.db3[ix * D3P + k] - qs[k];
+                    const double dw = d * wsh[k];
+                    tp[j][k] = d * d;
+                    tw[j][k] = dw * dw;
+                }
+            }
             __syncthreads();
             if (tid < 32 && r0 + tid < sc.nrows) best3(bd, bi, pw165_sum(tt + tid * D3), r0 + tid);
+            if (b == 0 && tid >= 64 && tid < 94) {   // their sums (wave 1), numpy's pairwise order
+                const bool pl = tid < 79;
+                const int j = pl ? tid - 64 : tid - 79;
+                if (rix[j] >= 0) {
+                    const double sq = sqrt(pw165_sum(pl ? tp[j] : tw[j]));
+                    if (pl) sump[j] = sq; else sumw[j] = sq * sq;
+                } else {
+                    if (pl) sump[j] = INFINITY; else sumw[j] = 0.0;
+                }
+            }
             __syncthreads();
         }
+        coh_done = ntl > 0;
     }
     for (int o = 32; o > 0; o >>= 1) {
         const double od = __shfl_xor(bd, o);
@@ -712,24 +753,6 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
         best3(bd, bi, od, oi);
     }
     if (lane == 0) { rd[wv] = bd; ri[wv] = bi; }
-    if (tid < 15) {
-        long long cix = -1;
-        int cr = 0, cc = 0, cim = 0;
-        if (!first) {
-            const int rr = y - 2 + tid / 5, rc = x - 2 + tid % 5;
-            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
-                const long sidx = (long)rr * W + rc;
-                const int sr = f.s[2 * sidx] + y - rr, sc = f.s[2 * sidx + 1] + x - rc;
-                if (sr >= 0 && sr < Ah && sc >= 0 && sc < Aw) {
-                    const int simg = f.im[sidx];
-                    cix = ((long)Ah * simg + sr) * Aw + sc;
-                    cr = sr; cc = sc; cim = simg;
-                }
-            }
-        }
-        rix[tid] = cix;
-        rpos[tid][0] = cr; rpos[tid][1] = cc; rpos[tid][2] = cim;
-    }
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < 4; ++w) best3(rd[0], ri[0], rd[w], ri[w]);
@@ -737,9 +760,11 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
     }
     __syncthreads();
     const long long app = rix[15];
-    // the terms: (row j, feature k) pairs spread over the block, each row read once
-    for (int e = tid; e < 16 * D3; e += 256) {
-        const int j = e / D3, k = e - j * D3;
+    // the terms: (row j, feature k) pairs spread over the block, each row read once (the
+    // coherence rows only when not done beside the exact stage: the winner's alone then)
+    const int j0 = coh_done ? 15 : 0;
+    for (int e = tid; e < (16 - j0) * D3; e += 256) {
+        const int j = j0 + e / D3, k = e - (j - j0) * D3;
         const long long ix = rix[j];
         if (ix < 0) continue;
         const double d = f.db3[ix * D3P + k] - qs[k];
@@ -748,7 +773,7 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
         tw[j][k] = dw * dw;
     }
     __syncthreads();
-    if (tid < 31) {   // one row per thread, numpy's pairwise order
+    if (tid < 31 && (!coh_done || tid == 30)) {   // one row per thread, numpy's pairwise order
         const bool pl = tid < 15;
         const int j = pl ? tid : tid - 15;
         const double *t = pl ? tp[j] : tw[j];
