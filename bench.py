@@ -114,6 +114,18 @@ def make_inputs(conf, seed):
     return A, Ap, B
 
 
+def pass_check(comm):
+    """After a pass: raise ExchangeTimeout if another rank's records never came over a
+    device-side exchange, else ScheduleFault if a neighbour-decision wait timed out (a fault
+    of the fused kernel).  The exchange is checked FIRST: a dead or slow peer also trips the
+    neighbour waits (the same 10 s limit), and such a cascade is an exchange failure, the
+    one error the RCCL fallback handles."""
+    torch.cuda.synchronize()
+    for cm in comm or []:
+        _ia.exchange_status(cm)
+    _ia.sched_status()
+
+
 class Job:
     """One analogy with its inputs resident in HBM."""
 
@@ -526,11 +538,7 @@ def main():
         run_jobs(lambda jb: jb.step(comm, rank, world, prof, check=False))
 
     def pass_status():
-        """After a pass: raise ScheduleFault (a neighbour-decision wait timed out, a fault of
-        the fused kernel) or ExchangeTimeout (another rank's records never came)."""
-        _ia.sched_status()
-        for cm in comm or []:
-            _ia.exchange_status(cm)
+        pass_check(comm)
 
     def timed_pass(prof):
         """K steps between two barrier + synchronize brackets; prof: HIP events around
@@ -649,7 +657,12 @@ def main():
     # its algorithmic fraction of the f16 dense peak is capped at 1/3; the
     # MFMA pipe's utilisation is reported beside it as pipe_frac
     per_pair = 2 * 55
-    pipe_per_pair = 3 * 2 * 55
+    # the rotated screen (R16) on strip-order levels of the fused kernel: 5
+    # MFMAs x 16 K-slots = 80 slots, 160 f16 flop issued per pair; else the split-f16 screen's
+    # 3 products per feature, 330
+    rot_used = (_ia.db_rot_enabled() and lsh is None and jobs[0].A.shape[1] % 128 == 0 and
+                _ia.db_image_enabled() and (comm is None or _ia.exchange_kind() == 'peer'))
+    pipe_per_pair = 2 * 80 if rot_used else 3 * 2 * 55
     inst = {}
     lv = {}
     for p in prof:
@@ -672,7 +685,8 @@ def main():
     screens = sum(v[1] for v in lv.values())
     pairs = sum(v[2] for v in lv.values())
     traffic, pmc = None, screen_pmc()
-    if pmc and args.config == 'c4' and world == 1 and domG == 11 and lsh is None:
+    if pmc and args.config == 'c4' and world == 1 and domG == 11 and lsh is None and \
+            pmc['kernel'].startswith('k_screen16r') == bool(rot_used):
         traffic = pmc['bytes']
     # the finest level's screen streams the DB's image form when it applies (k_screen16i;
     # k_screen16p, the producer / consumer form, on strip-order levels: every c4 / c5 level)
@@ -681,8 +695,8 @@ def main():
     # sharded finest level take the 4-wave k_screen16i)
     pc_used = (_ia.lib().ia_diag_set_screen_pc(-1) and batch == 1 and
                comm is None)
-    kname = ('k_screen16p<%s>' if pc_used else 'k_screen16i<%s>') \
-        if img_form else 'k_screen16<%s>'
+    kname = 'k_screen16r<%s>' if rot_used else (('k_screen16p<%s>' if pc_used else 'k_screen16i<%s>')
+                                                if img_form else 'k_screen16<%s>')
     roof = {'bound': 'mfma', 'kernel': kname % domG,
             'achieved': achieved,
             'peak': F16_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
@@ -691,8 +705,11 @@ def main():
                            '%.4g pairs (mean M %.1f queries)' % (per_pair, i_n, i_pairs,
                                                                  i_q / max(i_n, 1)),
             'pipe_frac': achieved * pipe_per_pair / per_pair / F16_MFMA_PEAK_TFLOPS,
-            'pipe_note': 'f16 MFMA pipe utilisation: the split issues %d f16 flop per pair '
-                         '(3 products x 2 x 55), so frac <= pipe_frac / 3' % pipe_per_pair,
+            'pipe_note': ('f16 MFMA pipe utilisation: the rotated split screen (R16) issues %d f16 '
+                          'flop per pair (5 MFMAs x 16 K-slots x 2), so frac <= pipe_frac x 110 / 160'
+                          if rot_used else
+                          'f16 MFMA pipe utilisation: the split issues %d f16 flop per pair '
+                          '(3 products x 2 x 55), so frac <= pipe_frac / 3') % pipe_per_pair,
             'screen_avg_us': i_ms * 1e3 / max(i_n, 1),
             'source': 'HIP events around every launch of this kernel in the timed steps',
             'fp32_equivalent_tflops': fp32eq,
@@ -743,8 +760,10 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak' if args.config == 'c5' else 'strong',
         'vs_baseline': None,
-        'dtype': 'f16x3 split (MFMA screen, f32 accumulate) + f32 (re-screen) + f64 (exact '
-                 'rescore, pyramids)',
+        'dtype': ('f16 rotated split (R16 MFMA screen: 11 principal components as f16 pairs, 44 as '
+                  'f16, f32 accumulate) + f64 (rotation, exact rescore, pyramids)' if rot_used else
+                  'f16x3 split (MFMA screen, f32 accumulate) + f32 (re-screen) + f64 (exact '
+                  'rescore, pyramids)'),
         'data': 'synthetic (gaussian-filtered noise; A\' = blur(A)); seeded',
         'config': {'workload': args.config + ': ' + conf['name'] +
                                (', LSH matcher' if lsh is not None else ', brute force'),
@@ -757,6 +776,11 @@ def main():
                    **({'exchange': _ia.exchange_kind() + (' (ranks share one GPU)' if share_gpu() else '')}
                       if comm is not None else {})},
         'roofline': roof,
+        # N > 1 with DB sharding: whether a device-side exchange wait timed out and the
+        # numbers are the RCCL exchange's (null: no fallback happened)
+        **({'exchange_fallback': exchange_fallback or (_ia._EXCHANGE_FALLBACK[-1]
+                                                       if _ia._EXCHANGE_FALLBACK else None)}
+           if comm is not None else {}),
         'matcher': {'kind': 'lsh' if lsh is not None else 'exact',
                     'rows_rescored_fp64': sum(p['rows_rescored'] for p in prof),
                     'candidate_segments': sum(p['candidate_segments'] for p in prof),
@@ -798,6 +822,10 @@ def main():
                 'jobs': len(jobs), 'pixels_per_step': sum(jb.pixels for jb in jobs),
                 'exchanges': list(_ia.EXCHANGE_INFO),
                 'exchange_fallback': list(_ia._EXCHANGE_FALLBACK),
+                # this rank's dominant screen (the MFMA utilisation at N GPUs): launch mean,
+                # algorithmic fraction of the f16 dense peak and the pipe's
+                'kernel': roof.get('kernel'), 'screen_avg_us': roof.get('screen_avg_us'),
+                'frac': roof.get('frac'), 'pipe_frac': roof.get('pipe_frac'),
                 'peer_wait_us_per_pixel': sum(p['peer_wait_us'] for p in prof) / max(1, rq),
                 'neighbour_wait_us_per_pixel': sum(p['neighbour_wait_us'] for p in prof) / max(1, rq),
                 'checksum': chk, **({'job_sums': job_sums} if job_sums is not None else {})}

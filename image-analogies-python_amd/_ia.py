@@ -55,7 +55,7 @@ class IaSynthArgs(ctypes.Structure):
                 ('kappa_factor', ctypes.c_double), ('s', _dp), ('im', _dp),
                 ('workspace', _dp), ('comm', _dp), ('lsh', ctypes.POINTER(IaLsh)),
                 ('flags', ctypes.c_int), ('tag', ctypes.c_int), ('dbg_px', _dp),
-                ('dbg_dist', _dp), ('dbi', _dp)]
+                ('dbg_dist', _dp), ('dbi', _dp), ('dbr', _dp), ('rot', _dp)]
 
 
 class IaShardDb(ctypes.Structure):
@@ -87,6 +87,12 @@ _SIGS = {
     'ia_db_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_db_chunk_rows': (ctypes.c_int, [ctypes.c_long]),
     'ia_set_chunk_target': (ctypes.c_long, [ctypes.c_long]),
+    'ia_db_rot_applies': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long]),
+    'ia_db_rot_bytes': (ctypes.c_size_t, [ctypes.c_long]),
+    'ia_db_cov_bytes': (ctypes.c_size_t, []),
+    'ia_db_cov': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp, _dp]),
+    'ia_db_build_rot': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp,
+                                       _dp, _dp, _dp]),
     'ia_db_build': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long,
                                    _dp, _dp, _dp, _dp]),
     'ia_db_image_bytes': (ctypes.c_size_t, [ctypes.POINTER(IaSrcLevel), ctypes.c_long,
@@ -166,6 +172,8 @@ _SIGS = {
     'ia_diag_peer_stress': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_int), _dp]),
     'ia_diag_peer_trace': (ctypes.c_int, [_dp, _dp]),
+    'ia_diag_screen16r': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp,
+                                         _dp, _dp, _dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp]),
     'ia_diag_synth_level_shards': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs),
                                                   ctypes.POINTER(IaShardDb), ctypes.c_int, _dp]),
 }
@@ -229,6 +237,16 @@ def db_image_enabled():
     """The screen streams the DB's image form where it applies (IA_DB_IMAGE, default 1;
     0: always the 224-B rows).  Both give the same results bit for bit."""
     return os.environ.get('IA_DB_IMAGE', '1') != '0'
+
+
+def db_rot_enabled():
+    """The synthesis screen streams the rotated split DB (R16, DESIGN.md §4d: 5 MFMAs per tile
+    instead of 11) where it applies (IA_DB_ROT, default 1; 0: the split-f16 image form).
+    Both give the same results bit for bit."""
+    return os.environ.get('IA_DB_ROT', '0') != '0'
+
+
+R16_ROT_FLOATS = 13 * 256     # the rotation buffer (ia_rot16.h): 56 x 56 fp32, padded
 
 
 def db_build_form(tiled=-1):

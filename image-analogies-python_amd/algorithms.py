@@ -90,7 +90,7 @@ class LevelIndex:
     distances; centring only tightens the screen's error bound.
     """
 
-    def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg, row0=0, nrows=None, rows=None):
+    def __init__(self, A_sm, A_lg, Ap_sm, Ap_lg, row0=0, nrows=None, rows=None, rot=False):
         self.A_sm, self.A_lg = A_sm.contiguous(), A_lg.contiguous()
         self.Ap_sm, self.Ap_lg = Ap_sm.contiguous(), Ap_lg.contiguous()
         self.src = _ia.src_level(self.A_sm, self.A_lg, self.Ap_sm, self.Ap_lg)
@@ -105,7 +105,7 @@ class LevelIndex:
         mAp = _ia.mean_dev(self.Ap_lg)
         self.center = torch.empty(55, dtype=torch.float64, device=dev)
         _ia.check(lib.ia_center_fill(_ia.ptr(self.center), mA, mAp, st), 'ia_center_fill')
-        self.amax = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.amax = torch.zeros(2, dtype=torch.float32, device=dev)   # {A, A_skip (R16)}
         # the image form where it applies: the matcher then reads only it, and
         # the 224-B rows are built only on request (rows=True: tests, the row-form bench leg)
         ibytes = (lib.ia_db_image_bytes(ctypes.byref(self.src), self.row0, self.nrows)
@@ -124,6 +124,32 @@ class LevelIndex:
                                             _ia.ptr(self.amax), _ia.ptr(self.dbi), st),
                       'ia_db_build_image')
         self.lsh = None
+        self.dbr = self.rot = None
+        if (rot and ibytes and _ia.db_rot_enabled() and
+                lib.ia_db_rot_applies(ctypes.byref(self.src), self.row0, self.nrows)):
+            self.build_rot()
+
+    def build_rot(self):
+        """The rotated split DB of the synthesis screen (R16): the covariance
+        of ~64 k sampled centred rows on device (ia_db_cov), its eigenvectors on the host
+        (55 x 55; any orthonormal basis keeps the matcher exact, the principal one keeps its
+        bound tight), then ia_db_build_rot (amax[1] = A_skip)."""
+        lib, st, dev = _ia.lib(), _ia.stream(), self.A_lg.device
+        cov = torch.empty(lib.ia_db_cov_bytes() // 8, dtype=torch.float64, device=dev)
+        _ia.check(lib.ia_db_cov(ctypes.byref(self.src), self.row0, self.nrows,
+                                _ia.ptr(self.center), _ia.ptr(cov), st), 'ia_db_cov')
+        C = cov[:56 * 56].view(56, 56)[:55, :55].cpu().numpy()
+        w, V = np.linalg.eigh(C)
+        V = V[:, ::-1]                       # components by decreasing variance
+        R = np.zeros(_ia.R16_ROT_FLOATS, dtype=np.float32)
+        R[:56 * 56].reshape(56, 56)[:55, :55] = V.astype(np.float32)
+        self.rot_var = w[::-1].copy()
+        self.rot = torch.as_tensor(R).to(dev)
+        self.dbr = torch.empty(lib.ia_db_rot_bytes(self.nrows), dtype=torch.uint8, device=dev)
+        _ia.check(lib.ia_db_build_rot(ctypes.byref(self.src), self.row0, self.nrows,
+                                      _ia.ptr(self.center), _ia.ptr(self.rot), _ia.ptr(self.amax),
+                                      _ia.ptr(self.dbr), st), 'ia_db_build_rot')
+        return self
 
     def dbi_ptr(self):
         return _ia.ptr(self.dbi).value if self.dbi is not None else None
@@ -250,16 +276,18 @@ class _LazyAs(list):
         return cur
 
 
-def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None, rows=None):
+def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None, rows=None, rot=None):
     """Device index of one level from device pyramids.  row_range(level, N) ->
     (row0, nrows) selects this rank's shard of the rows; lsh (dict of build_lsh
     arguments) switches it to the LSH matcher; rows=True keeps the row form next to the
-    image form."""
+    image form; rot (default: the exact matcher) also builds the synthesis screen's rotated
+    DB where it applies (R16)."""
     Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list])
     Ap_lg = torch.stack([p[level] for p in Ap_pyr_list])
     N = Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2]
     r0, nr = (0, N) if row_range is None else row_range(level, N)
-    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr, rows=rows)
+    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr, rows=rows,
+                       rot=(lsh is None) if rot is None else rot)
     if lsh is not None:
         index.build_lsh(**lsh)
     return index

@@ -9,11 +9,12 @@
 // screen and re-screen, whose error bounds are accounted for in ia_match.hip.
 #include "ia_common.h"
 #include "ia_internal.h"
+#include "ia_rot16.h"
 #include "ia_split16.h"
 
 namespace ia {
 
-std::atomic<long> g_db_chunk_target{DB_TARGET_CHUNKS};
+thread_local long g_db_chunk_target = DB_TARGET_CHUNKS;
 
 __global__ void k_level_features(ImgPair p, int full, double *out) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -680,14 +681,18 @@ __global__ void k_center_fill(double *c, double mA, double mAp) {
 
 // Query rows for the pixels of wave t (y = y_lo + m, x = t - 3y):
 // q64[m][k] (fp64 feature), qp[m][perm56(k)] = fp32(-2 (q_k - c_k)), qp[..55] = 1,
-// nq[m] = |q - c|^2.  One 64-lane wave per query, lane = feature index.
+// nq[m] = |q - c|^2.  One 64-lane wave per query, lane = feature index.  rot (nullable): the
+// level's R16 rotation (ia_rot16.h): q16 then holds the rotated split rows and q64[m][55]
+// the query's skipped-component norm |kappa_skip|^2 (the exact stage's bound)
 __global__ __launch_bounds__(64) void k_query_wave(ImgPair B, ImgPair Bp, int t, int y_lo,
                                                    const double *__restrict__ center,
                                                    double *__restrict__ q64,
                                                    float *__restrict__ qp,
                                                    double *__restrict__ nq,
                                                    const float *__restrict__ amax,
-                                                   _Float16 *__restrict__ q16) {
+                                                   _Float16 *__restrict__ q16,
+                                                   const float *__restrict__ rot) {
+    __shared__ double dq[64];
     const int m = blockIdx.x;
     const int y = y_lo + m, x = t - 3 * y;
     const int lane = threadIdx.x;
@@ -716,7 +721,12 @@ __global__ __launch_bounds__(64) void k_query_wave(ImgPair B, ImgPair Bp, int t,
     double d2 = d * d;
     for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
     if (lane == 0) nq[m] = d2;
-    if (q16) split16_write_query(q16 + (long)m * Q16_ROW * 8, lane, d, d2, amax[0]);
+    if (rot) {
+        const double s2 = r16_write_query(q16 + (long)m * Q16_ROW * 8, lane, d, d2, amax[0], rot, dq);
+        if (lane == 0) q64[(long)m * IA_DP + 55] = s2;
+    } else if (q16) {
+        split16_write_query(q16 + (long)m * Q16_ROW * 8, lane, d, d2, amax[0]);
+    }
 }
 
 // Query rows from caller-provided fp64 features (ia_match_batch).
@@ -743,8 +753,8 @@ __global__ __launch_bounds__(64) void k_query_rows(const double *__restrict__ qi
 
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
                       const double *center, double *q64, float *qp, double *nq,
-                      const float *amax, _Float16 *q16, hipStream_t st) {
-    k_query_wave<<<M, 64, 0, st>>>(B, Bp, t, y_lo, center, q64, qp, nq, amax, q16);
+                      const float *amax, _Float16 *q16, hipStream_t st, const float *rot) {
+    k_query_wave<<<M, 64, 0, st>>>(B, Bp, t, y_lo, center, q64, qp, nq, amax, q16, rot);
     IA_LAUNCH_CHECK("k_query_wave");
     return IA_OK;
 }
@@ -775,8 +785,8 @@ int ia_level_features_f64(const double *sm, int hs, int ws, const double *lg, in
 int ia_db_chunk_rows(long nrows) { return db_chunk_rows(nrows); }
 
 long ia_set_chunk_target(long chunks) {
-    const long prev = g_db_chunk_target.load();
-    if (chunks >= 4 && chunks <= DB_TARGET_CHUNKS) g_db_chunk_target.store(chunks);
+    const long prev = g_db_chunk_target;
+    if (chunks >= 4 && chunks <= DB_TARGET_CHUNKS) g_db_chunk_target = chunks;
     return prev;
 }
 long ia_db_rows_padded(long nrows) { return db_rows_padded(nrows); }
@@ -797,8 +807,10 @@ int ia_diag_set_db_build_form(int tiled) {
 
 // amax = max(amax, the bound of the level's four value ranges): k_db_range partials (part:
 // DBB_BLOCKS x 8 doubles of scratch), then k_db_bound
-static int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
-                          double *part, hipStream_t st) {
+}  // extern "C"
+
+int ia::launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
+                       double *part, hipStream_t st) {
     DbSpans sp;   // blocks per image in proportion to its size, at least one each
     sp.x[0] = src->A_sm; sp.n[0] = d.hws;
     sp.x[1] = src->A_lg; sp.n[1] = d.hw;
@@ -816,6 +828,8 @@ static int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *c
     IA_LAUNCH_CHECK("k_db_bound");
     return IA_OK;
 }
+
+extern "C" {
 
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
                 void *db, float *amax, void *stream) {

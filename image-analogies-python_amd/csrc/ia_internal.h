@@ -14,13 +14,15 @@ namespace ia {
 // rounded up to a multiple of 4 (the exact stage reads the segment minima as float4).
 constexpr long DB_TARGET_CHUNKS = 512;
 // the chunk target in force (ia_set_chunk_target): a batch of K DBs screened in one launch
-// asks for fewer, longer chunks per DB (the workgroups of K DBs fill the GPU anyway)
-extern std::atomic<long> g_db_chunk_target;
+// asks for fewer, longer chunks per DB (the workgroups of K DBs fill the GPU anyway).
+// Per host thread: a batch's target never reaches another thread's DB builds and syntheses
+// (every DB is built, sized and synthesised by one thread; one host thread per GPU stream)
+extern thread_local long g_db_chunk_target;
 constexpr int DB_CHUNK_MAX = 8192;     // 64 tiles
 constexpr int DB_SEG_MAX = 512;        // rows per segment (one minimum per query)
 
 static inline int db_chunk_rows(long nrows) {
-    const long target = g_db_chunk_target.load(std::memory_order_relaxed);
+    const long target = g_db_chunk_target;
     const long want = (nrows + target * 128 - 1) / (target * 128);
     long tpw = 1;   // 128-row units, a power of two in [1, 64]
     while (tpw < want && tpw < DB_CHUNK_MAX / 128) tpw <<= 1;
@@ -229,6 +231,8 @@ struct XJob {
     gptr<double> dbg_dist;
     gptr<unsigned long long> dbox;
     gptr<unsigned int> ctl;                         // tickets[2], error word
+    gptr<const void> dbr;                           // R16 rotated DB (nullable)
+    gptr<const float> rot;                          // R16 rotation (nullable)
 };
 constexpr int IA_BATCH_MAX = 128;
 
@@ -260,6 +264,8 @@ struct XArgs {
     FinishArgs f;                 // t, y_lo, W, ..., px (sharded DB: the device-side exchange)
     gptr<const XJob> jobs;        // nullable: a batch, job blockIdx.y's pointers override these
     gptr<unsigned long long> trace;  // diagnostic (nullable): phase stamps, XW_TRACE_* below
+    gptr<const float> rot;        // R16 level (k_xstrip only, nullable): the rotation; q16n rows in
+                                  // the R16 layout, q64 slot 55 = |kappa_skip|^2, amax[1] = A_skip
 };
 // k_xwave phase stamps (IA_XW_TRACE=<level tag>, ia_diag_xwave_trace): s_memrealtime (100
 // MHz) at XW_TRACE_N points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T
@@ -294,7 +300,16 @@ int exact_stage_mode();
 // re-screen), nq = |q - c|^2 and q16 (the split-f16 screen operand, Q16_ROW half8 each)
 int launch_query_wave(const ImgPair &B, const ImgPair &Bp, int t, int y_lo, int M,
                       const double *center, double *q64, float *qp, double *nq,
-                      const float *amax, _Float16 *q16, hipStream_t st);
+                      const float *amax, _Float16 *q16, hipStream_t st, const float *rot = nullptr);
+// the rotated split-f16 screen (R16, ia_screen16r.hip, ia_rot16.h) of M queries (q16 in the
+// R16 layout) over a rotated DB (ia_db_build_rot) -> segmin[M][db_nsegs(nrows)], the same
+// units as launch_screen16; jobs: a batch (each job's dbr, q16[parity], segmin)
+int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Float16 *q16, int M,
+                     float *segmin, hipStream_t st, const XJob *jobs = nullptr, int njobs = 1, int parity = 0);
+// amax = max(amax, the split scale's bound of a level's four value ranges) (ia_features.hip);
+// part: DBB_BLOCKS x 8 doubles of scratch
+int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
+                   double *part, hipStream_t st);
 int launch_query_rows(const double *qin, int M, const double *center, float *qp, double *nq,
                       const float *amax, _Float16 *q16, hipStream_t st);
 // the split-f16 segment screen (ia_screen16.hip) of M queries over the DB ->

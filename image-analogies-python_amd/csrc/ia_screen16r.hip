@@ -1,0 +1,496 @@
+// ia_screen16r.hip — the rotated split-f16 screen (R16, ia_rot16.h): the
+// level's rotation (covariance of the centred rows, ia_db_cov; the eigenvectors are taken
+// on the host), the rotated database (ia_db_build_rot: 160 B per row, 5 MFMA operand groups
+// per 32-row tile) and the screen k_screen16r: 5 v_mfma_f32_32x32x16_f16 per 32x32 (rows x
+// queries) tile instead of the 11 of ia_screen16.hip, same segment minima units, so the
+// exact stage (k_xstrip) is unchanged apart from its bound.
+//
+// The screen's structure is the row form's of ia_screen16.hip (k_screen16): queries are the
+// stationary MFMA B operand (5 half8 per query tile and lane); the DB streams through LDS in
+// 4-tile stages (20 KiB, global_load_lds_dwordx4, non-temporal, double-buffered, one barrier
+// per stage) and every byte fetched feeds the block's 4 waves; the stage's 4G (query tile,
+// stage tile) chains are cut into 4 equal runs (chain balance), each chain's 5 MFMAs run
+// back to back into one of two ping-pong accumulators and its running-minimum fold is issued
+// after the next chain's first MFMA; minima staged in LDS per chunk, written once.
+#include "ia_internal.h"
+#include "ia_rot16.h"
+
+#include <float.h>
+#include <type_traits>
+
+namespace ia {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int STAGE_TILES = 4;
+constexpr int STAGE_H8 = STAGE_TILES * R16_TILE_H8;   // 20 KiB
+constexpr int MAX_G = 11;
+constexpr int SPC_MAX = 16;
+
+// chain balance (as ia_screen16.hip): the 4G chains of a stage in the order 4t + u cut into
+// 4 equal runs of G, one per wave
+__host__ __device__ constexpr int bal_t0(int G, int W) { return (G * W) / 4; }
+__host__ __device__ constexpr int bal_ns(int G, int W) { return (G * W + G - 1) / 4 - (G * W) / 4 + 1; }
+__host__ __device__ constexpr bool bal_on(int G, int W, int k, int u) {
+    return 4 * (bal_t0(G, W) + k) + u >= G * W && 4 * (bal_t0(G, W) + k) + u < G * W + G;
+}
+template <int G, int W>
+__host__ __device__ constexpr int ch_count() {
+    int n = 0;
+    for (int u = 0; u < STAGE_TILES; ++u)
+        for (int k = 0; k < bal_ns(G, W); ++k) n += bal_on(G, W, k, u) ? 1 : 0;
+    return n;
+}
+template <int G, int W>
+__host__ __device__ constexpr int ch_u(int c) {
+    for (int u = 0; u < STAGE_TILES; ++u)
+        for (int k = 0; k < bal_ns(G, W); ++k)
+            if (bal_on(G, W, k, u) && c-- == 0) return u;
+    return -1;
+}
+template <int G, int W>
+__host__ __device__ constexpr int ch_k(int c) {
+    for (int u = 0; u < STAGE_TILES; ++u)
+        for (int k = 0; k < bal_ns(G, W); ++k)
+            if (bal_on(G, W, k, u) && c-- == 0) return k;
+    return -1;
+}
+template <int G, int W>
+__host__ __device__ constexpr int ch_uo(int c) {
+    int o = 0;
+    for (int i = 1; i <= c; ++i) o += ch_u<G, W>(i) != ch_u<G, W>(i - 1) ? 1 : 0;
+    return o;
+}
+template <int K, int N, typename F>
+__device__ __forceinline__ void sfor(F &&f) {
+    if constexpr (K < N) {
+        f(std::integral_constant<int, K>{});
+        sfor<K + 1, N>(f);
+    }
+}
+__device__ __forceinline__ int fkey(float x) {
+    const int b = __float_as_int(x);
+    return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float fkey_inv(int b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
+__device__ __forceinline__ void fold_min(const floatx16 &x, float &mn) {
+    const float t0 = fminf(fminf(x[0], x[1]), x[2]), t1 = fminf(fminf(x[3], x[4]), x[5]);
+    const float t2 = fminf(fminf(x[6], x[7]), x[8]), t3 = fminf(fminf(x[9], x[10]), x[11]);
+    const float t4 = fminf(fminf(x[12], x[13]), x[14]);
+    const float u0 = fminf(fminf(t0, t1), t2), u1 = fminf(fminf(t3, t4), x[15]);
+    mn = fminf(fminf(mn, u0), u1);
+}
+
+// wave W's chains of one stage (operand sb in LDS), chain-major with two operand sets
+template <int G, int W, int NS>
+__device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS][R16_MFMA], float (&mn)[NS],
+                                          int lane) {
+    constexpr int NC = ch_count<G, W>();
+    const floatx16 zero = {};
+    half8 a[2][R16_MFMA];
+    floatx16 acc[2];
+    {
+        const half8 *p = sb + ch_u<G, W>(0) * R16_TILE_H8 + lane;
+#pragma unroll
+        for (int m = 0; m < R16_MFMA; ++m) a[0][m] = p[m * 64];
+    }
+    sfor<0, NC>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        constexpr int k = ch_k<G, W>(c), ab = ch_uo<G, W>(c) & 1, cb = c & 1;
+        if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c)) {
+            const half8 *p = sb + ch_u<G, W>(c + 1) * R16_TILE_H8 + lane;
+#pragma unroll
+            for (int m = 0; m < R16_MFMA; ++m) a[ab ^ 1][m] = p[m * 64];
+        }
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
+        if constexpr (c > 0) fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
+#pragma unroll
+        for (int m = 1; m < R16_MFMA; ++m)
+            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][m], bq[k][m], acc[cb], 0, 0, 0);
+    });
+    fold_min(acc[(NC - 1) & 1], mn[ch_k<G, W>(NC - 1)]);
+}
+
+template <int G, int W, int NS>
+__device__ __forceinline__ void r16_close(int s, int tps, int *smin, float (&mn)[NS], int lane) {
+    constexpr int T0 = bal_t0(G, W);
+    const int done = (s + 1) * STAGE_TILES;
+    if (done % tps == 0) {
+        int *sm = smin + (done / tps - 1) * (G * 32);
+        const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
+            if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
+            mn[k] = FLT_MAX;
+        }
+    }
+}
+
+__device__ __forceinline__ void copies_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+template <int G, int W>
+__device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
+                                         const StageMap &sm, long chunk, int nstage, int tps,
+                                         const half8 *__restrict__ q16) {
+    constexpr int NS = bal_ns(G, W);
+    constexpr int T0 = bal_t0(G, W);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    half8 bq[NS][R16_MFMA];
+    {
+        const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const half8 *p = q16 + (long)((T0 + k) * 32 + j) * Q16_ROW + h * R16_MFMA;
+#pragma unroll
+            for (int m = 0; m < R16_MFMA; ++m) bq[k][m] = p[m];
+        }
+    }
+    // one stage = 4 consecutive tiles (5 KiB each): 20 wave-instructions of 1 KiB, 5 per wave
+    auto issue = [&](int s, int buf) {
+        const half8 *src = db16 + (stage_lrow(sm, chunk, s) >> 5) * R16_TILE_H8 + W * 64 + lane;
+        half8 *dst = sbuf + buf * STAGE_H8 + W * 64;
+#pragma unroll
+        for (int k = 0; k < R16_MFMA; ++k)
+            __builtin_amdgcn_global_load_lds((const void *)(src + k * 256), (void *)(dst + k * 256), 16, 0, 2);
+    };
+    float mn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
+    issue(0, 0);
+    copies_barrier();
+    for (int s = 0; s < nstage; ++s) {
+        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
+        r16_stage<G, W, NS>(sbuf + (s & 1) * STAGE_H8, bq, mn, lane);
+        r16_close<G, W, NS>(s, tps, smin, mn, lane);
+        copies_barrier();   // stage s + 1 landed, stage s free again
+    }
+}
+
+// grid: (nchunks rounded up to 8) x groups, XCD-aware (all groups of a chunk share
+// blockIdx % 8); group g holds query tiles [g G, g G + G); grid y = job of a batch
+template <int G>
+__global__ __launch_bounds__(256, 2) void k_screen16r(const half8 *__restrict__ db16, int nchunks, int ch,
+                                                      int seg_rows, StageMap sm,
+                                                      const half8 *__restrict__ q16, int M, int groups,
+                                                      float *__restrict__ segmin, long nseg,
+                                                      const XJob *jobs, int parity) {
+    __shared__ half8 sbuf[2 * STAGE_H8];
+    __shared__ int smin[SPC_MAX * G * 32];
+    if (jobs) {
+        const XJob &J = jobs[blockIdx.y];
+        db16 = reinterpret_cast<const half8 *>(J.dbr.get());
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity].get());
+        segmin = J.segmin;
+    }
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (chunk >= nchunks) return;   // uniform over the block, before any barrier
+    const int spc = ch / seg_rows;
+    for (int i = threadIdx.x; i < spc * G * 32; i += 256) smin[i] = 0x7fffffff;
+    const int nstage = ch / (STAGE_TILES * 32);
+    const int tps = seg_rows >> 5;
+    const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) r16_body<G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else if (wv == 1) r16_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else if (wv == 2) r16_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    else r16_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
+    __syncthreads();
+    const long seg0 = (long)chunk * spc;
+    const int q0 = group * G * 32;
+    for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
+        const int ql = i / spc, s = i - ql * spc;
+        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + s] = fkey_inv(smin[s * (G * 32) + ql]);
+    }
+}
+
+// ---- the level's covariance (ia_db_cov): sampled rows, centred, fp64 -------------------
+// Block b takes COV_ROWS sampled rows (row0 + i * step, i = b * COV_ROWS ...), their 55
+// centred features into LDS, and the 1540 upper-triangle sums over them into its partial;
+// k_db_cov_reduce adds the partials in block order (deterministic).
+constexpr int COV_ROWS = 128, COV_PAIRS = 55 * 56 / 2, COV_BLOCKS = 256;
+__global__ __launch_bounds__(256) void k_db_cov(DbSrc src, long row0, long nrows, long step, long nsamp,
+                                                const double *__restrict__ center, double *__restrict__ part) {
+    __shared__ double X[COV_ROWS][IA_DP];
+    double acc[(COV_PAIRS + 255) / 256];
+#pragma unroll
+    for (int i = 0; i < (COV_PAIRS + 255) / 256; ++i) acc[i] = 0.0;
+    for (long base = (long)blockIdx.x * COV_ROWS; base < nsamp; base += (long)gridDim.x * COV_ROWS) {
+        __syncthreads();
+        if (threadIdx.x < COV_ROWS) {
+            const long i = base + threadIdx.x;
+            double *x = X[threadIdx.x];
+            if (i < nsamp) {
+                ImgPair ap; int r, c;
+                src.locate(row0 + i * step, ap, r, c);
+                emit_feature(src.A, ap, r, c, [&](int k, double v) { x[k] = v - center[k]; });
+            } else {
+                for (int k = 0; k < IA_D; ++k) x[k] = 0.0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < (COV_PAIRS + 255) / 256; ++i) {
+            const int p = threadIdx.x + 256 * i;
+            if (p < COV_PAIRS) {
+                // pair p -> (a, b), a <= b: row-major upper triangle
+                int a = 0, rem = p;
+                while (rem >= 55 - a) { rem -= 55 - a; ++a; }
+                const int bb = a + rem;
+                double s = 0.0;
+                for (int r = 0; r < COV_ROWS; ++r) s += X[r][a] * X[r][bb];
+                acc[i] += s;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < (COV_PAIRS + 255) / 256; ++i) {
+        const int p = threadIdx.x + 256 * i;
+        if (p < COV_PAIRS) part[(long)blockIdx.x * COV_PAIRS + p] = acc[i];
+    }
+}
+__global__ __launch_bounds__(256) void k_db_cov_reduce(const double *__restrict__ part, int nb, double *__restrict__ cov) {
+    for (int p = threadIdx.x; p < COV_PAIRS; p += 256) {
+        double s = 0.0;
+        for (int b = 0; b < nb; ++b) s += part[(long)b * COV_PAIRS + p];
+        int a = 0, rem = p;
+        while (rem >= 55 - a) { rem -= 55 - a; ++a; }
+        const int bb = a + rem;
+        cov[a * R16_LD + bb] = s;
+        cov[bb * R16_LD + a] = s;
+    }
+}
+
+// ---- the rotated database (ia_db_build_rot) ---------------------------------------------
+// One thread per padded row (rows past nrows repeat the last real row): the 55 centred
+// features (fp64), rho = V^T a' (fp64 from the fp32 rotation), the split-f16 slots of
+// ia_rot16.h in the tile layout (10 half8 stores), and the skipped components' norm for
+// amax[1] (A_skip, rounded up).  amax[0] (A, the split scale's bound) is computed first by
+// the same range / bound kernels as every other form (launch_db_amax).
+__global__ __launch_bounds__(256) void k_db_build_rot(DbSrc src, long row0, long nrows, long npad,
+                                                      const double *__restrict__ center,
+                                                      const float *__restrict__ rot, float *amax,
+                                                      half8 *__restrict__ dbr) {
+    __shared__ __attribute__((aligned(16))) float R[R16_LD * R16_LD];
+    __shared__ float red[4];
+    for (int i = threadIdx.x; i < R16_LD * R16_LD / 4; i += 256)
+        reinterpret_cast<float4 *>(R)[i] = reinterpret_cast<const float4 *>(rot)[i];
+    __syncthreads();
+    const long p = (long)blockIdx.x * 256 + threadIdx.x;
+    float askip = 0.f;
+    if (p < npad) {
+        const long r = row0 + (p < nrows ? p : nrows - 1);
+        double d[IA_D];
+        double n2 = 0.0;
+        ImgPair ap; int rr, cc;
+        src.locate(r, ap, rr, cc);
+        emit_feature(src.A, ap, rr, cc, [&](int k, double v) {
+            d[k] = v - center[k];
+            n2 += d[k] * d[k];
+        });
+        const Split16Db sc = split16_db_scale(amax[0]);
+        half8 o[2 * R16_MFMA];
+        double sk = 0.0;
+#pragma unroll
+        for (int jb = 0; jb < R16_LD; jb += 4) {
+            double k0 = 0.0, k1 = 0.0, k2 = 0.0, k3 = 0.0;
+#pragma unroll
+            for (int k = 0; k < IA_D; ++k) {
+                const float4 v = *reinterpret_cast<const float4 *>(&R[k * R16_LD + jb]);
+                k0 = fma((double)v.x, d[k], k0);
+                k1 = fma((double)v.y, d[k], k1);
+                k2 = fma((double)v.z, d[k], k2);
+                k3 = fma((double)v.w, d[k], k3);
+            }
+            const double kk[4] = {k0, k1, k2, k3};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = jb + e;
+                if (j >= IA_D) continue;
+                const float r32 = (float)kk[e];
+                if (j >= R16_P) sk += (double)r32 * (double)r32;
+                _Float16 h, l;
+                split16f(ldexpf(r32, sc.ea), h, l);
+                const int s = 23 + j;
+                o[((s & 15) >> 3) * R16_MFMA + (s >> 4)][s & 7] = h;
+                if (j < R16_P) {
+                    const int s0 = 2 * j, s1 = 2 * j + 1;
+                    o[((s0 & 15) >> 3) * R16_MFMA + (s0 >> 4)][s0 & 7] = l;
+                    o[((s1 & 15) >> 3) * R16_MFMA + (s1 >> 4)][s1 & 7] = h;
+                }
+            }
+        }
+        _Float16 nh, nl;
+        split16f(ldexpf((float)n2, sc.ea - sc.R), nh, nl);
+        o[((22 & 15) >> 3) * R16_MFMA + (22 >> 4)][22 & 7] = nl;
+        o[((78 & 15) >> 3) * R16_MFMA + (78 >> 4)][78 & 7] = nh;
+        o[((79 & 15) >> 3) * R16_MFMA + (79 >> 4)][79 & 7] = (_Float16)0.f;
+        half8 *t = dbr + (p >> 5) * R16_TILE_H8 + (p & 31);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int m = 0; m < R16_MFMA; ++m) __builtin_nontemporal_store(o[h * R16_MFMA + m], t + m * 64 + h * 32);
+        const double a = sqrt(sk * (1.0 + 1e-12));
+        askip = (float)a;
+        if ((double)askip < a) askip = nextafterf(askip, INFINITY);
+    }
+    for (int o = 32; o > 0; o >>= 1) askip = fmaxf(askip, __shfl_xor(askip, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = askip;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        // non-negative floats order like their bit patterns
+        atomicMax(reinterpret_cast<unsigned int *>(amax + 1), __float_as_uint(m));
+    }
+}
+
+// query rows of caller-provided fp64 features (q64 rows of IA_DP), R16 layout (diagnostics)
+__global__ __launch_bounds__(64) void k_query_rows_r16(const double *__restrict__ qin,
+                                                       const double *__restrict__ center,
+                                                       const float *__restrict__ rot,
+                                                       const float *__restrict__ amax,
+                                                       double *__restrict__ nq, double *__restrict__ nsk,
+                                                       _Float16 *__restrict__ q16) {
+    __shared__ double dq[64];
+    const int m = blockIdx.x, lane = threadIdx.x;
+    const double d = lane < IA_D ? qin[(long)m * IA_DP + lane] - center[lane] : 0.0;
+    double d2 = d * d;
+    for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+    const double s2 = r16_write_query(q16 + (long)m * Q16_ROW * 8, lane, d, d2, amax[0], rot, dq);
+    if (lane == 0) {
+        nq[m] = d2;
+        nsk[m] = s2;
+    }
+}
+
+}  // namespace
+
+int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Float16 *q16, int M,
+                     float *segmin, hipStream_t st, const XJob *jobs, int njobs, int parity) {
+    const int ch = db_chunk_rows(nrows);
+    const long nchunks = db_nchunks(nrows);
+    const int seg_rows = db_seg_rows(nrows);
+    const long nseg = db_nsegs(nrows);
+    IA_ARG(M > 0 && ch % (STAGE_TILES * 32) == 0 && seg_rows % (STAGE_TILES * 32) == 0 &&
+               ch / seg_rows <= SPC_MAX,
+           "launch_screen16r: bad chunking");
+    IA_ARG(sm.sc == ch / 128, "launch_screen16r: stage map of another chunking");
+    IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || jobs), "launch_screen16r: bad batch");
+    const half8 *db16 = reinterpret_cast<const half8 *>(dbr);
+    const half8 *q = reinterpret_cast<const half8 *>(q16);
+    const int T = (M + 31) / 32;
+    const int groups = (T + MAX_G - 1) / MAX_G;
+    const int G = (T + groups - 1) / groups;
+    const long nb = ((nchunks + 7) / 8) * 8 * groups;
+    IA_ARG(nb < (1L << 31), "screen grid too large");
+    const dim3 grid((unsigned)nb, (unsigned)njobs);
+#define IA_R16_CASE(GG)                                                                             \
+    case GG:                                                                                        \
+        k_screen16r<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M, groups,   \
+                                              segmin, nseg, jobs, parity);                          \
+        break;
+    switch (G) {
+        IA_R16_CASE(1)
+        IA_R16_CASE(2)
+        IA_R16_CASE(3)
+        IA_R16_CASE(4)
+        IA_R16_CASE(5)
+        IA_R16_CASE(6)
+        IA_R16_CASE(7)
+        IA_R16_CASE(8)
+        IA_R16_CASE(9)
+        IA_R16_CASE(10)
+        IA_R16_CASE(11)
+        default: set_error("launch_screen16r: bad query split"); return IA_E_ARG;
+    }
+#undef IA_R16_CASE
+    IA_LAUNCH_CHECK("k_screen16r");
+    return IA_OK;
+}
+
+int launch_query_rows_r16(const double *q64, int M, const double *center, const float *rot,
+                          const float *amax, double *nq, double *nsk, _Float16 *q16, hipStream_t st) {
+    k_query_rows_r16<<<M, 64, 0, st>>>(q64, center, rot, amax, nq, nsk, q16);
+    IA_LAUNCH_CHECK("k_query_rows_r16");
+    return IA_OK;
+}
+
+int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
+                   double *part, hipStream_t st);
+
+}  // namespace ia
+
+using namespace ia;
+
+extern "C" {
+
+int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows) {
+    if (!src || nrows <= 0 || row0 < 0) return 0;
+    const DbSrc d = make_dbsrc(*src);
+    if (!xstrip_applies(d)) return 0;
+    return db_stage_map(row0, nrows, src->Aw, src->Ah).W > 0 ? 1 : 0;
+}
+
+size_t ia_db_rot_bytes(long nrows) { return nrows > 0 ? (size_t)db_rows_padded(nrows) * R16_ROW_B : 0; }
+
+size_t ia_db_cov_bytes(void) { return (size_t)(R16_LD * R16_LD + COV_BLOCKS * COV_PAIRS) * sizeof(double); }
+
+int ia_db_cov(const IaSrcLevel *src, long row0, long nrows, const double *center, double *cov, void *stream) {
+    IA_ARG(src && center && cov && nrows > 0 && row0 >= 0, "ia_db_cov: bad args");
+    IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_cov: rows out of range");
+    hipStream_t st = S(stream);
+    const DbSrc d = make_dbsrc(*src);
+    // ~64 k sampled rows, an odd step (no aliasing with the image width)
+    const long step = (nrows / 65536) | 1;
+    const long nsamp = (nrows + step - 1) / step;
+    double *part = cov + R16_LD * R16_LD;
+    const int nb = (int)std::min<long>(COV_BLOCKS, (nsamp + COV_ROWS - 1) / COV_ROWS);
+    IA_HIP(hipMemsetAsync(cov, 0, (size_t)R16_LD * R16_LD * sizeof(double), st));
+    k_db_cov<<<nb, 256, 0, st>>>(d, row0, nrows, step, nsamp, center, part);
+    IA_LAUNCH_CHECK("k_db_cov");
+    k_db_cov_reduce<<<1, 256, 0, st>>>(part, nb, cov);
+    IA_LAUNCH_CHECK("k_db_cov_reduce");
+    return IA_OK;
+}
+
+int ia_db_build_rot(const IaSrcLevel *src, long row0, long nrows, const double *center, const float *rot,
+                    float *amax, void *dbr, void *stream) {
+    IA_ARG(src && center && rot && amax && dbr && nrows > 0 && row0 >= 0, "ia_db_build_rot: bad args");
+    IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build_rot: rows out of range");
+    IA_ARG(row0 + nrows < (1L << 31), "ia_db_build_rot: rows past 2^31");
+    hipStream_t st = S(stream);
+    const DbSrc d = make_dbsrc(*src);
+    const long npad = db_rows_padded(nrows);
+    IA_ARG(npad * (long)R16_ROW_B >= 1024L * 8 * 8, "ia_db_build_rot: too few rows for the bound's partials");
+    // A (amax[0]) first: max with its prior value (the image form's, if built: the same bound)
+    const int rc = launch_db_amax(src, d, center, amax, reinterpret_cast<double *>(dbr), st);
+    if (rc) return rc;
+    k_db_build_rot<<<(unsigned)((npad + 255) / 256), 256, 0, st>>>(d, row0, nrows, npad, center, rot, amax,
+                                                                  reinterpret_cast<half8 *>(dbr));
+    IA_LAUNCH_CHECK("k_db_build_rot");
+    return IA_OK;
+}
+
+/* diagnostics: one R16 screen of M fp64 query rows (IA_DP each) over a rotated DB ->
+ * segmin[M][db_nsegs(nrows)] (screen units), nq[M], nsk[M]; q16: qrows_alloc(M) rows of
+ * Q16_ROW half8, zeroed by the caller */
+int ia_diag_screen16r(const IaSrcLevel *src, long row0, long nrows, const void *dbr, const float *rot,
+                      const float *amax, const double *center, const double *q64, int M, void *q16,
+                      double *nq, double *nsk, float *segmin, void *stream) {
+    IA_ARG(src && dbr && rot && amax && center && q64 && q16 && nq && nsk && segmin && M > 0,
+           "ia_diag_screen16r: bad args");
+    hipStream_t st = S(stream);
+    int rc = launch_query_rows_r16(q64, M, center, rot, amax, nq, nsk, reinterpret_cast<_Float16 *>(q16), st);
+    if (rc) return rc;
+    const StageMap sm = db_stage_map(row0, nrows, src->Aw, src->Ah);
+    return launch_screen16r(dbr, nrows, sm, reinterpret_cast<const _Float16 *>(q16), M, segmin, st, nullptr, 1, 0);
+}
+
+}  // extern "C"

@@ -379,6 +379,9 @@ struct LevelRun {
     // the launches; part[k - 1] holds job k's state (member runs record no profile)
     int K = 1;
     bool member = false;
+    // R16 (ia_rot16.h): the rotated DB and rotation given, on a strip-order level of the fused
+    // kernel: the rotated screen, rotated query rows and k_xstrip's R16 bound
+    bool r16 = false;
     std::vector<LevelRun> part;
     size_t ev0 = 0;
     unsigned long long *hstats = nullptr;
@@ -423,6 +426,8 @@ struct LevelRun {
         // on one GPU or over the device-side exchange (not the LSH matcher, the RCCL
         // exchange, the in-process shard simulation or a forced work list)
         xw = xwave_on() && !a->lsh && !sim && (!a->comm || peer) && exact_stage_mode() != 1;
+        r16 = xw && a->dbr && a->rot && a->dbi && xwave_on() == 2 && xstrip_applies(src) &&
+              db_stage_map(a->row0, a->nrows, src.A.w, src.A.h).W > 0;
         IA_HIP(hipMemsetAsync(ws.ctl, 0, 256, st));   // tickets, error word (ia_synth_status)
         if (xw) {
             IA_HIP(hipMemsetAsync(ws.qpb, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
@@ -529,6 +534,8 @@ struct LevelRun {
         J.s = a->s; J.im = a->im; J.dbg_px = a->dbg_px; J.dbg_dist = a->dbg_dist;
         J.dbox = ws.dbox;
         J.ctl = ws.ctl;
+        J.dbr = r16 ? a->dbr : nullptr;
+        J.rot = r16 ? a->rot : nullptr;
         return J;
     }
 
@@ -557,6 +564,7 @@ struct LevelRun {
             part[k - 1].member = true;
             if ((rc = part[k - 1].init(&b, st))) return rc;
             IA_ARG(part[k - 1].xw, "ia_synth_levels_batch: a job without the fused kernel");
+            IA_ARG(part[k - 1].r16 == r16, "ia_synth_levels_batch: jobs with and without the rotated DB");
         }
         pinned[0] = job_entry();
         for (int k = 1; k < K; ++k) pinned[k] = part[k - 1].job_entry();
@@ -574,12 +582,12 @@ struct LevelRun {
         double *nqs[2] = {ws.nq, ws.nqb};
         const int b = t & 1;
         if (t == 0 && (rc = launch_query_wave(B, Bp, 0, y_lo, M, a->center, q64s[0], qps[0], nqs[0],
-                                              a->amax, q16s[0], sq)))
+                                              a->amax, q16s[0], sq, r16 ? a->rot : nullptr)))
             return rc;
         for (int k = 1; k < K && t == 0; ++k) {
             const LevelRun &p = part[k - 1];
             if ((rc = launch_query_wave(p.B, p.Bp, 0, y_lo, M, p.a->center, p.ws.q64, p.ws.qp, p.ws.nq,
-                                        p.a->amax, p.ws.q16, sq)))
+                                        p.a->amax, p.ws.q16, sq, r16 ? p.a->rot : nullptr)))
                 return rc;
         }
         const XJob *jt = K > 1 ? ws.jtab : nullptr;
@@ -594,9 +602,13 @@ struct LevelRun {
         hipEvent_t e1 = timed ? prof_event(ev0 + 3 * nscreen + 1) : nullptr;
         if (e0) IA_HIP(hipEventRecord(e0, sq));
         const StageMap sm = db_stage_map(a->row0, a->nrows, src.A.w, src.A.h);
-        if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b,
-                                  a->comm != nullptr)))
+        if (r16) {
+            if ((rc = launch_screen16r(a->dbr, a->nrows, sm, q16s[b], M, segmin, sq, jt, K, b)))
+                return rc;
+        } else if ((rc = launch_screen16(a->db, im ? &img : nullptr, a->nrows, sm, q16s[b], M, segmin, sq, jt,
+                                         K, b, a->comm != nullptr))) {
             return rc;
+        }
         if (e1) IA_HIP(hipEventRecord(e1, sq));
         int y_lo_n = 0, M_n = 0;
         if (t + 1 < nw) wave_rows(H, W, t + 1, y_lo_n, M_n);
@@ -626,9 +638,11 @@ struct LevelRun {
         if (peer) x.f.px = comm_peer_wave(a->comm);
         x.jobs = jt;
         x.trace = xw_trace(a->tag);
+        x.rot = r16 ? a->rot : nullptr;
         const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
         const int form = !im ? XW_ROWS
                        : (xwave_on() == 2 && sm.W > 0 && xstrip_applies(src)) ? XW_STRIP : XW_IMG;
+        IA_ARG(!r16 || form == XW_STRIP, "ia_synth_level: the rotated DB on a level without the strip kernel");
         if ((rc = launch_xwave(x, R, form, sq, K))) return rc;
         if (timed) IA_HIP(hipEventRecord(prof_event(ev0 + 3 * nscreen + 2), sq));
         ++nscreen;

@@ -33,6 +33,7 @@
 // the awaited progress (forward progress).
 #include "ia_exact.h"
 #include "ia_finish.h"
+#include "ia_rot16.h"
 #include "../../include/ia_diag.h"
 
 #include <climits>
@@ -138,6 +139,7 @@ __device__ __forceinline__ void xjob_apply(XArgs &a, const XJob &J, int b) {
     a.f.kappa_factor = J.kappa_factor;
     a.f.Bp_lg = J.Bp_lg;
     a.f.s = J.s; a.f.im = J.im; a.f.dbg_px = J.dbg_px; a.f.dbg_dist = J.dbg_dist;
+    a.rot = J.rot;
 }
 
 // a workgroup barrier that orders LDS only: __syncthreads() also waits for every global load
@@ -222,9 +224,12 @@ __device__ __forceinline__ double xw_finish(const XArgs &a, int i, int y, int x,
 // step 5 (wave 0): the query row of (y, x + 1) for wave t + 1 (k_query_wave's arithmetic):
 // the prefetched features (nxw, LDS-DMA words), this pixel's new value own (dep 1) or the
 // upper neighbour's decision (dep 2, ticket i - 1 of this launch)
+// rotl (nullable): an R16 level's rotation in LDS (k_xstrip<.., true>): the query row in the
+// R16 layout (ia_rot16.h) and q64 slot 55 = |kappa_skip|^2; dq: 64 doubles of LDS scratch
 __device__ __forceinline__ void xw_next_query(const XArgs &a, int i, int y, int x, int lane, int dep, double own,
                                               float amx, const unsigned (*nxw)[64],
-                                              unsigned long long *trace) {
+                                              unsigned long long *trace, const float *rotl = nullptr,
+                                              double *dq = nullptr) {
     const int t = a.f.t;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the prefetched words have landed
     wave_lds_sync();
@@ -262,13 +267,18 @@ __device__ __forceinline__ void xw_next_query(const XArgs &a, int i, int y, int 
         d = vq - ncen;
         a.qpn[(long)m * IA_DP + perm56(lane)] = -2.0f * (float)d;
     } else if (lane == IA_D) {
-        a.q64n[(long)m * IA_DP + IA_D] = 0.0;
+        if (!rotl) a.q64n[(long)m * IA_DP + IA_D] = 0.0;
         a.qpn[(long)m * IA_DP + perm56(IA_D)] = 1.0f;
     }
     double d2 = d * d;
     for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);   // same sum in every lane
     if (lane == 0) a.nqn[m] = d2;
-    split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, amx);
+    if (rotl) {
+        const double s2 = r16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, amx, rotl, dq);
+        if (lane == 0) a.q64n[(long)m * IA_DP + IA_D] = s2;
+    } else {
+        split16_write_query(a.q16n + (long)m * Q16_ROW * 8, lane, d, d2, amx);
+    }
     xw_stamp(trace, 10);
 }
 
@@ -890,7 +900,9 @@ __device__ __forceinline__ void sync3(unsigned *cnt, unsigned g, int lane) {
     asm volatile("" ::: "memory");
 }
 
-template <bool BATCH>
+// ROT: an R16 level (ia_rot16.h): the exact stage's bound eps_R, and the next query row
+// rotated (the rotation copied into LDS by wave 0 at the start)
+template <bool BATCH, bool ROT>
 __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ __attribute__((aligned(16))) char sa_raw[BATCH ? sizeof(XArgs) : 16];
     XArgs &sa = *reinterpret_cast<XArgs *>(sa_raw);
@@ -919,12 +931,24 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     __shared__ long long ccix[XW_NCOH];
     __shared__ int cpos[XW_NCOH][3];
     __shared__ unsigned nxw[4][64];
+    // ROT: wave 0 copies the rotation into win once the rescore is done with it (no LDS of
+    // its own: the fused kernel's LDS decides how many of its workgroups a CU holds beside
+    // a screen block), with 64 doubles of scratch after it
+    static_assert(R16_ROT_B + 64 * 8 <= XS_LDS_B, "the rotation fits the window buffer");
+    float *const rotl = reinterpret_cast<float *>(win);
+    double *const dq = reinterpret_cast<double *>(win + R16_ROT_B);
 
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const FinishArgs &f = a.f;
     const DbSrc &src = a.src;
     const int t = f.t, W = f.W;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    auto rot_dma = [&]() {   // wave 0: 13 x 1 KiB, waited in xw_next_query (vmcnt(0))
+#pragma unroll
+        for (int pc = 0; pc < R16_ROT_FLOATS / 256; ++pc)
+            __builtin_amdgcn_global_load_lds((const void *)(a.rot.get() + pc * 256 + lane * 4),
+                                             (void *)(rotl + pc * 256), 16, 0, 0);
+    };
     if (tid == 0) {
         tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
         bar3 = 0;
@@ -967,7 +991,8 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         const double wk0 = f.weights[lane < IA_D ? lane : 0];
         const double wk = lane < IA_D ? wk0 : 0.0;
         const double nqq = a.nq[vidx(i)];
-        const float am = amx;
+        const double nsk = ROT ? a.q64[(long)i * IA_DP + IA_D] : 0.0;
+        const float am = amx, ask = ROT ? a.amax[vidx(1)] : 0.f;
         const long n4 = a.nseg / 4;
         const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
         float4 v[XS_REG];
@@ -1058,7 +1083,8 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             xw_stamp(trace, 2);
             double Tseg, Trow;
             bool force_full;
-            rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+            if constexpr (ROT) r16_thresholds(emin, am, ask, nqq, nsk, Tseg, force_full);
+            else rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
             seg3_select(sq4, n4, t3, v, Tseg, slist, &scount);
             sync3(&bar3, 2, lane);
             xw_stamp(trace, 3);
@@ -1218,6 +1244,9 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
         __syncthreads();   // the block's winner; the coherence pick is in cs
         xw_stamp(trace, 5);
         if (wv != 0) return;
+        if constexpr (ROT) {   // win is free: the rotation for the next query lands meanwhile
+            if (nxt) rot_dma();
+        }
         XRec lb{INFINITY, LLONG_MAX, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < 4; ++k) xrec_take(lb, XRec{bds[k], bis[k], bwd[k], bvl[k]});
@@ -1226,7 +1255,10 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     }
     xw_stamp(trace, 8);
     if (wv != 0 || !nxt) return;
-    xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace);
+    if constexpr (ROT) {
+        if (!cur) rot_dma();   // (a pixel of wave t + 1 only: win was never used)
+    }
+    xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace, ROT ? rotl : nullptr, ROT ? dq : nullptr);
 }
 
 int launch_xwave(const XArgs &a, int nblocks, int form, hipStream_t st, int njobs) {
@@ -1237,8 +1269,13 @@ int launch_xwave(const XArgs &a, int nblocks, int form, hipStream_t st, int njob
     const dim3 grid((unsigned)nblocks, (unsigned)njobs);
     const bool b = njobs > 1;
     if (form == XW_STRIP) {
-        if (b) k_xstrip<true><<<grid, 256, 0, st>>>(a);
-        else k_xstrip<false><<<grid, 256, 0, st>>>(a);
+        if (a.rot) {
+            if (b) k_xstrip<true, true><<<grid, 256, 0, st>>>(a);
+            else k_xstrip<false, true><<<grid, 256, 0, st>>>(a);
+        } else {
+            if (b) k_xstrip<true, false><<<grid, 256, 0, st>>>(a);
+            else k_xstrip<false, false><<<grid, 256, 0, st>>>(a);
+        }
     } else if (form == XW_IMG) {
         if (b) k_xwave<true, true><<<grid, 256, 0, st>>>(a);
         else k_xwave<true, false><<<grid, 256, 0, st>>>(a);

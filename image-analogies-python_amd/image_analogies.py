@@ -80,6 +80,8 @@ class _LevelCall:
         a.src = index.src
         a.db, a.row0, a.nrows, a.N_total = _ia.ptr(index.db).value, index.row0, index.nrows, index.N
         a.dbi = index.dbi_ptr()
+        if getattr(index, 'dbr', None) is not None:
+            a.dbr, a.rot = _ia.ptr(index.dbr).value, _ia.ptr(index.rot).value
         a.center, a.amax = _ia.ptr(index.center).value, _ia.ptr(index.amax).value
         a.B_sm, a.B_lg = _ia.ptr(B_sm).value, _ia.ptr(B_lg).value
         a.B_hs, a.B_ws = B_sm.shape

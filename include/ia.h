@@ -96,8 +96,9 @@ size_t ia_db_bytes(long nrows);
 int ia_db_chunk_rows(long nrows);
 /* the chunk target (chunks per database, 4 .. 512; default 512) from which every database's
  * chunking (ia_db_chunk_rows, the padded row counts, workspace sizes) derives; returns the
- * previous one (any value outside the range only queries).  Process-wide: a database must be
- * built, sized and synthesised under the same target.  synthesize_batch_dev uses
+ * previous one (any value outside the range only queries).  Per calling host thread: a
+ * database must be built, sized and synthesised under the same target by the same thread;
+ * other threads keep their own target (default 512).  synthesize_batch_dev uses
  * max(64, 512 / K) for a batch of K jobs (longer chunks, the same results). */
 long ia_set_chunk_target(long chunks);
 int ia_db_build(const IaSrcLevel *src, long row0, long nrows, const double *center,
@@ -168,6 +169,24 @@ int ia_coherence_pick(const double *rows, int n, const double *q, int32_t *out,
 int ia_wdist_batch(const double *a, const double *q, const double *w, int n, double *out,
                    void *stream);
 
+/* ---- the rotated split-f16 database (R16; replaces the screen's 11 MFMAs
+ * per 32x32 tile by 5).  Per level (shard): ia_db_cov -> the 55 x 55 covariance of ~64 k
+ * sampled centred rows (fp64, cov[0 .. 56*56) row-major, stride 56; the rest of the buffer,
+ * ia_db_cov_bytes() in all, is scratch); the caller takes its eigenvectors (host, any
+ * orthonormal basis is exact: the bound adapts) and passes rot = V as fp32, rot[k * 56 + j]
+ * = V[k][j] with the components j by decreasing variance, in a buffer of 13,312 B (zero
+ * padded).  ia_db_build_rot then writes the rotated split rows (ia_db_rot_bytes: 160 B per
+ * padded row) and amax[0] = A (as ia_db_build), amax[1] = A_skip (max over rows of the
+ * norm of components 11..54; zero it first).  ia_db_rot_applies: 1 where the synthesis
+ * uses it (strip-order levels of the fused per-wave kernel). */
+int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows);
+size_t ia_db_rot_bytes(long nrows);
+size_t ia_db_cov_bytes(void);
+int ia_db_cov(const IaSrcLevel *src, long row0, long nrows, const double *center, double *cov,
+              void *stream);
+int ia_db_build_rot(const IaSrcLevel *src, long row0, long nrows, const double *center,
+                    const float *rot, float *amax, void *dbr, void *stream);
+
 /* ---- 3-channel matching (config.py:29-42 num_ch = 3: convert=False on colour images) ----
  * Images are h x w x 3 fp64, channel-interleaved; IaSrcLevel / IaSynthArgs keep their
  * meaning with every image pointer 3-channel.  Feature rows have 165 values (the reference's
@@ -231,6 +250,12 @@ typedef struct {
     double *dbg_dist;
     const void *dbi;    /* NULL, or this shard's ia_db_build_image output (the matcher reads
                            it instead of the rows; db may then be NULL; same results) */
+    /* NULL, or this shard's rotated database (ia_db_build_rot) and its rotation: on levels
+     * where the fused strip kernel runs (ia_db_rot_applies, one GPU or the device-side
+     * exchange) the screen then streams it (5 MFMAs per tile instead of 11);
+     * amax must then hold 2 floats {A, A_skip}.  Same results. */
+    const void *dbr;
+    const float *rot;
 } IaSynthArgs;
 #define IA_SYNTH_EAGER 1
 #define IA_SYNTH_PROF 2

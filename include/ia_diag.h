@@ -38,6 +38,13 @@ int ia_diag_screen16_rows(const IaSrcLevel *src, long row0, long nrows, const vo
  * [row0, row0 + nrows) of src: the same minima bit for bit */
 int ia_diag_screen16_image(const IaSrcLevel *src, long row0, long nrows, const void *dbi,
                            const void *q16, int M, float *segmin, void *stream);
+/* the rotated (R16) screen of M fp64 query rows (IA_DP doubles each) over rows
+ * [row0, row0 + nrows) of src's rotated DB (ia_db_build_rot with rot, amax {A, A_skip}):
+ * the R16 query rows into q16 (qrows of 256 B, zeroed by the caller), nq[m] = |q'|^2,
+ * nsk[m] = |kappa_skip|^2, then segmin[M][nseg] in the product's stage order (screen units) */
+int ia_diag_screen16r(const IaSrcLevel *src, long row0, long nrows, const void *dbr, const float *rot,
+                      const float *amax, const double *center, const double *q64, int M, void *q16,
+                      double *nq, double *nsk, float *segmin, void *stream);
 /* exact stage form for this process: 0 one workgroup per query (k_rescore), 1 the work list
  * (k_select / k_items / k_gather), -1 the default (work list above 2^20 rows); other values
  * leave it; returns the previous value */

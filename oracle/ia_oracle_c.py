@@ -6,6 +6,7 @@ Used by tests/ (as the fast checker) and by bench.py's cpu_baseline leg.  Builds
 import ctypes
 import os
 import subprocess
+import time
 
 import numpy as np
 
@@ -48,6 +49,14 @@ def lib():
         _lib.ia_oracle_threads.restype = ctypes.c_int
         _lib.ia_oracle_nn_batch.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_long,
                                             ctypes.POINTER(ctypes.c_long), _dp]
+        _lib.ia_oracle_index_build.restype = ctypes.c_void_p
+        _lib.ia_oracle_index_build.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_int]
+        _lib.ia_oracle_index_free.argtypes = [ctypes.c_void_p]
+        _lib.ia_oracle_index_nn_batch.argtypes = [ctypes.c_void_p, _dp, _dp, ctypes.c_long,
+                                                  ctypes.POINTER(ctypes.c_long), _dp]
+        _lib.ia_oracle_synth_level_ix.restype = ctypes.c_long
+        _lib.ia_oracle_synth_level_ix.argtypes = [ctypes.POINTER(IaOracleLevel), _dp,
+                                                  ctypes.c_void_p]
     return _lib
 
 
@@ -112,9 +121,12 @@ class LevelJob:
             self.db = lib().ia_oracle_build_db(ctypes.byref(self.L))
         return self.db
 
-    def run(self, use_db=True):
-        db = self.build_db() if use_db else None
-        n = lib().ia_oracle_synth_level(ctypes.byref(self.L), db)
+    def run(self, use_db=True, index=None):
+        db = self.build_db() if use_db or index is not None else None
+        if index is not None:
+            n = lib().ia_oracle_synth_level_ix(ctypes.byref(self.L), db, index.ptr)
+        else:
+            n = lib().ia_oracle_synth_level(ctypes.byref(self.L), db)
         if n < 0:
             raise MemoryError('oracle db allocation failed')
         return n
@@ -125,16 +137,28 @@ class LevelJob:
             self.db = None
 
 
-def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels=None):
+def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels=None,
+               indexed=False):
     """All levels (scanline order) with the C oracle; updates Bp_pyr in place.
-    Returns {level: (Bp_level, s, im)} like ia_oracle.synthesize."""
+    Returns {level: (Bp_level, s, im)} like ia_oracle.synthesize.  indexed=True finds each
+    1-NN through a projection index (Index: the brute force's exact answer, faster on
+    large databases; fixture generation)."""
     out = {}
     for level in range(1, max_levels):
         if levels is not None and level not in levels:
             continue
         f = 1 + (2.0 ** (level - max_levels)) * k
         job = LevelJob(level, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, weights, f)
-        job.run()
+        if indexed:
+            db = job.build_db()
+            N = job.Ap_lg.size
+            rows = np.ctypeslib.as_array(db, shape=(N * 55,)).reshape(N, 55)
+            t0 = time.time()
+            job.run(index=Index(db, rows))
+            print('oracle level %d (%d x %d px, %d rows): %.1f s' % (
+                level, job.L.H, job.L.W, N, time.time() - t0), flush=True)
+        else:
+            job.run()
         Bp_pyr[level] = job.Bp_lg.reshape(Bp_pyr[level].shape)
         out[level] = (Bp_pyr[level].copy(), job.s.copy(), job.im.copy())
     return out
@@ -154,3 +178,49 @@ class LevelDB:
     def nn(self, Q):
         """Exact 1-NN rows and distances of Q (M x 55)."""
         return nn_batch(self.ptr, self.N, Q)
+
+    def index(self, P=4):
+        """An exact projection Index over these rows (same answers as nn, faster)."""
+        return Index(self.ptr, self.rows, P)
+
+
+class Index:
+    """Exact 1-NN index over an oracle database (ia_oracle_index_build): rows sorted by
+    their first principal projection, pruned by a Bessel lower bound over P principal
+    directions with rounding margins.  Returns the brute-force scan's (row, distance)
+    exactly (tests/test_oracle.py checks it, ties included).  Test infrastructure only:
+    it makes full-size fixtures affordable; the CPU baseline keeps the scan."""
+
+    def __init__(self, db_ptr, rows, P=4, sample=200000):
+        N = rows.shape[0]
+        step = max(1, N // sample)
+        sub = np.asarray(rows[::step], dtype=np.float64)
+        if len(sub) > 1:
+            C = np.cov((sub - sub.mean(0)).T)
+            _, V = np.linalg.eigh(C)
+            V = V[:, ::-1][:, :P].T.copy()
+        else:
+            V = np.eye(rows.shape[1])[:P]
+        V, _ = np.linalg.qr(V.T)          # re-orthonormalise
+        V = np.ascontiguousarray(V.T[:P], dtype=np.float64)
+        self.P = V.shape[0]
+        self.V = V
+        self.db = db_ptr
+        self.N = N
+        self.ptr = lib().ia_oracle_index_build(db_ptr, N, _d(V), self.P)
+        if not self.ptr:
+            raise MemoryError('oracle index allocation failed')
+
+    def nn(self, Q):
+        Q = np.ascontiguousarray(Q, dtype=np.float64)
+        M = Q.shape[0]
+        idx = np.empty(M, np.int64)
+        d = np.empty(M, np.float64)
+        lib().ia_oracle_index_nn_batch(self.ptr, self.db, _d(Q), M,
+                                       idx.ctypes.data_as(ctypes.POINTER(ctypes.c_long)), _d(d))
+        return idx, d
+
+    def __del__(self):
+        if getattr(self, 'ptr', None) and _lib is not None:
+            _lib.ia_oracle_index_free(self.ptr)
+            self.ptr = None

@@ -14,8 +14,14 @@ exact brute-force matcher, algorithms.py:73-75 restated):
                   1,048,576-row database): s, im and the SHA-256 of B' per level.
   c5_job.npz      config c5's first job (512x512, seed 1000 = bench.py's rank 0 job 0),
                   every level in full (349,184 B' pixels; 262,144 rows at the finest level).
+  c4_full.npz     config c4 (job seed 0) with EVERY level in full, the finest included
+                  (1,048,576 B' pixels against the 4,194,304-row database): s, im and the
+                  SHA-256 of B' per level.  The 1-NN goes through the oracle's projection
+                  index (ia_oracle_c.Index: the brute-force scan's exact answer, checked
+                  against it in tests/test_oracle.py and against c4_queries.npz), which
+                  makes the run minutes instead of a day.
 
-Usage:  python tests/golden/make_config_fixtures.py c3|c4|c4levels|c5 [threads]
+Usage:  python tests/golden/make_config_fixtures.py c3|c4|c4levels|c4full|c5 [threads]
 The inputs are rebuilt from bench.py's workload definitions, so the GPU tests regenerate
 them identically on the box.
 """
@@ -47,14 +53,14 @@ def bp_hash(x):
     return hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest()
 
 
-def full_run(name, fname, job_seed=0, skip_finest=False):
+def full_run(name, fname, job_seed=0, skip_finest=False, indexed=False):
     """The oracle's scanline run of a config's levels -> per-level s, im, B' hash."""
     A, Aps, B, k, cap, seed = workload(name, job_seed)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, cap=cap, seed=seed)
     w = o.compute_weights(3, 5, 12, 1)
     levels = range(1, L - 1) if skip_finest else None
     t0 = time.time()
-    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w, levels=levels)
+    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w, levels=levels, indexed=indexed)
     print('%s oracle: %d levels in %.1f s' % (name, len(out), time.time() - t0))
     rec = {'max_levels': np.int32(L), 'job_seed': np.int32(job_seed)}
     for l, (bp, s, im) in out.items():
@@ -71,6 +77,10 @@ def make_c3():
 
 def make_c4levels():
     full_run('c4', 'c4_levels.npz', skip_finest=True)
+
+
+def make_c4full():
+    full_run('c4', 'c4_full.npz', indexed=True)
 
 
 def make_c5():
@@ -102,4 +112,5 @@ def make_c4():
 if __name__ == '__main__':
     if len(sys.argv) > 2:
         oc.set_threads(int(sys.argv[2]))
-    {'c3': make_c3, 'c4': make_c4, 'c4levels': make_c4levels, 'c5': make_c5}[sys.argv[1]]()
+    {'c3': make_c3, 'c4': make_c4, 'c4levels': make_c4levels, 'c4full': make_c4full,
+     'c5': make_c5}[sys.argv[1]]()

@@ -1,0 +1,142 @@
+"""The rotated split-f16 screen (R16; csrc/ia_rot16.h, ia_screen16r.hip) on
+the GPU: its segment minima stay inside the bound eps_R the exact stage relies on (every
+block shape of the launcher, input scales 1e-3 / 1 / 1e3), A_skip bounds every row's
+skipped components, and syntheses through it equal the split-f16 image form bit for bit
+(the oracle fixtures of c4 / c5 run through it by default)."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import ia_oracle as o
+from conftest import analogy_inputs
+from test_gpu_split16 import U32, Q16_HALVES, _scales, _segment_order, dev
+
+pytestmark = pytest.mark.gpu
+
+R16_P = 11
+
+
+def _level(seed, shape, cap, scale=1.0):
+    import algorithms
+    A, Aps, _ = analogy_inputs(seed, shape, (8, 8), n_ap=1)
+    A, Aps = A * scale, [x * scale for x in Aps]
+    A_pyr = o.compute_gaussian_pyramid(A, 3, cap=cap)
+    Ap_pyr = o.compute_gaussian_pyramid(Aps[0], 3, cap=cap)
+    L = len(A_pyr)
+    idx = algorithms.level_index([dev(p) for p in A_pyr], [[dev(p) for p in Ap_pyr]], L - 1, rot=True)
+    assert idx.dbr is not None, 'the rotated DB applies to a 128-multiple-wide level'
+    As = o.create_index(A_pyr, [Ap_pyr], L)[L - 1]
+    return idx, As
+
+
+def _r16_vs_fp64(idx, As, Q, Ms):
+    """worst |segmin - exact| / eps_R over (query, segment) for each M of Ms"""
+    import _ia
+    lib = _ia.lib()
+    Mmax, N = max(Ms), len(As)
+    qrows = lib.ia_diag_qp_rows(Mmax)
+    q64 = torch.zeros((Mmax, _ia.IA_DP), dtype=torch.float64, device='cuda')
+    q64[:, :55] = dev(Q[:Mmax])
+    npad = lib.ia_db_rows_padded(N)
+    seg = min(lib.ia_db_chunk_rows(N), 512)
+    nseg = npad // seg
+    order = _segment_order(idx, N, npad, seg)
+    amax, askip = (float(x) for x in idx.amax.cpu().numpy())
+    c = idx.center.cpu().numpy()
+    a = As - c
+    na = np.einsum('ij,ij->i', a, a)
+    assert np.sqrt(na.max()) <= amax * (1 + 1e-6)
+    V = idx.rot.cpu().numpy()[:56 * 56].reshape(56, 56)[:55, :55].astype(np.float64)
+    rho = (a @ V).astype(np.float32).astype(np.float64)
+    assert np.sqrt((rho[:, R16_P:] ** 2).sum(1).max()) <= askip * (1 + 1e-6)
+    exact = np.empty((Mmax, nseg))
+    for m0 in range(0, Mmax, 64):
+        E = na[:, None] - 2.0 * (a @ (Q[m0:m0 + 64] - c).T)
+        E = np.concatenate([E, np.repeat(E[-1:], npad - N, 0)])
+        exact[m0:m0 + 64] = E[order].reshape(nseg, seg, -1).min(axis=1).T
+    worst = 0.0
+    for M in Ms:
+        q16 = torch.zeros((qrows, Q16_HALVES), dtype=torch.float16, device='cuda')
+        nq = torch.zeros(qrows, dtype=torch.float64, device='cuda')
+        nsk = torch.zeros(qrows, dtype=torch.float64, device='cuda')
+        segmin = torch.full((qrows, nseg), float('nan'), dtype=torch.float32, device='cuda')
+        _ia.check(lib.ia_diag_screen16r(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.dbr), _ia.ptr(idx.rot),
+                                        _ia.ptr(idx.amax), _ia.ptr(idx.center), _ia.ptr(q64), M, _ia.ptr(q16),
+                                        _ia.ptr(nq), _ia.ptr(nsk), _ia.ptr(segmin), _ia.stream()),
+                  'ia_diag_screen16r')
+        torch.cuda.synchronize()
+        got = segmin[:M].cpu().numpy().astype(np.float64)
+        assert np.isfinite(got).all(), M
+        nqs, nsks = nq.cpu().numpy(), nsk.cpu().numpy()
+        for m in range(M):
+            qq = Q[m] - c
+            assert nqs[m] == pytest.approx(float(qq @ qq), rel=1e-12)
+            kap = qq @ V
+            assert nsks[m] == pytest.approx(float((kap[R16_P:] ** 2).sum()), rel=1e-9, abs=1e-300)
+            ea, R, eq = _scales(amax, float(nqs[m]))
+            true = np.ldexp(exact[m], ea + eq)
+            eps = U32 * (360 * amax * math.sqrt(nqs[m]) + 60 * amax * amax) + \
+                2.0 ** -9 * 1.01 * askip * math.sqrt(nsks[m])
+            worst = max(worst, np.abs(got[m] - true).max() / np.ldexp(eps, ea + eq))
+    return worst
+
+
+@pytest.mark.parametrize('scale', [1.0, 1e3, 1e-3])
+def test_r16_segment_minima_within_bound(gpu, scale):
+    """k_screen16r at query counts hitting every block shape (G = 1..11 tiles, split
+    launches) on a 1M-row strip-order level: every segment minimum within eps_R of the fp64
+    value, at input scales 1e-3, 1, 1e3."""
+    idx, As = _level(45, (1024, 1024), 2, scale)
+    rs = np.random.RandomState(7)
+    n = len(As)
+    Q = np.vstack([As[rs.randint(0, n, 64)],                              # exact rows
+                   As[rs.randint(0, n, 64)] + rs.randn(64, 55) * 1e-7 * scale,
+                   As[rs.randint(0, n, 300)] + rs.randn(300, 55) * 0.01 * scale,
+                   rs.rand(271, 55) * As.max(),                          # far queries
+                   np.full((1, 55), As.mean())])
+    Ms = [1, 20, 64, 65, 100, 128, 160, 192, 224, 256, 288, 320, 342, 353, 500, 700] if scale == 1.0 \
+        else [342, 700]
+    worst = _r16_vs_fp64(idx, As, Q, Ms)
+    print('r16 screen (scale %g): worst |segmin - exact| / eps_R = %.3g' % (scale, worst))
+    assert worst < 1.0
+
+
+def _synth(shape_A, shape_B, cap, seed, rot_on, monkeypatch, batch=1):
+    import _ia
+    import image_analogies as ia
+    monkeypatch.setenv('IA_DB_ROT', '1' if rot_on else '0')
+    A, Aps, B = analogy_inputs(seed, shape_A, shape_B, n_ap=1)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, cap=cap, seed=seed)
+    w = _ia.to_dev(o.compute_weights(3, 5, 12, 1))
+    d = lambda p: [dev(x) for x in p]  # noqa: E731
+    if batch == 1:
+        Bp = d(Bp_pyr)
+        out = ia.synthesize_dev(d(A_pyr), [d(p) for p in Ap_list], d(B_pyr), Bp, L, 0.5, w)
+        return [(Bp[l].cpu().numpy(), s.cpu().numpy(), im.cpu().numpy()) for l, (s, im) in sorted(out.items())]
+    jobs = [(d(A_pyr), [d(p) for p in Ap_list], d(B_pyr), d(Bp_pyr)) for _ in range(batch)]
+    outs = ia.synthesize_batch_dev(jobs, L, 0.5, w)
+    return [[(j[3][l].cpu().numpy(), s.cpu().numpy(), im.cpu().numpy()) for l, (s, im) in sorted(o_.items())]
+            for j, o_ in zip(jobs, outs)]
+
+
+def test_r16_synthesis_equals_image_form(gpu, monkeypatch):
+    """A whole synthesis (A 1024^2, B 512^2, 4-level cap: strip levels of 65 k to 1 M rows)
+    through the rotated screen equals the split-f16 image form's, B', s and im bit for bit."""
+    r = _synth((1024, 1024), (512, 512), 4, 51, True, monkeypatch)
+    i = _synth((1024, 1024), (512, 512), 4, 51, False, monkeypatch)
+    assert len(r) == len(i)
+    for (b0, s0, m0), (b1, s1, m1) in zip(r, i):
+        assert np.array_equal(s0, s1) and np.array_equal(m0, m1) and np.array_equal(b0, b1)
+
+
+def test_r16_batch_equals_image_form(gpu, monkeypatch):
+    """A batch of 3 jobs (ia_synth_levels_batch) through the rotated screen equals the image
+    form's results."""
+    r = _synth((512, 512), (256, 256), 4, 53, True, monkeypatch, batch=3)
+    i = _synth((512, 512), (256, 256), 4, 53, False, monkeypatch, batch=3)
+    for jr, ji in zip(r, i):
+        for (b0, s0, m0), (b1, s1, m1) in zip(jr, ji):
+            assert np.array_equal(s0, s1) and np.array_equal(m0, m1) and np.array_equal(b0, b1)

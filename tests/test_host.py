@@ -435,3 +435,50 @@ def test_hot_kernels_do_not_spill():
                     bad.append((name, int(m.group(1))))
     assert seen > 20, seen
     assert not bad, bad
+
+
+def test_oracle_index_equals_scan():
+    """The oracle's projection index (ia_oracle_c.Index, used to generate full-size fixtures)
+    returns the brute-force scan's row and distance for every query, exact duplicates and
+    1e-12 near-ties included, and the indexed synthesis equals the scanning one."""
+    import ia_oracle_c as oc
+    rs = np.random.RandomState(7)
+    A, Aps, B = analogy_inputs(62, (70, 90), (40, 52), n_ap=2, flat=True)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=62)
+    db = oc.LevelDB(L - 1, A_pyr, Ap_list)
+    N = db.N
+    Q = np.vstack([db.rows[rs.randint(0, N, 30)], db.rows[rs.randint(0, N, 30)] + 1e-12,
+                   db.rows[rs.randint(0, N, 30)] + rs.randn(30, 55) * 1e-3, rs.rand(10, 55)])
+    i0, d0 = db.nn(Q)
+    for P in (1, 4):
+        i1, d1 = db.index(P).nn(Q)
+        assert np.array_equal(i0, i1) and np.array_equal(d0, d1)
+    w = o.compute_weights(3, 5, 12, 1)
+    outs = []
+    for indexed in (False, True):
+        bp = [b.copy() for b in Bp_pyr]
+        outs.append(oc.synthesize(A_pyr, Ap_list, B_pyr, bp, L, 0.5, w, indexed=indexed))
+    for l in outs[0]:
+        for a, b in zip(outs[0][l], outs[1][l]):
+            assert np.array_equal(a, b), l
+
+
+def test_chunk_target_is_per_thread():
+    """a batch's chunk target (ia_set_chunk_target) must not reach another
+    thread's DB builds and syntheses (their layouts derive from it)."""
+    import threading
+    import _ia
+    lib = _ia.lib()
+    N = 262144
+    base = lib.ia_db_chunk_rows(N)
+    prev = lib.ia_set_chunk_target(64)
+    try:
+        mine = lib.ia_db_chunk_rows(N)
+        other = []
+        th = threading.Thread(target=lambda: other.append(lib.ia_db_chunk_rows(N)))
+        th.start()
+        th.join()
+        assert mine > base and other == [base]
+    finally:
+        lib.ia_set_chunk_target(prev)
+    assert lib.ia_db_chunk_rows(N) == base
