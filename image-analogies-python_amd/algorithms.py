@@ -125,7 +125,7 @@ class LevelIndex:
                       'ia_db_build_image')
         self.lsh = None
         self.dbr = self.rot = None
-        if (rot and ibytes and _ia.db_rot_enabled() and
+        if (rot and ibytes and
                 lib.ia_db_rot_applies(ctypes.byref(self.src), self.row0, self.nrows)):
             self.build_rot()
 
@@ -287,7 +287,7 @@ def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None, rows=None, 
     N = Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2]
     r0, nr = (0, N) if row_range is None else row_range(level, N)
     index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr, rows=rows,
-                       rot=(lsh is None) if rot is None else rot)
+                       rot=(lsh is None and _ia.db_rot_enabled()) if rot is None else rot)
     if lsh is not None:
         index.build_lsh(**lsh)
     return index
