@@ -243,7 +243,7 @@ def db_rot_enabled():
     """The synthesis screen streams the rotated split DB (R16, DESIGN.md §4d: 5 MFMAs per tile
     instead of 11) where it applies (IA_DB_ROT, default 1; 0: the split-f16 image form).
     Both give the same results bit for bit."""
-    return os.environ.get('IA_DB_ROT', '0') != '0'
+    return os.environ.get('IA_DB_ROT', '1') != '0'
 
 
 R16_ROT_FLOATS = 13 * 256     # the rotation buffer (ia_rot16.h): 56 x 56 fp32, padded

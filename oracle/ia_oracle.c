@@ -7,7 +7,8 @@
  * called by the product library.
  *
  * It follows oracle/ia_oracle.py operation for operation (and is checked against it
- * bit for bit in tests/test_oracle.py):
+ * bit for bit in tests/test_oracle.py), for luminance (num_ch = 1, 55-dim rows) and colour
+ * (num_ch = 3: config.py:29-42, 165-dim rows of (row, col, channel)-flattened windows):
  *   features      algorithms.py:11-47, 78-89   symmetric-padded 3x3 coarse + 5x5 fine
  *   brute force   algorithms.py:73-75 (exact) d = pairwise8( (a-q)*(a-q) ), first min
  *   coherence     algorithms.py:92-130         argmin sqrt(pairwise8(x*x)), first min
@@ -58,17 +59,21 @@ static inline long symi(long i, long n) {   /* np.pad 'symmetric' index map */
     return i >= n ? p - 1 - i : i;
 }
 
-/* 1-channel feature of pixel (r, c): [3x3 of sm at (r/2, c/2) | 5x5 (or first 12) of lg] */
+/* feature of pixel (r, c) of a C-channel image pair (channel-interleaved, C = 1 or 3):
+ * [3x3 of sm at (r/2, c/2) | 5x5 (or the first 12 positions) of lg], each window flattened
+ * (row, col, channel) as extract_patches_2d + flatten do (algorithms.py:20-31) */
 static int pixel_feature(const double *sm, long hs, long ws, const double *lg, long h, long w,
-                         long r, long c, int full, double *out) {
+                         long r, long c, int full, int C, double *out) {
     int k = 0;
     for (int dr = -1; dr <= 1; dr++)
         for (int dc = -1; dc <= 1; dc++)
-            out[k++] = sm[symi(r / 2 + dr, hs) * ws + symi(c / 2 + dc, ws)];
+            for (int ch = 0; ch < C; ch++)
+                out[k++] = sm[(symi(r / 2 + dr, hs) * ws + symi(c / 2 + dc, ws)) * C + ch];
     int nfine = full ? NLG * NLG : NHALF;
     for (int t = 0; t < nfine; t++) {
         int dr = t / NLG - 2, dc = t % NLG - 2;
-        out[k++] = lg[symi(r + dr, h) * w + symi(c + dc, w)];
+        for (int ch = 0; ch < C; ch++)
+            out[k++] = lg[(symi(r + dr, h) * w + symi(c + dc, w)) * C + ch];
     }
     return k;
 }
@@ -86,25 +91,35 @@ typedef struct {
     int32_t *s;                  /* out: H*W*2 source pixel (row, col) in A'            */
     int32_t *im;                 /* out: H*W source image number                        */
     long max_pixels;             /* <0: whole level; else stop after this many pixels   */
+    int nch;                     /* channels (config.py:29-42 num_ch): 0 or 1, or 3     */
 } IaOracleLevel;
 
-#define D 55
+#define D 55          /* luminance row length (the scan and batch entries below)         */
+#define DMAX 165      /* 3 channels: 55 x 3                                              */
+static inline int lch(const IaOracleLevel *L) { return L->nch > 1 ? L->nch : 1; }
+int ia_oracle_threads(void);
+static int g_threads_build(void) { int t = ia_oracle_threads(); return t > 0 ? t : 1; }
 
-/* database row ix -> 55 features (algorithms.py:63-67: [A full | A'_img half]) */
+/* database row ix -> 55 C features (algorithms.py:63-67: [A full | A'_img half]) */
 static void db_row(const IaOracleLevel *L, long ix, double *f) {
+    const int C = lch(L);
     long hw = (long)L->Ah * L->Aw;
     long img = ix / hw, rem = ix - img * hw;
     long r = rem / L->Aw, c = rem % L->Aw;
-    int k = pixel_feature(L->A_sm, L->A_hs, L->A_ws, L->A_lg, L->Ah, L->Aw, r, c, 1, f);
-    pixel_feature(L->Ap_sm + img * (long)L->A_hs * L->A_ws, L->A_hs, L->A_ws,
-                  L->Ap_lg + img * hw, L->Ah, L->Aw, r, c, 0, f + k);
+    int k = pixel_feature(L->A_sm, L->A_hs, L->A_ws, L->A_lg, L->Ah, L->Aw, r, c, 1, C, f);
+    pixel_feature(L->Ap_sm + img * (long)L->A_hs * L->A_ws * C, L->A_hs, L->A_ws,
+                  L->Ap_lg + img * hw * C, L->Ah, L->Aw, r, c, 0, C, f + k);
 }
 
 double *ia_oracle_build_db(const IaOracleLevel *L) {
+    const int Dd = 55 * lch(L);
     long N = (long)L->nAp * L->Ah * L->Aw;
-    double *db = (double *)malloc(sizeof(double) * N * D);
+    double *db = (double *)malloc(sizeof(double) * N * Dd);
     if (!db) return NULL;
-    for (long ix = 0; ix < N; ix++) db_row(L, ix, db + ix * D);
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(g_threads_build())
+#endif
+    for (long ix = 0; ix < N; ix++) db_row(L, ix, db + ix * Dd);
     return db;
 }
 
@@ -122,6 +137,14 @@ static inline double dist55(const double *a, const double *q) {
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     for (int i = 48; i < D; i++) { double x = a[i] - q[i]; res += x * x; }
     return res;
+}
+
+/* pairwise8((a - q)^2) for n = 55 (dist55) or any n (165: numpy's halves of 80 and 85) */
+static inline double distn(const double *a, const double *q, int n) {
+    if (n == D) return dist55(a, q);
+    double t[DMAX];
+    for (int j = 0; j < n; j++) { double x = a[j] - q[j]; t[j] = x * x; }
+    return pairwise8(t, n);
 }
 
 /* threads of the 1-NN scan (0 = OpenMP's default, i.e. OMP_NUM_THREADS) */
@@ -214,15 +237,16 @@ void ia_oracle_nn_batch(const double *db, long N, const double *Q, long M, long 
 typedef struct {
     long N;
     int P;                      /* projections used (1..IX_PMAX)                      */
-    double v[IX_PMAX][D];       /* orthonormal projection vectors                     */
+    int dim;                    /* row length: 55 or 165                              */
+    double v[IX_PMAX][DMAX];    /* orthonormal projection vectors                     */
     long *orig;                 /* sorted position -> original row                    */
     double *proj;               /* N x P projections, sorted order                    */
     double *rows;               /* N x D rows, sorted order                           */
 } IaOracleIndex;
 
-static double dot55(const double *a, const double *v) {
+static double dotn(const double *a, const double *v, int n) {
     double s = 0.;
-    for (int k = 0; k < D; k++) s += a[k] * v[k];
+    for (int k = 0; k < n; k++) s += a[k] * v[k];
     return s;
 }
 
@@ -234,18 +258,19 @@ static int cmp_key(const void *x, const void *y) {
     return *(const long *)x < *(const long *)y ? -1 : (*(const long *)x > *(const long *)y);
 }
 
-/* build the index over db (N x 55) with P orthonormal vectors V (P x 55) */
-IaOracleIndex *ia_oracle_index_build(const double *db, long N, const double *V, int P) {
-    if (P < 1 || P > IX_PMAX) return NULL;
+/* build the index over db (N x Dn, Dn = 55 or 165) with P orthonormal vectors V (P x Dn) */
+IaOracleIndex *ia_oracle_index_build2(const double *db, long N, int Dn, const double *V, int P) {
+    if (P < 1 || P > IX_PMAX || Dn < 1 || Dn > DMAX) return NULL;
     IaOracleIndex *ix = (IaOracleIndex *)calloc(1, sizeof(IaOracleIndex));
     if (!ix) return NULL;
     ix->N = N;
     ix->P = P;
-    memcpy(ix->v, V, sizeof(double) * P * D);
+    ix->dim = Dn;
+    for (int p = 0; p < P; p++) memcpy(ix->v[p], V + (long)p * Dn, sizeof(double) * Dn);
     double *key = (double *)malloc(sizeof(double) * N);
     ix->orig = (long *)malloc(sizeof(long) * N);
     ix->proj = (double *)malloc(sizeof(double) * N * P);
-    ix->rows = (double *)malloc(sizeof(double) * N * D);
+    ix->rows = (double *)malloc(sizeof(double) * N * Dn);
     if (!key || !ix->orig || !ix->proj || !ix->rows) {
         free(key); free(ix->orig); free(ix->proj); free(ix->rows); free(ix);
         return NULL;
@@ -253,19 +278,22 @@ IaOracleIndex *ia_oracle_index_build(const double *db, long N, const double *V, 
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(ia_oracle_threads())
 #endif
-    for (long i = 0; i < N; i++) { key[i] = dot55(db + i * D, ix->v[0]); ix->orig[i] = i; }
+    for (long i = 0; i < N; i++) { key[i] = dotn(db + i * Dn, ix->v[0], Dn); ix->orig[i] = i; }
     g_sort_key = key;
     qsort(ix->orig, N, sizeof(long), cmp_key);
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(ia_oracle_threads())
 #endif
     for (long s = 0; s < N; s++) {
-        const double *a = db + ix->orig[s] * D;
-        memcpy(ix->rows + s * D, a, sizeof(double) * D);
-        for (int p = 0; p < P; p++) ix->proj[s * P + p] = dot55(a, ix->v[p]);
+        const double *a = db + ix->orig[s] * Dn;
+        memcpy(ix->rows + s * Dn, a, sizeof(double) * Dn);
+        for (int p = 0; p < P; p++) ix->proj[s * P + p] = dotn(a, ix->v[p], Dn);
     }
     free(key);
     return ix;
+}
+IaOracleIndex *ia_oracle_index_build(const double *db, long N, const double *V, int P) {
+    return ia_oracle_index_build2(db, N, D, V, P);
 }
 
 void ia_oracle_index_free(IaOracleIndex *ix) {
@@ -286,12 +314,12 @@ static inline double ix_bound(const double *pa, const double *pq, int P) {
 /* (d, row) lexicographic minimum over sorted positions [lo, hi), starting from (*bd, *bi) */
 static void ix_scan(const IaOracleIndex *ix, long lo, long hi, const double *q, const double *pq,
                     double *bd, long *bi) {
-    const int P = ix->P;
+    const int P = ix->P, Dn = ix->dim;
     double best = *bd;
     long bix = *bi;
     for (long s = lo; s < hi; s++) {
         if (ix_bound(ix->proj + s * P, pq, P) > best * IX_SLACK + 1e-300) continue;
-        double d = dist55(ix->rows + s * D, q);
+        double d = distn(ix->rows + s * Dn, q, Dn);
         long r = ix->orig[s];
         if (d < best || (d == best && r < bix)) { best = d; bix = r; }
     }
@@ -312,13 +340,13 @@ static long ix_lower(const IaOracleIndex *ix, double x) {
 /* exact 1-NN of q through the index; seeds (original rows, may be NULL) start the bound */
 long ia_oracle_index_nn(const IaOracleIndex *ix, const double *db, const double *q,
                         const long *seeds, int nseeds, double *dmin_out) {
-    const int P = ix->P;
+    const int P = ix->P, Dn = ix->dim;
     double pq[IX_PMAX];
-    for (int p = 0; p < P; p++) pq[p] = dot55(q, ix->v[p]);
+    for (int p = 0; p < P; p++) pq[p] = dotn(q, ix->v[p], Dn);
     double best = INFINITY;
     long bi = -1;
     for (int i = 0; i < nseeds; i++) {
-        double d = dist55(db + seeds[i] * D, q);
+        double d = distn(db + seeds[i] * Dn, q, Dn);
         if (d < best || (d == best && seeds[i] < bi)) { best = d; bi = seeds[i]; }
     }
     /* seed from the key neighbourhood too */
@@ -360,15 +388,43 @@ void ia_oracle_index_nn_batch(const IaOracleIndex *ix, const double *db, const d
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(T > 0 ? T : 1) schedule(dynamic, 1)
 #endif
-    for (long m = 0; m < M; m++) idx[m] = ia_oracle_index_nn(ix, db, Q + m * D, NULL, 0, &dmin[m]);
+    for (long m = 0; m < M; m++) idx[m] = ia_oracle_index_nn(ix, db, Q + m * ix->dim, NULL, 0, &dmin[m]);
     g_threads = saved;
 }
 
-static double wdist(const double *a, const double *q, const double *w) {
-    double t[D];
-    for (int j = 0; j < D; j++) { double v = (a[j] - q[j]) * w[j]; t[j] = v * v; }
-    double s = sqrt(pairwise8(t, D));
+static double wdist(const double *a, const double *q, const double *w, int n) {
+    double t[DMAX];
+    for (int j = 0; j < n; j++) { double v = (a[j] - q[j]) * w[j]; t[j] = v * v; }
+    double s = sqrt(pairwise8(t, n));
     return s * s;
+}
+
+/* exact 1-NN (first minimum) over any row length n, rows split over threads, combined in
+ * row order (the 3-channel synthesis without an index) */
+static long nn_n(const double *db, long N, int n, const double *q) {
+    int T = ia_oracle_threads();
+    if (T > 64) T = 64;
+    if (T < 1 || N < 4096) T = 1;
+    double bd[64];
+    long bix[64];
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+#endif
+    for (int t = 0; t < T; t++) {
+        double best = INFINITY;
+        long bi = -1;
+        for (long i = N * t / T; i < N * (t + 1) / T; i++) {
+            double d = distn(db + i * n, q, n);
+            if (d < best) { best = d; bi = i; }
+        }
+        bd[t] = best;
+        bix[t] = bi;
+    }
+    double best = INFINITY;
+    long bi = -1;
+    for (int t = 0; t < T; t++)
+        if (bix[t] >= 0 && bd[t] < best) { best = bd[t]; bi = bix[t]; }
+    return bi;
 }
 
 /* image_analogies.py:161-220 for one level (db may be NULL: rows built on the fly).
@@ -388,12 +444,14 @@ long ia_oracle_synth_level_ix(const IaOracleLevel *L, const double *db, const Ia
     if (!db) { own = ia_oracle_build_db(L); db = own; if (!db) return -1; }
     long npx = H * W;
     if (L->max_pixels >= 0 && L->max_pixels < npx) npx = L->max_pixels;
-    double q[D], x[D], t[D];
+    const int C = lch(L), Dn = 55 * C;
+    if (ix && ix->dim != Dn) return -2;
+    double q[DMAX], x[DMAX], t[DMAX];
     for (long qi = 0; qi < npx; qi++) {
         long row = qi / W, col = qi % W;
         /* BBp_feat = [B_features[level][ix] | extract_pixel_feature(Bp pads, half)] */
-        int k = pixel_feature(L->B_sm, L->B_hs, L->B_ws, L->B_lg, H, W, row, col, 1, q);
-        pixel_feature(L->Bp_sm, L->B_hs, L->B_ws, L->Bp_lg, H, W, row, col, 0, q + k);
+        int k = pixel_feature(L->B_sm, L->B_hs, L->B_ws, L->B_lg, H, W, row, col, 1, C, q);
+        pixel_feature(L->Bp_sm, L->B_hs, L->B_ws, L->Bp_lg, H, W, row, col, 0, C, q + k);
         long p_app_ix;
         if (ix) {
             long seeds[16];
@@ -410,7 +468,7 @@ long ia_oracle_synth_level_ix(const IaOracleLevel *L, const double *db, const Ia
             }
             p_app_ix = ia_oracle_index_nn(ix, db, q, seeds, ns, NULL);
         } else {
-            p_app_ix = ia_oracle_nn(db, N, q, NULL);
+            p_app_ix = Dn == 55 ? ia_oracle_nn(db, N, q, NULL) : nn_n(db, N, Dn, q);
         }
         long hw = Ah * Aw;
         long i_app = p_app_ix / hw, rem = p_app_ix - i_app * hw;
@@ -429,19 +487,20 @@ long ia_oracle_synth_level_ix(const IaOracleLevel *L, const double *db, const Ia
                     if (!(sr >= 0 && sr < Ah && sc >= 0 && sc < Aw)) continue;
                     long img = L->im[rix];
                     long ix = (Ah * img + sr) * Aw + sc;
-                    const double *a = db + ix * D;
-                    for (int j = 0; j < D; j++) { x[j] = a[j] - q[j]; t[j] = x[j] * x[j]; }
-                    double d = sqrt(pairwise8(t, D));
+                    const double *a = db + ix * Dn;
+                    for (int j = 0; j < Dn; j++) { x[j] = a[j] - q[j]; t[j] = x[j] * x[j]; }
+                    double d = sqrt(pairwise8(t, Dn));
                     if (d < bestd) { bestd = d; bsr = sr; bsc = sc; bim = img; bix = ix; }
                 }
             }
             if (bix >= 0) {
-                double d_app = wdist(db + p_app_ix * D, q, L->weights);
-                double d_coh = wdist(db + bix * D, q, L->weights);
+                double d_app = wdist(db + p_app_ix * Dn, q, L->weights, Dn);
+                double d_coh = wdist(db + bix * Dn, q, L->weights, Dn);
                 if (d_coh <= d_app * L->kappa_factor) { pr = bsr; pc = bsc; pi = bim; }
             }
         }
-        L->Bp_lg[row * W + col] = L->Ap_lg[pi * hw + pr * Aw + pc];
+        for (int ch = 0; ch < C; ch++)   /* image_analogies.py:214: every channel */
+            L->Bp_lg[(row * W + col) * C + ch] = L->Ap_lg[(pi * hw + pr * Aw + pc) * C + ch];
         L->s[2 * qi] = (int32_t)pr;
         L->s[2 * qi + 1] = (int32_t)pc;
         L->im[qi] = (int32_t)pi;

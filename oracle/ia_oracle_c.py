@@ -28,7 +28,7 @@ class IaOracleLevel(ctypes.Structure):
         ('W', ctypes.c_int),
         ('Bp_sm', _dp), ('Bp_lg', _dp), ('weights', _dp),
         ('kappa_factor', ctypes.c_double),
-        ('s', _ip), ('im', _ip), ('max_pixels', ctypes.c_long),
+        ('s', _ip), ('im', _ip), ('max_pixels', ctypes.c_long), ('nch', ctypes.c_int),
     ]
 
 
@@ -49,8 +49,8 @@ def lib():
         _lib.ia_oracle_threads.restype = ctypes.c_int
         _lib.ia_oracle_nn_batch.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_long,
                                             ctypes.POINTER(ctypes.c_long), _dp]
-        _lib.ia_oracle_index_build.restype = ctypes.c_void_p
-        _lib.ia_oracle_index_build.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_int]
+        _lib.ia_oracle_index_build2.restype = ctypes.c_void_p
+        _lib.ia_oracle_index_build2.argtypes = [_dp, ctypes.c_long, ctypes.c_int, _dp, ctypes.c_int]
         _lib.ia_oracle_index_free.argtypes = [ctypes.c_void_p]
         _lib.ia_oracle_index_nn_batch.argtypes = [ctypes.c_void_p, _dp, _dp, ctypes.c_long,
                                                   ctypes.POINTER(ctypes.c_long), _dp]
@@ -97,22 +97,25 @@ class LevelJob:
         self.Bp_sm = c(Bp_pyr[level - 1], np.float64)
         self.Bp_lg = np.array(Bp_pyr[level], dtype=np.float64, order='C')
         self.w = c(weights, np.float64)
-        H, W = self.B_lg.shape
+        H, W = self.B_lg.shape[:2]
+        self.nch = self.B_lg.shape[2] if self.B_lg.ndim == 3 else 1
+        self.D = 55 * self.nch
         self.s = np.zeros((H * W, 2), np.int32)
         self.im = np.zeros(H * W, np.int32)
         L = IaOracleLevel()
         L.A_sm, L.A_lg, L.Ap_sm, L.Ap_lg = _d(self.A_sm), _d(self.A_lg), _d(self.Ap_sm), _d(self.Ap_lg)
-        L.A_hs, L.A_ws = self.A_sm.shape
-        L.Ah, L.Aw = self.A_lg.shape
+        L.A_hs, L.A_ws = self.A_sm.shape[:2]
+        L.Ah, L.Aw = self.A_lg.shape[:2]
         L.nAp = len(Ap_pyr_list)
         L.B_sm, L.B_lg = _d(self.B_sm), _d(self.B_lg)
-        L.B_hs, L.B_ws = self.B_sm.shape
+        L.B_hs, L.B_ws = self.B_sm.shape[:2]
         L.H, L.W = H, W
         L.Bp_sm, L.Bp_lg, L.weights = _d(self.Bp_sm), _d(self.Bp_lg), _d(self.w)
         L.kappa_factor = kappa_factor
         L.s = self.s.ctypes.data_as(_ip)
         L.im = self.im.ctypes.data_as(_ip)
         L.max_pixels = max_pixels
+        L.nch = self.nch
         self.L = L
         self.db = None
 
@@ -127,6 +130,8 @@ class LevelJob:
             n = lib().ia_oracle_synth_level_ix(ctypes.byref(self.L), db, index.ptr)
         else:
             n = lib().ia_oracle_synth_level(ctypes.byref(self.L), db)
+        if n == -2:
+            raise ValueError('oracle index built for another row length')
         if n < 0:
             raise MemoryError('oracle db allocation failed')
         return n
@@ -151,8 +156,8 @@ def synthesize(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels
         job = LevelJob(level, A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, weights, f)
         if indexed:
             db = job.build_db()
-            N = job.Ap_lg.size
-            rows = np.ctypeslib.as_array(db, shape=(N * 55,)).reshape(N, 55)
+            N = job.A_lg.shape[0] * job.A_lg.shape[1] * job.Ap_lg.shape[0]
+            rows = np.ctypeslib.as_array(db, shape=(N * job.D,)).reshape(N, job.D)
             t0 = time.time()
             job.run(index=Index(db, rows))
             print('oracle level %d (%d x %d px, %d rows): %.1f s' % (
@@ -170,13 +175,19 @@ class LevelDB:
 
     def __init__(self, level, A_pyr, Ap_pyr_list):
         dummy = [np.zeros((2, 2))] * (level + 1)
-        self._job = LevelJob(level, A_pyr, Ap_pyr_list, dummy, dummy, np.zeros(55), 1.0)
+        C = A_pyr[level].shape[2] if A_pyr[level].ndim == 3 else 1
+        if C > 1:
+            dummy = [np.zeros((2, 2, C))] * (level + 1)
+        self._job = LevelJob(level, A_pyr, Ap_pyr_list, dummy, dummy, np.zeros(55 * C), 1.0)
         self.ptr = self._job.build_db()
-        self.N = self._job.Ap_lg.size
-        self.rows = np.ctypeslib.as_array(self.ptr, shape=(self.N * 55,)).reshape(self.N, 55)
+        self.D = 55 * C
+        self.N = A_pyr[level].shape[0] * A_pyr[level].shape[1] * len(Ap_pyr_list)
+        self.rows = np.ctypeslib.as_array(self.ptr, shape=(self.N * self.D,)).reshape(self.N, self.D)
 
     def nn(self, Q):
-        """Exact 1-NN rows and distances of Q (M x 55)."""
+        """Exact 1-NN rows and distances of Q (M x 55; 165-dim rows: through the index)."""
+        if self.D != 55:
+            return self.index().nn(Q)
         return nn_batch(self.ptr, self.N, Q)
 
     def index(self, P=4):
@@ -207,7 +218,8 @@ class Index:
         self.V = V
         self.db = db_ptr
         self.N = N
-        self.ptr = lib().ia_oracle_index_build(db_ptr, N, _d(V), self.P)
+        self.D = rows.shape[1]
+        self.ptr = lib().ia_oracle_index_build2(db_ptr, N, self.D, _d(V), self.P)
         if not self.ptr:
             raise MemoryError('oracle index allocation failed')
 

@@ -21,7 +21,14 @@ exact brute-force matcher, algorithms.py:73-75 restated):
                   against it in tests/test_oracle.py and against c4_queries.npz), which
                   makes the run minutes instead of a day.
 
-Usage:  python tests/golden/make_config_fixtures.py c3|c4|c4levels|c4full|c5 [threads]
+  c1rgb_oracle.npz  3-channel matching (convert=False, the reference's default: num_ch = 3,
+                  165-dim rows) at the c1 size (180 x 117 colour A = A' blur, B; kappa 0.5):
+                  every level in full (colour_workload: the pyramids are the oracle's per
+                  channel, skimage multichannel semantics).
+  c3rgb_oracle.npz  the same at the c3 size (362 x 638 colour, kappa 25, 5-level cap), every
+                  level below the finest.
+
+Usage:  python tests/golden/make_config_fixtures.py c3|c4|c4levels|c4full|c5|c1rgb|c3rgb [threads]
 The inputs are rebuilt from bench.py's workload definitions, so the GPU tests regenerate
 them identically on the box.
 """
@@ -83,6 +90,47 @@ def make_c4full():
     full_run('c4', 'c4_full.npz', indexed=True)
 
 
+COLOUR = {   # name: (A = B shape, kappa, level cap, seed)
+    'c1rgb': ((180, 117), 0.5, None, 7),
+    'c3rgb': ((362, 638), 25.0, 5, 10),
+}
+
+
+def colour_workload(name):
+    """3-channel inputs of a colour config: smooth colour noise A (channel ch seeded
+    seed + 17 ch), A' = gaussian_filter(A, 1.5) per channel, B (seed + 1), the oracle's
+    per-channel pyramids, B' init RandomState(seed + 2).  Returns (A_pyr, [Ap_pyr], B_pyr,
+    Bp_pyr, L, kappa)."""
+    from scipy.ndimage import gaussian_filter
+    import bench
+    shape, k, cap, seed = COLOUR[name]
+    A = np.dstack([bench.smooth_noise(seed + 17 * ch, shape) for ch in range(3)])
+    Ap = np.dstack([gaussian_filter(A[..., ch], 1.5) for ch in range(3)])
+    B = np.dstack([bench.smooth_noise(seed + 1 + 17 * ch, shape) for ch in range(3)])
+
+    def pyr3(img):
+        chans = [o.compute_gaussian_pyramid(img[..., ch], 3, cap) for ch in range(3)]
+        return [np.dstack([c[l] for c in chans]) for l in range(len(chans[0]))]
+    A_pyr, Ap_pyr, B_pyr = pyr3(A), pyr3(Ap), pyr3(B)
+    L = min(len(A_pyr), len(B_pyr))
+    return A_pyr, [Ap_pyr], B_pyr, o.initialize_Bp(B_pyr, True, seed + 2), L, k
+
+
+def colour_run(name, skip_finest=False):
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L, k = colour_workload(name)
+    w = o.compute_weights(3, 5, 12, 3)
+    levels = range(1, L - 1) if skip_finest else None
+    t0 = time.time()
+    out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w, levels=levels, indexed=True)
+    print('%s oracle: %d levels in %.1f s' % (name, len(out), time.time() - t0))
+    rec = {'max_levels': np.int32(L)}
+    for l, (bp, s, im) in out.items():
+        rec['s%d' % l] = s.astype(np.int16)
+        rec['im%d' % l] = im.astype(np.uint8)
+        rec['bp_sha%d' % l] = np.array(bp_hash(bp))
+    np.savez_compressed(os.path.join(HERE, name + '_oracle.npz'), **rec)
+
+
 def make_c5():
     full_run('c5', 'c5_job.npz', job_seed=1000)
 
@@ -113,4 +161,5 @@ if __name__ == '__main__':
     if len(sys.argv) > 2:
         oc.set_threads(int(sys.argv[2]))
     {'c3': make_c3, 'c4': make_c4, 'c4levels': make_c4levels, 'c4full': make_c4full,
-     'c5': make_c5}[sys.argv[1]]()
+     'c5': make_c5, 'c1rgb': lambda: colour_run('c1rgb'),
+     'c3rgb': lambda: colour_run('c3rgb')}[sys.argv[1]]()

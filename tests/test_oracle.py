@@ -187,6 +187,39 @@ def test_c_oracle_equals_numpy_oracle(case):
             assert np.array_equal(a, b), l
 
 
+def _colour_inputs(seed, A_shape, B_shape, n_ap):
+    """3-channel analogy pyramids (per-channel, skimage multichannel semantics)."""
+    from scipy.ndimage import gaussian_filter
+    from conftest import smooth_noise
+    A = np.dstack([smooth_noise(seed + 17 * ch, A_shape) for ch in range(3)])
+    Aps = [np.dstack([gaussian_filter(A[..., ch], 1.0 + 0.5 * i) for ch in range(3)]) for i in range(n_ap)]
+    B = np.dstack([smooth_noise(seed + 1 + 17 * ch, B_shape) for ch in range(3)])
+
+    def pyr3(img):
+        chans = [o.compute_gaussian_pyramid(img[..., ch], 3) for ch in range(3)]
+        return [np.dstack([c[l] for c in chans]) for l in range(len(chans[0]))]
+    A_pyr, B_pyr = pyr3(A), pyr3(B)
+    Ap_list = [pyr3(x) for x in Aps]
+    L = min(len(A_pyr), len(B_pyr))
+    return A_pyr, Ap_list, B_pyr, o.initialize_Bp(B_pyr, True, seed + 2), L
+
+
+@pytest.mark.parametrize('seed,A,B,n_ap,k', [(11, (30, 40), (20, 26), 1, 0.5), (12, (24, 22), (18, 20), 2, 25.0)])
+def test_c_oracle_colour_equals_numpy_oracle(seed, A, B, n_ap, k):
+    """The C oracle's 3-channel form (num_ch = 3, config.py:29-42: 165-dim rows, every
+    channel of B' updated) equals the numpy oracle end to end, with the scan and with the
+    projection index."""
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = _colour_inputs(seed, A, B, n_ap)
+    w = o.compute_weights(3, 5, 12, 3)
+    r1 = o.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, k)
+    for indexed in (False, True):
+        r2 = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, k, w, indexed=indexed)
+        assert set(r1) == set(r2) == set(range(1, L))
+        for l in r1:
+            for a, b in zip(r1[l], r2[l]):
+                assert np.array_equal(a, b), (l, indexed)
+
+
 # ---- LSH restatement (SURVEY §8(f)1; this build's definition, no reference code) -------
 
 def test_lsh_keys_kat():
