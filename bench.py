@@ -53,8 +53,9 @@ HBM_PEAK_GBS = 8000.0
 # MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process).
 # The file records a hash of the screen's sources; a file from other sources is stale and
 # the bench then reports traffic null.
-SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r04_screen_traffic_bench_pmc.json')
-SCREEN_SRCS = ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h')
+SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r05_screen_traffic_bench_pmc.json')
+SCREEN_SRCS = ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h', 'ia_screen16r.hip',
+               'ia_rot16.h')
 
 
 def screen_src_sha1():
@@ -74,7 +75,7 @@ def screen_pmc():
     return {'bytes': d['traffic_bytes'], 'kernel': d['kernel'], 'dispatches': d['dispatches'],
             'source': os.path.relpath(SCREEN_PMC_FILE, ROOT)}
 
-SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r04_screen_sq_pmc.json')
+SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r05_screen_sq_pmc.json')
 
 
 def screen_sq():
@@ -662,7 +663,7 @@ def main():
     # 3 products per feature, 330
     rot_used = (_ia.db_rot_enabled() and lsh is None and jobs[0].A.shape[1] % 128 == 0 and
                 _ia.db_image_enabled() and (comm is None or _ia.exchange_kind() == 'peer'))
-    pipe_per_pair = 2 * 80 if rot_used else 3 * 2 * 55
+    pipe_per_pair = 2 * _ia.lib().ia_db_rot_slots() if rot_used else 3 * 2 * 55
     inst = {}
     lv = {}
     for p in prof:
@@ -706,7 +707,7 @@ def main():
                                                                  i_q / max(i_n, 1)),
             'pipe_frac': achieved * pipe_per_pair / per_pair / F16_MFMA_PEAK_TFLOPS,
             'pipe_note': ('f16 MFMA pipe utilisation: the rotated split screen (R16) issues %d f16 '
-                          'flop per pair (5 MFMAs x 16 K-slots x 2), so frac <= pipe_frac x 110 / 160'
+                          'flop per pair (16 K-slots per MFMA x 2), so frac <= pipe_frac x 110 / that'
                           if rot_used else
                           'f16 MFMA pipe utilisation: the split issues %d f16 flop per pair '
                           '(3 products x 2 x 55), so frac <= pipe_frac / 3') % pipe_per_pair,

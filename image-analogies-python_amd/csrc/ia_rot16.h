@@ -36,9 +36,15 @@
 
 namespace ia {
 
-constexpr int R16_P = 11;                      // components with cross terms
-constexpr int R16_MFMA = 5;                    // MFMAs per 32x32 tile
-constexpr int R16_SLOTS = 16 * R16_MFMA;       // 80
+#ifndef IA_R16_P
+#define IA_R16_P 3
+#endif
+constexpr int R16_P = IA_R16_P;                // components with cross terms
+constexpr int R16_NL = 2 * R16_P;              // slot of the norm's lo part (after the cross terms)
+constexpr int R16_M0 = R16_NL + 1;             // slot of main term 0
+constexpr int R16_NH = R16_M0 + IA_D;          // slot of the norm's hi part (last used slot)
+constexpr int R16_SLOTS = (R16_NH + 16) / 16 * 16;   // 80 (P = 11) / 64 (P = 3)
+constexpr int R16_MFMA = R16_SLOTS / 16;       // MFMAs per 32x32 tile
 constexpr int R16_TILE_H8 = R16_MFMA * 64;     // half8 per 32-row tile (5 KiB)
 constexpr int R16_ROW_B = R16_SLOTS * 2;       // 160 B per row
 constexpr int R16_LD = 56;                     // rot[k * R16_LD + j] = V[k][j] (fp32)
@@ -110,17 +116,17 @@ __device__ __forceinline__ double r16_write_query(_Float16 *row, int lane, doubl
     if (lane < IA_D) {
         _Float16 h, l;
         split16d(ldexp(-2.0 * kap, eq), h, l);
-        row[r16_qpos(23 + lane)] = h;
+        row[r16_qpos(R16_M0 + lane)] = h;
         if (lane < R16_P) {
             row[r16_qpos(2 * lane)] = h;
             row[r16_qpos(2 * lane + 1)] = l;
         }
     } else if (lane == IA_D) {
         const _Float16 n = (_Float16)ldexpf(1.f, eq + sc.R);
-        row[r16_qpos(22)] = n;
-        row[r16_qpos(78)] = n;
-    } else if (lane == IA_D + 1) {
-        row[r16_qpos(79)] = (_Float16)0.f;
+        row[r16_qpos(R16_NL)] = n;
+        row[r16_qpos(R16_NH)] = n;
+    } else if (lane > IA_D && R16_NH + (lane - IA_D) < R16_SLOTS) {
+        row[r16_qpos(R16_NH + (lane - IA_D))] = (_Float16)0.f;   // the zero slots
     }
     return s2;
 }

@@ -7,11 +7,11 @@
 //
 // The screen's structure is the row form's of ia_screen16.hip (k_screen16): queries are the
 // stationary MFMA B operand (5 half8 per query tile and lane); the DB streams through LDS in
-// 4-tile stages (20 KiB, global_load_lds_dwordx4, non-temporal, double-buffered, one barrier
-// per stage) and every byte fetched feeds the block's 4 waves; the stage's 4G (query tile,
-// stage tile) chains are cut into 4 equal runs (chain balance), each chain's 5 MFMAs run
-// back to back into one of two ping-pong accumulators and its running-minimum fold is issued
-// after the next chain's first MFMA; minima staged in LDS per chunk, written once.
+// 4-tile stages (20 KiB, global_load_lds_dwordx4, non-temporal, a ring of 3 buffers, one
+// barrier per stage) and every byte fetched feeds the block's 4 waves; the stage's 4G (query
+// tile, stage tile) chains are cut into 4 equal runs (chain balance), each chain's 5 MFMAs
+// run back to back into one of two ping-pong accumulators and its running-minimum fold is
+// issued after the next chain's first MFMA; minima staged in LDS 8 segments at a time.
 #include "ia_internal.h"
 #include "ia_rot16.h"
 
@@ -26,6 +26,18 @@ constexpr int STAGE_TILES = 4;
 constexpr int STAGE_H8 = STAGE_TILES * R16_TILE_H8;   // 20 KiB
 constexpr int MAX_G = 11;
 constexpr int SPC_MAX = 16;
+constexpr int R16_RING = 3;      // stage buffers (r16_body)
+// A/B builds only (tools/build_variant.sh -DIA_R16_LAB=n): 1 no DB loads after the ring's
+// first stages (the compute floor), 2 one MFMA per chain (the streaming floor)
+#ifndef IA_R16_LAB
+#define IA_R16_LAB 0
+#endif
+// the stage's instruction order: 1 pins each chain as MFMA, 2 VALU of the previous chain's
+// fold, MFMA, ... (sched_group_barrier), 0 leaves it to the compiler
+#ifndef IA_R16_PIN
+#define IA_R16_PIN 1
+#endif
+constexpr int SPC_STAGE = 8;     // segments of minima staged in LDS at a time
 
 // chain balance (as ia_screen16.hip): the 4G chains of a stage in the order 4t + u cut into
 // 4 equal runs of G, one per wave
@@ -103,12 +115,40 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
             for (int m = 0; m < R16_MFMA; ++m) a[ab ^ 1][m] = p[m * 64];
         }
         acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
-        if constexpr (c > 0) fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
+        if constexpr (c > 0) {
+            if constexpr (IA_R16_LAB == 3) mn[ch_k<G, W>(c - 1)] = fminf(mn[ch_k<G, W>(c - 1)], acc[cb ^ 1][0]);
+            else fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
+        }
 #pragma unroll
-        for (int m = 1; m < R16_MFMA; ++m)
+        for (int m = 1; m < (IA_R16_LAB == 2 ? 1 : R16_MFMA); ++m)
             acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][m], bq[k][m], acc[cb], 0, 0, 0);
+        if constexpr (IA_R16_PIN && IA_R16_LAB <= 1) {
+            // [the next tile's 5 operand reads,] MFMA 0, then the previous chain's fold two
+            // VALU at a time between the remaining MFMAs
+            if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c))
+                __builtin_amdgcn_sched_group_barrier(0x100, R16_MFMA, 0);   // DS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
+            if constexpr (c > 0) {
+                sfor<0, R16_MFMA - 1>([&](auto) {
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);      // VALU
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      // MFMA
+                });
+            } else {
+                __builtin_amdgcn_sched_group_barrier(0x008, R16_MFMA - 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
     });
     fold_min(acc[(NC - 1) & 1], mn[ch_k<G, W>(NC - 1)]);
+}
+
+// LDS integer min as inline asm: the compiler's waitcnt pass treats an LDS atomic as a store
+// that may alias the DB stages' LDS-DMA destination and drains every stage in flight before
+// it (s_waitcnt vmcnt(0) at each segment close); smin and the stage ring never overlap
+__device__ __forceinline__ void lds_min_i32(int *p, int v) {
+    typedef __attribute__((address_space(3))) int lds_int;
+    const unsigned a = (unsigned)(unsigned long)(lds_int *)p;
+    asm volatile("ds_min_i32 %0, %1" :: "v"(a), "v"(v) : "memory");
 }
 
 template <int G, int W, int NS>
@@ -116,26 +156,37 @@ __device__ __forceinline__ void r16_close(int s, int tps, int *smin, float (&mn)
     constexpr int T0 = bal_t0(G, W);
     const int done = (s + 1) * STAGE_TILES;
     if (done % tps == 0) {
-        int *sm = smin + (done / tps - 1) * (G * 32);
+        int *sm = smin + ((done / tps - 1) % SPC_STAGE) * (G * 32);
         const int j = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
             const float m = fminf(mn[k], __shfl_xor(mn[k], 32));
-            if (h == 0) atomicMin(&sm[(T0 + k) * 32 + j], fkey(m));
+            if (h == 0) lds_min_i32(&sm[(T0 + k) * 32 + j], fkey(m));
             mn[k] = FLT_MAX;
         }
     }
 }
 
-__device__ __forceinline__ void copies_barrier() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+// a workgroup barrier that orders LDS only: __syncthreads()'s release fence would also wait
+// for every DB stage in flight (s_waitcnt vmcnt(0)), i.e. collapse the ring to one stage.
+// The caller has waited for the DMA stages the others must see (vmcnt) before it.
+__device__ __forceinline__ void stage_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
+
+// The DB stream needs ~60 KB in flight per CU to keep the MFMA pipe fed at HBM latency
+// (11.6 B per cycle and CU at full rate), so stages land in a ring of R16_RING buffers,
+// R16_RING - 1 stages ahead (2 blocks per CU: 80 KB in flight), and the chunk's segment
+// minima are staged for SPC_STAGE segments at a time (flushed to segmin as soon as they
+// close) to leave the LDS for the ring.
 
 template <int G, int W>
 __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
                                          const StageMap &sm, long chunk, int nstage, int tps,
-                                         const half8 *__restrict__ q16) {
+                                         const half8 *__restrict__ q16, float *__restrict__ segmin,
+                                         long seg0, long nseg, int q0, int M) {
     constexpr int NS = bal_ns(G, W);
     constexpr int T0 = bal_t0(G, W);
     const int tid = threadIdx.x;
@@ -151,9 +202,9 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
         }
     }
     // one stage = 4 consecutive tiles (5 KiB each): 20 wave-instructions of 1 KiB, 5 per wave
-    auto issue = [&](int s, int buf) {
+    auto issue = [&](int s) {
         const half8 *src = db16 + (stage_lrow(sm, chunk, s) >> 5) * R16_TILE_H8 + W * 64 + lane;
-        half8 *dst = sbuf + buf * STAGE_H8 + W * 64;
+        half8 *dst = sbuf + (s % R16_RING) * STAGE_H8 + W * 64;
 #pragma unroll
         for (int k = 0; k < R16_MFMA; ++k)
             __builtin_amdgcn_global_load_lds((const void *)(src + k * 256), (void *)(dst + k * 256), 16, 0, 2);
@@ -161,13 +212,37 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
     float mn[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) mn[k] = FLT_MAX;
-    issue(0, 0);
-    copies_barrier();
+    const int spc = nstage * STAGE_TILES / tps;
+#pragma unroll
+    for (int s = 0; s < R16_RING - 1; ++s)
+        if (s < nstage) issue(s);
+    // stage 0 landed (the later stages' loads may stay in flight)
+    if (nstage > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(R16_MFMA * (R16_RING - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stage_barrier();
     for (int s = 0; s < nstage; ++s) {
-        if (s + 1 < nstage) issue(s + 1, (s + 1) & 1);
-        r16_stage<G, W, NS>(sbuf + (s & 1) * STAGE_H8, bq, mn, lane);
+        const bool more = s + R16_RING - 1 < nstage && IA_R16_LAB != 1;
+        if (more) issue(s + R16_RING - 1);   // into the buffer stage s - 1 used (consumed)
+        r16_stage<G, W, NS>(sbuf + (s % R16_RING) * STAGE_H8, bq, mn, lane);
         r16_close<G, W, NS>(s, tps, smin, mn, lane);
-        copies_barrier();   // stage s + 1 landed, stage s free again
+        const int done = (s + 1) * STAGE_TILES;
+        if (done % tps == 0) {
+            const int sg = done / tps - 1;            // the segment this stage closed
+            if (sg % SPC_STAGE == SPC_STAGE - 1 || sg == spc - 1) {
+                stage_barrier();                      // every wave's minima of these segments
+                const int base = sg - sg % SPC_STAGE, n = sg - base + 1;
+                for (int i = tid; i < G * 32 * n; i += 256) {
+                    const int ql = i / n, k = i - ql * n;
+                    int *e = &smin[k * (G * 32) + ql];
+                    if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + base + k] = fkey_inv(*e);
+                    *e = 0x7fffffff;                  // this thread's entries only: no barrier
+                }
+            }
+        }
+        // stage s + 1 landed: the R16_RING - 2 stages issued after it may stay in flight
+        if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(R16_MFMA * (R16_RING - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stage_barrier();   // (every wave's reads of stage s done: its buffer is refilled next)
     }
 }
 
@@ -179,8 +254,8 @@ __global__ __launch_bounds__(256, 2) void k_screen16r(const half8 *__restrict__ 
                                                       const half8 *__restrict__ q16, int M, int groups,
                                                       float *__restrict__ segmin, long nseg,
                                                       const XJob *jobs, int parity) {
-    __shared__ half8 sbuf[2 * STAGE_H8];
-    __shared__ int smin[SPC_MAX * G * 32];
+    __shared__ half8 sbuf[R16_RING * STAGE_H8];
+    __shared__ int smin[SPC_STAGE * G * 32];
     if (jobs) {
         const XJob &J = jobs[blockIdx.y];
         db16 = reinterpret_cast<const half8 *>(J.dbr.get());
@@ -193,22 +268,17 @@ __global__ __launch_bounds__(256, 2) void k_screen16r(const half8 *__restrict__ 
     const int group = slot - (slot / groups) * groups;
     if (chunk >= nchunks) return;   // uniform over the block, before any barrier
     const int spc = ch / seg_rows;
-    for (int i = threadIdx.x; i < spc * G * 32; i += 256) smin[i] = 0x7fffffff;
+    for (int i = threadIdx.x; i < SPC_STAGE * G * 32; i += 256) smin[i] = 0x7fffffff;
     const int nstage = ch / (STAGE_TILES * 32);
     const int tps = seg_rows >> 5;
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv == 0) r16_body<G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    else if (wv == 1) r16_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    else if (wv == 2) r16_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    else r16_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg);
-    __syncthreads();
     const long seg0 = (long)chunk * spc;
     const int q0 = group * G * 32;
-    for (int i = threadIdx.x; i < G * 32 * spc; i += 256) {
-        const int ql = i / spc, s = i - ql * spc;
-        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + s] = fkey_inv(smin[s * (G * 32) + ql]);
-    }
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wv == 0) r16_body<G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    else if (wv == 1) r16_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    else if (wv == 2) r16_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    else r16_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
 }
 
 // ---- the level's covariance (ia_db_cov): sampled rows, centred, fp64 -------------------
@@ -318,7 +388,7 @@ __global__ __launch_bounds__(256) void k_db_build_rot(DbSrc src, long row0, long
                 if (j >= R16_P) sk += (double)r32 * (double)r32;
                 _Float16 h, l;
                 split16f(ldexpf(r32, sc.ea), h, l);
-                const int s = 23 + j;
+                const int s = R16_M0 + j;
                 o[((s & 15) >> 3) * R16_MFMA + (s >> 4)][s & 7] = h;
                 if (j < R16_P) {
                     const int s0 = 2 * j, s1 = 2 * j + 1;
@@ -329,9 +399,10 @@ __global__ __launch_bounds__(256) void k_db_build_rot(DbSrc src, long row0, long
         }
         _Float16 nh, nl;
         split16f(ldexpf((float)n2, sc.ea - sc.R), nh, nl);
-        o[((22 & 15) >> 3) * R16_MFMA + (22 >> 4)][22 & 7] = nl;
-        o[((78 & 15) >> 3) * R16_MFMA + (78 >> 4)][78 & 7] = nh;
-        o[((79 & 15) >> 3) * R16_MFMA + (79 >> 4)][79 & 7] = (_Float16)0.f;
+        o[((R16_NL & 15) >> 3) * R16_MFMA + (R16_NL >> 4)][R16_NL & 7] = nl;
+        o[((R16_NH & 15) >> 3) * R16_MFMA + (R16_NH >> 4)][R16_NH & 7] = nh;
+#pragma unroll
+        for (int z = R16_NH + 1; z < R16_SLOTS; ++z) o[((z & 15) >> 3) * R16_MFMA + (z >> 4)][z & 7] = (_Float16)0.f;
         half8 *t = dbr + (p >> 5) * R16_TILE_H8 + (p & 31);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -437,6 +508,9 @@ int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows) {
     if (!xstrip_applies(d)) return 0;
     return db_stage_map(row0, nrows, src->Aw, src->Ah).W > 0 ? 1 : 0;
 }
+
+int ia_db_rot_components(void) { return R16_P; }
+int ia_db_rot_slots(void) { return R16_SLOTS; }
 
 size_t ia_db_rot_bytes(long nrows) { return nrows > 0 ? (size_t)db_rows_padded(nrows) * R16_ROW_B : 0; }
 

@@ -180,6 +180,9 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
  * norm of components 11..54; zero it first).  ia_db_rot_applies: 1 where the synthesis
  * uses it (strip-order levels of the fused per-wave kernel). */
 int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows);
+/* the build's R16 form: components carried as split pairs (P), K-slots per row (16 per MFMA) */
+int ia_db_rot_components(void);
+int ia_db_rot_slots(void);
 size_t ia_db_rot_bytes(long nrows);
 size_t ia_db_cov_bytes(void);
 int ia_db_cov(const IaSrcLevel *src, long row0, long nrows, const double *center, double *cov,

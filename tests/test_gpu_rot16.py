@@ -16,7 +16,6 @@ from test_gpu_split16 import U32, Q16_HALVES, _scales, _segment_order, dev
 
 pytestmark = pytest.mark.gpu
 
-R16_P = 11
 
 
 def _level(seed, shape, cap, scale=1.0):
@@ -44,6 +43,7 @@ def _r16_vs_fp64(idx, As, Q, Ms):
     seg = min(lib.ia_db_chunk_rows(N), 512)
     nseg = npad // seg
     order = _segment_order(idx, N, npad, seg)
+    R16_P = lib.ia_db_rot_components()
     amax, askip = (float(x) for x in idx.amax.cpu().numpy())
     c = idx.center.cpu().numpy()
     a = As - c

@@ -84,8 +84,8 @@ pmc)
         || { tail -20 gpurun_out/$tag.log; exit 1; }
     python3 tools/pmc_summary.py gpurun_out/$tag/run_counter_collection.csv > gpurun_out/$tag/summary.txt
     [ "$KEEP_CSV" = 1 ] || rm -f gpurun_out/$tag/run_counter_collection.csv
-    grep -A12 -E "k_screen16[ip]ILi11E" gpurun_out/$tag/summary.txt | head -40
-    if grep -qE "k_screen16[ip]ILi11E" gpurun_out/$tag/summary.txt && grep -q SQ_VALU_MFMA_BUSY gpurun_out/$tag/summary.txt; then
+    grep -A12 -E "k_screen16[ipr]ILi11E" gpurun_out/$tag/summary.txt | head -40
+    if grep -qE "k_screen16[ipr]ILi11E" gpurun_out/$tag/summary.txt && grep -q SQ_VALU_MFMA_BUSY gpurun_out/$tag/summary.txt; then
         python3 tools/pmc_sq.py gpurun_out/$tag/summary.txt > gpurun_out/sq_$tag.json
     fi ;;
 traffic)

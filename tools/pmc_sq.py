@@ -26,7 +26,7 @@ def parse(path):
 
 def main(path, sub=None):
     b = parse(path)
-    subs = [sub] if sub else ['k_screen16pILi11E', 'k_screen16iILi11E']
+    subs = [sub] if sub else ['k_screen16rILi11E', 'k_screen16pILi11E', 'k_screen16iILi11E']
     name = next(k for s in subs for k in b if s in k)
     d = b[name]
     cyc = d['GRBM_GUI_ACTIVE'] / 8
@@ -34,7 +34,11 @@ def main(path, sub=None):
            'clock_ghz': cyc / (d['us'] * 1e3),
            'mfma_busy': d['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / cyc,
            'wait_inst_share': d['SQ_WAIT_INST_ANY'] / d['SQ_WAVE_CYCLES'],
-           'lds_bank_conflict_share': d['SQ_LDS_BANK_CONFLICT'] / d['SQ_ACTIVE_INST_LDS'],
+           'lds_bank_conflict_share': (d['SQ_LDS_BANK_CONFLICT'] / d['SQ_ACTIVE_INST_LDS']
+                                       if 'SQ_LDS_BANK_CONFLICT' in d else None),
+           'wait_any_share': d['SQ_WAIT_ANY'] / d['SQ_WAVE_CYCLES'] if 'SQ_WAIT_ANY' in d else None,
+           'mfma_coexec': (d['SQ_VALU_MFMA_COEXEC_CYCLES'] / 1024 / cyc
+                           if 'SQ_VALU_MFMA_COEXEC_CYCLES' in d else None),
            'screen_src_sha1': screen_src_sha1(),
            'note': 'one rocprofv3 --pmc pass over bench.py (GRBM_GUI_ACTIVE / 8 = cycles, '
                    'SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs / cycles = MFMA busy)'}

@@ -25,7 +25,7 @@ def screen_src_sha1():
     root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                         'image-analogies-python_amd', 'csrc')
     h = hashlib.sha1()
-    for f in ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h'):
+    for f in ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h', 'ia_screen16r.hip', 'ia_rot16.h'):
         h.update(open(os.path.join(root, f), 'rb').read())
     return h.hexdigest()
 
