@@ -246,3 +246,35 @@ def test_main_convert_false_colour_vs_oracle(gpu, tmp_path):
         assert np.array_equal(out[level]['color'], ref), level
         assert np.array_equal((out[level]['color'] * 255).astype(np.uint8),
                               (ref * 255).astype(np.uint8)), level
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('name', ['c1rgb', 'c3rgb'])
+def test_colour_config_full_size_vs_oracle(gpu, name):
+    """3-channel matching (the reference's default convert=False: num_ch = 3, 165-dim rows)
+    at the BASELINE sizes: c1 (180 x 117, kappa 0.5, every level) and c3 (362 x 638, kappa
+    25, 5-level cap, every level, the finest 231 k pixels against 231 k rows): s, im and the
+    B' hash of every level equal the C oracle's full scanline run
+    (tests/golden/<name>_oracle.npz, make_config_fixtures.py colour_workload)."""
+    import hashlib
+    import os
+    import sys
+    import image_analogies as ia
+    from conftest import ROOT, golden
+    sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+    import make_config_fixtures as mcf
+    g = golden(name + '_oracle.npz')
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L, k = mcf.colour_workload(name)
+    assert L == int(g['max_levels'])
+    w = o.compute_weights(3, 5, 12, 3)
+    Bp_dev = [dev(b) for b in Bp_pyr]
+    out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                            [dev(p) for p in B_pyr], Bp_dev, L, k, w)
+    torch.cuda.synchronize()
+    assert sorted(out) == list(range(1, L))
+    for level in range(1, L):
+        s, im = out[level][0], out[level][1]
+        assert np.array_equal(s.cpu().numpy(), g['s%d' % level].astype(np.int32)), level
+        assert np.array_equal(im.cpu().numpy(), g['im%d' % level].astype(np.int32)), level
+        bp = np.ascontiguousarray(Bp_dev[level].cpu().numpy(), dtype=np.float64)
+        assert hashlib.sha256(bp.tobytes()).hexdigest() == str(g['bp_sha%d' % level]), level
