@@ -3,34 +3,34 @@
 // The split-f16 screen of ia_split16.h carries every one of the 56 products a'_k q'_k as
 // three f16 products (a_h q_h + a_h q_l + a_l q_h): 11 v_mfma_f32_32x32x16_f16 per 32x32
 // tile, 7 of them for the cross terms, which are ~2^-11 of the main terms.  Neighbourhood
-// features of images are strongly correlated (c4's finest database: the top 11 principal
-// directions hold 98.8 % of the centred rows' energy), so in a rotated basis most
-// components are small, and dropping their cross terms costs little:
+// features of images are strongly correlated (c4's finest database: the top 3 principal
+// directions hold 92.8 % of the centred rows' energy, the top 11 98.8 %), so in a rotated
+// basis most components are small, and dropping their cross terms costs little:
 //
 //   rho = V^T a',  kappa = V^T q'   (V: 55 x 55, columns = principal directions of the
 //                                    level's centred rows, fp32 entries, fp64 arithmetic)
 //   a'.q' ~= rho . kappa            (V V^T = I up to its fp32 rounding: a bound term)
 //
 // The screen value e = |a'|^2 - 2 rho.kappa is then carried as
-//   * the top R16_P = 11 components: split pairs, three products each (as ia_split16.h);
-//   * the other 44: f16 hi parts only, one product each (error <= 2^-10 |rho_k kappa_k|,
+//   * the top R16_P components (IA_R16_P, default 3): split pairs, three products each;
+//   * the other 55 - P: f16 hi parts only, one product each (error <= 2^-10 |rho_k kappa_k|,
 //     summed by Cauchy-Schwarz into 2^-9 A_skip |q'_skip|, A_skip = max over rows of the
 //     skipped components' norm, |q'_skip| the query's; both exact inputs of the bound);
 //   * |a'|^2 (original coordinates): split pair times 2^R, as before.
-// 22 + 1 + 55 + 1 = 79 of 80 K-slots: 5 MFMAs per tile.  Slot order (the accumulation
-// bound of §4d: the small terms first, the norm in the last MFMA):
-//   slot   0..21   cross terms of component i = s/2:  DB a_l[i] | a_h[i]   query q_h[i] | q_l[i]
-//   slot   22      DB norm_l                          query sq 2^R
-//   slot   23..77  DB a_h[s-23]                       query q_h[s-23]
-//   slot   78      DB norm_h                          query sq 2^R
-//   slot   79      0                                  0
+// 2P + 1 + 55 + 1 slots rounded up to 16: P = 3 -> 64 slots = 4 MFMAs, 128 B per row (P = 11:
+// 80 = 5 MFMAs).  Slot order (the accumulation bound of DESIGN.md §4d: the small terms first,
+// the norm in the last MFMA):
+//   slot   0 .. 2P-1   cross terms of component i = s/2:  DB a_l[i] | a_h[i]   query q_h[i] | q_l[i]
+//   slot   R16_NL      DB norm_l                          query sq 2^R
+//   slot   R16_M0 + k  DB a_h[k] (k < 55)                 query q_h[k]
+//   slot   R16_NH      DB norm_h                          query sq 2^R
+//   the rest           0                                  0
 // Scales exactly as ia_split16.h (split16_db_scale / split16_q_scale): the screen minima
 // are in the same units sa sq e, so the exact stage (k_xstrip) only widens its bound.
 //
 // Layouts.  MFMA m covers slots 16m .. 16m + 15; lane half h supplies slots 16m + 8h ..+7.
-//   DB: per 32-row tile, 5 groups x 64 lanes x half8 (5 KiB): group m, lane (h * 32 + row).
-//       160 B per row (the row form streams 4.19 M rows of c4's finest level in 671 MB).
-//   query: a q16 row (Q16_ROW = 16 half8), half8 index h * 5 + m (10 used).
+//   DB: per 32-row tile, R16_MFMA groups x 64 lanes x half8: group m, lane (h * 32 + row).
+//   query: a q16 row (Q16_ROW = 16 half8), half8 index h * R16_MFMA + m.
 #pragma once
 #include "ia_split16.h"
 
@@ -45,8 +45,8 @@ constexpr int R16_M0 = R16_NL + 1;             // slot of main term 0
 constexpr int R16_NH = R16_M0 + IA_D;          // slot of the norm's hi part (last used slot)
 constexpr int R16_SLOTS = (R16_NH + 16) / 16 * 16;   // 80 (P = 11) / 64 (P = 3)
 constexpr int R16_MFMA = R16_SLOTS / 16;       // MFMAs per 32x32 tile
-constexpr int R16_TILE_H8 = R16_MFMA * 64;     // half8 per 32-row tile (5 KiB)
-constexpr int R16_ROW_B = R16_SLOTS * 2;       // 160 B per row
+constexpr int R16_TILE_H8 = R16_MFMA * 64;     // half8 per 32-row tile (4 KiB at P = 3)
+constexpr int R16_ROW_B = R16_SLOTS * 2;       // 128 B per row at P = 3
 constexpr int R16_LD = 56;                     // rot[k * R16_LD + j] = V[k][j] (fp32)
 // the rotation buffer: 56 x 56 floats, padded to whole 1 KiB LDS-DMA pieces (13)
 constexpr int R16_ROT_FLOATS = 13 * 256;
@@ -63,7 +63,7 @@ __host__ __device__ constexpr int r16_dgrp(int s, int j) { return (s >> 4) * 64 
 // The bound of DESIGN.md §4d: |s(r) / (sa sq) + |q'|^2 - D(r)| <= eps_R with
 //   eps_R = u (360 A|q'| + 60 A^2) + 2^-9 1.01 A_skip |q'_skip|,  u = 2^-24
 // (representation 14u(2A|q'| + A^2), f16 flush <= u(28.5 A|q'| + 7.1 A^2), accumulation over
-// 5 MFMAs with the main mass in the last four <= 32u(4 Y_dot + Y_norm + 5X) ~ u(256.4 A|q'|
+// <= 5 MFMAs with the main mass in at most four <= 32u(4 Y_dot + Y_norm + 5X) ~ u(256.4 A|q'|
 // + 32.1 A^2), the fp32 rotation's non-orthogonality 2 |V_f V_f^T - I| A|q'| <= 30u A|q'|;
 // the skipped components' dropped cross terms <= (2^-10 + 2^-21) |alpha_skip| |beta_skip|).
 __device__ __forceinline__ double r16_eps(double A, double nqq, double Askip, double nsk) {
