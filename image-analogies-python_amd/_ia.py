@@ -90,6 +90,8 @@ _SIGS = {
     'ia_db_rot_applies': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long]),
     'ia_db_rot_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_db_rot_components': (ctypes.c_int, []),
+    'ia_screen_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    'ia_fused_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'ia_db_rot_slots': (ctypes.c_int, []),
     'ia_db_cov_bytes': (ctypes.c_size_t, []),
     'ia_db_cov': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp, _dp]),

@@ -880,6 +880,13 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
 
 }  // namespace ia
 
+namespace ia {
+int screen16i_attributes(hipFuncAttributes *at) {
+    IA_HIP(hipFuncGetAttributes(at, reinterpret_cast<const void *>(&k_screen16i<11, 0>)));
+    return IA_OK;
+}
+}  // namespace ia
+
 extern "C" int ia_diag_set_screen_sched(int sched) {
     const int prev = ia::screen_sched();
     if (sched >= 0 && sched <= 1) ia::g_screen_sched.store(sched);

@@ -495,6 +495,7 @@ int launch_query_rows_r16(const double *q64, int M, const double *center, const 
 
 int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
                    double *part, hipStream_t st);
+int screen16i_attributes(hipFuncAttributes *at);
 
 }  // namespace ia
 
@@ -507,6 +508,24 @@ int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows) {
     const DbSrc d = make_dbsrc(*src);
     if (!xstrip_applies(d)) return 0;
     return db_stage_map(row0, nrows, src->Aw, src->Ah).W > 0 ? 1 : 0;
+}
+
+/* kernel resources of a sharded level's screen and fused kernel (the forward-progress rule
+ * of DESIGN.md §7): which = 0 the rotated screen's widest instance k_screen16r<11>, 1 the
+ * split-f16 4-wave k_screen16i<11> (the sharded screen without R16); LDS bytes per block and
+ * VGPRs per lane (hipFuncGetAttributes) */
+int ia_screen_resources(int which, int *lds, int *vgprs) {
+    IA_ARG(lds && vgprs && (which == 0 || which == 1), "ia_screen_resources: bad args");
+    hipFuncAttributes at{};
+    if (which == 0) {
+        IA_HIP(hipFuncGetAttributes(&at, reinterpret_cast<const void *>(&k_screen16r<11>)));
+    } else {
+        int rc = screen16i_attributes(&at);
+        if (rc) return rc;
+    }
+    *lds = (int)at.sharedSizeBytes;
+    *vgprs = at.numRegs;
+    return IA_OK;
 }
 
 int ia_db_rot_components(void) { return R16_P; }

@@ -1261,6 +1261,22 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
     xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace, ROT ? rotl : nullptr, ROT ? dq : nullptr);
 }
 
+}  // namespace ia
+
+/* the fused strip kernel's resources (DESIGN.md §7 forward-progress rule): rot 1 the R16
+ * form; LDS bytes per workgroup, VGPRs per lane */
+extern "C" int ia_fused_resources(int rot, int *lds, int *vgprs) {
+    IA_ARG(lds && vgprs, "ia_fused_resources: bad args");
+    hipFuncAttributes at{};
+    if (rot) IA_HIP(hipFuncGetAttributes(&at, reinterpret_cast<const void *>(&ia::k_xstrip<false, true>)));
+    else IA_HIP(hipFuncGetAttributes(&at, reinterpret_cast<const void *>(&ia::k_xstrip<false, false>)));
+    *lds = (int)at.sharedSizeBytes;
+    *vgprs = at.numRegs;
+    return IA_OK;
+}
+
+namespace ia {
+
 int launch_xwave(const XArgs &a, int nblocks, int form, hipStream_t st, int njobs) {
     if (nblocks <= 0) return IA_OK;
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || a.jobs), "launch_xwave: bad batch");

@@ -127,6 +127,57 @@ def synthesize_levels_dev(calls):
     return [c.result() for c in calls]
 
 
+def wave_max_queries(H, W):
+    """Most pixels of one wave of an H x W level (t = x + 3y), + 1 as ia_synth.hip's."""
+    return min(H, (W + 2) // 3) + 1
+
+
+def residency_ok(waiters, fused, screen, cus=256, lds_per_cu=160 * 1024, vgprs_per_simd=512, gran=8):
+    """Forward progress of sharded levels over the device-side exchange.
+    A fused workgroup that waits for other ranks' records holds its CU's LDS and one wave's
+    VGPRs on each SIMD (256 threads) while it waits; the screens that produce those records
+    (another level's, or another rank's on a shared GPU) must still find a CU.  A CU holding
+    j waiting workgroups still fits a screen block (also one wave per SIMD) while
+    j * fused_lds + screen_lds <= lds_per_cu and j * fused_vgprs + screen_vgprs <=
+    vgprs_per_simd (VGPRs in granules of 8).  If fewer than cus * (jmax + 1) workgroups can
+    wait at once, some CU holds at most jmax of them (pigeonhole): a screen block always fits.
+    fused / screen: (LDS bytes per workgroup, VGPRs per lane).  Returns (ok, jmax)."""
+    rnd = lambda v: -(-int(v) // gran) * gran  # noqa: E731
+    j_lds = (lds_per_cu - int(screen[0])) // max(1, int(fused[0]))
+    j_vgpr = (vgprs_per_simd - rnd(screen[1])) // max(1, rnd(fused[1]))
+    jmax = max(-1, min(j_lds, j_vgpr))
+    return waiters < cus * (jmax + 1), jmax
+
+
+def _kernel_resources(rot):
+    lib = _ia.lib()
+    out = []
+    for fn, arg in ((lib.ia_fused_resources, 1 if rot else 0), (lib.ia_screen_resources, 0 if rot else 1)):
+        lds, vg = ctypes.c_int(), ctypes.c_int()
+        _ia.check(fn(arg, ctypes.byref(lds), ctypes.byref(vg)), 'kernel resources')
+        out.append((lds.value, vg.value))
+    return out
+
+
+def sharded_schedule(level_shapes, pipeline, ranks_on_gpu, fused, screen, cus=256):
+    """The pipelining of a run's sharded levels (shapes H x W of their B' levels) that the
+    forward-progress rule (residency_ok) allows: pipeline as asked if every sharded level's
+    waiting workgroups together fit the rule, else one level at a time if one level's do;
+    raises if not even one level fits (e.g. too many ranks sharing one GPU)."""
+    ms = [wave_max_queries(H, W) for H, W in level_shapes]
+    if not ms:
+        return pipeline
+    if pipeline and residency_ok(ranks_on_gpu * sum(ms), fused, screen, cus)[0]:
+        return True
+    ok, jmax = residency_ok(ranks_on_gpu * max(ms), fused, screen, cus)
+    if not ok:
+        raise RuntimeError('sharded synthesis refused: %d waiting workgroups per GPU (%d ranks x %d '
+                           'queries) with at most %d per CU beside a screen block cannot guarantee '
+                           'forward progress (DESIGN.md §7)' % (ranks_on_gpu * max(ms), ranks_on_gpu,
+                                                                 max(ms), jmax))
+    return False
+
+
 def pipeline_default():
     """Levels run pipelined by default (IA_PIPELINE=0: one level at a time)."""
     return os.environ.get('IA_PIPELINE', '1') != '0'
@@ -223,6 +274,12 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         # one exchange cannot serve two levels running at once (their records would share
         # the exchange's box cells): levels one at a time then
         pipeline = False
+    if sharded and comm is not None and _ia.exchange_kind() == 'peer' and torch.cuda.is_available():
+        # fused workgroups that wait for other ranks must leave room for the screens
+        fused, screen = _kernel_resources(_ia.db_rot_enabled() and lsh is None)
+        share = nranks if os.environ.get('IA_SHARE_GPU', '0') == '1' else 1
+        pipeline = sharded_schedule([tuple(B_pyr[l].shape[:2]) for l in sharded], pipeline, share,
+                                    fused, screen, torch.cuda.get_device_properties(0).multi_processor_count)
     out = {}
     t_start = time.time()
     calls = []

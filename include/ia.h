@@ -182,6 +182,12 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
 int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows);
 /* the build's R16 form: components carried as split pairs (P), K-slots per row (16 per MFMA) */
 int ia_db_rot_components(void);
+/* resources (LDS bytes per workgroup, VGPRs per lane) of a sharded level's screen (which 0:
+ * the rotated k_screen16r, 1: k_screen16i) and of the fused strip kernel (rot 1: R16 form)
+ * that waits for other ranks: the forward-progress rule of DESIGN.md §7
+ * (image_analogies.residency_ok) */
+int ia_screen_resources(int which, int *lds, int *vgprs);
+int ia_fused_resources(int rot, int *lds, int *vgprs);
 int ia_db_rot_slots(void);
 size_t ia_db_rot_bytes(long nrows);
 size_t ia_db_cov_bytes(void);

@@ -103,10 +103,13 @@ def test_bench_c4_two_ranks_sharing_the_gpu_equal_one_rank(gpu):
     assert two['config']['exchange'].startswith('peer') and 'exchange_fallback' not in two['checks']
     assert two['checks']['replicas_identical'] is True and two['checks']['bp_equals_ap_at_s'] is True
     assert two['checks']['checksum'] == one['checks']['checksum']
-    for r in two['ranks']:       # each rank explains its exchange
+    assert two['exchange_fallback'] is None
+    for r in two['ranks']:       # each rank explains its exchange and its screen
         assert r['exchanges'] and all(e['kind'] == 'peer' for e in r['exchanges'])
         assert all(e['stress'].startswith('ok') for e in r['exchanges'])
         assert r['checksum'] == one['checks']['checksum'] and r['peer_wait_us_per_pixel'] >= 0
+        assert r['kernel'].startswith('k_screen16') and r['screen_avg_us'] > 0
+        assert 0 < r['frac'] < 1 and r['pipe_frac'] >= r['frac']
 
 
 @pytest.mark.gpu

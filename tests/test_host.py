@@ -482,3 +482,30 @@ def test_chunk_target_is_per_thread():
     finally:
         lib.ia_set_chunk_target(prev)
     assert lib.ia_db_chunk_rows(N) == base
+
+
+def test_residency_rule_refuses_the_known_starvation():
+    """The forward-progress rule for sharded levels over the device-side exchange
+    (image_analogies.residency_ok / sharded_schedule): workgroups of the fused
+    kernel that wait for other ranks must leave a CU for the screens.  The configuration
+    that timed out in round 4 (commit 1efae07: the producer / consumer screen, ~94 KB of LDS
+    and 256 VGPRs, beside 2 ranks' waiting k_xstrip workgroups on one GPU) is refused; the
+    production c4 layout (one rank per GPU, the finest and the 1 M-row level sharded and
+    pipelined, the rotated screen) pipelines; 2 ranks sharing a GPU serialize the sharded
+    levels; 3 are refused."""
+    import image_analogies as ia
+    c4 = [(1024, 1024), (512, 512)]
+    fused_r16, screen_r16 = (36864, 135), (60416, 158)
+    fused_r4, screen_pc = (36864, 148), (96 * 1024, 256)
+    ok, j = ia.residency_ok(2 * ia.wave_max_queries(1024, 1024), fused_r4, screen_pc)
+    assert not ok and j == 1
+    with pytest.raises(RuntimeError, match='forward progress'):
+        ia.sharded_schedule(c4, True, 2, fused_r4, screen_pc)
+    assert ia.sharded_schedule(c4, True, 1, fused_r16, screen_r16) is True
+    assert ia.sharded_schedule(c4, True, 2, fused_r16, screen_r16) is False
+    with pytest.raises(RuntimeError, match='forward progress'):
+        ia.sharded_schedule(c4, True, 3, fused_r16, screen_r16)
+    # the pigeonhole bound itself: cus * (jmax + 1) waiting workgroups can fill every CU
+    ok, j = ia.residency_ok(256 * 3 - 1, fused_r16, screen_r16)
+    assert ok and j == 2
+    assert not ia.residency_ok(256 * 3, fused_r16, screen_r16)[0]
