@@ -97,7 +97,7 @@ def _screen_vs_fp64(idx, As, Q, Ms):
     nseg = npad // seg
     order = _segment_order(idx, N, npad, seg)      # rows of segment s: order[s * seg:(s + 1) * seg]
     segmin = torch.empty((qrows, nseg), dtype=torch.float32, device='cuda')
-    amax = float(idx.amax.item())
+    amax = float(idx.amax[0].item())
     c = idx.center.cpu().numpy()
     a = As - c
     na = np.einsum('ij,ij->i', a, a)
@@ -206,7 +206,7 @@ def test_db_build_tiled_equals_per_row(gpu, shape, n_ap, shards):
                 idx = algorithms.level_index(A_pyr, Ap_pyr, L, lambda l, n: (r0, r1 - r0),
                                              rows=True)
                 torch.cuda.synchronize()
-                got.append((idx.db.cpu().numpy().copy(), float(idx.amax.item())))
+                got.append((idx.db.cpu().numpy().copy(), float(idx.amax[0].item())))
             finally:
                 _ia.db_build_form(prev)
         assert got[0][1] == got[1][1], (r0, r1)
@@ -314,7 +314,7 @@ def test_image_form_alone_equals_image_form_from_rows(gpu):
                                     None, _ia.ptr(amax), _ia.ptr(z_alone), _ia.stream()),
               'ia_db_build_image')
     torch.cuda.synchronize()
-    assert float(alone.amax.item()) == float(both.amax.item()) == float(amax.item())
+    assert float(alone.amax[0].item()) == float(both.amax[0].item()) == float(amax.item())
     assert torch.equal(z_alone[:n], z_rows[:n])         # all but the build's scratch
     As = o.create_index(A_pyr, Ap_pyr, L)[L - 1]
     rs = np.random.RandomState(5)
