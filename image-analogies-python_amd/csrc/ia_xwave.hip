@@ -285,8 +285,11 @@ __device__ __forceinline__ void xw_next_query(const XArgs &a, int i, int y, int 
 // BATCH: a0.jobs holds a batch's pointers; the block copies the launch arguments into LDS
 // once and overrides them with its job's (a private copy of the arguments would live in
 // scratch memory), then reads them from there
+#ifndef IA_XWAVE_OCC
+#define IA_XWAVE_OCC 2   // workgroups per CU k_xwave is built for (3: 168 VGPRs and 240-448 B of spills, c1 +8 %, c3 +11 %)
+#endif
 template <bool IMG, bool BATCH>
-__global__ __launch_bounds__(256, 3) void k_xwave(XArgs a0) {
+__global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
     __shared__ __attribute__((aligned(16))) char sa_raw[BATCH ? sizeof(XArgs) : 16];
     XArgs &sa = *reinterpret_cast<XArgs *>(sa_raw);
     if constexpr (BATCH) {

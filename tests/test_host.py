@@ -419,11 +419,21 @@ def test_hot_kernels_do_not_spill():
     res = glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'image-analogies-python_amd', 'csrc', '_build', '*.res'))
     if not res:
         pytest.skip('no resource reports (build with make -C image-analogies-python_amd/csrc)')
+    import hashlib
     hot = ('k_screen16', 'k_xstrip', 'k_pyr_wave', 'k_db_build_t', 'k_rgb_to_yiq', 'k_img_pad')
-    seen, bad = 0, []
+    # k_xwave (the fused kernel of non-strip levels: c1-c3) has no VGPR spill; its 96 B of
+    # scratch is the by-value argument of the cold row-list overflow path (row_rec, noinline)
+    no_vgpr_spill = ('k_xwave',)
+    seen, bad, stale = 0, [], []
     for f in res:
+        text = open(f).read()
+        src = os.path.join(os.path.dirname(os.path.dirname(f)), os.path.basename(f)[:-4] + '.hip')
+        m = re.search(r'source-sha1: ([0-9a-f]{40})', text)
+        if not m or hashlib.sha1(open(src, 'rb').read()).hexdigest() != m.group(1):
+            stale.append(os.path.basename(f))
+            continue
         name = None
-        for line in open(f):
+        for line in text.splitlines():
             m = re.search(r'Function Name: (\S+)', line)
             if m:
                 name = m.group(1)
@@ -433,6 +443,13 @@ def test_hot_kernels_do_not_spill():
                 seen += 1
                 if int(m.group(1)) != 0:
                     bad.append((name, int(m.group(1))))
+            m = re.search(r'VGPRs Spill: (\d+)', line)
+            if m and name and any(h in name for h in no_vgpr_spill):
+                seen += 1
+                if int(m.group(1)) != 0:
+                    bad.append((name, 'VGPR spill', int(m.group(1))))
+    if stale:
+        pytest.skip('resource reports older than their sources (rebuild): %s' % stale)
     assert seen > 20, seen
     assert not bad, bad
 
