@@ -761,8 +761,9 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak' if args.config == 'c5' else 'strong',
         'vs_baseline': None,
-        'dtype': ('f16 rotated split (R16 MFMA screen: 11 principal components as f16 pairs, 44 as '
-                  'f16, f32 accumulate) + f64 (rotation, exact rescore, pyramids)' if rot_used else
+        'dtype': ('f16 rotated split (R16 MFMA screen: %d principal components as f16 pairs, %d as '
+                  'f16, f32 accumulate) + f64 (rotation, exact rescore, pyramids)'
+                  % (_ia.lib().ia_db_rot_components(), 55 - _ia.lib().ia_db_rot_components()) if rot_used else
                   'f16x3 split (MFMA screen, f32 accumulate) + f32 (re-screen) + f64 (exact '
                   'rescore, pyramids)'),
         'data': 'synthetic (gaussian-filtered noise; A\' = blur(A)); seeded',

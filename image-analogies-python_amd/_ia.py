@@ -112,6 +112,11 @@ _SIGS = {
                                                    ctypes.c_int]),
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
     'ia_synth_level3': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_synth_levels3': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
+    'ia_db3_rot_bytes': (ctypes.c_size_t, [ctypes.c_long]),
+    'ia_db3_rot_components': (ctypes.c_int, []),
+    'ia_db3_rot_floats': (ctypes.c_int, []),
+    'ia_db3_build_rot': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp, _dp]),
     'ia_synth3_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long]),
     'ia_db3_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_match3_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_long]),
@@ -178,6 +183,8 @@ _SIGS = {
     'ia_diag_peer_trace': (ctypes.c_int, [_dp, _dp]),
     'ia_diag_screen16r': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp,
                                          _dp, _dp, _dp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp]),
+    'ia_diag_db3_askip': (ctypes.c_int, [_dp, ctypes.c_long, _dp]),
+    'ia_diag_screen3r': (ctypes.c_int, [_dp, _dp, _dp, ctypes.c_long, _dp, ctypes.c_int, _dp, _dp, _dp]),
     'ia_diag_synth_level_shards': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs),
                                                   ctypes.POINTER(IaShardDb), ctypes.c_int, _dp]),
 }

@@ -214,6 +214,24 @@ class LevelIndex:
         return torch.cat(rows, 0)
 
 
+def rot3_build(db3, N):
+    """The rotated split DB of the 3-channel screen (R16c) from an ia_db3_build
+    buffer: the covariance of ~64 k sampled rows around their mean (device GEMM), its
+    eigenvectors on the host (165 x 165; any orthonormal basis keeps the matcher exact, the
+    principal one keeps the bound tight), then ia_db3_build_rot.  Returns (rot, dbr)."""
+    lib, st = _ia.lib(), _ia.stream()
+    rows = db3[:N * 168].view(N, 168)[:, :165]
+    X = rows[::max(1, N // 65536)]
+    Xc = X - X.mean(0)
+    w, V = np.linalg.eigh((Xc.T @ Xc).cpu().numpy())
+    R = np.zeros(lib.ia_db3_rot_floats(), dtype=np.float32)
+    R.reshape(165, 168)[:, :165] = V[:, ::-1]
+    rot = torch.as_tensor(R).to(db3.device)
+    dbr = torch.empty(lib.ia_db3_rot_bytes(N), dtype=torch.uint8, device=db3.device)
+    _ia.check(lib.ia_db3_build_rot(_ia.ptr(db3), N, _ia.ptr(rot), _ia.ptr(dbr), st), 'ia_db3_build_rot')
+    return rot, dbr
+
+
 class LevelIndex3:
     """As[level] for 3-channel images (num_ch = 3): the materialised fp64 rows
     [A full | A'_i half], 165 values each (ia_db3_build, which also builds the split-f16
@@ -238,6 +256,12 @@ class LevelIndex3:
         _ia.check(lib.ia_db3_build(ctypes.byref(src), 0, self.N, _ia.ptr(self.db3), _ia.stream()),
                   'ia_db3_build')
         self.lsh = None
+        self.rot = self.dbr = None
+
+    def build_rot(self):
+        """The rotated split DB of the synthesis screen (R16c, rot3_build)."""
+        self.rot, self.dbr = rot3_build(self.db3, self.N)
+        return self
 
     def match(self, Q, exact=None):
         """1-NN rows (global index, fp64 distance) of queries Q (M x 165)."""

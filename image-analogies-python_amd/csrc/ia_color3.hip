@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <vector>
 
 namespace ia {
@@ -147,6 +148,7 @@ constexpr int C16_GRP = 2 * C16_CH;        // half8 groups per lane and tile: (c
 constexpr int C16_TILE = C16_GRP * 64;     // half8 per 32-row (or 32-query) tile
 constexpr int C3_NSLOT = 16 * C16_CH;      // 176
 constexpr int C3_CAND = 64;                // candidate tiles listed per query (more: all)
+constexpr int C3_REG = 8;                  // float4s of tile minima per thread in registers
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // lane (row / query l & 31, half h = l >> 5) of group (chunk c, part p) holds slots
@@ -168,6 +170,9 @@ struct Db3View {                           // the ia_db3_build buffer: fp64 rows
 };
 static inline size_t db3_rows_bytes(long nrows) { return align_up((size_t)nrows * D3P * sizeof(double), 256); }
 __host__ __device__ inline long db3_tiles(long nrows) { return (nrows + 31) / 32; }
+// row stride of the tile minima (M x stride floats): whole float4s, read into registers by
+// the exact stage in one round trip (the pad entries are never written nor read as minima)
+__host__ __device__ constexpr int c3_stride(int ntiles) { return (ntiles + 3) & ~3; }
 static inline size_t db3_split_bytes(long nrows) { return (size_t)db3_tiles(nrows) * C16_TILE * sizeof(half8); }
 static inline Db3View db3_view(void *base, long nrows) {
     char *b = reinterpret_cast<char *>(base);
@@ -344,20 +349,24 @@ __global__ __launch_bounds__(256) void k_qsplit3(const double *__restrict__ q165
 }
 
 // diagnostic: the screen's tile minima in unscaled units (e = s / (sa sq)), eps3 per query
+// (R16c: nsk, rmeta given, eps = r3_eps)
+struct Rot3Meta;
+__device__ double r3_eps_m(const Rot3Meta *rm, double A, double nqq, double nsk);
 __global__ void k_screen3_unscale(const float *__restrict__ smin, int M, int ntiles,
                                   const double *__restrict__ qn, const Col16Meta *__restrict__ meta,
-                                  double *__restrict__ e, double *__restrict__ eps) {
+                                  double *__restrict__ e, double *__restrict__ eps,
+                                  const double *__restrict__ nsk = nullptr, const Rot3Meta *rm = nullptr) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (long)M * ntiles) return;
-    const int m = (int)(i / ntiles);
+    const int m = (int)(i / ntiles), tl = (int)(i - (long)m * ntiles);
     const float amax = __uint_as_float(meta->amax_bits);
     const Split16Db sc = split16_db_scale(amax);
     const int eq = split16_q_scale(qn[m], sc.R);
-    e[i] = ldexp((double)smin[i], -(sc.ea + eq));
+    e[i] = ldexp((double)smin[(long)m * c3_stride(ntiles) + tl], -(sc.ea + eq));
     if (i % ntiles == 0) {
         constexpr double U32 = 5.9604644775390625e-08;
         const double A = (double)amax;
-        eps[m] = U32 * (900.0 * A * sqrt(qn[m]) + 450.0 * A * A);
+        eps[m] = nsk ? r3_eps_m(rm, A, qn[m], nsk[m]) : U32 * (900.0 * A * sqrt(qn[m]) + 450.0 * A * A);
     }
 }
 
@@ -413,7 +422,7 @@ __global__ __launch_bounds__(256, 1) void k_screen3(const half8 *__restrict__ db
             for (int i = 1; i < 16; ++i) mn = fminf(mn, acc[i]);
             mn = fminf(mn, __shfl_xor(mn, 32));
             const int q = (qt0 + j) * 32 + lane;
-            if (lane < 32 && q < M) smin[(long)q * ntiles + t] = mn;
+            if (lane < 32 && q < M) smin[(long)q * c3_stride(ntiles) + t] = mn;
         }
         if (!more) break;
 #pragma unroll
@@ -430,6 +439,261 @@ static inline dim3 screen3_grid(int ntiles, int M, int &tpw) {
     const int QG = ((M + 31) / 32 + S3_QG - 1) / S3_QG;
     tpw = (int)std::max(1L, ((long)ntiles * QG + 4L * 512 - 1) / (4L * 512));
     return dim3((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QG);
+}
+
+// ---- the rotated split screen for 3-channel rows (R16c) -----------------
+// As ia_rot16.h for D = 165: per level the principal directions V (165 x 165, fp32, host
+// eigh of the centred rows' covariance), rows rho = V^T a', queries kappa = V^T q'; the top
+// R3_P components keep f16 split pairs (three products), the other 162 one f16 product, the
+// norm its split pair: 2P cross slots, norm_lo, 165 main slots, norm_hi, zeros -> 176 slots =
+// 11 MFMAs per 32x32 tile (33 in k_screen3), 352 B per row (704).  Same scales and units as
+// §4c; the bound adds the skipped components' dropped cross terms (A_skip, |kappa_skip|).
+constexpr int R3_P = 3;
+constexpr int R3_NL = 2 * R3_P, R3_M0 = R3_NL + 1, R3_NH = R3_M0 + D3;   // 6, 7, 172
+constexpr int R3_SLOTS = (R3_NH + 16) / 16 * 16;                           // 176
+constexpr int R3_MFMA = R3_SLOTS / 16;                                     // 11
+constexpr int R3_TILE = R3_MFMA * 64;                                      // half8 per tile
+constexpr int R3_LD = 168;                                                 // rot[k * R3_LD + j]
+constexpr int R3_ROT_FLOATS = D3 * R3_LD;
+static_assert(R3_MFMA == 11, "R16c: 11 MFMAs per tile at P = 3");
+// half8 index of slot s of tile row (or query column) j, and its element s & 7
+__host__ __device__ constexpr int r3_h8(int s, int j) { return (s >> 4) * 64 + ((s & 15) >> 3) * 32 + j; }
+
+struct Rot3Meta {   // after the rotated tiles: A_skip (fp32 bits, rounded up; atomicMax)
+    unsigned int askip_bits;
+    unsigned int pad[63];
+};
+static inline size_t db3r_tiles_bytes(long nrows) { return align_up((size_t)db3_tiles(nrows) * R3_TILE * sizeof(half8), 256); }
+static inline Rot3Meta *db3r_meta(void *dbr, long nrows) {
+    return reinterpret_cast<Rot3Meta *>(reinterpret_cast<char *>(dbr) + db3r_tiles_bytes(nrows));
+}
+
+// the rotated tiles: one 256-thread block per 32-row tile (rows past nrows repeat the last);
+// V and the tile's centred rows staged in LDS; thread (row r = tid & 31, g = tid >> 5) takes
+// components j = g + 8i in fp64 from the fp32 V; then the split slots through an LDS stage
+// (reusing the rows' space) into the tile layout, and A_skip = max ||fl32(rho_skip)||
+__global__ __launch_bounds__(256, 1) void k_db3_rot(const double *__restrict__ rows, long nrows,
+                                                    const Col16Meta *__restrict__ meta,
+                                                    const float *__restrict__ rot, half8 *__restrict__ dbr,
+                                                    Rot3Meta *__restrict__ rmeta) {
+    __shared__ __attribute__((aligned(16))) float V[R3_ROT_FLOATS];      // 110,880 B
+    __shared__ __attribute__((aligned(16))) double X[32 * D3];          // 42,240 B (odd row stride)
+    __shared__ double skp[32][8];
+    __shared__ double nrm[32];
+    __shared__ float red[4];
+    const int tid = threadIdx.x, r = tid & 31, g = tid >> 5;
+    for (int i = tid; i < R3_ROT_FLOATS / 4; i += 256)
+        reinterpret_cast<float4 *>(V)[i] = reinterpret_cast<const float4 *>(rot)[i];
+    const long t = blockIdx.x;
+    for (int i = tid; i < 32 * D3; i += 256) {
+        const int rr = i / D3, k = i - rr * D3;
+        const long row = t * 32 + rr < nrows ? t * 32 + rr : nrows - 1;
+        X[i] = rows[row * D3P + k] - meta->center[k];
+    }
+    __syncthreads();
+    constexpr int NJ = (D3 + 7) / 8;   // 21 components per thread
+    double acc[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) acc[i] = 0.0;
+    double n2 = 0.0;
+    for (int k = 0; k < D3; ++k) {
+        const double dk = X[r * D3 + k];
+        if (g == 0) n2 += dk * dk;
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) {
+            const int j = g + 8 * i;
+            if (j < D3) acc[i] = fma((double)V[k * R3_LD + j], dk, acc[i]);
+        }
+    }
+    __syncthreads();   // every read of X done: it becomes the slot stage
+    _Float16 *stage = reinterpret_cast<_Float16 *>(X);   // [32][R3_SLOTS]
+    const Split16Db sc = split16_db_scale(__uint_as_float(meta->amax_bits));
+    double sk = 0.0;
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+        const int j = g + 8 * i;
+        if (j >= D3) continue;
+        const float r32 = (float)acc[i];
+        if (j >= R3_P) sk += (double)r32 * (double)r32;
+        _Float16 h, l;
+        split16f(ldexpf(r32, sc.ea), h, l);
+        stage[r * R3_SLOTS + R3_M0 + j] = h;
+        if (j < R3_P) {
+            stage[r * R3_SLOTS + 2 * j] = l;
+            stage[r * R3_SLOTS + 2 * j + 1] = h;
+        }
+    }
+    skp[r][g] = sk;
+    if (g == 0) nrm[r] = n2;
+    __syncthreads();
+    float askip = 0.f;
+    if (g == 0) {
+        _Float16 nh, nl;
+        split16f(ldexpf((float)nrm[r], sc.ea - sc.R), nh, nl);
+        stage[r * R3_SLOTS + R3_NL] = nl;
+        stage[r * R3_SLOTS + R3_NH] = nh;
+        for (int z = R3_NH + 1; z < R3_SLOTS; ++z) stage[r * R3_SLOTS + z] = (_Float16)0.f;
+        double s = 0.0;
+        for (int q = 0; q < 8; ++q) s += skp[r][q];
+        const double a = sqrt(s * (1.0 + 1e-12));
+        askip = (float)a;
+        if ((double)askip < a) askip = nextafterf(askip, INFINITY);
+    }
+    for (int o = 32; o > 0; o >>= 1) askip = fmaxf(askip, __shfl_xor(askip, o));
+    if ((tid & 63) == 0) red[tid >> 6] = askip;
+    __syncthreads();
+    if (tid == 0)
+        atomicMax(&rmeta->askip_bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    // the tile layout: half8 (m, hh, j) = slots 16 m + 8 hh .. +7 of row j
+    half8 *out = dbr + t * R3_TILE;
+    for (int i = tid; i < R3_TILE; i += 256) {
+        const int m = i >> 6, hh = (i >> 5) & 1, j = i & 31;
+        out[i] = *reinterpret_cast<const half8 *>(&stage[j * R3_SLOTS + 16 * m + 8 * hh]);
+    }
+}
+
+// the R16c query operand of query m from thread k's centred feature d (256 threads):
+// kappa_j = sum_k V[k][j] d_k (thread j, fp64 from the fp32 V in global memory), |q'|^2 ->
+// qn, |kappa_skip|^2 -> nsk, the slots into the query tile (m >= M: zero columns)
+__device__ __forceinline__ void r3_query(int m, int M, int k, double v, const Col16Meta *meta,
+                                         const float *__restrict__ rot, double *qn, double *nsk,
+                                         half8 *q16, double *ds, double *red) {
+    _Float16 *qt = reinterpret_cast<_Float16 *>(q16 + (long)(m >> 5) * R3_TILE);
+    const int col = m & 31;
+    auto put = [&](int slot, _Float16 x) { qt[r3_h8(slot, col) * 8 + (slot & 7)] = x; };
+    if (m >= M) {
+        if (k < R3_SLOTS) put(k, (_Float16)0.f);
+        return;
+    }
+    const double d = k < D3 ? v - meta->center[k] : 0.0;
+    if (k < D3) ds[k] = d;
+    double n = d * d;
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if ((k & 63) == 0) red[k >> 6] = n;
+    __syncthreads();
+    const double nq = (red[0] + red[1]) + (red[2] + red[3]);
+    double kap = 0.0;
+    if (k < D3) {
+        double k0 = 0.0, k1 = 0.0, k2 = 0.0, k3 = 0.0;
+        int i = 0;
+        // unrolled: the loads of V (L2-resident) issue far ahead of their FMAs
+#pragma unroll 10
+        for (; i + 4 <= D3; i += 4) {
+            k0 = fma((double)rot[(i + 0) * R3_LD + k], ds[i + 0], k0);
+            k1 = fma((double)rot[(i + 1) * R3_LD + k], ds[i + 1], k1);
+            k2 = fma((double)rot[(i + 2) * R3_LD + k], ds[i + 2], k2);
+            k3 = fma((double)rot[(i + 3) * R3_LD + k], ds[i + 3], k3);
+        }
+        for (; i < D3; ++i) k0 = fma((double)rot[i * R3_LD + k], ds[i], k0);
+        kap = (k0 + k1) + (k2 + k3);
+    }
+    double s2 = k >= R3_P && k < D3 ? kap * kap : 0.0;
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+    __syncthreads();   // red reused
+    if ((k & 63) == 0) red[k >> 6] = s2;
+    __syncthreads();
+    if (k == 0) {
+        qn[m] = nq;
+        nsk[m] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+    const Split16Db sc = split16_db_scale(__uint_as_float(meta->amax_bits));
+    const int eq = split16_q_scale(nq, sc.R);
+    if (k < D3) {
+        _Float16 h, l;
+        split16d(ldexp(-2.0 * kap, eq), h, l);
+        put(R3_M0 + k, h);
+        if (k < R3_P) {
+            put(2 * k, h);
+            put(2 * k + 1, l);
+        }
+    } else if (k == D3) {
+        const _Float16 nn = (_Float16)ldexpf(1.f, eq + sc.R);
+        put(R3_NL, nn);
+        put(R3_NH, nn);
+    } else if (R3_NH + (k - D3) < R3_SLOTS) {
+        put(R3_NH + (k - D3), (_Float16)0.f);
+    }
+}
+
+// queries of wave t for the R16c screen (as k_query3s; qin: caller-given rows, diagnostics)
+__global__ __launch_bounds__(256) void k_query3r(Img3 Bsm, Img3 Blg, Img3 Bpsm, Img3 Bplg, int t,
+                                                 int y_lo, int M, const Col16Meta *__restrict__ meta,
+                                                 const float *__restrict__ rot, const double *__restrict__ qin,
+                                                 double *__restrict__ q3, double *__restrict__ qn,
+                                                 double *__restrict__ nsk, half8 *__restrict__ q16) {
+    __shared__ double red[4];
+    __shared__ double ds[D3];
+    const int m = blockIdx.x, k = threadIdx.x;
+    double v = 0.0;
+    if (m < M) {
+        if (qin) {
+            v = k < D3 ? qin[(long)m * D3 + k] : 0.0;
+        } else {
+            const int y = y_lo + m, x = t - 3 * y;
+            if (k < D3_FULL) v = feat3(Bsm, Blg, y, x, k);
+            else if (k < D3) v = feat3(Bpsm, Bplg, y, x, k - D3_FULL);
+            if (k < D3P) q3[(long)m * D3P + k] = v;
+        }
+    }
+    r3_query(m, M, k, v, meta, rot, qn, nsk, q16, ds, red);
+}
+
+// the R16c screen: as k_screen3 with 11 operand groups per tile and 11 MFMAs per (row tile,
+// query tile); up to 8 query tiles staged per workgroup (a c3 wave's 213 queries: one group,
+// each DB tile read once per wave)
+constexpr int S3R_QG = 8;                 // query tiles per group (LDS: 8 x 11 KiB)
+__global__ __launch_bounds__(256, 1) void k_screen3r(const half8 *__restrict__ db16, int ntiles,
+                                                     const half8 *__restrict__ q16, int M, int tpw,
+                                                     float *__restrict__ smin) {
+    __shared__ half8 qsh[S3R_QG * R3_TILE];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int qt0 = blockIdx.y * S3R_QG;
+    const int QT = (M + 31) / 32;
+    const int nq = QT - qt0 < S3R_QG ? QT - qt0 : S3R_QG;
+    for (int i = threadIdx.x; i < nq * R3_TILE; i += 256) qsh[i] = q16[(long)qt0 * R3_TILE + i];
+    __syncthreads();
+    const floatx16 zero = {};
+    int t = blockIdx.x * tpw * 4 + wv;
+    if (t >= ntiles) return;   // (after the only barrier)
+    half8 a[R3_MFMA], n[R3_MFMA];
+#pragma unroll
+    for (int c = 0; c < R3_MFMA; ++c) a[c] = db16[(long)t * R3_TILE + c * 64 + lane];
+    for (int it = 0; it < tpw; ++it, t += 4) {
+        const int tn = t + 4;
+        const bool more = it + 1 < tpw && tn < ntiles;
+        if (more)
+#pragma unroll
+            for (int c = 0; c < R3_MFMA; ++c) n[c] = db16[(long)tn * R3_TILE + c * 64 + lane];
+        for (int j = 0; j < nq; ++j) {
+            const half8 *qb = qsh + j * R3_TILE + lane;
+            floatx16 acc = zero;
+#pragma unroll
+            for (int c = 0; c < R3_MFMA; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[c], qb[c * 64], acc, 0, 0, 0);
+            float mn = acc[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) mn = fminf(mn, acc[i]);
+            mn = fminf(mn, __shfl_xor(mn, 32));
+            const int q = (qt0 + j) * 32 + lane;
+            if (lane < 32 && q < M) smin[(long)q * c3_stride(ntiles) + t] = mn;
+        }
+        if (!more) break;
+#pragma unroll
+        for (int c = 0; c < R3_MFMA; ++c) a[c] = n[c];
+    }
+}
+static inline dim3 screen3r_grid(int ntiles, int M, int &tpw) {
+    const int QG = ((M + 31) / 32 + S3R_QG - 1) / S3R_QG;
+    tpw = (int)std::max(1L, ((long)ntiles * QG + 4L * 512 - 1) / (4L * 512));
+    return dim3((unsigned)((ntiles + 4 * tpw - 1) / (4 * tpw)), (unsigned)QG);
+}
+
+// eps of the R16c screen: u (850 A|q'| + 60 A^2) + 2^-9 1.01 A_skip |kappa_skip|
+__device__ __forceinline__ double r3_eps(double A, double nqq, double askip, double nsk) {
+    constexpr double U32 = 5.9604644775390625e-08;
+    return U32 * (850.0 * A * sqrt(nqq) + 60.0 * A * A) + 0x1p-9 * 1.01 * askip * sqrt(nsk);
+}
+__device__ double r3_eps_m(const Rot3Meta *rm, double A, double nqq, double nsk) {
+    return r3_eps(A, nqq, (double)__uint_as_float(rm->askip_bits), nsk);
 }
 
 // exhaustive fp64 search: a block takes 32 rows (staged in LDS) against every query, 8 at
@@ -612,21 +876,272 @@ struct Scr3 {
     const double *qn;
     const Col16Meta *meta;
     unsigned long long *stats;   // [candidate tiles, full scans] (diagnostic, may be null)
+    const double *nsk;           // R16c: |kappa_skip|^2 per query (null: the split-f16 screen)
+    const Rot3Meta *rmeta;       // R16c: A_skip
 };
 
 // Thresholds of the colour exact stage: Tseg = e* + 2 eps3 in screen units,
 // eps3 = u (900 A|q'| + 450 A^2); full scan when the norm slot nears the f16 floor
-__device__ __forceinline__ double c3_tseg(float emin, float amax0, double nqq, bool &force_full) {
+// (R16c, nsk >= 0: eps3 = r3_eps)
+__device__ __forceinline__ double c3_tseg(float emin, float amax0, double nqq, bool &force_full,
+                                          float askip = 0.f, double nsk = -1.0) {
     constexpr double U32 = 5.9604644775390625e-08;
     const double A = (double)amax0;
     const Split16Db sc = split16_db_scale(amax0);
     const int eq = split16_q_scale(nqq, sc.R);
     const int e2 = sc.ea + eq;
     const double em = ldexp((double)emin, -e2);
-    const double eps3 = U32 * (900.0 * A * sqrt(nqq) + 450.0 * A * A);
+    const double eps3 = nsk >= 0.0 ? r3_eps(A, nqq, (double)askip, nsk)
+                                   : U32 * (900.0 * A * sqrt(nqq) + 450.0 * A * A);
     const double slack = 1e-12 * (fabs(em) + nqq + A * A);
     force_full = eq + sc.R < -10;
     return ldexp(em + 2.0 * eps3 + slack, e2);
+}
+
+// ---- the exact stage + tail of the screened colour paths (k_exact3) ----------------------
+// 8 threads per row: thread part j of a row holds features k = j + 8 i (i < 21), i.e. exactly
+// Pw165's accumulator j of both halves (i < 10: k < 80; 10 <= i < 20: 80 <= k < 160) and,
+// for j < 5, the tail term k = 160 + j.  All 21 loads issue before any use (one round trip),
+// the accumulators are summed in Pw165's order in registers, and the row's part 0 finishes the
+// two trees and the tail from LDS: the same value as pw165_sum / row3_dist, with no 165-term
+// serial sum and no (row, feature) term array.
+constexpr int R8_N = 21;
+struct Acc8 {
+    double p1, p2, pt, w1, w2, wt;   // plain / weighted: half 1, half 2, tail term
+};
+// thread part j's accumulators of row `row` (global fp64 rows, D3P stride) against qs / ws (LDS)
+__device__ __forceinline__ Acc8 acc8_row(const double *__restrict__ row, int j, const double *qs,
+                                         const double *ws) {
+    double x[R8_N];
+#pragma unroll
+    for (int i = 0; i < R8_N; ++i) {
+        const int k = j + 8 * i;
+        x[i] = row[k < D3 ? k : 0];   // unconditional: every load before any use
+    }
+    Acc8 a{};
+#pragma unroll
+    for (int i = 0; i < R8_N; ++i) {
+        const int k = j + 8 * i;
+        const double d = x[i] - qs[k < D3 ? k : 0];
+        const double dw = d * ws[k < D3 ? k : 0];
+        const double tp = d * d, tw = dw * dw;
+        if (i == 0) { a.p1 = tp; a.w1 = tw; }
+        else if (i < 10) { a.p1 += tp; a.w1 += tw; }
+        else if (i == 10) { a.p2 = tp; a.w2 = tw; }
+        else if (i < 20) { a.p2 += tp; a.w2 += tw; }
+        else if (k < D3) { a.pt = tp; a.wt = tw; }
+    }
+    return a;
+}
+// part 0 of a row: Pw165's value from the 8 parts' accumulators (LDS, acc[0..7])
+__device__ __forceinline__ double acc8_sum(const Acc8 *acc, bool weighted) {
+    double r1[8], r2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        r1[j] = weighted ? acc[j].w1 : acc[j].p1;
+        r2[j] = weighted ? acc[j].w2 : acc[j].p2;
+    }
+    const double h1 = Pw165::tree(r1);
+    double h2 = Pw165::tree(r2);
+#pragma unroll
+    for (int j = 0; j < D3 - 160; ++j) h2 += weighted ? acc[j].wt : acc[j].pt;
+    return h1 + h2;
+}
+
+// The exact stage of the screened paths (k_screen3 / k_screen3r) and the per-pixel tail, one
+// 256-thread workgroup per pixel: the query, weights, the coherence window's s / im and the
+// query's tile minima (float4s in registers) in one round trip; e* and the tiles within the
+// threshold; then per candidate tile its 32 rows, 8 threads each (acc8_row: plain and weighted
+// sums, so the winner's weighted distance needs no second read), with the 15 coherence rows
+// in the first tile's round trip; the lexicographic (distance, row) minimum carries its
+// weighted distance; coherence pick, kappa test and the B' update as k_finish3w.
+__global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
+    __shared__ double qs[D3P], wsh[D3P];
+    __shared__ Acc8 acc[32 * 8];                // a tile's rows (32 x 8 parts)
+    __shared__ Acc8 cacc[15 * 8];               // the coherence rows
+    __shared__ double sump[15], sumw[15];
+    __shared__ long long rix[15];
+    __shared__ int rpos[15][3];
+    __shared__ double rd[4], rw[4];
+    __shared__ long long ri[4];
+    __shared__ float fmn[4];
+    __shared__ int clist[C3_CAND], ccount;
+    const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ro = tid >> 3, j = tid & 7;
+    const int y = f.y_lo + m, x = f.t - 3 * y;
+    const int W = f.W, Ah = f.Ah, Aw = f.Aw;
+    const long hw = (long)Ah * Aw;
+    const bool first = y == 0 && x == 0;
+    // ---- one round trip: query, weights, coherence s / im, tile minima
+    if (tid < D3P) {
+        qs[tid] = f.q3[(long)m * D3P + tid];
+        wsh[tid] = tid < D3 ? f.weights[tid] : 0.0;
+    }
+    if (tid < 15) {
+        long long cix = -1;
+        int cr = 0, cc = 0, cim = 0;
+        if (!first) {
+            const int rr = y - 2 + tid / 5, rc = x - 2 + tid % 5;
+            if (rr >= 0 && rc >= 0 && rc < W && (rr < y || rc < x)) {
+                const long sidx = (long)rr * W + rc;
+                const int sr = f.s[2 * sidx] + y - rr, scc = f.s[2 * sidx + 1] + x - rc;
+                if (sr >= 0 && sr < Ah && scc >= 0 && scc < Aw) {
+                    const int simg = f.im[sidx];
+                    cix = ((long)Ah * simg + sr) * Aw + scc;
+                    cr = sr; cc = scc; cim = simg;
+                }
+            }
+        }
+        rix[tid] = cix;
+        rpos[tid][0] = cr; rpos[tid][1] = cc; rpos[tid][2] = cim;
+    }
+    const int stride = c3_stride(sc.ntiles);
+    const float4 *sm4 = reinterpret_cast<const float4 *>(sc.smin + (long)m * stride);
+    const int n4 = stride / 4;
+    float4 v[C3_REG];
+#pragma unroll
+    for (int q = 0; q < C3_REG; ++q) {
+        const int i = tid + 256 * q;
+        v[q] = sm4[i < n4 ? i : 0];
+    }
+    auto masked = [&](float4 xx, int i) {   // +inf past the tiles (and the float4 pad)
+        const int b = 4 * i;
+        xx.x = b + 0 < sc.ntiles && i < n4 ? xx.x : INFINITY;
+        xx.y = b + 1 < sc.ntiles && i < n4 ? xx.y : INFINITY;
+        xx.z = b + 2 < sc.ntiles && i < n4 ? xx.z : INFINITY;
+        xx.w = b + 3 < sc.ntiles && i < n4 ? xx.w : INFINITY;
+        return xx;
+    };
+    float mn = INFINITY;
+#pragma unroll
+    for (int q = 0; q < C3_REG; ++q) {
+        v[q] = masked(v[q], tid + 256 * q);
+        mn = fminf(mn, fminf(fminf(v[q].x, v[q].y), fminf(v[q].z, v[q].w)));
+    }
+    for (int i = tid + 256 * C3_REG; i < n4; i += 256) {
+        const float4 xx = masked(sm4[i], i);
+        mn = fminf(mn, fminf(fminf(xx.x, xx.y), fminf(xx.z, xx.w)));
+    }
+    for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o));
+    if (lane == 0) fmn[wv] = mn;
+    if (tid == 0) ccount = 0;
+    __syncthreads();
+    // ---- the candidate tiles
+    mn = fminf(fminf(fmn[0], fmn[1]), fminf(fmn[2], fmn[3]));
+    bool full;
+    const float amax = __uint_as_float(sc.meta->amax_bits);
+    const double Tseg = sc.nsk ? c3_tseg(mn, amax, sc.qn[m], full, __uint_as_float(sc.rmeta->askip_bits), sc.nsk[m])
+                               : c3_tseg(mn, amax, sc.qn[m], full);
+    if (!full) {
+        auto pick = [&](float4 xx, int i) {
+            const float e4[4] = {xx.x, xx.y, xx.z, xx.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if ((double)e4[e] <= Tseg) {
+                    const int c = atomicAdd(&ccount, 1);
+                    if (c < C3_CAND) clist[c] = 4 * i + e;
+                }
+        };
+#pragma unroll
+        for (int q = 0; q < C3_REG; ++q) pick(v[q], tid + 256 * q);
+        for (int i = tid + 256 * C3_REG; i < n4; i += 256) pick(masked(sm4[i], i), i);
+    }
+    __syncthreads();
+    const int nc = ccount;
+    full = full || nc > C3_CAND;
+    const int ntl = full ? sc.ntiles : nc;
+    if (tid == 0 && sc.stats) {
+        atomicAdd(&sc.stats[0], (unsigned long long)ntl);
+        if (full) atomicAdd(&sc.stats[1], 1ull);
+    }
+    // ---- every row of the candidate tiles (and, with the first, the coherence rows)
+    double bd = INFINITY, bw = 0.0;
+    long long bi = 0x7fffffffffffffffLL;
+    const int nit = ntl > 0 ? ntl : 1;
+    for (int b = 0; b < nit; ++b) {
+        Acc8 ta{}, ca{};
+        const long r0 = ntl > 0 ? (long)(full ? b : clist[b]) * 32 : 0;
+        const long r = r0 + ro < sc.nrows ? r0 + ro : sc.nrows - 1;   // (rows past nrows: not taken)
+        if (ntl > 0) ta = acc8_row(f.db3 + r * D3P, j, qs, wsh);
+        if (b == 0 && tid < 15 * 8) {
+            const long long ix = rix[ro];
+            ca = acc8_row(f.db3 + (ix >= 0 ? ix : 0) * D3P, j, qs, wsh);
+        }
+        acc[tid] = ta;
+        if (b == 0 && tid < 15 * 8) cacc[tid] = ca;
+        __syncthreads();
+        if (j == 0 && ntl > 0 && r0 + ro < sc.nrows) {
+            const double d = acc8_sum(acc + 8 * ro, false);
+            if (d < bd || (d == bd && r0 + ro < bi)) {
+                bd = d;
+                bi = r0 + ro;
+                const double sq = sqrt(acc8_sum(acc + 8 * ro, true));
+                bw = sq * sq;
+            }
+        }
+        if (b == 0 && j == 0 && tid < 15 * 8) {
+            if (rix[ro] >= 0) {
+                sump[ro] = sqrt(acc8_sum(cacc + 8 * ro, false));
+                const double sq = sqrt(acc8_sum(cacc + 8 * ro, true));
+                sumw[ro] = sq * sq;
+            } else {
+                sump[ro] = INFINITY;
+                sumw[ro] = 0.0;
+            }
+        }
+        __syncthreads();   // acc is refilled by the next tile
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(bd, o), ow = __shfl_xor(bw, o);
+        const long long oi = __shfl_xor(bi, o);
+        if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; bw = ow; }
+    }
+    if (lane == 0) { rd[wv] = bd; ri[wv] = bi; rw[wv] = bw; }
+    __syncthreads();
+    if (wv != 0) return;
+    double wd = rd[0], ww = rw[0];
+    long long wi = ri[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+        if (rd[w] < wd || (rd[w] == wd && ri[w] < wi)) { wd = rd[w]; wi = ri[w]; ww = rw[w]; }
+    const long long app = wi;
+    // coherence: the first minimum of the plain distances in (row, col) candidate order
+    double cd = lane < 15 && rix[lane] >= 0 ? sump[lane] : INFINITY;
+    long long cl = lane < 15 && rix[lane] >= 0 ? lane : 0x7fffffffffffffffLL;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(cd, o);
+        const long long ol = __shfl_xor(cl, o);
+        best3(cd, cl, od, ol);
+    }
+    const bool valid = cl != 0x7fffffffffffffffLL;
+    const int win = valid ? (int)cl : 0;
+    const int wr = rpos[win][0], wc = rpos[win][1], wim = rpos[win][2];
+    const double d_app = valid ? ww : 0.0, d_coh = valid ? sumw[win] : 0.0;
+    long img = app / hw;
+    long rem = app - img * hw;
+    const int ar = (int)(rem / Aw), ac = (int)(rem - (long)(rem / Aw) * Aw);
+    int pr = ar, pc = ac;
+    if (valid && d_coh <= d_app * f.kappa_factor) { pr = wr; pc = wc; img = wim; }
+    const long qpx = (long)y * W + x;
+    if (lane < 3)
+        f.Bp_lg[qpx * 3 + lane] = f.Ap_lg[((img * hw) + (long)pr * Aw + pc) * 3 + lane];
+    if (lane == 0) {
+        f.s[2 * qpx] = pr;
+        f.s[2 * qpx + 1] = pc;
+        f.im[qpx] = (int32_t)img;
+        if (f.dbg_px) {
+            int32_t *o = f.dbg_px + 7 * qpx;
+            o[0] = ar;
+            o[1] = ac;
+            o[2] = valid ? wr : 0;
+            o[3] = valid ? wc : 0;
+            o[4] = valid ? y - 2 + win / 5 : 0;
+            o[5] = valid ? x - 2 + win % 5 : 0;
+            o[6] = valid;
+            f.dbg_dist[2 * qpx] = valid ? d_app : 0.0;
+            f.dbg_dist[2 * qpx + 1] = valid ? d_coh : 0.0;
+        }
+    }
 }
 
 // The per-pixel tail, one 256-thread workgroup per pixel (k_finish3 took one wave and summed
@@ -686,22 +1201,58 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
     if constexpr (!SCR) {
         for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
     } else {
-        const float *sm = sc.smin + (long)m * sc.ntiles;
+        // the query's tile minima: float4 i = tid + 256 j in registers (one round trip for
+        // C3_REG * 1024 tiles: c3's 7,223), the rest streamed; e* and the selection from them
+        const float *sm = sc.smin + (long)m * c3_stride(sc.ntiles);
+        const float4 *sm4 = reinterpret_cast<const float4 *>(sm);
+        const int n4 = c3_stride(sc.ntiles) / 4;
+        float4 v[C3_REG];
+#pragma unroll
+        for (int j = 0; j < C3_REG; ++j) {
+            const int i = tid + 256 * j;
+            v[j] = sm4[i < n4 ? i : 0];   // unconditional (a valid index past the end)
+        }
+        auto masked = [&](float4 x, int i) {   // +inf past the tiles (and the float4 pad)
+            const int b = 4 * i;
+            x.x = b + 0 < sc.ntiles && i < n4 ? x.x : INFINITY;
+            x.y = b + 1 < sc.ntiles && i < n4 ? x.y : INFINITY;
+            x.z = b + 2 < sc.ntiles && i < n4 ? x.z : INFINITY;
+            x.w = b + 3 < sc.ntiles && i < n4 ? x.w : INFINITY;
+            return x;
+        };
         float mn = INFINITY;
-        for (int i = tid; i < sc.ntiles; i += 256) mn = fminf(mn, sm[i]);
+#pragma unroll
+        for (int j = 0; j < C3_REG; ++j) {
+            v[j] = masked(v[j], tid + 256 * j);
+            mn = fminf(mn, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
+        }
+        for (int i = tid + 256 * C3_REG; i < n4; i += 256) {
+            const float4 x = masked(sm4[i], i);
+            mn = fminf(mn, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
+        }
         for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o));
         if (lane == 0) fmn[wv] = mn;
         if (tid == 0) ccount = 0;
         __syncthreads();
         mn = fminf(fminf(fmn[0], fmn[1]), fminf(fmn[2], fmn[3]));
         bool full;
-        const double Tseg = c3_tseg(mn, __uint_as_float(sc.meta->amax_bits), sc.qn[m], full);
-        if (!full)
-            for (int i = tid; i < sc.ntiles; i += 256)
-                if ((double)sm[i] <= Tseg) {
-                    const int j = atomicAdd(&ccount, 1);
-                    if (j < C3_CAND) clist[j] = i;
-                }
+        const double Tseg = sc.nsk ? c3_tseg(mn, __uint_as_float(sc.meta->amax_bits), sc.qn[m], full,
+                                             __uint_as_float(sc.rmeta->askip_bits), sc.nsk[m])
+                                   : c3_tseg(mn, __uint_as_float(sc.meta->amax_bits), sc.qn[m], full);
+        if (!full) {
+            auto pick = [&](float4 x, int i) {
+                const float e4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if ((double)e4[e] <= Tseg) {
+                        const int j = atomicAdd(&ccount, 1);
+                        if (j < C3_CAND) clist[j] = 4 * i + e;
+                    }
+            };
+#pragma unroll
+            for (int j = 0; j < C3_REG; ++j) pick(v[j], tid + 256 * j);
+            for (int i = tid + 256 * C3_REG; i < n4; i += 256) pick(masked(sm4[i], i), i);
+        }
         __syncthreads();
         const int nc = ccount;
         full = full || nc > C3_CAND;
@@ -882,10 +1433,11 @@ static unsigned long long *g_c3_stats = nullptr;   // diagnostic counters (ia_di
 struct Ws3 {
     double *q3;
     Best *best, *part;
-    half8 *q16;
-    double *qn;
+    half8 *q16;              // the query tiles of either screen (C16_TILE >= R3_TILE)
+    double *qn, *nsk;
     float *smin;
 };
+static_assert(C16_TILE >= R3_TILE, "query tiles");
 static inline size_t ws3_layout(int H, int W, long nrows, char *base, Ws3 *w) {
     const size_t M = (size_t)max_wave(H, W), Mp = (M + 31) / 32 * 32;
     size_t o = 0;
@@ -895,17 +1447,127 @@ static inline size_t ws3_layout(int H, int W, long nrows, char *base, Ws3 *w) {
     char *part = take(M * (size_t)match3_blocks(nrows) * sizeof(Best));
     char *q16 = take(Mp / 32 * C16_TILE * sizeof(half8));
     char *qn = take(Mp * sizeof(double));
-    char *smin = take(M * (size_t)db3_tiles(nrows) * sizeof(float));
+    char *nsk = take(Mp * sizeof(double));
+    char *smin = take(M * (size_t)c3_stride((int)db3_tiles(nrows)) * sizeof(float));
     if (w) {
         w->q3 = reinterpret_cast<double *>(q3);
         w->best = reinterpret_cast<Best *>(best);
         w->part = reinterpret_cast<Best *>(part);
         w->q16 = reinterpret_cast<half8 *>(q16);
         w->qn = reinterpret_cast<double *>(qn);
+        w->nsk = reinterpret_cast<double *>(nsk);
         w->smin = reinterpret_cast<float *>(smin);
     }
     return o;
 }
+
+// one 3-channel level on one GPU: the wave loop of ia_synth_level3 (per wave: the query
+// rows and split operand, the screen, the exact stage + tail; or the exhaustive fp64 search)
+struct Level3 {
+    const IaSynthArgs *a = nullptr;
+    Ws3 w{};
+    Db3View v{};
+    Fin3 f{};
+    Scr3 sc{};
+    Img3 Bsm{}, Blg{}, Bpsm{}, Bplg{};
+    int H = 0, W = 0, nw = 0, nb = 0, ntiles = 0;
+    bool split = true, rot = false;   // rot: the R16c screen (a->dbr, a->rot: ia_db3_build_rot)
+    const half8 *dbr = nullptr;
+    int init(const IaSynthArgs *a_) {
+        a = a_;
+        IA_ARG(a && a->db && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg && a->weights && a->s && a->im &&
+                   a->workspace && a->H > 0 && a->W > 0,
+               "ia_synth_level3: bad args");
+        IA_ARG(!a->comm && !a->lsh && a->row0 == 0 && a->nrows == (long)a->src.nAp * a->src.Ah * a->src.Aw,
+               "ia_synth_level3: 3-channel matching runs unsharded with the exact matcher");
+        IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level3: debug outputs come in pairs");
+        H = a->H;
+        W = a->W;
+        ws3_layout(H, W, a->nrows, reinterpret_cast<char *>(a->workspace), &w);
+        nb = match3_blocks(a->nrows);
+        Bsm = Img3{a->B_sm, a->B_hs, a->B_ws};
+        Blg = Img3{a->B_lg, H, W};
+        Bpsm = Img3{a->Bp_sm, a->B_hs, a->B_ws};
+        Bplg = Img3{a->Bp_lg, H, W};
+        v = db3_view(const_cast<void *>(a->db), a->nrows);
+        f = Fin3{v.rows, w.q3, w.best, a->src.Ap_lg, a->src.Ah, a->src.Aw,
+                 0, 0, W, a->weights, a->kappa_factor, a->Bp_lg, a->s, a->im, a->dbg_px, a->dbg_dist};
+        split = g_color16.load(std::memory_order_relaxed) != 0;
+        ntiles = (int)v.ntiles;
+        rot = split && a->dbr && a->rot;
+        dbr = reinterpret_cast<const half8 *>(a->dbr);
+        sc = Scr3{w.smin, ntiles, a->nrows, w.qn, v.meta, g_c3_stats, rot ? w.nsk : nullptr,
+                  rot ? db3r_meta(const_cast<void *>(a->dbr), a->nrows) : nullptr};
+        nw = (W - 1) + 3 * (H - 1) + 1;
+        return IA_OK;
+    }
+    static void rows(int H, int W, int t, int &y_lo, int &M) {
+        y_lo = std::max(0, (t - (W - 1) + 2) / 3);
+        M = std::min(H - 1, t / 3) - y_lo + 1;
+    }
+    int wave(int t, hipStream_t st) {
+        int y_lo, M;
+        rows(H, W, t, y_lo, M);
+        if (M <= 0) return IA_OK;
+        f.t = t;
+        f.y_lo = y_lo;
+        if (rot) {
+            const int QT = (M + 31) / 32;
+            int tpw;
+            const dim3 grid = screen3r_grid(ntiles, M, tpw);
+            k_query3r<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, a->rot, nullptr, w.q3,
+                                               w.qn, w.nsk, w.q16);
+            k_screen3r<<<grid, 256, 0, st>>>(dbr, ntiles, w.q16, M, tpw, w.smin);
+            k_exact3<<<M, 256, 0, st>>>(f, sc);
+        } else if (split) {
+            const int QT = (M + 31) / 32;
+            int tpw;
+            const dim3 grid = screen3_grid(ntiles, M, tpw);
+            k_query3s<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, w.q3, w.qn,
+                                               reinterpret_cast<_Float16 *>(w.q16));
+            k_screen3<<<grid, 256, 0, st>>>(v.db16, ntiles, w.q16, M, tpw, w.smin);
+            k_exact3<<<M, 256, 0, st>>>(f, sc);
+        } else {
+            k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, w.q3);
+            k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, w.q3, M, w.part);
+            k_finish3w<false><<<M, 256, 0, st>>>(f, w.part, nb, sc);
+        }
+        IA_LAUNCH_CHECK("ia_synth_level3 wave");
+        return IA_OK;
+    }
+};
+
+// the coarse waves wave t of level a reads (ia_synth.hip coarse_need: the 3x3 coarse window
+// of pixel (y, x) reaches (y/2 + 1, x/2 + 1), clamped to the coarse level)
+static int c3_need(const IaSynthArgs &a, int t) {
+    int y_lo, M;
+    Level3::rows(a.H, a.W, t, y_lo, M);
+    int need = 0;
+    for (int y = y_lo; y < y_lo + M; ++y) {
+        const int x = t - 3 * y;
+        const int cy = std::min(y / 2 + 1, a.B_hs - 1), cx = std::min(x / 2 + 1, a.B_ws - 1);
+        need = std::max(need, cx + 3 * cy);
+    }
+    return need;
+}
+constexpr int C3_PIPE_BLOCK = 4;   // waves per recorded event
+
+struct Pipe3 {   // per host thread: the level streams and events of ia_synth_levels3
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;
+    size_t next = 0;
+    hipError_t event(hipEvent_t *e) {
+        if (next == events.size()) {
+            hipEvent_t x;
+            hipError_t r = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+            if (r != hipSuccess) return r;
+            events.push_back(x);
+        }
+        *e = events[next++];
+        return hipSuccess;
+    }
+};
+static thread_local Pipe3 g_pipe3;
 
 }  // namespace ia
 
@@ -988,48 +1650,103 @@ int ia_match3_batch(const double *db3, long nrows, const double *q165, int M, in
 
 size_t ia_synth3_workspace_bytes(int H, int W, long nrows) { return ws3_layout(H, W, nrows, nullptr, nullptr); }
 
-int ia_synth_level3(const IaSynthArgs *a, void *stream) {
-    IA_ARG(a && a->db && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg && a->weights && a->s && a->im &&
-               a->workspace && a->H > 0 && a->W > 0,
-           "ia_synth_level3: bad args");
-    IA_ARG(!a->comm && !a->lsh && a->row0 == 0 && a->nrows == (long)a->src.nAp * a->src.Ah * a->src.Aw,
-           "ia_synth_level3: 3-channel matching runs unsharded with the exact matcher");
-    IA_ARG(!a->dbg_px == !a->dbg_dist, "ia_synth_level3: debug outputs come in pairs");
+size_t ia_db3_rot_bytes(long nrows) { return nrows > 0 ? db3r_tiles_bytes(nrows) + sizeof(Rot3Meta) : 0; }
+int ia_db3_rot_components(void) { return R3_P; }
+int ia_db3_rot_floats(void) { return R3_ROT_FLOATS; }
+
+int ia_db3_build_rot(const double *db3, long nrows, const float *rot, void *dbr, void *stream) {
+    IA_ARG(db3 && rot && dbr && nrows > 0, "ia_db3_build_rot: bad args");
     hipStream_t st = S(stream);
-    const int H = a->H, W = a->W;
-    Ws3 w;
-    ws3_layout(H, W, a->nrows, reinterpret_cast<char *>(a->workspace), &w);
-    const int nb = match3_blocks(a->nrows);
-    const Img3 Bsm{a->B_sm, a->B_hs, a->B_ws}, Blg{a->B_lg, H, W};
-    const Img3 Bpsm{a->Bp_sm, a->B_hs, a->B_ws}, Bplg{a->Bp_lg, H, W};
-    const Db3View v = db3_view(const_cast<void *>(a->db), a->nrows);
-    Fin3 f{v.rows, w.q3, w.best, a->src.Ap_lg, a->src.Ah, a->src.Aw,
-           0, 0, W, a->weights, a->kappa_factor, a->Bp_lg, a->s, a->im, a->dbg_px, a->dbg_dist};
-    const bool split = g_color16.load(std::memory_order_relaxed) != 0;
-    const int ntiles = (int)v.ntiles;
-    const Scr3 sc{w.smin, ntiles, a->nrows, w.qn, v.meta, g_c3_stats};
-    const int nwaves = (W - 1) + 3 * (H - 1) + 1;
-    for (int t = 0; t < nwaves; ++t) {
-        const int y_lo = std::max(0, (t - (W - 1) + 2) / 3);
-        const int y_hi = std::min(H - 1, t / 3);
-        const int M = y_hi - y_lo + 1;
-        if (M <= 0) continue;
-        f.t = t;
-        f.y_lo = y_lo;
-        if (split) {
-            const int QT = (M + 31) / 32;
-            int tpw;
-            const dim3 grid = screen3_grid(ntiles, M, tpw);
-            k_query3s<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, w.q3, w.qn,
-                                               reinterpret_cast<_Float16 *>(w.q16));
-            k_screen3<<<grid, 256, 0, st>>>(v.db16, ntiles, w.q16, M, tpw, w.smin);
-            k_finish3w<true><<<M, 256, 0, st>>>(f, nullptr, 0, sc);
-        } else {
-            k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, w.q3);
-            k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, w.q3, M, w.part);
-            k_finish3w<false><<<M, 256, 0, st>>>(f, w.part, nb, sc);
+    const Db3View v = db3_view(const_cast<double *>(db3), nrows);
+    Rot3Meta *rm = db3r_meta(dbr, nrows);
+    IA_HIP(hipMemsetAsync(rm, 0, sizeof(Rot3Meta), st));
+    k_db3_rot<<<(unsigned)v.ntiles, 256, 0, st>>>(v.rows, nrows, v.meta, rot, reinterpret_cast<half8 *>(dbr), rm);
+    IA_LAUNCH_CHECK("ia_db3_build_rot");
+    return IA_OK;
+}
+
+/* diagnostics: A_skip of a rotated 3-channel DB and the R16c screen of M given query rows
+ * (M x 165): tile minima in unscaled units e[M][ntiles], eps (r3_eps) and |q'|^2 per query */
+int ia_diag_db3_askip(const void *dbr, long nrows, float *out) {
+    IA_ARG(dbr && out && nrows > 0, "ia_diag_db3_askip: bad args");
+    unsigned int b = 0;
+    IA_HIP(hipMemcpy(&b, &db3r_meta(const_cast<void *>(dbr), nrows)->askip_bits, 4, hipMemcpyDeviceToHost));
+    std::memcpy(out, &b, 4);
+    return IA_OK;
+}
+
+int ia_synth_level3(const IaSynthArgs *a, void *stream) {
+    hipStream_t st = S(stream);
+    Level3 run;
+    int rc = run.init(a);
+    if (rc) return rc;
+    for (int t = 0; t < run.nw; ++t)
+        if ((rc = run.wave(t, st))) return rc;
+    return IA_OK;
+}
+
+/* n consecutive 3-channel levels, pipelined as ia_synth_levels (ia_synth.hip): one stream per
+ * level (the coarser ones at high priority), level j's wave t launched behind an event of
+ * level j - 1 covering the coarse waves its pixels read (c3_need). */
+int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
+    IA_ARG(levels && n >= 1 && n <= 64, "ia_synth_levels3: bad level count");
+    for (int j = 1; j < n; ++j)
+        IA_ARG(levels[j].Bp_sm == levels[j - 1].Bp_lg && levels[j].B_hs == levels[j - 1].H &&
+                   levels[j].B_ws == levels[j - 1].W,
+               "ia_synth_levels3: levels must be consecutive (level j's coarse B' = level j-1's B')");
+    hipStream_t st = S(stream);
+    Pipe3 &P = g_pipe3;
+    while ((int)P.streams.size() < n) {
+        int lo = 0, hi = 0;
+        IA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        (void)lo;
+        hipStream_t s;
+        // stream j runs level j of a call: all but the last created at high priority (the
+        // finest level of an n-level call is always stream n - 1, created last or plain)
+        if ((int)P.streams.size() < n - 1) IA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+        else IA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        P.streams.push_back(s);
+    }
+    P.next = 0;
+    hipEvent_t start;
+    IA_HIP(P.event(&start));
+    IA_HIP(hipEventRecord(start, st));
+    std::vector<Level3> run(n);
+    std::vector<std::vector<hipEvent_t>> blk(n);   // blk[j][b]: level j done through block b
+    for (int j = 0; j < n; ++j) {
+        int rc = run[j].init(&levels[j]);
+        if (rc) return rc;
+        blk[j].assign((run[j].nw + C3_PIPE_BLOCK - 1) / C3_PIPE_BLOCK, nullptr);
+    }
+    // every level whole, coarse to fine: a level's waits name events already recorded
+    for (int j = 0; j < n; ++j) {
+        hipStream_t sj = P.streams[j];
+        IA_HIP(hipStreamWaitEvent(sj, start, 0));
+        int waited = -1;
+        for (int t = 0; t < run[j].nw; ++t) {
+            if (j > 0) {
+                const int w = c3_need(levels[j], t);
+                if (w > waited) {
+                    const int b = w / C3_PIPE_BLOCK;
+                    IA_HIP(hipStreamWaitEvent(sj, blk[j - 1][b], 0));
+                    waited = b * C3_PIPE_BLOCK + C3_PIPE_BLOCK - 1;
+                }
+            }
+            int rc = run[j].wave(t, sj);
+            if (rc) return rc;
+            if ((t + 1) % C3_PIPE_BLOCK == 0 || t == run[j].nw - 1) {
+                hipEvent_t e;
+                IA_HIP(P.event(&e));
+                IA_HIP(hipEventRecord(e, sj));
+                blk[j][t / C3_PIPE_BLOCK] = e;
+            }
         }
-        IA_LAUNCH_CHECK("ia_synth_level3 wave");
+    }
+    for (int j = 0; j < n; ++j) {
+        hipEvent_t e;
+        IA_HIP(P.event(&e));
+        IA_HIP(hipEventRecord(e, P.streams[j]));
+        IA_HIP(hipStreamWaitEvent(st, e, 0));
     }
     return IA_OK;
 }
@@ -1042,7 +1759,7 @@ int ia_diag_screen3(const void *db3, long nrows, const double *q165, int M, doub
     half8 *q16 = nullptr;
     float *smin = nullptr;
     IA_HIP(hipMalloc(&q16, (size_t)QT * C16_TILE * sizeof(half8)));
-    IA_HIP(hipMalloc(&smin, (size_t)M * ntiles * sizeof(float)));
+    IA_HIP(hipMalloc(&smin, (size_t)M * c3_stride(ntiles) * sizeof(float)));
     k_qsplit3<<<QT * 32, 256>>>(q165, M, v.meta, qn, reinterpret_cast<_Float16 *>(q16));
     int tpw;
     k_screen3<<<screen3_grid(ntiles, M, tpw), 256>>>(v.db16, ntiles, q16, M, tpw, smin);
@@ -1052,6 +1769,33 @@ int ia_diag_screen3(const void *db3, long nrows, const double *q165, int M, doub
     IA_HIP(hipDeviceSynchronize());
     IA_HIP(hipFree(q16));
     IA_HIP(hipFree(smin));
+    return IA_OK;
+}
+
+int ia_diag_screen3r(const void *db3, const void *dbr, const float *rot, long nrows, const double *q165, int M,
+                     double *e, double *eps, double *qn) {
+    IA_ARG(db3 && dbr && rot && q165 && e && eps && qn && nrows > 0 && M > 0, "ia_diag_screen3r: bad args");
+    const Db3View v = db3_view(const_cast<void *>(db3), nrows);
+    const int QT = (M + 31) / 32, ntiles = (int)v.ntiles;
+    half8 *q16 = nullptr;
+    float *smin = nullptr;
+    double *nsk = nullptr;
+    IA_HIP(hipMalloc(&q16, (size_t)QT * R3_TILE * sizeof(half8)));
+    IA_HIP(hipMalloc(&smin, (size_t)M * c3_stride(ntiles) * sizeof(float)));
+    IA_HIP(hipMalloc(&nsk, (size_t)QT * 32 * sizeof(double)));
+    const Img3 z{nullptr, 0, 0};
+    k_query3r<<<QT * 32, 256>>>(z, z, z, z, 0, 0, M, v.meta, rot, q165, nullptr, qn, nsk, q16);
+    int tpw;
+    k_screen3r<<<screen3r_grid(ntiles, M, tpw), 256>>>(reinterpret_cast<const half8 *>(dbr), ntiles, q16, M, tpw,
+                                                        smin);
+    const long n = (long)M * ntiles;
+    k_screen3_unscale<<<(unsigned)((n + 255) / 256), 256>>>(smin, M, ntiles, qn, v.meta, e, eps, nsk,
+                                                            db3r_meta(const_cast<void *>(dbr), nrows));
+    IA_LAUNCH_CHECK("ia_diag_screen3r");
+    IA_HIP(hipDeviceSynchronize());
+    IA_HIP(hipFree(q16));
+    IA_HIP(hipFree(smin));
+    IA_HIP(hipFree(nsk));
     return IA_OK;
 }
 

@@ -268,8 +268,9 @@ struct XArgs {
                                   // the R16 layout, q64 slot 55 = |kappa_skip|^2, amax[1] = A_skip
 };
 // k_xwave phase stamps (IA_XW_TRACE=<level tag>, ia_diag_xwave_trace): s_memrealtime (100
-// MHz) at XW_TRACE_N points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T
-constexpr int XW_TRACE_N = 16, XW_TRACE_PX = 8, XW_TRACE_T = 4096;
+// MHz) at XW_TRACE_N - 1 points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T;
+// slot XW_TRACE_N - 1 holds the pixel's candidate segment count (k_xstrip)
+constexpr int XW_TRACE_N = 17, XW_TRACE_PX = 512, XW_TRACE_T = 4096;
 // form: XW_ROWS (split-f16 rows), XW_IMG (image-form windows, fp32 re-screen), XW_STRIP
 // (strip-order image form: k_xstrip, fp64 windows; xstrip_applies)
 constexpr int XW_ROWS = 0, XW_IMG = 1, XW_STRIP = 2;

@@ -1,17 +1,19 @@
 // ia_screen16r.hip — the rotated split-f16 screen (R16, ia_rot16.h): the
 // level's rotation (covariance of the centred rows, ia_db_cov; the eigenvectors are taken
-// on the host), the rotated database (ia_db_build_rot: 160 B per row, 5 MFMA operand groups
-// per 32-row tile) and the screen k_screen16r: 5 v_mfma_f32_32x32x16_f16 per 32x32 (rows x
-// queries) tile instead of the 11 of ia_screen16.hip, same segment minima units, so the
-// exact stage (k_xstrip) is unchanged apart from its bound.
+// on the host), the rotated database (ia_db_build_rot: R16_ROW_B bytes per row, R16_MFMA
+// operand groups per 32-row tile: 128 B and 4 at the default P = 3) and the screen
+// k_screen16r: R16_MFMA v_mfma_f32_32x32x16_f16 per 32x32 (rows x queries) tile instead of
+// the 11 of ia_screen16.hip, same segment minima units, so the exact stage (k_xstrip) is
+// unchanged apart from its bound.
 //
 // The screen's structure is the row form's of ia_screen16.hip (k_screen16): queries are the
-// stationary MFMA B operand (5 half8 per query tile and lane); the DB streams through LDS in
-// 4-tile stages (20 KiB, global_load_lds_dwordx4, non-temporal, a ring of 3 buffers, one
-// barrier per stage) and every byte fetched feeds the block's 4 waves; the stage's 4G (query
-// tile, stage tile) chains are cut into 4 equal runs (chain balance), each chain's 5 MFMAs
-// run back to back into one of two ping-pong accumulators and its running-minimum fold is
-// issued after the next chain's first MFMA; minima staged in LDS 8 segments at a time.
+// stationary MFMA B operand (R16_MFMA half8 per query tile and lane); the DB streams through
+// LDS in 4-tile stages (16 KiB at P = 3, global_load_lds_dwordx4, non-temporal, a ring of 3
+// buffers, one LDS-only barrier per stage) and every byte fetched feeds the block's 4 waves;
+// the stage's 4G (query tile, stage tile) chains are cut into 4 equal runs (chain balance),
+// each chain's MFMAs run back to back into one of two ping-pong accumulators and its
+// running-minimum fold is interleaved with the next chain's MFMAs; minima staged in LDS 8
+// segments at a time.
 #include "ia_internal.h"
 #include "ia_rot16.h"
 
@@ -23,7 +25,7 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int STAGE_TILES = 4;
-constexpr int STAGE_H8 = STAGE_TILES * R16_TILE_H8;   // 20 KiB
+constexpr int STAGE_H8 = STAGE_TILES * R16_TILE_H8;   // 16 KiB (P = 3)
 constexpr int MAX_G = 11;
 constexpr int SPC_MAX = 16;
 constexpr int R16_RING = 3;      // stage buffers (r16_body)
@@ -201,7 +203,7 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
             for (int m = 0; m < R16_MFMA; ++m) bq[k][m] = p[m];
         }
     }
-    // one stage = 4 consecutive tiles (5 KiB each): 20 wave-instructions of 1 KiB, 5 per wave
+    // one stage = 4 consecutive tiles: 4 R16_MFMA wave-instructions of 1 KiB, R16_MFMA per wave
     auto issue = [&](int s) {
         const half8 *src = db16 + (stage_lrow(sm, chunk, s) >> 5) * R16_TILE_H8 + W * 64 + lane;
         half8 *dst = sbuf + (s % R16_RING) * STAGE_H8 + W * 64;

@@ -1094,6 +1094,7 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             ns = scount;
             full = ns > RESCORE_SEGCAP || force_full;
             if (tid == 0) sfull = full ? 1 : 0;
+            if (trace && tid == 0) trace[XW_TRACE_N - 1] = (unsigned long long)(full ? a.nseg : ns);
         }
 
         auto coherence = [&]() {

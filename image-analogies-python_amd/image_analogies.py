@@ -195,15 +195,20 @@ def _src_level3(A_sm, A_lg, Ap_sm, Ap_lg):
 
 
 def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels=None,
-                    debug=False):
-    """3-channel synthesis (num_ch = 3: convert=False on colour images, 165-dim rows), one
-    level at a time through ia_synth_level3: the materialised fp64 database
-    (ia_db3_build), exhaustive exact search, the coherence / kappa tail and the 3-channel
-    B' update.  Same return value as synthesize_dev."""
+                    debug=False, pipeline=None):
+    """3-channel synthesis (num_ch = 3: convert=False on colour images, 165-dim rows): per
+    level the materialised fp64 database (ia_db3_build: the exact stage's rows and the
+    split-f16 operand of the MFMA screen k_screen3), then every wave's query rows, screen
+    and exact fp64 rescore of the candidate tiles (the oracle's first minimum, DESIGN.md
+    §4c), the coherence / kappa tail and the 3-channel B' update.  pipeline (default
+    pipeline_default()): the levels run concurrently (ia_synth_levels3), else one after the
+    other (ia_synth_level3); the same results.  Same return value as synthesize_dev."""
     lib = _ia.lib()
     st = _ia.stream()
     weights = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
-    out = {}
+    if pipeline is None:
+        pipeline = pipeline_default()
+    out, args, keep = {}, [], []
     for level in range(1, max_levels):
         if levels is not None and level not in levels:
             continue
@@ -215,6 +220,9 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
         dev = A_lg.device
         db3 = torch.empty(lib.ia_db3_bytes(N) // 8, dtype=torch.float64, device=dev)
         _ia.check(lib.ia_db3_build(ctypes.byref(src), 0, N, _ia.ptr(db3), st), 'ia_db3_build')
+        rot = dbr = None
+        if _ia.db_rot_enabled():   # the rotated split screen (R16c), bit-identical results
+            rot, dbr = algorithms.rot3_build(db3, N)
         B_sm, B_lg = B_pyr[level - 1].contiguous(), B_pyr[level].contiguous()
         Bp_sm, Bp_lg = Bp_pyr[level - 1], Bp_pyr[level]
         assert Bp_lg.is_contiguous() and Bp_sm.is_contiguous()
@@ -236,10 +244,30 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
         a.weights = _ia.ptr(weights).value
         a.kappa_factor = kappa_factor(level, max_levels, k)
         a.s, a.im, a.workspace = _ia.ptr(s).value, _ia.ptr(im).value, _ia.ptr(ws).value
+        if rot is not None:
+            a.dbr, a.rot = _ia.ptr(dbr).value, _ia.ptr(rot).value
         if dbg is not None:
             a.dbg_px, a.dbg_dist = _ia.ptr(dbg[0]).value, _ia.ptr(dbg[1]).value
-        _ia.check(lib.ia_synth_level3(ctypes.byref(a), st), 'ia_synth_level3')
+        if not pipeline:
+            _ia.check(lib.ia_synth_level3(ctypes.byref(a), st), 'ia_synth_level3')
+        else:
+            args.append(a)
+            keep.append((A_sm, A_lg, Ap_sm, Ap_lg, B_sm, B_lg, db3, ws, rot, dbr))
         out[level] = (s, im) if dbg is None else (s, im, dbg)
+    if args:
+        # consecutive runs of levels go through one pipelined call each
+        lv = sorted(out)
+        i = 0
+        while i < len(args):
+            j = i + 1
+            while j < len(args) and lv[j] == lv[j - 1] + 1:
+                j += 1
+            arr = (_ia.IaSynthArgs * (j - i))(*args[i:j])
+            _ia.check(lib.ia_synth_levels3(arr, j - i, st), 'ia_synth_levels3')
+            i = j
+        # the level streams are joined into st: buffers freed after this return are reused
+        # only by work queued on st behind that join (the caching allocator's stream order)
+        del keep
     return out
 
 
@@ -261,7 +289,8 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         if comm is not None or nranks > 1 or lsh is not None:
             raise NotImplementedError('3-channel matching runs on one GPU with the exact matcher')
         return synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
-                               levels=levels, debug=debug)
+                               levels=levels, debug=debug,
+                               pipeline=False if eager else pipeline)
     w = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
     if pipeline is None:
         pipeline = pipeline_default() and not eager

@@ -205,9 +205,14 @@ int ia_db_build_rot(const IaSrcLevel *src, long row0, long nrows, const double *
  *   ia_db3_bytes) of rows [row0, row0 + nrows).
  * ia_level_features3_f64: compute_feature_array (algorithms.py:11-47) of one level pair,
  *   h*w x 102 (full) or x 63 (half).
- * ia_synth_level3: one level on one GPU with the exact matcher (exhaustive fp64 search of
- *   the materialised rows), the coherence / kappa tail and the 3-channel B' update;
- *   a->db = ia_db3_build output over all rows; workspace of ia_synth3_workspace_bytes. */
+ * ia_synth_level3: one level on one GPU with the exact matcher (the split-f16 MFMA screen
+ *   k_screen3 and an exact fp64 rescore of its candidate tiles in the oracle's order;
+ *   IA_COLOR16=0: exhaustive fp64 search of the materialised rows), the coherence / kappa
+ *   tail and the 3-channel B' update; a->db = ia_db3_build output over all rows; workspace
+ *   of ia_synth3_workspace_bytes.
+ * ia_synth_levels3: n consecutive 3-channel levels at once, pipelined as ia_synth_levels
+ *   (one stream per level, wave t of level j behind the waves of level j-1 its coarse
+ *   windows read); the same results as n ia_synth_level3 calls in order. */
 size_t ia_db3_bytes(long nrows);
 int ia_db3_build(const IaSrcLevel *src, long row0, long nrows, double *db3, void *stream);
 int ia_level_features3_f64(const double *sm, int hs, int ws, const double *lg, int h, int w,
@@ -271,6 +276,18 @@ typedef struct {
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);
 int ia_synth_level3(const IaSynthArgs *a, void *stream);
+int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream);
+/* the rotated split screen for 3-channel rows (R16c): after ia_db3_build, the
+ * caller takes the principal directions V of the level's centred rows (165 x 165, columns by
+ * decreasing variance; any orthonormal V keeps the matcher exact) and passes them as fp32
+ * rot[k * 168 + j] = V[k][j] (ia_db3_rot_floats floats); ia_db3_build_rot writes the rotated
+ * split tiles (352 B per row: ia_db3_rot_components components as f16 pairs, the rest as f16)
+ * and A_skip into dbr (ia_db3_rot_bytes).  IaSynthArgs.dbr / .rot then select the R16c screen
+ * in ia_synth_level3 / ia_synth_levels3 (11 MFMAs per 32 x 32 tile instead of 33). */
+size_t ia_db3_rot_bytes(long nrows);
+int ia_db3_rot_components(void);
+int ia_db3_rot_floats(void);
+int ia_db3_build_rot(const double *db3, long nrows, const float *rot, void *dbr, void *stream);
 /* n consecutive levels (coarse to fine: levels[j].Bp_sm == levels[j-1].Bp_lg) at once, with
  * the same results as n ia_synth_level calls in order: each level runs on its own stream
  * and wave t of level j waits only for the waves of level j-1 its 3x3 coarse windows read

@@ -120,6 +120,13 @@ int ia_diag_peer_stress(void *comm, int nwaves, int M, int *bad, void *stream);
  * doubles) */
 int ia_diag_peer_trace(void *comm, double *out);
 
+/* R16c (3-channel rotated screen): A_skip of a rotated DB (fp32); one screen of M given query
+ * rows (M x 165) -> tile minima in unscaled units e[M][ntiles], eps[M] (the exact stage's
+ * bound), qn[M] = |q'|^2 */
+int ia_diag_db3_askip(const void *dbr, long nrows, float *out);
+int ia_diag_screen3r(const void *db3, const void *dbr, const float *rot, long nrows, const double *q165, int M,
+                     double *e, double *eps, double *qn);
+
 #ifdef __cplusplus
 }
 #endif

@@ -143,12 +143,65 @@ def test_screen3_error_bound(gpu, scale):
     assert worst > 0.0
 
 
+@pytest.mark.parametrize('scale', [1e-3, 1.0, 1e3])
+def test_screen3r_error_bound(gpu, scale):
+    """The rotated colour screen's tile minima (R16c, DESIGN.md §4e: 3 principal components
+    as f16 pairs, 162 as f16, 11 MFMAs per tile) are within eps_Rc of the exact min over the
+    tile of |a - q|^2 - |q'|^2 at input scales 1e-3 .. 1e3, near and far from the rows, and
+    A_skip bounds every row's skipped components."""
+    import ctypes
+    import _ia
+    import algorithms
+    A_pyr, Ap_list, _, _, L = inputs(85, (45, 70), (20, 20), n_ap=2)
+    lv = L - 1
+    sc = lambda p: dev(p * scale)  # noqa: E731
+    idx = algorithms.LevelIndex3(sc(A_pyr[lv - 1]), sc(A_pyr[lv]),
+                                 torch.stack([sc(p[lv - 1]) for p in Ap_list]),
+                                 torch.stack([sc(p[lv]) for p in Ap_list])).build_rot()
+    rows = idx.features().cpu().numpy()
+    N = rows.shape[0]
+    P = _ia.lib().ia_db3_rot_components()
+    V = idx.rot.cpu().numpy().reshape(165, 168)[:, :165].astype(np.float64)
+    c = rows.min(0) * 0.5 + rows.max(0) * 0.5       # the DB's centre (midrange)
+    rho = ((rows - c) @ V).astype(np.float32).astype(np.float64)
+    ask = ctypes.c_float()
+    _ia.check(_ia.lib().ia_diag_db3_askip(_ia.ptr(idx.dbr), N, ctypes.byref(ask)), 'askip')
+    assert np.sqrt((rho[:, P:] ** 2).sum(1)).max() <= ask.value * (1 + 1e-6)
+    rs = np.random.RandomState(5)
+    Q = np.vstack([rows[rs.randint(0, N, 40)] + rs.randn(40, 165) * 1e-3 * scale,
+                   rs.rand(24, 165) * scale, rows[rs.randint(0, N, 6)]])
+    M = Q.shape[0]
+    nt = (N + 31) // 32
+    e = torch.empty((M, nt), dtype=torch.float64, device='cuda')
+    eps = torch.empty(M, dtype=torch.float64, device='cuda')
+    qn = torch.empty(M, dtype=torch.float64, device='cuda')
+    Qd = dev(Q)
+    _ia.check(_ia.lib().ia_diag_screen3r(_ia.ptr(idx.db3), _ia.ptr(idx.dbr), _ia.ptr(idx.rot), N, _ia.ptr(Qd),
+                                         M, _ia.ptr(e), _ia.ptr(eps), _ia.ptr(qn)), 'ia_diag_screen3r')
+    torch.cuda.synchronize()
+    e, eps, qn = e.cpu().numpy(), eps.cpu().numpy(), qn.cpu().numpy()
+    pad = np.vstack([rows, np.repeat(rows[-1:], nt * 32 - N, 0)])
+    worst = 0.0
+    for m in range(M):
+        assert qn[m] == pytest.approx(float(((Q[m] - c) ** 2).sum()), rel=1e-12)
+        D = ((pad - Q[m]) ** 2).sum(1) - qn[m]
+        x = D.reshape(nt, 32).min(1)
+        err = np.abs(e[m] - x).max()
+        slack = 1e-12 * (np.abs(x).max() + qn[m])
+        assert err <= eps[m] + slack, (m, err, eps[m])
+        worst = max(worst, err / eps[m])
+    print('R16c screen (scale %g): worst |tile min - exact| / eps = %.3g' % (scale, worst))
+    assert worst > 0.0
+
+
+@pytest.mark.parametrize('pipeline', [True, False])
 @pytest.mark.parametrize('matcher', [1, 0])
 @pytest.mark.parametrize('n_ap,k', [(1, 1.0), (2, 25.0)])
-def test_synthesis3_vs_oracle(gpu, color16, n_ap, k, matcher):
+def test_synthesis3_vs_oracle(gpu, color16, n_ap, k, matcher, pipeline):
     """Whole-level 3-channel synthesis: B' (all channels), s, im and the debug lists equal
     the oracle's scanline run (image_analogies.py:130-240 with num_ch = 3), with the
-    split-f16 screen + exact stage (1) and the exhaustive fp64 search (0)."""
+    split-f16 screen + exact stage (1) and the exhaustive fp64 search (0), the levels
+    pipelined (ia_synth_levels3) or one at a time (ia_synth_level3)."""
     import image_analogies as ia
     color16(matcher)
     A_pyr, Ap_list, B_pyr, Bp_pyr, L = inputs(83 + n_ap, (36, 44), (30, 34), n_ap=n_ap)
@@ -163,7 +216,7 @@ def test_synthesis3_vs_oracle(gpu, color16, n_ap, k, matcher):
         ref[level] = (s, im, dbg)
     Bp_dev = [dev(b) for b in Bp_pyr]
     out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
-                            [dev(p) for p in B_pyr], Bp_dev, L, k, w, debug=True)
+                            [dev(p) for p in B_pyr], Bp_dev, L, k, w, debug=True, pipeline=pipeline)
     for level in range(1, L):
         s, im, dbg = out[level]
         rs, rim, rd = ref[level]
@@ -204,6 +257,38 @@ def test_synthesis3_split_larger_vs_oracle(gpu, color16):
         assert np.array_equal(Bp_dev[level].cpu().numpy(), Bp_ref[level]), level
     queries = sum(B_pyr[l].shape[0] * B_pyr[l].shape[1] for l in range(1, L))
     print('candidate tiles per query %.3f, full scans %d' % (st[0] / queries, st[1]))
+    assert st[1] == 0 and st[0] < 8 * queries
+
+
+@pytest.mark.parametrize('rot', ['1', '0'])
+def test_synthesis3_screen_forms_vs_oracle(gpu, color16, monkeypatch, rot):
+    """The colour synthesis through the rotated screen (R16c, IA_DB_ROT=1, the default) and
+    the split-f16 one (IA_DB_ROT=0): both equal the oracle (A 72 x 90, two A' images, every
+    level), with few candidate tiles per query and no full scans."""
+    import ctypes
+    import _ia
+    import image_analogies as ia
+    color16(1)
+    monkeypatch.setenv('IA_DB_ROT', rot)
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L = inputs(89, (72, 90), (60, 66), n_ap=2)
+    w = o.compute_weights(3, 5, 12, 3)
+    As = o.create_index(A_pyr, Ap_list, L)
+    Bp_ref = [b.copy() for b in Bp_pyr]
+    ref = {l: o.synthesize_level(l, L, A_pyr, Ap_list, B_pyr, Bp_ref, As[l], w, 5.0)
+           for l in range(1, L)}
+    st = (ctypes.c_ulonglong * 2)()
+    _ia.check(_ia.lib().ia_diag_color16_stats(st), 'stats')
+    Bp_dev = [dev(b) for b in Bp_pyr]
+    out = ia.synthesize_dev([dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list],
+                            [dev(p) for p in B_pyr], Bp_dev, L, 5.0, w)
+    _ia.check(_ia.lib().ia_diag_color16_stats(st), 'stats')
+    for level in range(1, L):
+        s, im = out[level]
+        assert np.array_equal(s.cpu().numpy(), ref[level][0]), level
+        assert np.array_equal(im.cpu().numpy(), ref[level][1]), level
+        assert np.array_equal(Bp_dev[level].cpu().numpy(), Bp_ref[level]), level
+    queries = sum(B_pyr[l].shape[0] * B_pyr[l].shape[1] for l in range(1, L))
+    print('IA_DB_ROT=%s: candidate tiles per query %.3f, full scans %d' % (rot, st[0] / queries, st[1]))
     assert st[1] == 0 and st[0] < 8 * queries
 
 

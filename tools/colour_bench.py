@@ -4,6 +4,9 @@ luminance path on the same images (their Y channel): B' pixels per second of who
 syntheses (device pyramids, B' reset, every level), inputs resident in HBM.
 
 usage: python tools/colour_bench.py [H W] [steps]      (default 180 117 (c1 size), 3 steps)
+       COLOUR_PIPE=0: the colour levels one at a time (default: pipelined, ia_synth_levels3)
+Also reports the colour exact stage's candidate tiles per query (ia_diag_color16_stats) and a
+B' checksum (equal with and without the pipeline).
 """
 import json
 import os
@@ -30,7 +33,10 @@ def main():
     B = np.dstack([bench.smooth_noise(8 + 17 * c, (H, W)) for c in range(3)])
     w = torch.as_tensor(cfg.compute_weights(3, 5, 12, 3)).to(dev)
     w1 = torch.as_tensor(cfg.compute_weights(3, 5, 12, 1)).to(dev)
-    out = {'size': [H, W]}
+    import ctypes
+    import _ia
+    pipe = os.environ.get('COLOUR_PIPE', '1') != '0'
+    out = {'size': [H, W], 'pipeline': pipe}
     for name, (a, ap, b, ww) in {
             'rgb': (A, Ap, B, w),
             'luminance': (A[..., 0], Ap[..., 0], B[..., 0], w1)}.items():
@@ -52,16 +58,23 @@ def main():
             B_pyr = ip.gaussian_pyramid_dev(b, cfg.n_sm)
             for d, s in zip(Bp, init):
                 d.copy_(s)
-            ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, Bp, L, 0.5, ww)
+            ia.synthesize_dev(A_pyr, [Ap_pyr], B_pyr, Bp, L, 0.5, ww, pipeline=pipe)
 
+        st = (ctypes.c_ulonglong * 2)()
+        _ia.check(_ia.lib().ia_diag_color16_stats(st), 'stats')   # (reads and clears)
         step()
         torch.cuda.synchronize()
+        _ia.check(_ia.lib().ia_diag_color16_stats(st), 'stats')
+        cand = (st[0] / pixels, int(st[1]))
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
-        out[name] = {'ms_per_step': dt * 1e3, 'px_per_s': pixels / dt, 'pixels': pixels}
+        out[name] = {'ms_per_step': dt * 1e3, 'px_per_s': pixels / dt, 'pixels': pixels,
+                     'bp_checksum': float(sum(float(x.sum()) for x in Bp[1:L]))}
+        if name == 'rgb':
+            out[name]['candidate_tiles_per_query'], out[name]['full_scans'] = cand
     out['rgb_vs_luminance_slowdown'] = out['luminance']['px_per_s'] / out['rgb']['px_per_s']
     print(json.dumps(out))
 

@@ -32,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--M', default='342,256,128')
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--sleep', type=int, default=0, help='GPU cycles of idle spin after each launch '
+                    '(torch.cuda._sleep: the product\'s gaps between screens); not counted')
     args = ap.parse_args()
     Ms = [int(x) for x in args.M.split(',')]
     dev = torch.device('cuda', 0)
@@ -64,18 +66,29 @@ def main():
             run()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.reps):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / args.reps
+        if args.sleep:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.reps)]
+            for a, b in ev:
+                a.record()
+                run()
+                b.record()
+                torch.cuda._sleep(args.sleep)
+            torch.cuda.synchronize()
+            us = sum(a.elapsed_time(b) for a, b in ev) * 1e3 / args.reps
+        else:
+            e0.record()
+            for _ in range(args.reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.reps
         pairs = M * N
         out.append({'M': M, 'us': round(us, 1), 'frac': 110 * pairs / (us * 1e-6) / 1e12 / F16_PEAK,
                     'pipe_frac': 2 * lib.ia_db_rot_slots() * pairs / (us * 1e-6) / 1e12 / F16_PEAK,
                     'P': lib.ia_db_rot_components(),
                     'db_gbs': lib.ia_db_rot_bytes(N) / (us * 1e-6) / 1e9,
-                    'lib': os.environ.get('IA_LIB_PATH', 'libia.so')})
+                    'sleep': args.sleep, 'lib': os.environ.get('IA_LIB_PATH', 'libia.so')})
         print(json.dumps(out[-1]), flush=True)
 
 

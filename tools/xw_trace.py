@@ -1,9 +1,11 @@
 """Phase breakdown of the fused per-wave kernel k_xwave (diagnostic).
 
 Runs a bench.py workload's synthesis (or the simulated G-shard rank of tools/shard_sim.py
-with --shards G) twice with IA_XW_TRACE=<level>, reads the phase stamps of the first 8
-pixels of every wave of that level (ia_diag_xwave_trace: 100 MHz s_memrealtime) and prints
-the median time of each phase over the plateau waves (the most queries) and over all.
+with --shards G) twice with IA_XW_TRACE=<level>, reads the phase stamps of every pixel of
+every wave of that level (ia_diag_xwave_trace: 100 MHz s_memrealtime; slot 16: the pixel's
+candidate segment count) and prints the median time of each phase over the first 8 pixels
+of the plateau waves (the most queries) and over all, then the per-wave span (first
+pixel's start to last pixel's end) against the slowest pixel's candidate count.
 
 usage: python tools/xw_trace.py [--config c4] [--level 5] [--shards G]
 """
@@ -16,6 +18,49 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PHASES = ['ticket', 'e*', 'candidates', 're-screen', 'rescore(w0)', 'coherence+barrier',
           'exchange', 'update', 'neighbour', 'query build']
+
+
+def wave_profile(full):
+    """per wave: span = last end - first start over ALL its pixels; the slowest pixel's
+    candidate segments; the p50 pixel's start->end"""
+    import numpy as np
+    st = full[:, :, 0].astype(np.float64) * 0.01
+    en = full[:, :, 10].astype(np.float64) * 0.01
+    ns = full[:, :, 16].astype(np.int64)
+    ok = (full[:, :, 0] > 0) & (full[:, :, 10] > 0)
+    npx = ok.sum(1)
+    waves = np.nonzero(npx >= max(npx.max() // 2, 1))[0]   # the plateau-ish waves
+    if not len(waves):
+        return
+    span, slow, slow_ns, p50, mx_ns, startsk = [], [], [], [], [], []
+    for t in waves:
+        o = ok[t]
+        s0, e0, n0 = st[t][o], en[t][o], ns[t][o]
+        span.append(e0.max() - s0.min())
+        j = np.argmax(e0)
+        slow.append(e0[j] - s0[j])
+        slow_ns.append(n0[j])
+        mx_ns.append(n0.max())
+        p50.append(np.median(e0 - s0))
+        startsk.append(np.percentile(s0 - s0.min(), 90))
+    span, slow, slow_ns, p50, mx_ns = map(np.array, (span, slow, slow_ns, p50, mx_ns))
+    print('per wave over all pixels (%d waves with >= %d pixels): span p50 %.1f us (p10 %.1f, p90 %.1f); '
+          'slowest pixel start->end p50 %.1f us; median pixel %.1f us; start spread p90 %.1f us' % (
+              len(waves), max(npx.max() // 2, 1), np.median(span), np.percentile(span, 10),
+              np.percentile(span, 90), np.median(slow), np.median(p50), np.median(startsk)))
+    allns = ns[ok]
+    print('candidate segments per pixel: mean %.3f; per wave max: mean %.2f; the slowest pixel\'s: mean %.2f' % (
+        allns.mean(), mx_ns.mean(), slow_ns.mean()))
+    for k in range(1, 8):
+        sel = slow_ns == k
+        if sel.any():
+            print('  slowest pixel with %d segments: %4d waves, its start->end p50 %.1f us, span p50 %.1f us' % (
+                k, sel.sum(), np.median(slow[sel]), np.median(span[sel])))
+    for k in range(1, 8):
+        sel = (allns == k)
+        if sel.any():
+            d = (en - st)[ok][sel]
+            print('  pixels with %d segments: %6d, start->end p50 %.1f us' % (k, sel.sum(), np.median(d)))
 
 
 def main():
@@ -37,9 +82,12 @@ def main():
     for _ in range(2):
         job.step(comm, 0, args.shards or 1)
     torch.cuda.synchronize()
-    buf = np.zeros(4096 * 8 * 16, dtype=np.uint64)
+    T, PX, N = 4096, 512, 17
+    buf = np.zeros(T * PX * N, dtype=np.uint64)
     _ia.check(_ia.lib().ia_diag_xwave_trace(buf.ctypes.data_as(ctypes.c_void_p)), 'ia_diag_xwave_trace')
-    tr = buf.reshape(4096, 8, 16).astype(np.float64) * 0.01      # us
+    full = buf.reshape(T, PX, N)
+    wave_profile(full)
+    tr = full[:, :8, :16].astype(np.float64) * 0.01      # us
     have = (tr[:, :, 0] > 0) & (tr[:, :, 7] > 0) & (tr[:, :, 10] > 0)
     waves = np.nonzero(have.any(axis=1))[0]
     npx = have.sum(axis=1)
