@@ -7,11 +7,15 @@
 // (two halves of 80 and 85, 8 accumulators each, algorithms.py:74 / :126 / :135 through
 // norm / add.reduce), so the matcher is exact against the oracle.
 //
-// The path is built for the reference's colour workloads (c1-c3 sizes): the database rows
-// are materialised in fp64 (1,344 B per row) and searched exhaustively in fp64 — 32 rows x
-// 8 queries per block step, both staged in LDS — with the lexicographic (distance, row)
-// minimum, then the per-pixel tail (coherence over the causal 3x5 window, kappa test, B'
-// update of all three channels) runs one 64-lane wave per pixel.  Single GPU, exact matcher.
+// Per level (ia_db3_build) the rows are materialised in fp64 (1,344 B per row: the exact
+// stage's input) with the split-f16 screen operand (704 B per row) after them;
+// ia_db3_build_rot adds the rotated split operand (R16c, 352 B per row, §4e).  Per wave: the
+// query rows (k_query3s / k_query3r), the MFMA screen's minimum per (query, 32-row tile)
+// (k_screen3: 33 MFMAs per 32x32 tile; k_screen3r: 11), then k_exact3: every row of the tiles
+// within the bound rescored in fp64 in the oracle's order, the coherence pick over the causal
+// 3x5 window, the kappa test and the B' update of all three channels, one 256-thread
+// workgroup per pixel.  IA_COLOR16=0 keeps the exhaustive fp64 search (k_match3 +
+// k_finish3w).  ia_synth_levels3 runs the levels pipelined.  Single GPU, exact matcher.
 #include "ia_common.h"
 #include "ia_internal.h"
 #include "ia_split16.h"
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(256) void k_query3(Img3 Bsm, Img3 Blg, Img3 Bpsm, I
 // chunks of 16, each one v_mfma_f32_32x32x16_f16 per product: the 22 cross-term MFMAs
 // (a_h q_l, a_l q_h) first, then the 11 main ones (a_h q_h, the norm slot in the last): 33
 // per 32x32 tile.  The screen keeps the minimum per (query, 32-row tile); the exact stage
-// (k_finish3w<true>) rescores in fp64 every row of the tiles whose minimum is within 2 eps3
+// (k_exact3) rescores in fp64 every row of the tiles whose minimum is within 2 eps3
 // of the smallest (the error bound of DESIGN.md §4c).
 constexpr int C16_CH = 11;                 // 16-slot chunks
 constexpr int C16_GRP = 2 * C16_CH;        // half8 groups per lane and tile: (chunk, hi / lo)
@@ -1144,33 +1148,25 @@ __global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
     }
 }
 
-// The per-pixel tail, one 256-thread workgroup per pixel (k_finish3 took one wave and summed
-// each distance serially from global memory).  The winner: SCR = false reduces k_match3's
-// partials (a lexicographic minimum: order free); SCR = true is the exact stage of the
-// split-f16 screen: e* over the query's tile minima, the tiles within the threshold, and
-// every row of those tiles rescored in fp64 (terms lane-parallel into LDS, one thread per
-// row summing them in numpy's pairwise order, Pw165), lexicographic (distance, row) minimum.
-// Then the 15 coherence candidates' and the winner's rows are read once, lane-parallel over
-// (row, feature); their plain and weighted squared terms go to LDS, and 31 threads sum one
-// row each (Pw165): the same values as row3_dist.
-template <bool SCR>
-__global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict__ part, int nb, Scr3 sc) {
+// The per-pixel tail of the exhaustive fp64 search (IA_COLOR16=0), one 256-thread workgroup
+// per pixel: the winner is the lexicographic minimum of k_match3's partials (order free); the
+// 15 coherence candidates' and the winner's rows are read once, lane-parallel over (row,
+// feature); their plain and weighted squared terms go to LDS, and 31 threads sum one row each
+// (Pw165): the same values as row3_dist.
+__global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict__ part, int nb) {
     __shared__ double qs[D3P], wsh[D3P];
-    __shared__ double tt[32 * D3];              // exact-stage terms
     __shared__ double tp[15][D3], tw[16][D3];   // coherence rows: plain, weighted (+ winner)
     __shared__ double sump[15], sumw[16];
     __shared__ long long rix[16];               // rows: candidates 0..14, winner 15 (-1: none)
     __shared__ int rpos[15][3];
     __shared__ double rd[4];
     __shared__ long long ri[4];
-    __shared__ float fmn[4];
-    __shared__ int clist[C3_CAND], ccount;
     const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int y = f.y_lo + m, x = f.t - 3 * y;
     const int W = f.W, Ah = f.Ah, Aw = f.Aw;
     const long hw = (long)Ah * Aw;
     const bool first = y == 0 && x == 0;
-    // the query, the weights, the partials' minimum (or the tile minima's) and the
+    // the query, the weights, the partials' minimum and the
     // candidates' rows: one round trip
     if (tid < D3P) {
         qs[tid] = f.q3[(long)m * D3P + tid];
@@ -1197,107 +1193,7 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
     }
     double bd = INFINITY;
     long long bi = 0x7fffffffffffffffLL;
-    bool coh_done = false;   // the coherence rows' sums (SCR: beside the first tile's)
-    if constexpr (!SCR) {
-        for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
-    } else {
-        // the query's tile minima: float4 i = tid + 256 j in registers (one round trip for
-        // C3_REG * 1024 tiles: c3's 7,223), the rest streamed; e* and the selection from them
-        const float *sm = sc.smin + (long)m * c3_stride(sc.ntiles);
-        const float4 *sm4 = reinterpret_cast<const float4 *>(sm);
-        const int n4 = c3_stride(sc.ntiles) / 4;
-        float4 v[C3_REG];
-#pragma unroll
-        for (int j = 0; j < C3_REG; ++j) {
-            const int i = tid + 256 * j;
-            v[j] = sm4[i < n4 ? i : 0];   // unconditional (a valid index past the end)
-        }
-        auto masked = [&](float4 x, int i) {   // +inf past the tiles (and the float4 pad)
-            const int b = 4 * i;
-            x.x = b + 0 < sc.ntiles && i < n4 ? x.x : INFINITY;
-            x.y = b + 1 < sc.ntiles && i < n4 ? x.y : INFINITY;
-            x.z = b + 2 < sc.ntiles && i < n4 ? x.z : INFINITY;
-            x.w = b + 3 < sc.ntiles && i < n4 ? x.w : INFINITY;
-            return x;
-        };
-        float mn = INFINITY;
-#pragma unroll
-        for (int j = 0; j < C3_REG; ++j) {
-            v[j] = masked(v[j], tid + 256 * j);
-            mn = fminf(mn, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
-        }
-        for (int i = tid + 256 * C3_REG; i < n4; i += 256) {
-            const float4 x = masked(sm4[i], i);
-            mn = fminf(mn, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
-        }
-        for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o));
-        if (lane == 0) fmn[wv] = mn;
-        if (tid == 0) ccount = 0;
-        __syncthreads();
-        mn = fminf(fminf(fmn[0], fmn[1]), fminf(fmn[2], fmn[3]));
-        bool full;
-        const double Tseg = sc.nsk ? c3_tseg(mn, __uint_as_float(sc.meta->amax_bits), sc.qn[m], full,
-                                             __uint_as_float(sc.rmeta->askip_bits), sc.nsk[m])
-                                   : c3_tseg(mn, __uint_as_float(sc.meta->amax_bits), sc.qn[m], full);
-        if (!full) {
-            auto pick = [&](float4 x, int i) {
-                const float e4[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if ((double)e4[e] <= Tseg) {
-                        const int j = atomicAdd(&ccount, 1);
-                        if (j < C3_CAND) clist[j] = 4 * i + e;
-                    }
-            };
-#pragma unroll
-            for (int j = 0; j < C3_REG; ++j) pick(v[j], tid + 256 * j);
-            for (int i = tid + 256 * C3_REG; i < n4; i += 256) pick(masked(sm4[i], i), i);
-        }
-        __syncthreads();
-        const int nc = ccount;
-        full = full || nc > C3_CAND;
-        const int ntl = full ? sc.ntiles : nc;
-        if (tid == 0 && sc.stats) {
-            atomicAdd(&sc.stats[0], (unsigned long long)ntl);
-            if (full) atomicAdd(&sc.stats[1], 1ull);
-        }
-        for (int b = 0; b < ntl; ++b) {
-            const long r0 = (long)(full ? b : clist[b]) * 32;
-            for (int e = tid; e < 32 * D3; e += 256) {
-                const int j = e / D3, k = e - j * D3;
-                const long r = r0 + j;
-                if (r < sc.nrows) {
-                    const double d = f.db3[r * D3P + k] - qs[k];
-                    tt[e] = d * d;
-                }
-            }
-            if (b == 0) {   // with the first tile: the coherence rows' terms
-                for (int e = tid; e < 15 * D3; e += 256) {
-                    const int j = e / D3, k = e - j * D3;
-                    const long long ix = rix[j];
-                    if (ix < 0) continue;
-                    const double d = f.db3[ix * D3P + k] - qs[k];
-                    const double dw = d * wsh[k];
-                    tp[j][k] = d * d;
-                    tw[j][k] = dw * dw;
-                }
-            }
-            __syncthreads();
-            if (tid < 32 && r0 + tid < sc.nrows) best3(bd, bi, pw165_sum(tt + tid * D3), r0 + tid);
-            if (b == 0 && tid >= 64 && tid < 94) {   // their sums (wave 1), numpy's pairwise order
-                const bool pl = tid < 79;
-                const int j = pl ? tid - 64 : tid - 79;
-                if (rix[j] >= 0) {
-                    const double sq = sqrt(pw165_sum(pl ? tp[j] : tw[j]));
-                    if (pl) sump[j] = sq; else sumw[j] = sq * sq;
-                } else {
-                    if (pl) sump[j] = INFINITY; else sumw[j] = 0.0;
-                }
-            }
-            __syncthreads();
-        }
-        coh_done = ntl > 0;
-    }
+    for (int i = tid; i < nb; i += 256) best3(bd, bi, part[(long)m * nb + i].d, part[(long)m * nb + i].idx);
     for (int o = 32; o > 0; o >>= 1) {
         const double od = __shfl_xor(bd, o);
         const long long oi = __shfl_xor(bi, o);
@@ -1311,11 +1207,9 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
     }
     __syncthreads();
     const long long app = rix[15];
-    // the terms: (row j, feature k) pairs spread over the block, each row read once (the
-    // coherence rows only when not done beside the exact stage: the winner's alone then)
-    const int j0 = coh_done ? 15 : 0;
-    for (int e = tid; e < (16 - j0) * D3; e += 256) {
-        const int j = j0 + e / D3, k = e - (j - j0) * D3;
+    // the terms: (row j, feature k) pairs spread over the block, each row read once
+    for (int e = tid; e < 16 * D3; e += 256) {
+        const int j = e / D3, k = e - j * D3;
         const long long ix = rix[j];
         if (ix < 0) continue;
         const double d = f.db3[ix * D3P + k] - qs[k];
@@ -1324,7 +1218,7 @@ __global__ __launch_bounds__(256) void k_finish3w(Fin3 f, const Best *__restrict
         tw[j][k] = dw * dw;
     }
     __syncthreads();
-    if (tid < 31 && (!coh_done || tid == 30)) {   // one row per thread, numpy's pairwise order
+    if (tid < 31) {   // one row per thread, numpy's pairwise order
         const bool pl = tid < 15;
         const int j = pl ? tid : tid - 15;
         const double *t = pl ? tp[j] : tw[j];
@@ -1530,7 +1424,7 @@ struct Level3 {
         } else {
             k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, w.q3);
             k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, w.q3, M, w.part);
-            k_finish3w<false><<<M, 256, 0, st>>>(f, w.part, nb, sc);
+            k_finish3w<<<M, 256, 0, st>>>(f, w.part, nb);
         }
         IA_LAUNCH_CHECK("ia_synth_level3 wave");
         return IA_OK;
