@@ -499,7 +499,15 @@ def main():
     # its own host thread (ctypes drops the GIL inside ia_synth_level, so the threads enqueue
     # their latency-bound waves concurrently); results are per job and stream-independent
     batch = (args.batch or len(jobs)) if args.config == 'c5' and lsh is None else 1
-    nstreams = max(1, min(args.streams, len(jobs))) if args.config == 'c5' and batch == 1 else 1
+    # --batch B < jobs: the batches run --streams at a time, each on its own stream and host
+    # thread (one batch's latency-bound per-wave tails beside another's HBM-bound screens)
+    nbatches = (len(jobs) + batch - 1) // batch
+    if args.config != 'c5':
+        nstreams = 1
+    elif batch == 1:
+        nstreams = max(1, min(args.streams, len(jobs)))
+    else:
+        nstreams = max(1, min(args.streams, nbatches))
     pool = streams = None
     if nstreams > 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -523,13 +531,30 @@ def main():
         return [r for part in res for r in part]
 
     def run_batches(prof=False, check=True):
-        outs = []
-        for b0 in range(0, len(jobs), batch):
-            part = jobs[b0:b0 + batch]
+        groups = [jobs[b0:b0 + batch] for b0 in range(0, len(jobs), batch)]
+
+        def one(part):
             ins = [jb.prepare() for jb in part]
-            outs += ia.synthesize_batch_dev(ins, part[0].max_levels, [jb.k for jb in part],
-                                            part[0].weights, prof=prof, check=check)
-        return outs
+            return ia.synthesize_batch_dev(ins, part[0].max_levels, [jb.k for jb in part],
+                                           part[0].weights, prof=prof, check=check)
+        if pool is None:
+            return [o for part in groups for o in one(part)]
+        main = torch.cuda.current_stream(dev)
+
+        def lane(i):
+            torch.cuda.set_device(dev)
+            st = streams[i]
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                return [one(part) for part in groups[i::nstreams]]
+        res = list(pool.map(lane, range(nstreams)))
+        for st in streams:
+            main.wait_stream(st)
+        outs = [None] * len(groups)
+        for i, r in enumerate(res):
+            for j, o in enumerate(r):
+                outs[i + j * nstreams] = o
+        return [o for part in outs for o in part]
 
     def run_step(prof=False):
         # no per-step ia_synth_status (a host sync per step): every level folds its error

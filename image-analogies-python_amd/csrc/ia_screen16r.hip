@@ -28,7 +28,14 @@ constexpr int STAGE_TILES = 4;
 constexpr int STAGE_H8 = STAGE_TILES * R16_TILE_H8;   // 16 KiB (P = 3)
 constexpr int MAX_G = 11;
 constexpr int SPC_MAX = 16;
-constexpr int R16_RING = 3;      // stage buffers (r16_body)
+// stage buffers (r16_body) and blocks per CU the kernel is built for (A/B builds)
+#ifndef IA_R16_RING
+#define IA_R16_RING 3
+#endif
+#ifndef IA_R16_OCC
+#define IA_R16_OCC 2
+#endif
+constexpr int R16_RING = IA_R16_RING;
 // A/B builds only (tools/build_variant.sh -DIA_R16_LAB=n): 1 no DB loads after the ring's
 // first stages (the compute floor), 2 one MFMA per chain (the streaming floor)
 #ifndef IA_R16_LAB
@@ -251,7 +258,7 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
 // grid: (nchunks rounded up to 8) x groups, XCD-aware (all groups of a chunk share
 // blockIdx % 8); group g holds query tiles [g G, g G + G); grid y = job of a batch
 template <int G>
-__global__ __launch_bounds__(256, 2) void k_screen16r(const half8 *__restrict__ db16, int nchunks, int ch,
+__global__ __launch_bounds__(256, IA_R16_OCC) void k_screen16r(const half8 *__restrict__ db16, int nchunks, int ch,
                                                       int seg_rows, StageMap sm,
                                                       const half8 *__restrict__ q16, int M, int groups,
                                                       float *__restrict__ segmin, long nseg,

@@ -708,38 +708,74 @@ struct XsFix {
     double v[XS_DMA][2];
     unsigned mask;
 };
+// piece p's source: its (reflected) image row, first column C (maybe outside the image) and
+// the image width
+__device__ __forceinline__ const double *xs_piece(const XsWin &w, const ImgPair &A, int p, int &C, int &iw) {
+    constexpr int FP = XS_FW / 2, CP = XS_CW / 2;   // pieces per window row
+    const double *img = w.fa;
+    int sr = 0;
+    iw = A.w;
+    C = 0;
+    if (p < 8 * FP) {
+        const int r = p / FP;
+        sr = symi2(min(w.y0 - 2 + r, w.y0 + w.nst + 1), A.h);
+        C = w.x0 - 4 + 2 * (p - r * FP);
+    } else if ((p -= 8 * FP) < 6 * FP) {
+        const int r = p / FP;
+        img = w.fp;
+        sr = symi2(min(w.y0 - 2 + r, w.y0 + w.nst - 1), A.h);
+        C = w.x0 - 4 + 2 * (p - r * FP);
+    } else if ((p -= 6 * FP) < 8 * CP) {
+        const int r = p / CP;
+        img = r < 4 ? w.ca : w.cp;
+        iw = A.ws;
+        sr = symi2(min((w.y0 >> 1) - 1 + (r & 3), ((w.y0 + w.nst - 1) >> 1) + 1), A.hs);
+        C = (w.x0 >> 1) - 2 + 2 * (p - r * CP);
+    }
+    return img + (long)sr * iw;
+}
 __device__ __forceinline__ void xs_dma(const XsWin &w, const ImgPair &A, char *win, int dr, int lane, XsFix &fx) {
     asm volatile("" : "+v"(lane));   // the piece addresses are computed here, not hoisted
-    constexpr int FP = XS_FW / 2, CP = XS_CW / 2;   // pieces per window row
     fx.mask = 0;
 #pragma unroll
     for (int j = 0; j < XS_DMA; ++j) {
-        int p = 192 * j + 64 * dr + lane;
-        const double *img = w.fa;
-        int iw = A.w, sr = 0, C = 0;
-        if (p < 8 * FP) {
-            const int r = p / FP;
-            sr = symi2(min(w.y0 - 2 + r, w.y0 + w.nst + 1), A.h);
-            C = w.x0 - 4 + 2 * (p - r * FP);
-        } else if ((p -= 8 * FP) < 6 * FP) {
-            const int r = p / FP;
-            img = w.fp;
-            sr = symi2(min(w.y0 - 2 + r, w.y0 + w.nst - 1), A.h);
-            C = w.x0 - 4 + 2 * (p - r * FP);
-        } else if ((p -= 6 * FP) < 8 * CP) {
-            const int r = p / CP;
-            img = r < 4 ? w.ca : w.cp;
-            iw = A.ws;
-            sr = symi2(min((w.y0 >> 1) - 1 + (r & 3), ((w.y0 + w.nst - 1) >> 1) + 1), A.hs);
-            C = (w.x0 >> 1) - 2 + 2 * (p - r * CP);
-        }
-        const double *row = img + (long)sr * iw;
+        const int p = 192 * j + 64 * dr + lane;
+        int C, iw;
+        const double *row = xs_piece(w, A, p, C, iw);
         __builtin_amdgcn_global_load_lds((const void *)(row + clampi(C, 0, iw - 2)),
                                          (void *)(win + (192 * j + 64 * dr) * 16), 16, 0, 0);
         if (C < 0 || C + 1 >= iw) {
             fx.mask |= 1u << j;
             fx.v[j][0] = row[symi2(clampi(C, -2, iw + 1), iw)];
             fx.v[j][1] = row[symi2(clampi(C + 1, -2, iw + 1), iw)];
+        }
+    }
+}
+// the next candidate segment's windows staged in registers while the current one is
+// rescored (all 256 threads, pieces 256 j + tid: two reflected 8-B loads each, issued
+// unconditionally), stored into the windows after the last reads of the current one
+constexpr int XS_PRE = (XS_PIECES + 255) / 256;   // 5
+struct XsPre {
+    double v[XS_PRE][2];
+};
+__device__ __forceinline__ void xs_pre_load(const XsWin &w, const ImgPair &A, int tid, XsPre &pr) {
+#pragma unroll
+    for (int j = 0; j < XS_PRE; ++j) {
+        const int p = 256 * j + tid;
+        int C, iw;
+        const double *row = xs_piece(w, A, p < XS_PIECES ? p : XS_PIECES - 1, C, iw);
+        pr.v[j][0] = row[symi2(clampi(C, -2, iw + 1), iw)];
+        pr.v[j][1] = row[symi2(clampi(C + 1, -2, iw + 1), iw)];
+    }
+}
+__device__ __forceinline__ void xs_pre_store(const XsPre &pr, char *win, int tid) {
+#pragma unroll
+    for (int j = 0; j < XS_PRE; ++j) {
+        const int p = 256 * j + tid;
+        if (p < XS_PIECES) {
+            double *d = reinterpret_cast<double *>(win + p * 16);
+            d[0] = pr.v[j][0];
+            d[1] = pr.v[j][1];
         }
     }
 }
@@ -905,8 +941,12 @@ __device__ __forceinline__ void sync3(unsigned *cnt, unsigned g, int lane) {
 
 // ROT: an R16 level (ia_rot16.h): the exact stage's bound eps_R, and the next query row
 // rotated (the rotation copied into LDS by wave 0 at the start)
+// workgroups per CU the batch form (k_xstrip<true>) is built for (A/B builds)
+#ifndef IA_XSTRIP_BOCC
+#define IA_XSTRIP_BOCC 3
+#endif
 template <bool BATCH, bool ROT>
-__global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
+__global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArgs a0) {
     __shared__ __attribute__((aligned(16))) char sa_raw[BATCH ? sizeof(XArgs) : 16];
     XArgs &sa = *reinterpret_cast<XArgs *>(sa_raw);
     if constexpr (BATCH) {
@@ -1168,16 +1208,20 @@ __global__ __launch_bounds__(256, 3) void k_xstrip(XArgs a0) {
             if (nit > 0) w = xs_window(a, full ? 0 : slist[0]);
         }
         const long nscan = nit;
+        // segments after the first: their windows are loaded into registers while the one
+        // before is rescored, and stored after its last read (one LDS window, no DMA wait)
+        XsPre pre;
+        XsWin wn{};
         for (long si = 0; si < nit; ++si) {
             if (si > 0) {
-                __syncthreads();   // every row of the last segment is read before the copies
-                w = xs_window(a, full ? si : slist[si]);
-                if (wv != 1) {
-                    xs_dma(w, src.A, win, dr, lane, fx);
-                    win_dma_wait();
-                    xs_fix(fx, win, 64 * dr + lane);
-                }
+                __syncthreads();   // every row of the last segment is read before the stores
+                xs_pre_store(pre, win, tid);
+                w = wn;
                 __syncthreads();   // the windows are complete
+            }
+            if (si + 1 < nit) {
+                wn = xs_window(a, full ? si + 1 : slist[si + 1]);
+                xs_pre_load(wn, src.A, tid, pre);
             }
             if (si == 0) {
                 xw_stamp(trace, 4);
