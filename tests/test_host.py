@@ -526,3 +526,38 @@ def test_residency_rule_refuses_the_known_starvation():
     ok, j = ia.residency_ok(256 * 3 - 1, fused_r16, screen_r16)
     assert ok and j == 2
     assert not ia.residency_ok(256 * 3, fused_r16, screen_r16)[0]
+
+
+def test_pass_check_classifies_a_cascade_as_an_exchange_failure(monkeypatch):
+    """A dead or slow peer also trips the fused kernel's neighbour-decision waits (the same
+    10 s limit): with both error words set, bench.pass_check raises ExchangeTimeout (the one
+    error its RCCL fallback handles), not ScheduleFault; the neighbour fault alone still
+    raises ScheduleFault (a fake lib reports the words; no GPU)."""
+    import _ia
+    import bench
+
+    class FakeLib:
+        def __init__(self, peer, sched):
+            self.peer, self.sched = peer, sched
+
+        def ia_peer_mem_kind(self, comm):
+            return 0
+
+        def ia_peer_status(self, comm):
+            return self.peer
+
+        def ia_sched_status(self, clear):
+            return self.sched
+
+        def ia_last_error(self):
+            return b'a wait timed out'
+
+    monkeypatch.setattr(bench.torch.cuda, 'synchronize', lambda *a: None)
+    monkeypatch.setattr(_ia, 'lib', lambda: FakeLib(_ia.IA_E_TIMEOUT, _ia.IA_E_SCHED))
+    with pytest.raises(_ia.ExchangeTimeout):
+        bench.pass_check([object()])
+    monkeypatch.setattr(_ia, 'lib', lambda: FakeLib(0, _ia.IA_E_SCHED))
+    with pytest.raises(_ia.ScheduleFault):
+        bench.pass_check([object()])
+    monkeypatch.setattr(_ia, 'lib', lambda: FakeLib(0, 0))
+    bench.pass_check([object()])
