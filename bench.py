@@ -683,11 +683,13 @@ def main():
     # its algorithmic fraction of the f16 dense peak is capped at 1/3; the
     # MFMA pipe's utilisation is reported beside it as pipe_frac
     per_pair = 2 * 55
-    # the rotated screen (R16) on strip-order levels of the fused kernel: 5
-    # MFMAs x 16 K-slots = 80 slots, 160 f16 flop issued per pair; else the split-f16 screen's
-    # 3 products per feature, 330
-    rot_used = (_ia.db_rot_enabled() and lsh is None and jobs[0].A.shape[1] % 128 == 0 and
-                _ia.db_image_enabled() and (comm is None or _ia.exchange_kind() == 'peer'))
+    # the rotated screen (R16) on the fused kernel's levels of at least
+    # rot_min_rows() rows: 4 MFMAs x 16 K-slots = 64 slots, 128 f16 flop issued per pair; else
+    # the split-f16 screen's 3 products per feature, 330
+    # (the finest level's DB, or this rank's shard of it, holds enough rows: level_index)
+    fin_rows = max((p['rows'] for p in prof), default=0)
+    rot_used = (_ia.db_rot_enabled() and lsh is None and fin_rows >= _ia.rot_min_rows() and
+                (comm is None or _ia.exchange_kind() == 'peer'))
     pipe_per_pair = 2 * _ia.lib().ia_db_rot_slots() if rot_used else 3 * 2 * 55
     inst = {}
     lv = {}

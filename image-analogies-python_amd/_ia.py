@@ -250,6 +250,14 @@ def db_image_enabled():
     return os.environ.get('IA_DB_IMAGE', '1') != '0'
 
 
+def rot_min_rows():
+    """Levels (shards) with fewer DB rows keep the split-f16 screen (IA_ROT_MIN_ROWS, default
+    131072): their waves are latency-bound, and the rotated form's per-level build (a
+    covariance read back for the host eigh) and per-wave query rotation cost more than its
+    faster screen saves there (c1: 19.5 -> 21.9 ms/step with R16 on every level)."""
+    return int(os.environ.get('IA_ROT_MIN_ROWS', '131072'))
+
+
 def db_rot_enabled():
     """The synthesis screen streams the rotated split DB (R16, DESIGN.md §4d: 5 MFMAs per tile
     instead of 11) where it applies (IA_DB_ROT, default 1; 0: the split-f16 image form).

@@ -125,8 +125,7 @@ class LevelIndex:
                       'ia_db_build_image')
         self.lsh = None
         self.dbr = self.rot = None
-        if (rot and ibytes and
-                lib.ia_db_rot_applies(ctypes.byref(self.src), self.row0, self.nrows)):
+        if rot and lib.ia_db_rot_applies(ctypes.byref(self.src), self.row0, self.nrows):
             self.build_rot()
 
     def build_rot(self):
@@ -304,14 +303,15 @@ def level_index(A_pyr, Ap_pyr_list, level, row_range=None, lsh=None, rows=None, 
     """Device index of one level from device pyramids.  row_range(level, N) ->
     (row0, nrows) selects this rank's shard of the rows; lsh (dict of build_lsh
     arguments) switches it to the LSH matcher; rows=True keeps the row form next to the
-    image form; rot (default: the exact matcher) also builds the synthesis screen's rotated
-    DB where it applies (R16)."""
+    image form; rot (default: the exact matcher on a level or shard of at least
+    _ia.rot_min_rows() rows) also builds the synthesis screen's rotated DB (R16)."""
     Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list])
     Ap_lg = torch.stack([p[level] for p in Ap_pyr_list])
     N = Ap_lg.shape[0] * Ap_lg.shape[1] * Ap_lg.shape[2]
     r0, nr = (0, N) if row_range is None else row_range(level, N)
-    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr, rows=rows,
-                       rot=(lsh is None and _ia.db_rot_enabled()) if rot is None else rot)
+    if rot is None:
+        rot = lsh is None and _ia.db_rot_enabled() and nr >= _ia.rot_min_rows()
+    index = LevelIndex(A_pyr[level - 1], A_pyr[level], Ap_sm, Ap_lg, r0, nr, rows=rows, rot=rot)
     if lsh is not None:
         index.build_lsh(**lsh)
     return index

@@ -86,6 +86,26 @@ __device__ __forceinline__ void r16_thresholds(float emin, float amax0, float as
     force_full = eq + sc.R < -10;
 }
 
+// the same for k_xwave's exact stage (non-strip levels), which re-screens the candidate
+// segments' rows in fp32 (error eps_q = 70u (2A|q'| + A^2), ia_exact.h) before the fp64
+// rescore: the oracle winner has e'(r_o) <= e* + eps_R + eps_q, so Trow (fp32 re-screen units,
+// 2^ea) takes eps_R where the split-f16 form takes eps16
+__device__ __forceinline__ void r16_thresholds_rows(float emin, float amax0, float askip, double nqq, double nsk,
+                                                    double &Tseg, double &Trow, bool &force_full) {
+    constexpr double U32 = 5.9604644775390625e-08;
+    const double A = (double)amax0;
+    const Split16Db sc = split16_db_scale(amax0);
+    const int eq = split16_q_scale(nqq, sc.R);
+    const int e2 = sc.ea + eq;
+    const double em = ldexp((double)emin, -e2);
+    const double eps = r16_eps(A, nqq, (double)askip, nsk);
+    const double epsq = 70.0 * U32 * (2.0 * A * sqrt(nqq) + A * A);
+    const double slack = 1e-12 * (fabs(em) + nqq + A * A);
+    Tseg = ldexp(em + 2.0 * eps + slack, e2);
+    Trow = ldexp(em + eps + epsq + slack, sc.ea);
+    force_full = eq + sc.R < -10;
+}
+
 // lane-parallel query row (64 lanes): d = this lane's centred feature q'_k (lane k < 55),
 // nq = |q'|^2 (every lane).  kappa_j = sum_k V[k][j] d_k in fp64 (lane j), split into the
 // row's slots; returns |kappa_skip|^2 = sum_{j >= R16_P} kappa_j^2 (every lane).  rot: the

@@ -513,10 +513,10 @@ using namespace ia;
 extern "C" {
 
 int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows) {
+    // every level: the screen streams the rotated rows in the level's stage order (strips or
+    // linear chunks); the fused kernel of either form takes the R16 bound
     if (!src || nrows <= 0 || row0 < 0) return 0;
-    const DbSrc d = make_dbsrc(*src);
-    if (!xstrip_applies(d)) return 0;
-    return db_stage_map(row0, nrows, src->Aw, src->Ah).W > 0 ? 1 : 0;
+    return row0 + nrows <= (long)src->nAp * src->Ah * src->Aw ? 1 : 0;
 }
 
 /* kernel resources of a sharded level's screen and fused kernel (the forward-progress rule

@@ -426,8 +426,8 @@ struct LevelRun {
         // on one GPU or over the device-side exchange (not the LSH matcher, the RCCL
         // exchange, the in-process shard simulation or a forced work list)
         xw = xwave_on() && !a->lsh && !sim && (!a->comm || peer) && exact_stage_mode() != 1;
-        r16 = xw && a->dbr && a->rot && a->dbi && xwave_on() == 2 && xstrip_applies(src) &&
-              db_stage_map(a->row0, a->nrows, src.A.w, src.A.h).W > 0;
+        // (any form of the fused kernel: k_xstrip on strip-order levels, k_xwave elsewhere)
+        r16 = xw && a->dbr && a->rot;
         IA_HIP(hipMemsetAsync(ws.ctl, 0, 256, st));   // tickets, error word (ia_synth_status)
         if (xw) {
             IA_HIP(hipMemsetAsync(ws.qpb, 0, (size_t)qrows_alloc(Mmax) * IA_DP * sizeof(float), st));
@@ -642,7 +642,6 @@ struct LevelRun {
         const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
         const int form = !im ? XW_ROWS
                        : (xwave_on() == 2 && sm.W > 0 && xstrip_applies(src)) ? XW_STRIP : XW_IMG;
-        IA_ARG(!r16 || form == XW_STRIP, "ia_synth_level: the rotated DB on a level without the strip kernel");
         if ((rc = launch_xwave(x, R, form, sq, K))) return rc;
         if (timed) IA_HIP(hipEventRecord(prof_event(ev0 + 3 * nscreen + 2), sq));
         ++nscreen;

@@ -329,6 +329,17 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
     const FinishArgs &f = a.f;
     const DbSrc &src = a.src;
     const int t = f.t, W = f.W;
+    // an R16 level (a.rot): wave 0 copies the rotation into the pool once the exact stage is
+    // done with it, for the next query row (as k_xstrip), 64 doubles of scratch after it
+    static_assert(R16_ROT_B + 64 * 8 <= (POOL > RESB ? POOL : RESB), "the rotation fits the pool");
+    float *const rotl = reinterpret_cast<float *>(pool);
+    double *const dq = reinterpret_cast<double *>(pool + R16_ROT_B);
+    auto rot_dma = [&]() {   // wave 0: 13 x 1 KiB, waited in xw_next_query (vmcnt(0))
+#pragma unroll
+        for (int pc = 0; pc < R16_ROT_FLOATS / 256; ++pc)
+            __builtin_amdgcn_global_load_lds((const void *)(a.rot.get() + pc * 256 + lane * 4),
+                                             (void *)(rotl + pc * 256), 16, 0, 0);
+    };
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) tk = (int)atomicAdd(&a.tickets[t & 1], 1u);
     __syncthreads();
@@ -375,6 +386,7 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
             wk = tid < IA_D ? f.weights[tid] : 0.0;
         }
         const double nqq = a.nq[vidx(i)];
+        const double nskq = a.rot ? a.q64[(long)i * IA_DP + IA_D] : 0.0;
         const float am = amx;
         const long n4 = a.nseg / 4;
         const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
@@ -402,7 +414,9 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
         }
         double Tseg, Trow;
         bool force_full;
-        rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+        // an R16 level (a.rot): the screen's bound eps_R (|kappa_skip|^2 in q64 slot 55)
+        if (a.rot) r16_thresholds_rows(emin, am, a.amax[vidx(1)], nqq, nskq, Tseg, Trow, force_full);
+        else rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
         const float twoR = ldexpf(1.f, split16_db_scale(am).R);
         segmin_select(sq4, n4, v, Tseg, slist, &scount);
         __syncthreads();
@@ -621,6 +635,7 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
         __syncthreads();
         stamp(6);
         if (wv != 0) return;
+        if (a.rot && nxt) rot_dma();   // the pool is free: the rotation lands meanwhile
 
         // ---- 4. this rank's winner; sharded DB: publish it, collect every rank's; tail
         XRec lb = wbest[0];
@@ -630,8 +645,10 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
     }
     stamp(8);
     if (wv != 0 || !nxt) return;
-    // ---- 5. the query row of (y, x + 1) for wave t + 1
-    xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace);
+    if (a.rot && !cur) rot_dma();   // (a pixel of wave t + 1 only: the pool was never used)
+    // ---- 5. the query row of (y, x + 1) for wave t + 1 (an R16 level: the rotated row, the
+    // rotation staged in the pool)
+    xw_next_query(a, i, y, x, lane, pdep, own, amx, nxw, trace, a.rot ? rotl : nullptr, a.rot ? dq : nullptr);
 }
 
 // ---- strip-order image-form levels: the exact stage from fp64 windows (k_xstrip) ---------

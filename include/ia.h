@@ -170,15 +170,15 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
                    void *stream);
 
 /* ---- the rotated split-f16 database (R16; replaces the screen's 11 MFMAs
- * per 32x32 tile by 5).  Per level (shard): ia_db_cov -> the 55 x 55 covariance of ~64 k
+ * per 32x32 tile by 4 at P = 3).  Per level (shard): ia_db_cov -> the 55 x 55 covariance of ~64 k
  * sampled centred rows (fp64, cov[0 .. 56*56) row-major, stride 56; the rest of the buffer,
  * ia_db_cov_bytes() in all, is scratch); the caller takes its eigenvectors (host, any
  * orthonormal basis is exact: the bound adapts) and passes rot = V as fp32, rot[k * 56 + j]
  * = V[k][j] with the components j by decreasing variance, in a buffer of 13,312 B (zero
- * padded).  ia_db_build_rot then writes the rotated split rows (ia_db_rot_bytes: 160 B per
- * padded row) and amax[0] = A (as ia_db_build), amax[1] = A_skip (max over rows of the
- * norm of components 11..54; zero it first).  ia_db_rot_applies: 1 where the synthesis
- * uses it (strip-order levels of the fused per-wave kernel). */
+ * padded).  ia_db_build_rot then writes the rotated split rows (ia_db_rot_bytes: 128 B per
+ * padded row at P = 3) and amax[0] = A (as ia_db_build), amax[1] = A_skip (max over rows of
+ * the norm of components P..54; zero it first).  ia_db_rot_applies: 1 where the synthesis
+ * can use it (every level of the fused per-wave kernel, strip-order or not). */
 int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows);
 /* the build's R16 form: components carried as split pairs (P), K-slots per row (16 per MFMA) */
 int ia_db_rot_components(void);
@@ -265,9 +265,9 @@ typedef struct {
     const void *dbi;    /* NULL, or this shard's ia_db_build_image output (the matcher reads
                            it instead of the rows; db may then be NULL; same results) */
     /* NULL, or this shard's rotated database (ia_db_build_rot) and its rotation: on levels
-     * where the fused strip kernel runs (ia_db_rot_applies, one GPU or the device-side
-     * exchange) the screen then streams it (5 MFMAs per tile instead of 11);
-     * amax must then hold 2 floats {A, A_skip}.  Same results. */
+     * where the fused per-wave kernel runs (one GPU or the device-side exchange) the screen
+     * then streams it (4 MFMAs per tile instead of 11) and the exact stage
+     * takes its bound; amax must then hold 2 floats {A, A_skip}.  Same results. */
     const void *dbr;
     const float *rot;
 } IaSynthArgs;
