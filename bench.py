@@ -714,7 +714,7 @@ def main():
     pairs = sum(v[2] for v in lv.values())
     traffic, pmc = None, screen_pmc()
     if pmc and args.config == 'c4' and world == 1 and domG == 11 and lsh is None and \
-            pmc['kernel'].startswith('k_screen16r') == bool(rot_used):
+            ('k_screen16r' in pmc['kernel']) == bool(rot_used):
         traffic = pmc['bytes']
     # the finest level's screen streams the DB's image form when it applies (k_screen16i;
     # k_screen16p, the producer / consumer form, on strip-order levels: every c4 / c5 level)
@@ -756,8 +756,8 @@ def main():
     if traffic is not None:
         roof['traffic_note'] = ('HBM bytes per launch (mean of %d dispatches of %s), PMC FETCH_SIZE '
                                 'x 2 + WRITE_SIZE of bench.py under rocprofv3 (%s); algorithmic: '
-                                'the DB read once (image form: 59 MB of split pixel pairs and '
-                                'norm slots; row form: 939.5 MB) + 11 MB of segment minima'
+                                'the DB read once (R16 rotated rows: 128 B x 4,194,304 = 536.9 MB; '
+                                'split-f16 row form: 939.5 MB) + 11 MB of segment minima'
                                 % (pmc['dispatches'], pmc['kernel'], pmc['source']))
         sq = screen_sq()
         if sq is not None:
