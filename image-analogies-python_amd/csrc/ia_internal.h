@@ -73,6 +73,19 @@ __host__ __device__ __forceinline__ long seg_lrow(const StageMap &m, long seg, i
     const int s = (int)(seg - (chunk << lspc)) * (seg_rows >> 7) + (int)(k >> 7);
     return stage_lrow(m, chunk, s) + (k & 127);
 }
+// the segment holding local row lrow (the inverse of seg_lrow; stages are 128 aligned rows, so
+// every 64-aligned run of 64 rows lies in one segment)
+__host__ __device__ __forceinline__ long seg_of_lrow(const StageMap &m, long lrow, int seg_rows) {
+    const int lspc = __builtin_ctz((unsigned)(m.sc * 128 / seg_rows));
+    const int lsst = __builtin_ctz((unsigned)(seg_rows >> 7));   // log2 stages per segment
+    if (m.W == 0) return lrow / seg_rows;
+    const long y = lrow / m.W;
+    const int x = (int)(lrow - y * m.W);
+    const long yb = y / m.sc;
+    const int s = (int)(y - yb * m.sc);
+    const long chunk = yb * m.nstrip + (x >> 7);
+    return (chunk << lspc) + (s >> lsst);
+}
 static inline bool db_strips_enabled() {
     static const int v = env_int("IA_DB_STRIPS", 1);
     return v != 0;
@@ -233,6 +246,7 @@ struct XJob {
     gptr<unsigned int> ctl;                         // tickets[2], error word
     gptr<const void> dbr;                           // R16 rotated DB (nullable)
     gptr<const float> rot;                          // R16 rotation (nullable)
+    gptr<const unsigned char> askc;                 // R16 per-segment skip codes (nullable)
 };
 constexpr int IA_BATCH_MAX = 128;
 
@@ -266,6 +280,7 @@ struct XArgs {
     gptr<unsigned long long> trace;  // diagnostic (nullable): phase stamps, XW_TRACE_* below
     gptr<const float> rot;        // R16 level (k_xstrip only, nullable): the rotation; q16n rows in
                                   // the R16 layout, q64 slot 55 = |kappa_skip|^2, amax[1] = A_skip
+    gptr<const unsigned char> askc;  // R16 level: per-segment skip codes (r16_askc, ia_rot16.h)
 };
 // k_xwave phase stamps (IA_XW_TRACE=<level tag>, ia_diag_xwave_trace): s_memrealtime (100
 // MHz) at XW_TRACE_N - 1 points of the pixels with ticket < XW_TRACE_PX of waves < XW_TRACE_T;

@@ -32,6 +32,7 @@
 //   DB: per 32-row tile, R16_MFMA groups x 64 lanes x half8: group m, lane (h * 32 + row).
 //   query: a q16 row (Q16_ROW = 16 half8), half8 index h * R16_MFMA + m.
 #pragma once
+#include "ia_internal.h"
 #include "ia_split16.h"
 
 namespace ia {
@@ -51,6 +52,17 @@ constexpr int R16_LD = 56;                     // rot[k * R16_LD + j] = V[k][j] 
 // the rotation buffer: 56 x 56 floats, padded to whole 1 KiB LDS-DMA pieces (13)
 constexpr int R16_ROT_FLOATS = 13 * 256;
 constexpr int R16_ROT_B = R16_ROT_FLOATS * 4;  // 13,312 B
+
+// the rotated DB buffer (ia_db_rot_bytes): the rows (R16_ROW_B each, padded), then per
+// segment A_skip,j (fp32, rounded up: max over the segment's rows of |fl32(rho_skip)|), then per
+// segment the code c_j with A_skip c_j / 255 >= A_skip,j (u8; the exact stage's skip bound)
+static inline size_t r16_askseg_off(long nrows) { return (size_t)db_rows_padded(nrows) * R16_ROW_B; }
+static inline size_t r16_askc_off(long nrows) {
+    return r16_askseg_off(nrows) + img_align((size_t)db_nsegs(nrows) * 4);
+}
+static inline const unsigned char *r16_askc(const void *dbr, long nrows) {
+    return reinterpret_cast<const unsigned char *>(dbr) + r16_askc_off(nrows);
+}
 static_assert(R16_LD * R16_LD <= R16_ROT_FLOATS, "rotation buffer");
 
 // f16 index of slot s inside a query row (h * 5 + m) * 8 + e
@@ -83,6 +95,31 @@ __device__ __forceinline__ void r16_thresholds(float emin, float amax0, float as
     const double eps = r16_eps(A, nqq, (double)askip, nsk);
     const double slack = 1e-12 * (fabs(em) + nqq + A * A);
     Tseg = ldexp(em + 2.0 * eps + slack, e2);
+    force_full = eq + sc.R < -10;
+}
+
+// Per-segment skip bound (k_xstrip): segment j's rows have |rho_skip| <=
+// A_skip,j <= A_skip c_j / 255 (r16_askc), so eps_j = eps_0 + K c_j with eps_0 = r16_eps(.., 0, ..)
+// and K = 2^-9 1.01 |q'_skip| A_skip / 255.  The oracle winner r_o (segment o) has
+// m_o - eps_o <= D(r_o) <= min_i (m_i + eps_i) =: U, so segment j is a candidate iff
+// m_j <= U + eps_j = (U - eps_0) + 2 eps_0 + K c_j.  In screen units (2^e2): r16_kseg gives K
+// before the minima are reduced; the reduction forms u = min_i fl32(m_i + Kf c_i) (Kf = K rounded
+// up to fp32, so u >= min_i (m_i + K c_i) up to the rounding 2^-24 |u|, covered by 2^-23 |u|);
+// r16_tseg0 gives T0 and the test is m_j <= T0 + K c_j.
+__device__ __forceinline__ double r16_kseg(float amax0, float askip, double nqq, double nsk) {
+    const Split16Db sc = split16_db_scale(amax0);
+    const int e2 = sc.ea + split16_q_scale(nqq, sc.R);
+    return ldexp(0x1p-9 * 1.01 * sqrt(nsk) * (double)askip / 255.0, e2);
+}
+__device__ __forceinline__ void r16_tseg0(float umin, float amax0, double nqq, double &T0, bool &force_full) {
+    const double A = (double)amax0;
+    const Split16Db sc = split16_db_scale(amax0);
+    const int eq = split16_q_scale(nqq, sc.R);
+    const int e2 = sc.ea + eq;
+    const double em = ldexp((double)umin, -e2);
+    const double eps0 = r16_eps(A, nqq, 0.0, 0.0);
+    const double slack = 1e-12 * (fabs(em) + nqq + A * A) + 0x1p-23 * fabs(em);
+    T0 = ldexp(em + 2.0 * eps0 + slack, e2);
     force_full = eq + sc.R < -10;
 }
 

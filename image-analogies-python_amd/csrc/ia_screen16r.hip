@@ -356,7 +356,8 @@ __global__ __launch_bounds__(256) void k_db_cov_reduce(const double *__restrict_
 __global__ __launch_bounds__(256) void k_db_build_rot(DbSrc src, long row0, long nrows, long npad,
                                                       const double *__restrict__ center,
                                                       const float *__restrict__ rot, float *amax,
-                                                      half8 *__restrict__ dbr) {
+                                                      half8 *__restrict__ dbr, StageMap sm, int seg_rows,
+                                                      unsigned *__restrict__ askseg) {
     __shared__ __attribute__((aligned(16))) float R[R16_LD * R16_LD];
     __shared__ float red[4];
     for (int i = threadIdx.x; i < R16_LD * R16_LD / 4; i += 256)
@@ -422,6 +423,10 @@ __global__ __launch_bounds__(256) void k_db_build_rot(DbSrc src, long row0, long
         if ((double)askip < a) askip = nextafterf(askip, INFINITY);
     }
     for (int o = 32; o > 0; o >>= 1) askip = fmaxf(askip, __shfl_xor(askip, o));
+    // the wave's 64 rows lie in one segment (64-aligned rows of one 128-row stage): its
+    // A_skip,j (non-negative floats order like their bit patterns)
+    const long pw = p - (threadIdx.x & 63);
+    if ((threadIdx.x & 63) == 0 && pw < npad) atomicMax(askseg + seg_of_lrow(sm, pw, seg_rows), __float_as_uint(askip));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = askip;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -429,6 +434,22 @@ __global__ __launch_bounds__(256) void k_db_build_rot(DbSrc src, long row0, long
         // non-negative floats order like their bit patterns
         atomicMax(reinterpret_cast<unsigned int *>(amax + 1), __float_as_uint(m));
     }
+}
+
+// per segment j the code c_j = ceil(255 A_skip,j / A_skip) (so A_skip c_j / 255 >= A_skip,j,
+// checked in fp64 and bumped), the exact stage's per-segment skip bound (r16_askc)
+__global__ __launch_bounds__(256) void k_askseg_codes(const float *__restrict__ askseg, const float *__restrict__ amax,
+                                                      long nseg, unsigned char *__restrict__ codes) {
+    const long j = (long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nseg) return;
+    const double ag = (double)amax[1], aj = (double)askseg[j];
+    int c = 0;
+    if (ag > 0.0 && aj > 0.0) {
+        c = (int)ceil(255.0 * aj / ag);
+        c = c < 1 ? 1 : (c > 255 ? 255 : c);
+        while (c < 255 && ag * c / 255.0 < aj) ++c;
+    }
+    codes[j] = (unsigned char)c;
 }
 
 // query rows of caller-provided fp64 features (q64 rows of IA_DP), R16 layout (diagnostics)
@@ -540,7 +561,7 @@ int ia_screen_resources(int which, int *lds, int *vgprs) {
 int ia_db_rot_components(void) { return R16_P; }
 int ia_db_rot_slots(void) { return R16_SLOTS; }
 
-size_t ia_db_rot_bytes(long nrows) { return nrows > 0 ? (size_t)db_rows_padded(nrows) * R16_ROW_B : 0; }
+size_t ia_db_rot_bytes(long nrows) { return nrows > 0 ? r16_askc_off(nrows) + img_align((size_t)db_nsegs(nrows)) : 0; }
 
 size_t ia_db_cov_bytes(void) { return (size_t)(R16_LD * R16_LD + COV_BLOCKS * COV_PAIRS) * sizeof(double); }
 
@@ -574,9 +595,19 @@ int ia_db_build_rot(const IaSrcLevel *src, long row0, long nrows, const double *
     // A (amax[0]) first: max with its prior value (the image form's, if built: the same bound)
     const int rc = launch_db_amax(src, d, center, amax, reinterpret_cast<double *>(dbr), st);
     if (rc) return rc;
+    const StageMap sm = db_stage_map(row0, nrows, src->Aw, src->Ah);
+    const long nseg = db_nsegs(nrows);
+    char *tail = reinterpret_cast<char *>(dbr);
+    unsigned *askseg = reinterpret_cast<unsigned *>(tail + r16_askseg_off(nrows));
+    IA_HIP(hipMemsetAsync(askseg, 0, (size_t)nseg * 4, st));
     k_db_build_rot<<<(unsigned)((npad + 255) / 256), 256, 0, st>>>(d, row0, nrows, npad, center, rot, amax,
-                                                                  reinterpret_cast<half8 *>(dbr));
+                                                                  reinterpret_cast<half8 *>(dbr), sm,
+                                                                  db_seg_rows(nrows), askseg);
     IA_LAUNCH_CHECK("k_db_build_rot");
+    k_askseg_codes<<<(unsigned)((nseg + 255) / 256), 256, 0, st>>>(
+        reinterpret_cast<const float *>(askseg), amax, nseg,
+        reinterpret_cast<unsigned char *>(tail + r16_askc_off(nrows)));
+    IA_LAUNCH_CHECK("k_askseg_codes");
     return IA_OK;
 }
 

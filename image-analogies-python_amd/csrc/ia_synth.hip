@@ -17,6 +17,7 @@
 //   k_finish      -> coherence, kappa test, B'/s/im update (this file)
 #include "ia_finish.h"
 #include "ia_split16.h"
+#include "ia_rot16.h"
 #include "../../include/ia_diag.h"
 
 #include <cstdio>
@@ -535,6 +536,7 @@ struct LevelRun {
         J.dbox = ws.dbox;
         J.ctl = ws.ctl;
         J.dbr = r16 ? a->dbr : nullptr;
+        J.askc = r16 ? r16_askc(a->dbr, a->nrows) : nullptr;
         J.rot = r16 ? a->rot : nullptr;
         return J;
     }
@@ -639,6 +641,7 @@ struct LevelRun {
         x.jobs = jt;
         x.trace = xw_trace(a->tag);
         x.rot = r16 ? a->rot : nullptr;
+        x.askc = r16 ? r16_askc(a->dbr, a->nrows) : nullptr;
         const int R = M > y_lo_n + M_n - y_lo ? M : y_lo_n + M_n - y_lo;
         const int form = !im ? XW_ROWS
                        : (xwave_on() == 2 && sm.W > 0 && xstrip_applies(src)) ? XW_STRIP : XW_IMG;

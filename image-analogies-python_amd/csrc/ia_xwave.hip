@@ -140,6 +140,7 @@ __device__ __forceinline__ void xjob_apply(XArgs &a, const XJob &J, int b) {
     a.f.Bp_lg = J.Bp_lg;
     a.f.s = J.s; a.f.im = J.im; a.f.dbg_px = J.dbg_px; a.f.dbg_dist = J.dbg_dist;
     a.rot = J.rot;
+    a.askc = J.askc;
 }
 
 // a workgroup barrier that orders LDS only: __syncthreads() also waits for every global load
@@ -946,6 +947,69 @@ __device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, 
         }
     }
 }
+// R16 levels: the same phases with the per-segment skip bound (ia_rot16.h r16_kseg): cv[j] holds
+// the codes of the 4 segments of v[j] (one byte each, r16_askc); the reduction takes
+// min fl32(m + Kf c) and the selection m <= T0 + K c
+__device__ __forceinline__ void seg3_load_codes(const unsigned *ac4, long n4, int t3, unsigned (&cv)[XS_REG]) {
+#pragma unroll
+    for (int j = 0; j < XS_REG; ++j) {
+        const long i = t3 + (long)j * 192;
+        cv[j] = ac4[i < n4 ? i : 0];
+    }
+}
+__device__ __forceinline__ float seg_uval(float m, unsigned c, int b, float Kf) {
+    return fmaf(Kf, (float)((c >> (8 * b)) & 255u), m);
+}
+__device__ __forceinline__ float seg3_wave_umin(const float4 *sq4, const unsigned *ac4, long n4, int t3,
+                                                const float4 (&v)[XS_REG], const unsigned (&cv)[XS_REG], float Kf) {
+    float u = FLT_MAX;
+#pragma unroll
+    for (int j = 0; j < XS_REG; ++j)
+        u = fminf(u, fminf(fminf(seg_uval(v[j].x, cv[j], 0, Kf), seg_uval(v[j].y, cv[j], 1, Kf)),
+                           fminf(seg_uval(v[j].z, cv[j], 2, Kf), seg_uval(v[j].w, cv[j], 3, Kf))));
+    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+        const float4 x = sq4[i];
+        const unsigned c = ac4[i];
+        u = fminf(u, fminf(fminf(seg_uval(x.x, c, 0, Kf), seg_uval(x.y, c, 1, Kf)),
+                           fminf(seg_uval(x.z, c, 2, Kf), seg_uval(x.w, c, 3, Kf))));
+    }
+    for (int o = 32; o > 0; o >>= 1) u = fminf(u, __shfl_xor(u, o));
+    return u;
+}
+__device__ __forceinline__ unsigned seg_sel4(const float4 &x, unsigned c, double T0, double K) {
+    return ((double)x.x <= fma(K, (double)(c & 255u), T0) ? 1u : 0u) |
+           ((double)x.y <= fma(K, (double)((c >> 8) & 255u), T0) ? 2u : 0u) |
+           ((double)x.z <= fma(K, (double)((c >> 16) & 255u), T0) ? 4u : 0u) |
+           ((double)x.w <= fma(K, (double)(c >> 24), T0) ? 8u : 0u);
+}
+__device__ __forceinline__ void seg3_select_codes(const float4 *sq4, const unsigned *ac4, long n4, int t3,
+                                                  const float4 (&v)[XS_REG], const unsigned (&cv)[XS_REG],
+                                                  double T0, double K, int *slist, int *scount) {
+    unsigned long long m = 0;
+#pragma unroll
+    for (int j = 0; j < XS_REG; ++j) m |= (unsigned long long)seg_sel4(v[j], cv[j], T0, K) << (4 * j);
+    if (m) {
+        int pos = atomicAdd(scount, __builtin_popcountll(m));
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            if (pos < RESCORE_SEGCAP) slist[pos] = 4 * (t3 + (b >> 2) * 192) + (b & 3);
+            ++pos;
+        }
+    }
+    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+        unsigned mt = seg_sel4(sq4[i], ac4[i], T0, K);
+        if (mt) {
+            int pos = atomicAdd(scount, __builtin_popcount(mt));
+            while (mt) {
+                const int b = __builtin_ctz(mt);
+                mt &= mt - 1;
+                if (pos < RESCORE_SEGCAP) slist[pos] = (int)(4 * i + b);
+                ++pos;
+            }
+        }
+    }
+}
 // a barrier of waves 0, 2 and 3 only (an LDS counter; wave 1 never takes part): generation g
 // releases when all three have arrived for the g-th time
 __device__ __forceinline__ void sync3(unsigned *cnt, unsigned g, int lane) {
@@ -1056,7 +1120,12 @@ __global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArg
         const long n4 = a.nseg / 4;
         const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
         float4 v[XS_REG];
-        if (wv != 1) seg3_load(sq4, n4, t3, v);
+        unsigned sgc[XS_REG];
+        const unsigned *ac4 = ROT ? reinterpret_cast<const unsigned *>(a.askc.get()) : nullptr;
+        if (wv != 1) {
+            seg3_load(sq4, n4, t3, v);
+            if constexpr (ROT) seg3_load_codes(ac4, n4, t3, sgc);
+        }
         const int rr0 = y - 2 + lane / 5, rc0 = x - 2 + lane % 5;
         const bool cpos_ok = wv == 1 && lane < XW_NCOH && rr0 >= 0 && rc0 >= 0 && rc0 < W &&
                              (rr0 < y || rc0 < x);
@@ -1067,8 +1136,18 @@ __global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArg
         // the loads above stay in this round trip (not sunk to their first use, after the
         // segment minima's wait: one more round trip on wave 1's path)
         asm volatile("" ::: "memory");
+        // R16: K of the per-segment skip bound, and Kf = K rounded up to fp32
+        double Kd = 0.0;
+        if constexpr (ROT) Kd = r16_kseg(am, ask, nqq, nsk);
         if (wv != 1) {
-            const float ewv = seg3_wave_min(sq4, n4, t3, v);
+            float ewv;
+            if constexpr (ROT) {
+                float Kf = (float)Kd;
+                if ((double)Kf < Kd) Kf = nextafterf(Kf, INFINITY);
+                ewv = seg3_wave_umin(sq4, ac4, n4, t3, v, sgc, Kf);
+            } else {
+                ewv = seg3_wave_min(sq4, n4, t3, v);
+            }
             if (lane == 0) redf[wv] = ewv;
         }
         if (wv == 1) wstamp(14);
@@ -1143,9 +1222,13 @@ __global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArg
             xw_stamp(trace, 2);
             double Tseg, Trow;
             bool force_full;
-            if constexpr (ROT) r16_thresholds(emin, am, ask, nqq, nsk, Tseg, force_full);
-            else rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
-            seg3_select(sq4, n4, t3, v, Tseg, slist, &scount);
+            if constexpr (ROT) {
+                r16_tseg0(emin, am, nqq, Tseg, force_full);   // emin: min (m + Kf c)
+                seg3_select_codes(sq4, ac4, n4, t3, v, sgc, Tseg, Kd, slist, &scount);
+            } else {
+                rescore_thresholds(emin, am, nqq, Tseg, Trow, force_full);
+                seg3_select(sq4, n4, t3, v, Tseg, slist, &scount);
+            }
             sync3(&bar3, 2, lane);
             xw_stamp(trace, 3);
             ns = scount;

@@ -1,7 +1,8 @@
 """The rotated split-f16 screen (R16; csrc/ia_rot16.h, ia_screen16r.hip) on
 the GPU: its segment minima stay inside the bound eps_R the exact stage relies on (every
-block shape of the launcher, input scales 1e-3 / 1 / 1e3), A_skip bounds every row's
-skipped components, and syntheses through it equal the split-f16 image form bit for bit
+block shape of the launcher, input scales 1e-3 / 1 / 1e3), even with the per-segment skip
+bound eps_j of k_xstrip; A_skip bounds every row's skipped components and A_skip,j every row of
+segment j; and syntheses through it equal the split-f16 image form bit for bit
 (the oracle fixtures of c4 / c5 run through it by default)."""
 import ctypes
 import math
@@ -51,7 +52,18 @@ def _r16_vs_fp64(idx, As, Q, Ms):
     assert np.sqrt(na.max()) <= amax * (1 + 1e-6)
     V = idx.rot.cpu().numpy()[:56 * 56].reshape(56, 56)[:55, :55].astype(np.float64)
     rho = (a @ V).astype(np.float32).astype(np.float64)
-    assert np.sqrt((rho[:, R16_P:] ** 2).sum(1).max()) <= askip * (1 + 1e-6)
+    skn = np.sqrt((rho[:, R16_P:] ** 2).sum(1))
+    assert skn.max() <= askip * (1 + 1e-6)
+    # per segment (ia_rot16.h r16_askc): A_skip,j bounds the segment's rows, and its code's
+    # decoded value A_skip c_j / 255 bounds A_skip,j
+    tail = idx.dbr.view(torch.uint8)[npad * lib.ia_db_rot_slots() * 2:]
+    ask_seg = tail[:4 * nseg].view(torch.float32).cpu().numpy().astype(np.float64)
+    codes = tail[(4 * nseg + 255) // 256 * 256:][:nseg].cpu().numpy().astype(np.float64)
+    skp = np.concatenate([skn, np.repeat(skn[-1:], npad - N)])
+    assert (skp[order].reshape(nseg, seg).max(1) <= ask_seg).all()
+    ask_dec = askip * codes / 255.0
+    assert (ask_dec >= ask_seg).all() and (codes <= 255).all()
+    assert ask_dec.mean() < 0.9 * askip, 'per-segment bounds tighter than the global one'
     exact = np.empty((Mmax, nseg))
     for m0 in range(0, Mmax, 64):
         E = na[:, None] - 2.0 * (a @ (Q[m0:m0 + 64] - c).T)
@@ -78,9 +90,10 @@ def _r16_vs_fp64(idx, As, Q, Ms):
             assert nsks[m] == pytest.approx(float((kap[R16_P:] ** 2).sum()), rel=1e-9, abs=1e-300)
             ea, R, eq = _scales(amax, float(nqs[m]))
             true = np.ldexp(exact[m], ea + eq)
+            # eps_j of segment j (the per-segment skip bound k_xstrip uses; <= the global eps_R)
             eps = U32 * (360 * amax * math.sqrt(nqs[m]) + 60 * amax * amax) + \
-                2.0 ** -9 * 1.01 * askip * math.sqrt(nsks[m])
-            worst = max(worst, np.abs(got[m] - true).max() / np.ldexp(eps, ea + eq))
+                2.0 ** -9 * 1.01 * ask_dec * math.sqrt(nsks[m])
+            worst = max(worst, (np.abs(got[m] - true) / np.ldexp(eps, ea + eq)).max())
     return worst
 
 
