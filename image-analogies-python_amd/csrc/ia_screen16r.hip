@@ -41,6 +41,17 @@ constexpr int R16_RING = IA_R16_RING;
 #ifndef IA_R16_LAB
 #define IA_R16_LAB 0
 #endif
+// A/B builds only: IA_R16_NOBAR=1 drops the per-stage barrier (wrong minima; timing of the
+// compute floor without it), IA_R16_NOFOLD=1 folds one accumulator element per chain
+#ifndef IA_R16_NOBAR
+#define IA_R16_NOBAR 0
+#endif
+#ifndef IA_R16_NOFOLD
+#define IA_R16_NOFOLD 0
+#endif
+#ifndef IA_R16_NOLDS
+#define IA_R16_NOLDS 0   // A/B builds only: the tile operands read once per stage (wrong minima)
+#endif
 // the stage's instruction order: 1 pins each chain as MFMA, 2 VALU of the previous chain's
 // fold, MFMA, ... (sched_group_barrier), 0 leaves it to the compiler
 #ifndef IA_R16_PIN
@@ -82,6 +93,26 @@ __host__ __device__ constexpr int ch_uo(int c) {
     for (int i = 1; i <= c; ++i) o += ch_u<G, W>(i) != ch_u<G, W>(i - 1) ? 1 : 0;
     return o;
 }
+// the first chain after chain c's tile run (the next tile's first chain), or -1
+template <int G, int W>
+__host__ __device__ constexpr int ch_next(int c) {
+    for (int i = c + 1; i < ch_count<G, W>(); ++i)
+        if (ch_u<G, W>(i) != ch_u<G, W>(c)) return i;
+    return -1;
+}
+// chain c starts a tile run
+template <int G, int W>
+__host__ __device__ constexpr bool ch_first(int c) { return c == 0 || ch_u<G, W>(c) != ch_u<G, W>(c - 1); }
+// when the next tile's operands are read from LDS: 1 at the first chain of the current tile's
+// run (2-3 chains ahead), 0 at its last chain (one chain ahead)
+#ifndef IA_R16_PF
+#define IA_R16_PF 1
+#endif
+template <int G, int W>
+__host__ __device__ constexpr bool ch_reads_next(int c) {
+    return IA_R16_PF ? (ch_first<G, W>(c) && ch_next<G, W>(c) >= 0)
+                     : (c + 1 < ch_count<G, W>() && ch_u<G, W>(c + 1) != ch_u<G, W>(c));
+}
 template <int K, int N, typename F>
 __device__ __forceinline__ void sfor(F &&f) {
     if constexpr (K < N) {
@@ -114,18 +145,25 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
         const half8 *p = sb + ch_u<G, W>(0) * R16_TILE_H8 + lane;
 #pragma unroll
         for (int m = 0; m < R16_MFMA; ++m) a[0][m] = p[m * 64];
+        if constexpr (IA_R16_NOLDS) {
+#pragma unroll
+            for (int m = 0; m < R16_MFMA; ++m) a[1][m] = a[0][m];
+        }
     }
     sfor<0, NC>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         constexpr int k = ch_k<G, W>(c), ab = ch_uo<G, W>(c) & 1, cb = c & 1;
-        if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c)) {
-            const half8 *p = sb + ch_u<G, W>(c + 1) * R16_TILE_H8 + lane;
+        if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c)) {
+            const half8 *p = sb + ch_u<G, W>(ch_next<G, W>(c)) * R16_TILE_H8 + lane;
 #pragma unroll
             for (int m = 0; m < R16_MFMA; ++m) a[ab ^ 1][m] = p[m * 64];
+        } else if constexpr (IA_R16_NOLDS == 2 && ch_reads_next<G, W>(c)) {
+#pragma unroll
+            for (int m = 0; m < R16_MFMA; ++m) asm volatile("" : "+v"(a[ab ^ 1][m]));   // opaque: no CSE
         }
         acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
         if constexpr (c > 0) {
-            if constexpr (IA_R16_LAB == 3) mn[ch_k<G, W>(c - 1)] = fminf(mn[ch_k<G, W>(c - 1)], acc[cb ^ 1][0]);
+            if constexpr (IA_R16_LAB == 3 || IA_R16_NOFOLD) mn[ch_k<G, W>(c - 1)] = fminf(mn[ch_k<G, W>(c - 1)], acc[cb ^ 1][0]);
             else fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
         }
 #pragma unroll
@@ -134,7 +172,7 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
         if constexpr (IA_R16_PIN && IA_R16_LAB <= 1) {
             // [the next tile's 5 operand reads,] MFMA 0, then the previous chain's fold two
             // VALU at a time between the remaining MFMAs
-            if constexpr (c + 1 < NC && ch_u<G, W>(c + 1) != ch_u<G, W>(c))
+            if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c))
                 __builtin_amdgcn_sched_group_barrier(0x100, R16_MFMA, 0);   // DS reads
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
             if constexpr (c > 0) {
@@ -251,7 +289,7 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
         // stage s + 1 landed: the R16_RING - 2 stages issued after it may stay in flight
         if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(R16_MFMA * (R16_RING - 2)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stage_barrier();   // (every wave's reads of stage s done: its buffer is refilled next)
+        if constexpr (!IA_R16_NOBAR) stage_barrier();   // (every wave's reads of stage s done: its buffer is refilled next)
     }
 }
 
