@@ -133,6 +133,14 @@ __device__ __forceinline__ void fold_min(const floatx16 &x, float &mn) {
     mn = fminf(fminf(mn, u0), u1);
 }
 
+// the chain whose accumulator chain c's MFMAs fold (IA_R16_LAG = 1: the previous chain, right
+// after its last MFMA (the compiler pads the MFMA -> VALU hazard with s_nop); 2: the one before,
+// with one more accumulator, far enough back that no pad is needed)
+#ifndef IA_R16_LAG
+#define IA_R16_LAG 2
+#endif
+constexpr int R16_NACC = IA_R16_LAG + 1;
+
 // wave W's chains of one stage (operand sb in LDS), chain-major with two operand sets
 template <int G, int W, int NS>
 __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS][R16_MFMA], float (&mn)[NS],
@@ -140,7 +148,7 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
     constexpr int NC = ch_count<G, W>();
     const floatx16 zero = {};
     half8 a[2][R16_MFMA];
-    floatx16 acc[2];
+    floatx16 acc[R16_NACC];
     {
         const half8 *p = sb + ch_u<G, W>(0) * R16_TILE_H8 + lane;
 #pragma unroll
@@ -152,7 +160,8 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
     }
     sfor<0, NC>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
-        constexpr int k = ch_k<G, W>(c), ab = ch_uo<G, W>(c) & 1, cb = c & 1;
+        constexpr int k = ch_k<G, W>(c), ab = ch_uo<G, W>(c) & 1, cb = c % R16_NACC;
+        constexpr int cf = c - IA_R16_LAG, fb = (c + 1) % R16_NACC;   // the chain folded here
         if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c)) {
             const half8 *p = sb + ch_u<G, W>(ch_next<G, W>(c)) * R16_TILE_H8 + lane;
 #pragma unroll
@@ -162,9 +171,9 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
             for (int m = 0; m < R16_MFMA; ++m) asm volatile("" : "+v"(a[ab ^ 1][m]));   // opaque: no CSE
         }
         acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
-        if constexpr (c > 0) {
-            if constexpr (IA_R16_LAB == 3 || IA_R16_NOFOLD) mn[ch_k<G, W>(c - 1)] = fminf(mn[ch_k<G, W>(c - 1)], acc[cb ^ 1][0]);
-            else fold_min(acc[cb ^ 1], mn[ch_k<G, W>(c - 1)]);
+        if constexpr (cf >= 0) {
+            if constexpr (IA_R16_LAB == 3 || IA_R16_NOFOLD) mn[ch_k<G, W>(cf)] = fminf(mn[ch_k<G, W>(cf)], acc[fb][0]);
+            else fold_min(acc[fb], mn[ch_k<G, W>(cf)]);
         }
 #pragma unroll
         for (int m = 1; m < (IA_R16_LAB == 2 ? 1 : R16_MFMA); ++m)
@@ -175,7 +184,7 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
             if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c))
                 __builtin_amdgcn_sched_group_barrier(0x100, R16_MFMA, 0);   // DS reads
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
-            if constexpr (c > 0) {
+            if constexpr (cf >= 0) {
                 sfor<0, R16_MFMA - 1>([&](auto) {
                     __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);      // VALU
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      // MFMA
@@ -186,7 +195,10 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
             __builtin_amdgcn_sched_barrier(0);
         }
     });
-    fold_min(acc[(NC - 1) & 1], mn[ch_k<G, W>(NC - 1)]);
+    sfor<(NC > IA_R16_LAG ? NC - IA_R16_LAG : 0), NC>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        fold_min(acc[c % R16_NACC], mn[ch_k<G, W>(c)]);
+    });
 }
 
 // LDS integer min as inline asm: the compiler's waitcnt pass treats an LDS atomic as a store
