@@ -93,6 +93,7 @@ _SIGS = {
     'ia_screen_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'ia_fused_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'ia_db_rot_slots': (ctypes.c_int, []),
+    'ia_db_rot_eps_a2': (ctypes.c_double, []),
     'ia_db_cov_bytes': (ctypes.c_size_t, []),
     'ia_db_cov': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp, _dp]),
     'ia_db_build_rot': (ctypes.c_int, [ctypes.POINTER(IaSrcLevel), ctypes.c_long, ctypes.c_long, _dp, _dp,

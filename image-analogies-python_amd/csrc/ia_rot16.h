@@ -72,15 +72,25 @@ __host__ __device__ constexpr int r16_qpos(int s) {
 // half8 index (in a tile) and element of slot s of tile row j (0..31)
 __host__ __device__ constexpr int r16_dgrp(int s, int j) { return (s >> 4) * 64 + ((s & 15) >> 3) * 32 + j; }
 
+// The screen's MFMA shape (ia_screen16r.hip): 16 = two v_mfma_f32_16x16x32_f16 per 16x16 block
+// (P = 3 only), 32 = R16_MFMA v_mfma_f32_32x32x16_f16 per 32x32 tile
+#ifndef IA_R16_SHAPE
+#define IA_R16_SHAPE 16
+#endif
+constexpr bool R16_S16 = IA_R16_SHAPE == 16 && R16_MFMA == 4;
 // The bound of DESIGN.md §4d: |s(r) / (sa sq) + |q'|^2 - D(r)| <= eps_R with
-//   eps_R = u (360 A|q'| + 60 A^2) + 2^-9 1.01 A_skip |q'_skip|,  u = 2^-24
-// (representation 14u(2A|q'| + A^2), f16 flush <= u(28.5 A|q'| + 7.1 A^2), accumulation over
-// <= 5 MFMAs with the main mass in at most four <= 32u(4 Y_dot + Y_norm + 5X) ~ u(256.4 A|q'|
-// + 32.1 A^2), the fp32 rotation's non-orthogonality 2 |V_f V_f^T - I| A|q'| <= 30u A|q'|;
-// the skipped components' dropped cross terms <= (2^-10 + 2^-21) |alpha_skip| |beta_skip|).
+//   eps_R = u (360 A|q'| + E2 A^2) + 2^-9 1.01 A_skip |q'_skip|,  u = 2^-24
+// (representation 14u(2A|q'| + A^2), f16 flush <= u(28.5 A|q'| + 7.1 A^2), the fp32 rotation's
+// non-orthogonality 2 |V_f V_f^T - I| A|q'| <= 30u A|q'|, the skipped components' dropped cross
+// terms <= (2^-10 + 2^-21) |alpha_skip| |beta_skip|, and the accumulation: an MFMA adding K
+// products to C costs <= 2Ku (|C_in| + sum |p|); 32x32x16 (K = 16), <= 5 MFMAs with the main
+// mass in at most four: <= 32u(4 Y_dot + Y_norm + 5X) ~ u(256.4 A|q'| + 32.1 A^2), E2 = 60;
+// 16x16x32 (K = 32), 2 MFMAs: <= 64u(2 Y_dot + Y_norm (1 + 2^-10) + 2X) ~ u(256.3 A|q'| + 64.2
+// A^2), E2 = 90 (the A^2 terms sum to 85.4)).
+constexpr double R16_EPS_A2 = R16_S16 ? 90.0 : 60.0;
 __device__ __forceinline__ double r16_eps(double A, double nqq, double Askip, double nsk) {
     constexpr double U32 = 5.9604644775390625e-08;
-    return U32 * (360.0 * A * sqrt(nqq) + 60.0 * A * A) + 0x1p-9 * 1.01 * Askip * sqrt(nsk);
+    return U32 * (360.0 * A * sqrt(nqq) + R16_EPS_A2 * A * A) + 0x1p-9 * 1.01 * Askip * sqrt(nsk);
 }
 
 // the exact stage's segment threshold (and force_full) for an R16 screen, as

@@ -175,10 +175,19 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
             if constexpr (IA_R16_LAB == 3 || IA_R16_NOFOLD) mn[ch_k<G, W>(cf)] = fminf(mn[ch_k<G, W>(cf)], acc[fb][0]);
             else fold_min(acc[fb], mn[ch_k<G, W>(cf)]);
         }
+        if constexpr (IA_R16_LAB == 4) {
+            // A/B only: the chain's other MFMAs independent of each other (wrong minima; timing of
+            // the same MFMA and fold count without the accumulate dependency)
+            floatx16 x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][1], bq[k][1], zero, 0, 0, 0);
+            floatx16 x2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][2], bq[k][2], zero, 0, 0, 0);
+            floatx16 x3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][3], bq[k][3], zero, 0, 0, 0);
+            asm volatile("" :: "v"(x1), "v"(x2), "v"(x3));   // kept (no instruction, no hazard)
+        } else {
 #pragma unroll
-        for (int m = 1; m < (IA_R16_LAB == 2 ? 1 : R16_MFMA); ++m)
-            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][m], bq[k][m], acc[cb], 0, 0, 0);
-        if constexpr (IA_R16_PIN && IA_R16_LAB <= 1) {
+            for (int m = 1; m < (IA_R16_LAB == 2 ? 1 : R16_MFMA); ++m)
+                acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][m], bq[k][m], acc[cb], 0, 0, 0);
+        }
+        if constexpr (IA_R16_PIN && (IA_R16_LAB <= 1 || IA_R16_LAB == 4)) {
             // [the next tile's 5 operand reads,] MFMA 0, then the previous chain's fold two
             // VALU at a time between the remaining MFMAs
             if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c))
@@ -198,6 +207,102 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
     sfor<(NC > IA_R16_LAG ? NC - IA_R16_LAG : 0), NC>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         fold_min(acc[c % R16_NACC], mn[ch_k<G, W>(c)]);
+    });
+}
+
+// ---- the 16x16x32 form (IA_R16_SHAPE = 16): v_mfma_f32_16x16x32_f16, 2 per 16x16 (rows x
+// queries) block at K = 64 slots.  Same DB stages and LDS layout (a lane's 8 slots of a row are
+// one half8 of the 32x32 layout), same units and minima.  Per stage 8 row blocks (v: tile v / 2,
+// rows 16 (v % 2) ..) x 2G query blocks of 16; the 16 G chains (t, v), order 8t + v, are cut
+// into 4 equal runs, one per wave (as bal_*), each run walked row-block-major so that a row
+// block's two operand reads serve all its chains.  Output: lane l holds rows 4 (l / 16) .. + 3
+// of query l % 16, folded per lane, reduced over the 4 lane groups at each segment close.
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+template <int G, int W>
+__host__ __device__ constexpr int c16_lo() { return 4 * G * W; }   // first chain of wave W
+template <int G, int W>
+__host__ __device__ constexpr int c16_t0() { return c16_lo<G, W>() / 8; }
+template <int G, int W>
+__host__ __device__ constexpr int c16_ns() { return (c16_lo<G, W>() + 4 * G - 1) / 8 - c16_t0<G, W>() + 1; }
+template <int G, int W>
+__host__ __device__ constexpr bool c16_on(int k, int v) {
+    return 8 * (c16_t0<G, W>() + k) + v >= c16_lo<G, W>() && 8 * (c16_t0<G, W>() + k) + v < c16_lo<G, W>() + 4 * G;
+}
+template <int G, int W>
+__host__ __device__ constexpr int c16_count() { return 4 * G; }
+template <int G, int W>
+__host__ __device__ constexpr int c16_v(int c) {
+    for (int v = 0; v < 8; ++v)
+        for (int k = 0; k < c16_ns<G, W>(); ++k)
+            if (c16_on<G, W>(k, v) && c-- == 0) return v;
+    return -1;
+}
+template <int G, int W>
+__host__ __device__ constexpr int c16_k(int c) {
+    for (int v = 0; v < 8; ++v)
+        for (int k = 0; k < c16_ns<G, W>(); ++k)
+            if (c16_on<G, W>(k, v) && c-- == 0) return k;
+    return -1;
+}
+template <int G, int W>
+__host__ __device__ constexpr int c16_vo(int c) {   // row blocks started before chain c
+    int o = 0;
+    for (int i = 1; i <= c; ++i) o += c16_v<G, W>(i) != c16_v<G, W>(i - 1) ? 1 : 0;
+    return o;
+}
+template <int G, int W>
+__host__ __device__ constexpr int c16_next(int c) {
+    for (int i = c + 1; i < c16_count<G, W>(); ++i)
+        if (c16_v<G, W>(i) != c16_v<G, W>(c)) return i;
+    return -1;
+}
+template <int G, int W>
+__host__ __device__ constexpr bool c16_first(int c) { return c == 0 || c16_v<G, W>(c) != c16_v<G, W>(c - 1); }
+// half8 offset (in a stage) of lane l's operand of MFMA n for row block v: row 16 (v % 2) +
+// l % 16 of tile v / 2, slots 32 n + 8 (l / 16) .. + 7 = 32x32 group 2n + (l / 16) / 2, half
+// (l / 16) % 2
+__device__ __forceinline__ int s16_aoff(int v, int n, int lane) {
+    const int q = lane >> 4, r = lane & 15;
+    return (v >> 1) * R16_TILE_H8 + ((2 * n + (q >> 1)) * 64 + (q & 1) * 32 + 16 * (v & 1) + r);
+}
+constexpr int S16_LAG = 3;   // chain c folds chain c - S16_LAG (no MFMA -> VALU pads)
+constexpr int S16_NACC = S16_LAG + 1;
+
+template <int G, int W, int NS>
+__device__ __forceinline__ void r16_stage_s16(const half8 *sb, const half8 (&bq)[NS][2], float (&mn)[NS], int lane) {
+    constexpr int NC = c16_count<G, W>();
+    const floatx4 zero = {};
+    half8 a[2][2];
+    floatx4 acc[S16_NACC];
+    a[0][0] = sb[s16_aoff(c16_v<G, W>(0), 0, lane)];
+    a[0][1] = sb[s16_aoff(c16_v<G, W>(0), 1, lane)];
+    sfor<0, NC>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        constexpr int k = c16_k<G, W>(c), ab = c16_vo<G, W>(c) & 1, cb = c % S16_NACC;
+        constexpr int cf = c - S16_LAG, fb = (c + 1) % S16_NACC;
+        constexpr bool rd = c16_first<G, W>(c) && c16_next<G, W>(c) >= 0;
+        if constexpr (rd) {
+            constexpr int vn = c16_v<G, W>(c16_next<G, W>(c));
+            a[ab ^ 1][0] = sb[s16_aoff(vn, 0, lane)];
+            a[ab ^ 1][1] = sb[s16_aoff(vn, 1, lane)];
+        }
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
+        if constexpr (cf >= 0) mn[c16_k<G, W>(cf)] = fminf(mn[c16_k<G, W>(cf)], fminf(acc[fb][0], acc[fb][1]));
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ab][1], bq[k][1], acc[cb], 0, 0, 0);
+        if constexpr (cf >= 0) mn[c16_k<G, W>(cf)] = fminf(mn[c16_k<G, W>(cf)], fminf(acc[fb][2], acc[fb][3]));
+        if constexpr (IA_R16_PIN) {
+            if constexpr (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                     // MFMA
+            if constexpr (cf >= 0) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if constexpr (cf >= 0) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    });
+    sfor<(NC > S16_LAG ? NC - S16_LAG : 0), NC>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        const floatx4 &x = acc[c % S16_NACC];
+        mn[c16_k<G, W>(c)] = fminf(fminf(mn[c16_k<G, W>(c)], fminf(x[0], x[1])), fminf(x[2], x[3]));
     });
 }
 
@@ -225,6 +330,21 @@ __device__ __forceinline__ void r16_close(int s, int tps, int *smin, float (&mn)
         }
     }
 }
+template <int G, int W, int NS>
+__device__ __forceinline__ void r16_close_s16(int s, int tps, int *smin, float (&mn)[NS], int lane) {
+    constexpr int T0 = c16_t0<G, W>();
+    const int done = (s + 1) * STAGE_TILES;
+    if (done % tps == 0) {
+        int *sm = smin + ((done / tps - 1) % SPC_STAGE) * (G * 32);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            float m = fminf(mn[k], __shfl_xor(mn[k], 16));
+            m = fminf(m, __shfl_xor(m, 32));
+            if (lane < 16) lds_min_i32(&sm[(T0 + k) * 16 + lane], fkey(m));
+            mn[k] = FLT_MAX;
+        }
+    }
+}
 
 // a workgroup barrier that orders LDS only: __syncthreads()'s release fence would also wait
 // for every DB stage in flight (s_waitcnt vmcnt(0)), i.e. collapse the ring to one stage.
@@ -246,12 +366,22 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
                                          const StageMap &sm, long chunk, int nstage, int tps,
                                          const half8 *__restrict__ q16, float *__restrict__ segmin,
                                          long seg0, long nseg, int q0, int M) {
-    constexpr int NS = bal_ns(G, W);
+    constexpr int NS = R16_S16 ? c16_ns<G, W>() : bal_ns(G, W);
     constexpr int T0 = bal_t0(G, W);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    half8 bq[NS][R16_MFMA];
-    {
+    half8 bq[NS][R16_S16 ? 2 : R16_MFMA];
+    if constexpr (R16_S16) {
+        // query block T + k, lane l: query 16 (T + k) + l % 16, slots 32 n + 8 (l / 16) .. + 7,
+        // i.e. the half8 (l / 16) % 2 * R16_MFMA + 2n + (l / 16) / 2 of its q16 row
+        const int q = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const half8 *p = q16 + (long)((c16_t0<G, W>() + k) * 16 + c) * Q16_ROW + (q & 1) * R16_MFMA + (q >> 1);
+            bq[k][0] = p[0];
+            bq[k][1] = p[2];
+        }
+    } else {
         const int j = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
@@ -280,10 +410,15 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stage_barrier();
     for (int s = 0; s < nstage; ++s) {
-        const bool more = s + R16_RING - 1 < nstage && IA_R16_LAB != 1;
+        const bool more = s + R16_RING - 1 < nstage && IA_R16_LAB != 1 && IA_R16_LAB != 4;
         if (more) issue(s + R16_RING - 1);   // into the buffer stage s - 1 used (consumed)
-        r16_stage<G, W, NS>(sbuf + (s % R16_RING) * STAGE_H8, bq, mn, lane);
-        r16_close<G, W, NS>(s, tps, smin, mn, lane);
+        if constexpr (R16_S16) {
+            r16_stage_s16<G, W, NS>(sbuf + (s % R16_RING) * STAGE_H8, bq, mn, lane);
+            r16_close_s16<G, W, NS>(s, tps, smin, mn, lane);
+        } else {
+            r16_stage<G, W, NS>(sbuf + (s % R16_RING) * STAGE_H8, bq, mn, lane);
+            r16_close<G, W, NS>(s, tps, smin, mn, lane);
+        }
         const int done = (s + 1) * STAGE_TILES;
         if (done % tps == 0) {
             const int sg = done / tps - 1;            // the segment this stage closed
@@ -610,6 +745,7 @@ int ia_screen_resources(int which, int *lds, int *vgprs) {
 
 int ia_db_rot_components(void) { return R16_P; }
 int ia_db_rot_slots(void) { return R16_SLOTS; }
+double ia_db_rot_eps_a2(void) { return R16_EPS_A2; }
 
 size_t ia_db_rot_bytes(long nrows) { return nrows > 0 ? r16_askc_off(nrows) + img_align((size_t)db_nsegs(nrows)) : 0; }
 

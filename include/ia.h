@@ -175,9 +175,11 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
  * ia_db_cov_bytes() in all, is scratch); the caller takes its eigenvectors (host, any
  * orthonormal basis is exact: the bound adapts) and passes rot = V as fp32, rot[k * 56 + j]
  * = V[k][j] with the components j by decreasing variance, in a buffer of 13,312 B (zero
- * padded).  ia_db_build_rot then writes the rotated split rows (ia_db_rot_bytes: 128 B per
- * padded row at P = 3) and amax[0] = A (as ia_db_build), amax[1] = A_skip (max over rows of
- * the norm of components P..54; zero it first).  ia_db_rot_applies: 1 where the synthesis
+ * padded).  ia_db_build_rot then writes the rotated split rows (128 B per padded row at
+ * P = 3), after them per 512-row segment A_skip,j (fp32, the max over the segment's rows of
+ * the norm of components P..54) and a byte c_j with A_skip c_j / 255 >= A_skip,j (the exact
+ * stage's per-segment bound), ia_db_rot_bytes in all; and amax[0] = A (as ia_db_build),
+ * amax[1] = A_skip (max over all rows; zero it first).  ia_db_rot_applies: 1 where the synthesis
  * can use it (every level of the fused per-wave kernel, strip-order or not). */
 int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows);
 /* the build's R16 form: components carried as split pairs (P), K-slots per row (16 per MFMA) */
@@ -189,6 +191,9 @@ int ia_db_rot_components(void);
 int ia_screen_resources(int which, int *lds, int *vgprs);
 int ia_fused_resources(int rot, int *lds, int *vgprs);
 int ia_db_rot_slots(void);
+/* the A^2 coefficient E2 of the screen's bound eps_R = u (360 A|q'| + E2 A^2) + 2^-9 1.01
+ * A_skip |q'_skip| (90 for the 16x16x32 MFMA form, 60 for 32x32x16) */
+double ia_db_rot_eps_a2(void);
 size_t ia_db_rot_bytes(long nrows);
 size_t ia_db_cov_bytes(void);
 int ia_db_cov(const IaSrcLevel *src, long row0, long nrows, const double *center, double *cov,

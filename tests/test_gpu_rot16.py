@@ -91,7 +91,7 @@ def _r16_vs_fp64(idx, As, Q, Ms):
             ea, R, eq = _scales(amax, float(nqs[m]))
             true = np.ldexp(exact[m], ea + eq)
             # eps_j of segment j (the per-segment skip bound k_xstrip uses; <= the global eps_R)
-            eps = U32 * (360 * amax * math.sqrt(nqs[m]) + 60 * amax * amax) + \
+            eps = U32 * (360 * amax * math.sqrt(nqs[m]) + lib.ia_db_rot_eps_a2() * amax * amax) + \
                 2.0 ** -9 * 1.01 * ask_dec * math.sqrt(nsks[m])
             worst = max(worst, (np.abs(got[m] - true) / np.ldexp(eps, ea + eq)).max())
     return worst
