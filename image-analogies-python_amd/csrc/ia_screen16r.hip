@@ -2,18 +2,19 @@
 // level's rotation (covariance of the centred rows, ia_db_cov; the eigenvectors are taken
 // on the host), the rotated database (ia_db_build_rot: R16_ROW_B bytes per row, R16_MFMA
 // operand groups per 32-row tile: 128 B and 4 at the default P = 3) and the screen
-// k_screen16r: R16_MFMA v_mfma_f32_32x32x16_f16 per 32x32 (rows x queries) tile instead of
-// the 11 of ia_screen16.hip, same segment minima units, so the exact stage (k_xstrip) is
-// unchanged apart from its bound.
+// k_screen16r: at P = 3 (the default, IA_R16_SHAPE = 16) two v_mfma_f32_16x16x32_f16 per
+// 16 x 16 (rows x queries) block, else R16_MFMA v_mfma_f32_32x32x16_f16 per 32x32 tile (the
+// split-f16 screen of ia_screen16.hip needs 11), same segment minima units, so the exact stage
+// (k_xstrip) is unchanged apart from its bound (ia_rot16.h r16_eps, per shape).
 //
 // The screen's structure is the row form's of ia_screen16.hip (k_screen16): queries are the
-// stationary MFMA B operand (R16_MFMA half8 per query tile and lane); the DB streams through
-// LDS in 4-tile stages (16 KiB at P = 3, global_load_lds_dwordx4, non-temporal, a ring of 3
-// buffers, one LDS-only barrier per stage) and every byte fetched feeds the block's 4 waves;
-// the stage's 4G (query tile, stage tile) chains are cut into 4 equal runs (chain balance),
-// each chain's MFMAs run back to back into one of two ping-pong accumulators and its
-// running-minimum fold is interleaved with the next chain's MFMAs; minima staged in LDS 8
-// segments at a time.
+// stationary MFMA B operand (half8 per query block and lane); the DB streams through LDS in
+// 4-tile stages (16 KiB at P = 3, global_load_lds_dwordx4, non-temporal, a ring of 3 buffers,
+// one LDS-only barrier per stage) and every byte fetched feeds the block's 4 waves; the
+// stage's (query block, row block) chains are cut into 4 equal runs (chain balance), each
+// chain's MFMAs run back to back and its running-minimum fold is taken a few chains later
+// (no MFMA -> VALU hazard pads), interleaved with the later chains' MFMAs; minima staged in
+// LDS 8 segments at a time.
 #include "ia_internal.h"
 #include "ia_rot16.h"
 
