@@ -50,6 +50,9 @@ constexpr int R16_RING = IA_R16_RING;
 #ifndef IA_R16_NOFOLD
 #define IA_R16_NOFOLD 0
 #endif
+#ifndef IA_R16_NTMIN
+#define IA_R16_NTMIN 0   // segment minima written non-temporally (less dirty L2 at the kernel's end)
+#endif
 #ifndef IA_R16_NOLDS
 #define IA_R16_NOLDS 0   // A/B builds only: the tile operands read once per stage (wrong minima)
 #endif
@@ -429,7 +432,11 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
                 for (int i = tid; i < G * 32 * n; i += 256) {
                     const int ql = i / n, k = i - ql * n;
                     int *e = &smin[k * (G * 32) + ql];
-                    if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + base + k] = fkey_inv(*e);
+                    if (q0 + ql < M) {
+                        float *dst = segmin + ((long)(q0 + ql) * nseg + seg0 + base + k);
+                        if constexpr (IA_R16_NTMIN) __builtin_nontemporal_store(fkey_inv(*e), dst);
+                        else *dst = fkey_inv(*e);
+                    }
                     *e = 0x7fffffff;                  // this thread's entries only: no barrier
                 }
             }
