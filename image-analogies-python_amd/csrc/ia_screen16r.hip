@@ -61,7 +61,10 @@ constexpr int R16_RING = IA_R16_RING;
 #ifndef IA_R16_PIN
 #define IA_R16_PIN 1
 #endif
-constexpr int SPC_STAGE = 8;     // segments of minima staged in LDS at a time
+#ifndef IA_R16_SPC
+#define IA_R16_SPC 8
+#endif
+constexpr int SPC_STAGE = IA_R16_SPC;   // segments of minima staged in LDS at a time
 
 // chain balance (as ia_screen16.hip): the 4G chains of a stage in the order 4t + u cut into
 // 4 equal runs of G, one per wave
