@@ -6,5 +6,7 @@ set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 rm -rf _ab/csrc && mkdir -p _ab && cp -r image-analogies-python_amd/csrc _ab/csrc && rm -rf _ab/csrc/_build
-make -s -C _ab/csrc -j8 OUT=../libia_$name.so HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result $*" > /dev/null
-grep -A12 "Function Name: _ZN2ia11k_screen16pILi11ELb0E" _ab/csrc/_build/ia_screen16.res | grep -E "VGPRs:|Scratch" | sed "s/^/$name: /"
+# EXTRA (not HIPFLAGS): a command-line HIPFLAGS would override the Makefile's per-object
+# screen flags (-fno-honor-nans, -amdgpu-mfma-vgpr-form=1) and handicap every variant
+make -s -C _ab/csrc -j8 OUT=../libia_$name.so EXTRA="$*" > /dev/null
+grep -A12 "Function Name: _ZN2ia12_GLOBAL__N_111k_screen16rILi11E" _ab/csrc/_build/ia_screen16r.res | grep -E "VGPRs:|Scratch" | sed "s/^/$name: /"
