@@ -483,15 +483,20 @@ def main():
         # one exchange per sharded level (the levels run pipelined, each exchange ordered
         # on its own level's stream): the device-side exchange (IA_EXCHANGE=peer, default)
         # or one RCCL all-gather per wave (IA_EXCHANGE=rccl)
-        nshard = Job(conf, 0, dev).sharded_levels(world)
-        comm = [_ia.exchange(rank, world) for _ in range(max(nshard, 1))]
+        j0 = Job(conf, 0, dev)
+        comm = ia.level_exchanges([ip.gaussian_pyramid_dev(j0.Ap, cfg.n_sm, j0.levels)],
+                                  j0.max_levels, rank, world)
+        del j0
 
     lsh = None
     if args.matcher == 'lsh':
         t_, h_, w_ = args.lsh.split(',')
         lsh = dict(tables=int(t_), hashes=int(h_), width=float(w_), seed=0)
     if args.config == 'c5':
-        jobs = [Job(conf, 1000 + 3 * (rank + world * j), dev, lsh) for j in range(args.jobs)]
+        # the whole batch is args.jobs per GPU; this rank's share by the package's split
+        # (image_analogies.rank_jobs: job j on rank j mod world, seed 1000 + 3 j)
+        my_jobs = ia.rank_jobs(args.jobs * world, rank, world)
+        jobs = [Job(conf, 1000 + 3 * j, dev, lsh) for j in my_jobs]
     else:
         jobs = [Job(conf, 0, dev, lsh)]
 
@@ -538,7 +543,15 @@ def main():
             return ia.synthesize_batch_dev(ins, part[0].max_levels, [jb.k for jb in part],
                                            part[0].weights, prof=prof, check=check)
         if pool is None:
-            return [o for part in groups for o in one(part)]
+            # the package's multi-GPU batch entry: the whole job list with this rank's entries
+            # (the others' are never read), split j = rank (mod world), `batch` per launch set
+            whole = [None] * (len(jobs) * world)
+            for j, jb in zip(my_jobs, jobs):
+                whole[j] = jb.prepare
+            res = ia.synthesize_jobs(whole, jobs[0].max_levels, [jobs[0].k] * len(whole),
+                                     jobs[0].weights, rank, world, batch=batch, prof=prof,
+                                     check=check)
+            return [res[j] for j in my_jobs]
         main = torch.cuda.current_stream(dev)
 
         def lane(i):

@@ -92,6 +92,7 @@ _SIGS = {
     'ia_db_rot_components': (ctypes.c_int, []),
     'ia_screen_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'ia_fused_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    'ia_level_resources': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     'ia_db_rot_slots': (ctypes.c_int, []),
     'ia_db_rot_eps_a2': (ctypes.c_double, []),
     'ia_db_cov_bytes': (ctypes.c_size_t, []),
@@ -162,6 +163,7 @@ _SIGS = {
     'ia_diag_set_xwave': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_sched': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_screen_pc': (ctypes.c_int, [ctypes.c_int]),
+    'ia_diag_set_r16_form': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_set_img_fused': (ctypes.c_int, [ctypes.c_int]),
     'ia_diag_screen_trace': (ctypes.c_int, [_dp]),
     'ia_diag_set_color16': (ctypes.c_int, [ctypes.c_int]),

@@ -1447,9 +1447,39 @@ static int c3_need(const IaSynthArgs &a, int t) {
 constexpr int C3_PIPE_BLOCK = 4;   // waves per recorded event
 
 struct Pipe3 {   // per host thread: the level streams and events of ia_synth_levels3
-    std::vector<hipStream_t> streams;
+    std::vector<hipStream_t> hi;   // levels 0 .. n-2 of a call (the coarser ones): high priority
+    hipStream_t plain = nullptr;   // level n-1 (the finest): plain priority
     std::vector<hipEvent_t> events;
     size_t next = 0;
+    // the streams of an n-level call: the pools grow as needed, and the finest level always
+    // takes the plain stream whatever n the first call had
+    hipError_t streams(int n, std::vector<hipStream_t> &out) {
+        hipError_t r = hipSuccess;
+        int lo = 0, pr = 0;
+        if ((r = hipDeviceGetStreamPriorityRange(&lo, &pr)) != hipSuccess) return r;
+        while ((int)hi.size() < n - 1) {
+            hipStream_t s;
+            if ((r = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pr)) != hipSuccess) return r;
+            hi.push_back(s);
+        }
+        if (!plain && (r = hipStreamCreateWithFlags(&plain, hipStreamNonBlocking)) != hipSuccess) return r;
+        out.assign(hi.begin(), hi.begin() + (n - 1));
+        out.push_back(plain);
+        return r;
+    }
+    hipError_t release() {
+        hipError_t r = hipSuccess;
+        for (hipStream_t s : hi)
+            if (r == hipSuccess) r = hipStreamDestroy(s);
+        if (plain && r == hipSuccess) r = hipStreamDestroy(plain);
+        for (hipEvent_t e : events)
+            if (r == hipSuccess) r = hipEventDestroy(e);
+        hi.clear();
+        plain = nullptr;
+        events.clear();
+        next = 0;
+        return r;
+    }
     hipError_t event(hipEvent_t *e) {
         if (next == events.size()) {
             hipEvent_t x;
@@ -1462,6 +1492,11 @@ struct Pipe3 {   // per host thread: the level streams and events of ia_synth_le
     }
 };
 static thread_local Pipe3 g_pipe3;
+// ia_release_thread_resources (ia_synth.hip): this thread's colour pipeline streams and events
+int release_pipe3() {
+    IA_HIP(g_pipe3.release());
+    return IA_OK;
+}
 
 }  // namespace ia
 
@@ -1551,6 +1586,10 @@ int ia_db3_rot_floats(void) { return R3_ROT_FLOATS; }
 int ia_db3_build_rot(const double *db3, long nrows, const float *rot, void *dbr, void *stream) {
     IA_ARG(db3 && rot && dbr && nrows > 0, "ia_db3_build_rot: bad args");
     hipStream_t st = S(stream);
+    {
+        const int rc = rot_check_orthonormal(rot, D3, R3_LD, st, "ia_db3_build_rot");
+        if (rc) return rc;
+    }
     const Db3View v = db3_view(const_cast<double *>(db3), nrows);
     Rot3Meta *rm = db3r_meta(dbr, nrows);
     IA_HIP(hipMemsetAsync(rm, 0, sizeof(Rot3Meta), st));
@@ -1590,17 +1629,8 @@ int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
                "ia_synth_levels3: levels must be consecutive (level j's coarse B' = level j-1's B')");
     hipStream_t st = S(stream);
     Pipe3 &P = g_pipe3;
-    while ((int)P.streams.size() < n) {
-        int lo = 0, hi = 0;
-        IA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        (void)lo;
-        hipStream_t s;
-        // stream j runs level j of a call: all but the last created at high priority (the
-        // finest level of an n-level call is always stream n - 1, created last or plain)
-        if ((int)P.streams.size() < n - 1) IA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
-        else IA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        P.streams.push_back(s);
-    }
+    std::vector<hipStream_t> ss;   // ss[j] runs level j: high priority but the finest
+    IA_HIP(P.streams(n, ss));
     P.next = 0;
     hipEvent_t start;
     IA_HIP(P.event(&start));
@@ -1614,7 +1644,7 @@ int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
     }
     // every level whole, coarse to fine: a level's waits name events already recorded
     for (int j = 0; j < n; ++j) {
-        hipStream_t sj = P.streams[j];
+        hipStream_t sj = ss[j];
         IA_HIP(hipStreamWaitEvent(sj, start, 0));
         int waited = -1;
         for (int t = 0; t < run[j].nw; ++t) {
@@ -1639,7 +1669,7 @@ int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
     for (int j = 0; j < n; ++j) {
         hipEvent_t e;
         IA_HIP(P.event(&e));
-        IA_HIP(hipEventRecord(e, P.streams[j]));
+        IA_HIP(hipEventRecord(e, ss[j]));
         IA_HIP(hipStreamWaitEvent(st, e, 0));
     }
     return IA_OK;

@@ -9,12 +9,40 @@
 // screen and re-screen, whose error bounds are accounted for in ia_match.hip.
 #include "ia_common.h"
 #include "ia_internal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
 #include "ia_rot16.h"
 #include "ia_split16.h"
 
 namespace ia {
 
 thread_local long g_db_chunk_target = DB_TARGET_CHUNKS;
+
+int rot_check_orthonormal(const float *rot, int n, int ld, hipStream_t st, const char *who) {
+    std::vector<float> V((size_t)n * ld);
+    IA_HIP(hipMemcpyAsync(V.data(), rot, V.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+    IA_HIP(hipStreamSynchronize(st));
+    double fro = 0.0;
+    for (int a = 0; a < n; ++a)
+        for (int b = 0; b < n; ++b) {
+            double e = a == b ? -1.0 : 0.0;
+            for (int k = 0; k < n; ++k) e += (double)V[(size_t)k * ld + a] * (double)V[(size_t)k * ld + b];
+            fro += e * e;
+        }
+    const double budget = 2.0 * std::sqrt((double)n) * 0x1p-24;
+    if (!(std::sqrt(fro) <= budget)) {
+        char msg[256];
+        std::snprintf(msg, sizeof msg,
+                      "%s: the rotation is not orthonormal to fp32 rounding (||V^T V - I||_F = %.3g > %.3g = "
+                      "2 sqrt(%d) 2^-24, the bound's budget; pass an fp64-orthonormal basis rounded to fp32)",
+                      who, std::sqrt(fro), budget, n);
+        set_error(msg);
+        return IA_E_ARG;
+    }
+    return IA_OK;
+}
 
 __global__ void k_level_features(ImgPair p, int full, double *out) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;

@@ -6,13 +6,24 @@
 
 namespace ia {
 
+// ---- the rotations' precondition ----------------------------------------------
+// The R16 / R16c bounds charge the fp32 rotation's non-orthogonality as
+// 2 ||V_f V_f^T - I|| A|q'| <= 2 (2 sqrt(n) u) A|q'| (u = 2^-24): true for the fp32 rounding of a
+// basis orthonormal to fp64 precision, not for any matrix.  The public builders check it: the
+// n x n rotation rot[k * ld + j] (device memory, ordered on st) read back once per level, and
+// ||V_f^T V_f - I||_F (>= the spectral norm, which equals ||V_f V_f^T - I||'s) <= 2 sqrt(n) u.
+int rot_check_orthonormal(const float *rot, int n, int ld, hipStream_t st, const char *who);
+
 // ---- database chunking (shared by ia_db_build, the screen and the exact stage) ------
 // A screen workgroup owns one chunk of ch rows (32-row tiles, 4-tile stages).  ch is
 // chosen so a DB produces ~DB_TARGET_CHUNKS chunks (one per screen slot at 2 blocks per
 // CU: measured 4-10 % faster than 1024 at 0.5-1 M rows, equal at 4.19 M rows;
 // profiles/r01_screen_bench_shard_sizes.txt, r01_chunks_ab_end.txt).  The chunk count is
 // rounded up to a multiple of 4 (the exact stage reads the segment minima as float4).
-constexpr long DB_TARGET_CHUNKS = 512;
+#ifndef IA_DB_TARGET_CHUNKS
+#define IA_DB_TARGET_CHUNKS 512
+#endif
+constexpr long DB_TARGET_CHUNKS = IA_DB_TARGET_CHUNKS;
 // the chunk target in force (ia_set_chunk_target): a batch of K DBs screened in one launch
 // asks for fewer, longer chunks per DB (the workgroups of K DBs fill the GPU anyway).
 // Per host thread: a batch's target never reaches another thread's DB builds and syntheses

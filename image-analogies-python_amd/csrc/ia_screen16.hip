@@ -487,15 +487,11 @@ constexpr bool PC_PIN = IA_PC_PIN;   // k_screen16p pins its MFMA stage's schedu
 #define IA_PC_AHEAD 3
 #endif
 constexpr int PC_AHEAD = IA_PC_AHEAD;
-// A/B build knobs (diagnostic builds only; the product uses the defaults): IA_PC_PRIO raises
-// the MFMA waves' issue priority (s_setprio); IA_PC_NOEXP=1 makes the expanders skip the
-// operand expansion (wrong minima: the MFMA waves' time without that contention)
+// A/B build knob (diagnostic builds only; the product uses the default): IA_PC_PRIO raises
+// the MFMA waves' issue priority (s_setprio)
 #ifndef IA_PC_PRIO
 #define IA_PC_PRIO 0
 #endif
-#ifndef IA_PC_NOEXP
-#define IA_PC_NOEXP 0
-#endif   // stages ahead the expanders request window rows (2, 3)
 static_assert(PC_AHEAD == 2 || PC_AHEAD == 3, "ring depth");
 constexpr int RP_FA = 0, RP_FP = RP_FA + 8 * FROW_B, RP_CA = RP_FP + 8 * FROW_B;
 constexpr int RP_CP = RP_CA + 8 * CROW_B, RP_NM = RP_CP + 8 * CROW_B, RP_B = RP_NM + 4 * 512;
@@ -639,7 +635,7 @@ __device__ __forceinline__ void pc_expand(const ImgDb &im, half8 *E, char *ring,
             wl = w3;
         }
         if (s + 1 < nstage) {
-            if (!IA_PC_NOEXP) rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
+            rp_expand<X>(ring, wn.y, (s + 1) & 3, E + ((s + 1) & 1) * STAGE_H8, lane);
             if (s + 2 < nstage) wn = win_src(im, stage_lrow(sm, chunk, s + 2));
         }
         pc_stamp(tr, s, 2);
@@ -883,6 +879,13 @@ int launch_screen16(const void *db, const ImgDb *img, long nrows, const StageMap
 namespace ia {
 int screen16i_attributes(hipFuncAttributes *at) {
     IA_HIP(hipFuncGetAttributes(at, reinterpret_cast<const void *>(&k_screen16i<11, 0>)));
+    return IA_OK;
+}
+// the 4-wave screen a sharded level launches (launch_screen16, sharded): the image form
+// k_screen16i or the row form k_screen16, widest instance (G = 11)
+int screen16_attributes(bool img, hipFuncAttributes *at) {
+    if (img) return screen16i_attributes(at);
+    IA_HIP(hipFuncGetAttributes(at, reinterpret_cast<const void *>(&k_screen16<11, 0>)));
     return IA_OK;
 }
 }  // namespace ia

@@ -37,24 +37,11 @@ constexpr int SPC_MAX = 16;
 #define IA_R16_OCC 2
 #endif
 constexpr int R16_RING = IA_R16_RING;
-// A/B builds only (tools/build_variant.sh -DIA_R16_LAB=n): 1 no DB loads after the ring's
-// first stages (the compute floor), 2 one MFMA per chain (the streaming floor)
-#ifndef IA_R16_LAB
-#define IA_R16_LAB 0
-#endif
-// A/B builds only: IA_R16_NOBAR=1 drops the per-stage barrier (wrong minima; timing of the
-// compute floor without it), IA_R16_NOFOLD=1 folds one accumulator element per chain
-#ifndef IA_R16_NOBAR
-#define IA_R16_NOBAR 0
-#endif
-#ifndef IA_R16_NOFOLD
-#define IA_R16_NOFOLD 0
-#endif
+// (Round 5's lab builds that skipped loads, barriers, folds or operand reads to time the
+// kernel's floors broke the minima; they are not part of this source: every knob left here
+// keeps the minima bit-identical, tests/test_gpu_rot16.py.)
 #ifndef IA_R16_NTMIN
 #define IA_R16_NTMIN 0   // segment minima written non-temporally (less dirty L2 at the kernel's end)
-#endif
-#ifndef IA_R16_NOLDS
-#define IA_R16_NOLDS 0   // A/B builds only: the tile operands read once per stage (wrong minima)
 #endif
 // the stage's instruction order: 1 pins each chain as MFMA, 2 VALU of the previous chain's
 // fold, MFMA, ... (sched_group_barrier), 0 leaves it to the compiler
@@ -160,44 +147,25 @@ __device__ __forceinline__ void r16_stage(const half8 *sb, const half8 (&bq)[NS]
         const half8 *p = sb + ch_u<G, W>(0) * R16_TILE_H8 + lane;
 #pragma unroll
         for (int m = 0; m < R16_MFMA; ++m) a[0][m] = p[m * 64];
-        if constexpr (IA_R16_NOLDS) {
-#pragma unroll
-            for (int m = 0; m < R16_MFMA; ++m) a[1][m] = a[0][m];
-        }
     }
     sfor<0, NC>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         constexpr int k = ch_k<G, W>(c), ab = ch_uo<G, W>(c) & 1, cb = c % R16_NACC;
         constexpr int cf = c - IA_R16_LAG, fb = (c + 1) % R16_NACC;   // the chain folded here
-        if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c)) {
+        if constexpr (ch_reads_next<G, W>(c)) {
             const half8 *p = sb + ch_u<G, W>(ch_next<G, W>(c)) * R16_TILE_H8 + lane;
 #pragma unroll
             for (int m = 0; m < R16_MFMA; ++m) a[ab ^ 1][m] = p[m * 64];
-        } else if constexpr (IA_R16_NOLDS == 2 && ch_reads_next<G, W>(c)) {
-#pragma unroll
-            for (int m = 0; m < R16_MFMA; ++m) asm volatile("" : "+v"(a[ab ^ 1][m]));   // opaque: no CSE
         }
         acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][0], bq[k][0], zero, 0, 0, 0);
-        if constexpr (cf >= 0) {
-            if constexpr (IA_R16_LAB == 3 || IA_R16_NOFOLD) mn[ch_k<G, W>(cf)] = fminf(mn[ch_k<G, W>(cf)], acc[fb][0]);
-            else fold_min(acc[fb], mn[ch_k<G, W>(cf)]);
-        }
-        if constexpr (IA_R16_LAB == 4) {
-            // A/B only: the chain's other MFMAs independent of each other (wrong minima; timing of
-            // the same MFMA and fold count without the accumulate dependency)
-            floatx16 x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][1], bq[k][1], zero, 0, 0, 0);
-            floatx16 x2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][2], bq[k][2], zero, 0, 0, 0);
-            floatx16 x3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][3], bq[k][3], zero, 0, 0, 0);
-            asm volatile("" :: "v"(x1), "v"(x2), "v"(x3));   // kept (no instruction, no hazard)
-        } else {
+        if constexpr (cf >= 0) fold_min(acc[fb], mn[ch_k<G, W>(cf)]);
 #pragma unroll
-            for (int m = 1; m < (IA_R16_LAB == 2 ? 1 : R16_MFMA); ++m)
-                acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][m], bq[k][m], acc[cb], 0, 0, 0);
-        }
-        if constexpr (IA_R16_PIN && (IA_R16_LAB <= 1 || IA_R16_LAB == 4)) {
+        for (int m = 1; m < R16_MFMA; ++m)
+            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ab][m], bq[k][m], acc[cb], 0, 0, 0);
+        if constexpr (IA_R16_PIN) {
             // [the next tile's 5 operand reads,] MFMA 0, then the previous chain's fold two
             // VALU at a time between the remaining MFMAs
-            if constexpr (!IA_R16_NOLDS && ch_reads_next<G, W>(c))
+            if constexpr (ch_reads_next<G, W>(c))
                 __builtin_amdgcn_sched_group_barrier(0x100, R16_MFMA, 0);   // DS reads
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
             if constexpr (cf >= 0) {
@@ -417,7 +385,7 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stage_barrier();
     for (int s = 0; s < nstage; ++s) {
-        const bool more = s + R16_RING - 1 < nstage && IA_R16_LAB != 1 && IA_R16_LAB != 4;
+        const bool more = s + R16_RING - 1 < nstage;
         if (more) issue(s + R16_RING - 1);   // into the buffer stage s - 1 used (consumed)
         if constexpr (R16_S16) {
             r16_stage_s16<G, W, NS>(sbuf + (s % R16_RING) * STAGE_H8, bq, mn, lane);
@@ -447,7 +415,7 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
         // stage s + 1 landed: the R16_RING - 2 stages issued after it may stay in flight
         if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(R16_MFMA * (R16_RING - 2)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (!IA_R16_NOBAR) stage_barrier();   // (every wave's reads of stage s done: its buffer is refilled next)
+        stage_barrier();   // (every wave's reads of stage s done: its buffer is refilled next)
     }
 }
 
@@ -484,6 +452,151 @@ __global__ __launch_bounds__(256, IA_R16_OCC) void k_screen16r(const half8 *__re
     else if (wv == 1) r16_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
     else if (wv == 2) r16_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
     else r16_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+}
+
+// ---- the wave-owned form (IA_R16_FORM = 1): DB tiles straight into each wave's registers ----
+// The block form above streams every DB byte through LDS (DMA ring, one barrier per 128-row
+// stage) so that the block's 4 waves, each holding a quarter of the query blocks in VGPRs,
+// share it.  Here the roles are swapped: the block's 8 waves share the QUERIES, staged once
+// in LDS in MFMA operand order (2G blocks of 16 x 2 MFMAs x 64 lanes x half8: 44 KiB at
+// G = 11), and each wave owns a contiguous run of DB tiles (32 rows, 4 KiB each) that it
+// loads straight into its registers (4 x 16 B per lane, the 16x16x32 operands of its two row
+// blocks), W_RING tiles in flight.  Per tile: every query block's two half8 read from LDS
+// (ds_read_b128, conflict-free), 4 MFMAs (two 16-row blocks x two K = 32 steps), the lagged
+// minimum fold.  No DB staging, no per-stage barrier: the waves never wait for each other
+// until the block's end.  Segment minima: a wave closing a segment (or its run) reduces its
+// lane groups and ds_min's the 16 values per query block into the block's LDS minima
+// (waves sharing a segment combine there); after one barrier the block writes runs of spb
+// consecutive segments per query.  Same products, same two-MFMA chain per (16 rows, 16
+// queries) and the same minima as the block form, bit for bit.
+#ifndef IA_R16W_RING
+#define IA_R16W_RING 3
+#endif
+constexpr int W_RING = IA_R16W_RING;   // tiles in flight per wave
+constexpr int W_WAVES = 8;             // waves per workgroup
+constexpr int W_SPB_MAX = 16;          // segments per workgroup (LDS minima)
+constexpr int W_LAG = 2;               // query blocks between an MFMA pair and its fold
+
+__device__ __forceinline__ void w_fold(const floatx4 &x, const floatx4 &y, float &mn) {
+    mn = fminf(fminf(mn, fminf(x[0], x[1])), fminf(fminf(x[2], x[3]), fminf(fminf(y[0], y[1]), fminf(y[2], y[3]))));
+}
+
+// one tile (two 16-row blocks: a[0..1] = block 0 MFMA 0..1, a[2..3] = block 1) against the 2G
+// query blocks of the LDS operand array qs[(k * 2 + n) * 64 + lane]
+template <int NQB>
+__device__ __forceinline__ void w_tile(const half8 (&a)[4], const half8 *qs, float (&mn)[NQB], int lane) {
+    const floatx4 zero = {};
+    half8 bq[2][2];
+    floatx4 acc[W_LAG + 1][2];
+    bq[0][0] = qs[lane];
+    bq[0][1] = qs[64 + lane];
+    sfor<0, NQB>([&](auto kk) {
+        constexpr int k = decltype(kk)::value, cb = k % (W_LAG + 1), b = k & 1;
+        if constexpr (k + 1 < NQB) {
+            bq[b ^ 1][0] = qs[((k + 1) * 2) * 64 + lane];
+            bq[b ^ 1][1] = qs[((k + 1) * 2 + 1) * 64 + lane];
+        }
+        acc[cb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], bq[b][0], zero, 0, 0, 0);
+        acc[cb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[2], bq[b][0], zero, 0, 0, 0);
+        acc[cb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], bq[b][1], acc[cb][0], 0, 0, 0);
+        acc[cb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[3], bq[b][1], acc[cb][1], 0, 0, 0);
+        if constexpr (k >= W_LAG) {
+            constexpr int f = (k - W_LAG) % (W_LAG + 1);
+            w_fold(acc[f][0], acc[f][1], mn[k - W_LAG]);
+        }
+    });
+    sfor<(NQB > W_LAG ? NQB - W_LAG : 0), NQB>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        w_fold(acc[k % (W_LAG + 1)][0], acc[k % (W_LAG + 1)][1], mn[k]);
+    });
+}
+
+// grid: (segment blocks rounded up to 8) x query groups, XCD-aware (the groups of a segment
+// block share blockIdx % 8); grid y = job of a batch.  Block sbk covers segments
+// [sbk spb, (sbk + 1) spb); wave w its tiles [w tpw, (w + 1) tpw) (tpw = spb tps / 8).
+template <int G>
+__global__ __launch_bounds__(512, 4) void k_screen16w(const half8 *__restrict__ db16, int nsb, int spb, int tps,
+                                                      int seg_rows, StageMap sm, const half8 *__restrict__ q16,
+                                                      int M, int groups, float *__restrict__ segmin, long nseg,
+                                                      const XJob *jobs, int parity) {
+    constexpr int NQB = 2 * G;
+    __shared__ half8 qs[NQB * 2 * 64];
+    __shared__ int smin[W_SPB_MAX * NQB * 16];
+    if (jobs) {
+        const XJob &J = jobs[blockIdx.y];
+        db16 = reinterpret_cast<const half8 *>(J.dbr.get());
+        q16 = reinterpret_cast<const half8 *>(J.q16[parity].get());
+        segmin = J.segmin;
+    }
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int sbk = (slot / groups) * 8 + (b & 7);
+    const int group = slot - (slot / groups) * groups;
+    if (sbk >= nsb) return;   // uniform over the block, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the group's queries in operand order: block k, MFMA n, lane l -> query 16 k + l % 16,
+    // half8 (l / 16) % 2 * R16_MFMA + 2 n + (l / 16) / 2 of its q16 row (as r16_body)
+    const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
+    for (int i = tid; i < NQB * 128; i += 512) {
+        const int k = i >> 7, n = (i >> 6) & 1, l = i & 63, lq = l >> 4;
+        qs[i] = qg[(long)(k * 16 + (l & 15)) * Q16_ROW + (lq & 1) * R16_MFMA + (lq >> 1) + 2 * n];
+    }
+    for (int i = tid; i < spb * NQB * 16; i += 512) smin[i] = 0x7fffffff;
+    __syncthreads();
+    const long seg0 = (long)sbk * spb;
+    const int tpw = spb * tps / W_WAVES;
+    const int jw = wv * tpw;                       // the wave's first block-local tile
+    const int lts = __builtin_ctz((unsigned)tps);  // log2 tiles per segment
+    const int q = lane >> 4, r = lane & 15;
+    const int o0 = (q >> 1) * 64 + (q & 1) * 32 + r;   // (v, n) -> o0 + n * 128 + v * 16
+    // block-local tile j (clamped to the wave's last: the ring's overrun re-reads a line the
+    // wave loads anyway) -> its half8 base
+    auto tile = [&](int j) -> const half8 * {
+        j = j < tpw ? j : tpw - 1;
+        const int jj = jw + j;
+        const long lrow = seg_lrow(sm, seg0 + (jj >> lts), seg_rows, (long)(jj & (tps - 1)) * 32);
+        return db16 + (lrow >> 5) * R16_TILE_H8 + o0;
+    };
+    half8 a[W_RING][4];
+    auto issue = [&](half8 (&d)[4], int j) {
+        const half8 *t = tile(j);
+        d[0] = __builtin_nontemporal_load(t);
+        d[1] = __builtin_nontemporal_load(t + 128);
+        d[2] = __builtin_nontemporal_load(t + 16);
+        d[3] = __builtin_nontemporal_load(t + 144);
+    };
+    float mn[NQB];
+#pragma unroll
+    for (int k = 0; k < NQB; ++k) mn[k] = FLT_MAX;
+    sfor<0, W_RING - 1>([&](auto ss) { issue(a[decltype(ss)::value], decltype(ss)::value); });
+    for (int j0 = 0; j0 < tpw; j0 += W_RING) {
+        sfor<0, W_RING>([&](auto ss) {
+            constexpr int s = decltype(ss)::value;
+            const int j = j0 + s;
+            issue(a[(s + W_RING - 1) % W_RING], j + W_RING - 1);
+            if (j < tpw) {
+                w_tile<NQB>(a[s], qs, mn, lane);
+                const int jj = jw + j;
+                if (((jj + 1) & (tps - 1)) == 0 || j + 1 == tpw) {   // the wave leaves a segment
+                    int *sm0 = smin + (jj >> lts) * (NQB * 16);
+#pragma unroll
+                    for (int k = 0; k < NQB; ++k) {
+                        float m = fminf(mn[k], __shfl_xor(mn[k], 16));
+                        m = fminf(m, __shfl_xor(m, 32));
+                        if (lane < 16) lds_min_i32(&sm0[k * 16 + lane], fkey(m));
+                        mn[k] = FLT_MAX;
+                    }
+                }
+            }
+        });
+    }
+    stage_barrier();   // every wave's minima in LDS
+    const int q0 = group * G * 32;
+    for (int i = tid; i < NQB * 16 * spb; i += 512) {
+        const int ql = i / spb, k = i - ql * spb;
+        if (q0 + ql < M) segmin[(long)(q0 + ql) * nseg + seg0 + k] = fkey_inv(smin[k * (NQB * 16) + ql]);
+    }
 }
 
 // ---- the level's covariance (ia_db_cov): sampled rows, centred, fp64 -------------------
@@ -669,6 +782,12 @@ __global__ __launch_bounds__(64) void k_query_rows_r16(const double *__restrict_
 
 }  // namespace
 
+// the rotated screen's form (IA_R16_FORM / ia_diag_set_r16_form): 0 the block form k_screen16r
+// (DB staged through LDS), 1 the wave-owned form k_screen16w (queries in LDS, DB tiles in each
+// wave's registers); the same minima
+static std::atomic<int> g_r16_form{env_int("IA_R16_FORM", 1)};
+static int r16_form() { return g_r16_form.load(std::memory_order_relaxed); }
+
 int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Float16 *q16, int M,
                      float *segmin, hipStream_t st, const XJob *jobs, int njobs, int parity) {
     const int ch = db_chunk_rows(nrows);
@@ -688,10 +807,23 @@ int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Flo
     const long nb = ((nchunks + 7) / 8) * 8 * groups;
     IA_ARG(nb < (1L << 31), "screen grid too large");
     const dim3 grid((unsigned)nb, (unsigned)njobs);
+    // the wave-owned form (k_screen16w): segments per workgroup spb, a power of two dividing
+    // nseg with >= 1 tile per wave, doubled while ~2 workgroups per CU stay busy
+    const int tps = seg_rows / 32;
+    int spb = 1;
+    while (spb * tps < W_WAVES) spb <<= 1;
+    while (spb < W_SPB_MAX && nseg % (2L * spb) == 0 && (nseg / (2L * spb)) * groups * njobs >= 512) spb <<= 1;
+    const bool wform = r16_form() == 1 && R16_S16 && nseg % spb == 0;
+    const long nsb = nseg / spb;
+    const dim3 gridw((unsigned)(((nsb + 7) / 8) * 8 * groups), (unsigned)njobs);
 #define IA_R16_CASE(GG)                                                                             \
     case GG:                                                                                        \
-        k_screen16r<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M, groups,   \
-                                              segmin, nseg, jobs, parity);                          \
+        if (wform)                                                                                  \
+            k_screen16w<GG><<<gridw, 512, 0, st>>>(db16, (int)nsb, spb, tps, seg_rows, sm, q, M,    \
+                                                   groups, segmin, nseg, jobs, parity);             \
+        else                                                                                        \
+            k_screen16r<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,       \
+                                                  groups, segmin, nseg, jobs, parity);              \
         break;
     switch (G) {
         IA_R16_CASE(1)
@@ -722,6 +854,11 @@ int launch_query_rows_r16(const double *q64, int M, const double *center, const 
 int launch_db_amax(const IaSrcLevel *src, const DbSrc &d, const double *center, float *amax,
                    double *part, hipStream_t st);
 int screen16i_attributes(hipFuncAttributes *at);
+// the rotated screen's widest instance (a sharded R16 level's screen)
+int screen_resources_r16(hipFuncAttributes *at) {
+    IA_HIP(hipFuncGetAttributes(at, reinterpret_cast<const void *>(&k_screen16r<11>)));
+    return IA_OK;
+}
 
 }  // namespace ia
 
@@ -752,6 +889,12 @@ int ia_screen_resources(int which, int *lds, int *vgprs) {
     *lds = (int)at.sharedSizeBytes;
     *vgprs = at.numRegs;
     return IA_OK;
+}
+
+int ia_diag_set_r16_form(int form) {
+    const int prev = r16_form();
+    if (form == 0 || form == 1) g_r16_form.store(form);
+    return prev;
 }
 
 int ia_db_rot_components(void) { return R16_P; }
@@ -786,6 +929,10 @@ int ia_db_build_rot(const IaSrcLevel *src, long row0, long nrows, const double *
     IA_ARG(row0 + nrows <= (long)src->nAp * src->Ah * src->Aw, "ia_db_build_rot: rows out of range");
     IA_ARG(row0 + nrows < (1L << 31), "ia_db_build_rot: rows past 2^31");
     hipStream_t st = S(stream);
+    {
+        const int rc = rot_check_orthonormal(rot, IA_D, R16_LD, st, "ia_db_build_rot");
+        if (rc) return rc;
+    }
     const DbSrc d = make_dbsrc(*src);
     const long npad = db_rows_padded(nrows);
     IA_ARG(npad * (long)R16_ROW_B >= 1024L * 8 * 8, "ia_db_build_rot: too few rows for the bound's partials");

@@ -313,6 +313,10 @@ static void prof_push(const ProfRec &r) {
 static std::atomic<int> g_graph_mode{env_int("IA_GRAPH", 0)};
 static int graph_mode() { return g_graph_mode.load(std::memory_order_relaxed); }
 
+int xwave_attributes(int form, bool rot, hipFuncAttributes *at);
+int release_pipe3();
+int screen16_attributes(bool img, hipFuncAttributes *at);
+int screen_resources_r16(hipFuncAttributes *at);
 int comm_allgather(void *comm, const void *send, void *recv, size_t bytes, hipStream_t st);
 int comm_nranks(void *comm);
 PeerView comm_peer_wave(void *comm);
@@ -718,7 +722,8 @@ static int coarse_need(const IaSynthArgs *a, int t) {
 }
 
 struct PipeRes {   // per host thread: the level streams and events of ia_synth_levels
-    std::vector<hipStream_t> streams;
+    std::vector<hipStream_t> streams;   // levels 0 .. n-2 of a call (coarser): high priority
+    hipStream_t plain = nullptr;        // level n-1 of a call (the finest): plain priority
     std::vector<hipEvent_t> events;
     size_t next_event = 0;
     // pinned staging of the batch job tables: reused after the previous call's copies ran
@@ -773,6 +778,36 @@ int ia_diag_set_xwave(int on) {
     return prev;
 }
 
+int ia_level_resources(const IaSynthArgs *a, int *out) {
+    // the kernels this level launches per wave, decided as LevelRun::init / xw_wave decide:
+    // out = {waiting kernel LDS bytes, VGPRs; screen LDS bytes, VGPRs} (the forward-progress
+    // rule of DESIGN.md §7, per level: ADVICE r05)
+    IA_ARG(a && out && a->nrows > 0, "ia_level_resources: bad args");
+    const bool peer = a->comm && comm_peer_mcap(a->comm) > 0;
+    const bool xw = xwave_on() && !a->lsh && (!a->comm || peer) && exact_stage_mode() != 1;
+    const bool r16 = xw && a->dbr && a->rot;
+    const bool im = a->dbi != nullptr;
+    const DbSrc src = make_dbsrc(a->src);
+    const StageMap sm = db_stage_map(a->row0, a->nrows, src.A.w, src.A.h);
+    hipFuncAttributes f{}, sc{};
+    int rc;
+    if (xw) {
+        const int form = !im ? XW_ROWS : (xwave_on() == 2 && sm.W > 0 && xstrip_applies(src)) ? XW_STRIP : XW_IMG;
+        rc = xwave_attributes(form, r16, &f);
+    } else {
+        IA_HIP(hipFuncGetAttributes(&f, reinterpret_cast<const void *>(&k_peer_finish)));
+        rc = IA_OK;
+    }
+    if (rc) return rc;
+    rc = r16 ? screen_resources_r16(&sc) : screen16_attributes(im, &sc);
+    if (rc) return rc;
+    out[0] = (int)f.sharedSizeBytes;
+    out[1] = f.numRegs;
+    out[2] = (int)sc.sharedSizeBytes;
+    out[3] = sc.numRegs;
+    return IA_OK;
+}
+
 int ia_synth_status(const IaSynthArgs *levels, int n, void *stream) {
     IA_ARG(levels && n >= 1, "ia_synth_status: bad args");
     IA_HIP(hipStreamSynchronize(S(stream)));
@@ -822,8 +857,14 @@ int ia_release_thread_resources(void) {
     IA_HIP(g_graphs.retire());
     IA_HIP(hipDeviceSynchronize());
     for (hipStream_t s : g_pipe.streams) IA_HIP(hipStreamDestroy(s));
+    if (g_pipe.plain) IA_HIP(hipStreamDestroy(g_pipe.plain));
+    g_pipe.plain = nullptr;
     for (hipEvent_t e : g_pipe.events) IA_HIP(hipEventDestroy(e));
     g_pipe.streams.clear();
+    {
+        const int rc = release_pipe3();
+        if (rc) return rc;
+    }
     g_pipe.events.clear();
     if (g_pipe.pin) IA_HIP(hipHostFree(g_pipe.pin));
     if (g_pipe.staged) IA_HIP(hipEventDestroy(g_pipe.staged));
@@ -995,18 +1036,22 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
     // level's plateau screens undisturbed: k_screen16<11> 400 vs 396 us); enqueued just
     // ahead of their need 1619-1621 ms but the plateau screens contended (414 us)
     static const int prio_on = env_int("IA_PIPE_PRIO", 1);
-    while ((int)g_pipe.streams.size() < n) {
-        const int j = (int)g_pipe.streams.size();
+    // the pools grow as needed; the finest level always takes the plain-priority stream,
+    // whatever n the first call had (a pool sized by a smaller first call used to hand a
+    // later call's coarse level a plain stream and its finest a high-priority one)
+    while ((int)g_pipe.streams.size() < n - 1) {
         int lo = 0, hi = 0;
         IA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         hipStream_t s;
-        if (prio_on && j < n - 1)
+        if (prio_on)
             IA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
         else
             IA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         (void)lo;
         g_pipe.streams.push_back(s);
     }
+    if (!g_pipe.plain) IA_HIP(hipStreamCreateWithFlags(&g_pipe.plain, hipStreamNonBlocking));
+    auto level_stream = [&](int j) { return j == n - 1 ? g_pipe.plain : g_pipe.streams[j]; };
     g_pipe.next_event = 0;
     hipEvent_t start;
     IA_HIP(g_pipe.event(&start));
@@ -1021,7 +1066,7 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
     std::vector<std::vector<hipEvent_t>> blk(n);   // blk[j][b]: level j done through block b
     std::vector<int> next(n, 0), waited(n, -1), need_max(n, 0);
     for (int j = 0; j < n; ++j) {
-        hipStream_t sj = g_pipe.streams[j];
+        hipStream_t sj = level_stream(j);
         IA_HIP(hipStreamWaitEvent(sj, start, 0));
         int rc = run[j].init_batch(&levels[(size_t)j * K], K, sj, pinned + (size_t)j * K);
         if (rc) return rc;
@@ -1050,7 +1095,7 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
     };
     std::function<int(int, int)> advance;
     advance = [&](int j, int target) -> int {
-        hipStream_t sj = g_pipe.streams[j];
+        hipStream_t sj = level_stream(j);
         if (target > run[j].nw - 1) target = run[j].nw - 1;
         if (next[j] == 0 && target >= 0 && multi_rank(j)) {
             for (int i = j - 1; i >= 0; --i) {
@@ -1098,7 +1143,7 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
         if (rc) return rc;
     }
     for (int j = 0; j < n; ++j) {
-        hipStream_t sj = g_pipe.streams[j];
+        hipStream_t sj = level_stream(j);
         int rc = run[j].done(sj);
         if (rc) return rc;
         hipEvent_t e;

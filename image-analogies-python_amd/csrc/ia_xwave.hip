@@ -1425,6 +1425,17 @@ extern "C" int ia_fused_resources(int rot, int *lds, int *vgprs) {
 
 namespace ia {
 
+// the one-job fused kernel of a form (launch_xwave): k_xstrip<false, rot> (XW_STRIP),
+// k_xwave<true / false, false> (XW_IMG / XW_ROWS)
+int xwave_attributes(int form, bool rot, hipFuncAttributes *at) {
+    const void *f = form == XW_STRIP ? (rot ? reinterpret_cast<const void *>(&k_xstrip<false, true>)
+                                            : reinterpret_cast<const void *>(&k_xstrip<false, false>))
+                    : form == XW_IMG ? reinterpret_cast<const void *>(&k_xwave<true, false>)
+                                     : reinterpret_cast<const void *>(&k_xwave<false, false>);
+    IA_HIP(hipFuncGetAttributes(at, f));
+    return IA_OK;
+}
+
 int launch_xwave(const XArgs &a, int nblocks, int form, hipStream_t st, int njobs) {
     if (nblocks <= 0) return IA_OK;
     IA_ARG(njobs >= 1 && njobs <= IA_BATCH_MAX && (njobs == 1 || a.jobs), "launch_xwave: bad batch");

@@ -149,32 +149,39 @@ def residency_ok(waiters, fused, screen, cus=256, lds_per_cu=160 * 1024, vgprs_p
     return waiters < cus * (jmax + 1), jmax
 
 
-def _kernel_resources(rot):
-    lib = _ia.lib()
-    out = []
-    for fn, arg in ((lib.ia_fused_resources, 1 if rot else 0), (lib.ia_screen_resources, 0 if rot else 1)):
-        lds, vg = ctypes.c_int(), ctypes.c_int()
-        _ia.check(fn(arg, ctypes.byref(lds), ctypes.byref(vg)), 'kernel resources')
-        out.append((lds.value, vg.value))
-    return out
+def level_resources(call):
+    """(waiting kernel, screen) resources, each (LDS bytes per workgroup, VGPRs per lane), of
+    the kernels a level's synthesis launches per wave, as ia_synth_level decides them from
+    the level's arguments (ia_level_resources): the fused kernel's form (k_xstrip, or k_xwave
+    on image-form or row-form levels) and the rotated or split-f16 screen (one
+    global choice under-counted k_xwave levels)."""
+    out = (ctypes.c_int * 4)()
+    _ia.check(_ia.lib().ia_level_resources(ctypes.byref(call.args), out), 'ia_level_resources')
+    return (out[0], out[1]), (out[2], out[3])
 
 
 def sharded_schedule(level_shapes, pipeline, ranks_on_gpu, fused, screen, cus=256):
     """The pipelining of a run's sharded levels (shapes H x W of their B' levels) that the
     forward-progress rule (residency_ok) allows: pipeline as asked if every sharded level's
     waiting workgroups together fit the rule, else one level at a time if one level's do;
-    raises if not even one level fits (e.g. too many ranks sharing one GPU)."""
+    raises if not even one level fits (e.g. too many ranks sharing one GPU).  fused / screen:
+    one (LDS, VGPRs) pair for every level, or one pair per level (level_resources); the
+    pipelined check takes the worst of each over the levels."""
     ms = [wave_max_queries(H, W) for H, W in level_shapes]
     if not ms:
         return pipeline
-    if pipeline and residency_ok(ranks_on_gpu * sum(ms), fused, screen, cus)[0]:
+    per = lambda x: list(x) if x and isinstance(x[0], (tuple, list)) else [x] * len(ms)  # noqa: E731
+    fl, sl = per(fused), per(screen)
+    worst = lambda xs: (max(x[0] for x in xs), max(x[1] for x in xs))  # noqa: E731
+    if pipeline and residency_ok(ranks_on_gpu * sum(ms), worst(fl), worst(sl), cus)[0]:
         return True
-    ok, jmax = residency_ok(ranks_on_gpu * max(ms), fused, screen, cus)
-    if not ok:
-        raise RuntimeError('sharded synthesis refused: %d waiting workgroups per GPU (%d ranks x %d '
-                           'queries) with at most %d per CU beside a screen block cannot guarantee '
-                           'forward progress (DESIGN.md §7)' % (ranks_on_gpu * max(ms), ranks_on_gpu,
-                                                                 max(ms), jmax))
+    for m, f, sc in zip(ms, fl, sl):
+        ok, jmax = residency_ok(ranks_on_gpu * m, f, sc, cus)
+        if not ok:
+            raise RuntimeError('sharded synthesis refused: %d waiting workgroups per GPU (%d ranks x %d '
+                               'queries) with at most %d per CU beside a screen block cannot guarantee '
+                               'forward progress (DESIGN.md §7)' % (ranks_on_gpu * m, ranks_on_gpu,
+                                                                     m, jmax))
     return False
 
 
@@ -303,25 +310,34 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         # one exchange cannot serve two levels running at once (their records would share
         # the exchange's box cells): levels one at a time then
         pipeline = False
-    if sharded and comm is not None and _ia.exchange_kind() == 'peer' and torch.cuda.is_available():
-        # fused workgroups that wait for other ranks must leave room for the screens
-        fused, screen = _kernel_resources(_ia.db_rot_enabled() and lsh is None)
-        share = nranks if os.environ.get('IA_SHARE_GPU', '0') == '1' else 1
-        pipeline = sharded_schedule([tuple(B_pyr[l].shape[:2]) for l in sharded], pipeline, share,
-                                    fused, screen, torch.cuda.get_device_properties(0).multi_processor_count)
+    peer_rule = sharded and comm is not None and _ia.exchange_kind() == 'peer' and torch.cuda.is_available()
     out = {}
     t_start = time.time()
     calls = []
     done = []
-    for level in todo:
+
+    def make_call(level):
         lcomm, row_range = None, None
         if level in sharded:
             # one exchange per sharded level; fewer only with the levels one at a time
             lcomm = comms[min(sharded.index(level), len(comms) - 1)] if comms else comm
             row_range = lambda level, N: shard_rows(N, rank, nranks)  # noqa: E731
         index = algorithms.level_index(A_pyr, Ap_pyr_list, level, row_range, lsh)
-        call = _LevelCall(level, max_levels, index, B_pyr[level - 1], B_pyr[level],
+        return _LevelCall(level, max_levels, index, B_pyr[level - 1], B_pyr[level],
                           Bp_pyr[level - 1], Bp_pyr[level], w, k, lcomm, prof, eager, debug)
+    early = {}
+    if peer_rule:
+        # fused workgroups that wait for other ranks must leave room for the screens: the
+        # rule takes each sharded level's own kernels (its DB form and rotation decide them)
+        for level in sharded:
+            early[level] = make_call(level)
+        res = [level_resources(early[l]) for l in sharded]
+        share = nranks if os.environ.get('IA_SHARE_GPU', '0') == '1' else 1
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        pipeline = sharded_schedule([tuple(B_pyr[l].shape[:2]) for l in sharded], pipeline, share,
+                                    [r[0] for r in res], [r[1] for r in res], cus)
+    for level in todo:
+        call = early.pop(level, None) or make_call(level)
         if pipeline:
             calls.append((level, call))
             continue
@@ -329,7 +345,7 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
                   'ia_synth_level')
         out[level] = call.result()
         done.append(call)
-        del index
+        del call
         if os.environ.get('IA_VERBOSE'):
             torch.cuda.synchronize()
             print('[ia] level %d/%d done %.3f s' % (level, max_levels - 1, time.time() - t_start),
@@ -392,6 +408,82 @@ def synthesize_batch_dev(jobs, max_levels, k, weights, prof=False, debug=False, 
         lib.ia_set_chunk_target(prev)
     return [{level: calls[j * K + q].result() for j, level in enumerate(levels)}
             for q in range(K)]
+
+
+# ---- multi-GPU: one process per GPU ------------------------------------------
+
+def dist_world():
+    """(rank, world size) of the initialised torch.distributed group, else (0, 1)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def rank_jobs(n_jobs, rank, world):
+    """Indices of the independent analogies one rank runs when n_jobs of them (the
+    multi_script loop, multi_script.py:13-32, which runs them one after the other in one
+    process) are spread over `world` ranks: j = rank (mod world).  No collective: each rank's
+    results are its own (weak scaling)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError('rank %d of world %d' % (rank, world))
+    return list(range(rank, n_jobs, world))
+
+
+def sharded_level_count(Ap_pyr_list, max_levels, world):
+    """Levels 1..max_levels-1 whose database is sharded over `world` ranks (shard_level)."""
+    return sum(shard_level(level_rows(Ap_pyr_list, l), world) for l in range(1, max_levels))
+
+
+def level_exchanges(Ap_pyr_list, max_levels, rank, world, kind=None):
+    """The `comm` of a DB-sharded synthesis (synthesize_dev): one exchange per sharded level
+    (pipelined sharded levels each need their own), over the initialised torch.distributed
+    group.  Every rank calls it at the same point with pyramids of the same shapes.
+    kind: None (IA_EXCHANGE: the device-side exchange, RCCL as the agreed fallback) or
+    'rccl'.  Release with release_exchanges."""
+    n = sharded_level_count(Ap_pyr_list, max_levels, world)
+    return [_ia.exchange(rank, world, kind) for _ in range(max(n, 1))]
+
+
+def release_exchanges(comms):
+    """Check (a device-side wait that timed out raises) and destroy level_exchanges' objects."""
+    try:
+        for cm in comms or []:
+            _ia.exchange_status(cm)
+    finally:
+        for cm in comms or []:
+            _ia.lib().ia_comm_destroy(cm)
+
+
+def synthesize_jobs(jobs, max_levels, k, weights, rank=0, world=1, batch=0, prof=False,
+                    debug=False, check=True):
+    """Independent analogies of identical shapes spread over ranks (SURVEY §8(e) config 5,
+    multi_script.py:13-32): this rank synthesises jobs[j] for j in rank_jobs(len(jobs),
+    rank, world), `batch` of them per set of launches (synthesize_batch_dev; 0 = all of this
+    rank's jobs in one batch, 1 = one synthesize_dev call per job), one GPU per rank, no
+    collective.  jobs: the WHOLE job list, (A_pyr, Ap_pyr_list, B_pyr, Bp_pyr) device
+    pyramids per job (Bp_pyr updated in place); entries of other ranks' jobs are never read
+    and may be None (or a callable returning the tuple, called only for this rank's jobs).
+    k: one kappa or one per job (whole list).  Returns {j: {level: (s, im[, debug])}} for this
+    rank's jobs."""
+    mine = rank_jobs(len(jobs), rank, world)
+    ks = list(k) if isinstance(k, (list, tuple)) else [k] * len(jobs)
+    if len(ks) != len(jobs):
+        raise ValueError('synthesize_jobs: %d kappas for %d jobs' % (len(ks), len(jobs)))
+    step = batch if batch and batch > 0 else max(1, len(mine))
+    out = {}
+    for g0 in range(0, len(mine), step):
+        group = mine[g0:g0 + step]
+        ins = [jobs[j]() if callable(jobs[j]) else jobs[j] for j in group]
+        if len(group) == 1:
+            A_pyr, Ap_list, B_pyr, Bp_pyr = ins[0]
+            res = [synthesize_dev(A_pyr, Ap_list, B_pyr, Bp_pyr, max_levels, ks[group[0]], weights,
+                                  prof=prof, debug=debug, check=check)]
+        else:
+            res = synthesize_batch_dev(ins, max_levels, [ks[j] for j in group], weights, prof=prof,
+                                       debug=debug, check=check)
+        out.update(zip(group, res))
+    return out
 
 
 # ---- setup (image_analogies.py:17-94) ------------------------------------------------------
@@ -541,15 +633,28 @@ def save_debug(out_path, level, rec, Bp_level):
 
 
 def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False,
-                         outputs=None):
+                         outputs=None, comm=None, rank=None, nranks=None):
     """Full run (image_analogies.py:97-268): setup, per-level synthesis on device, colour
     output images.  debug=True also writes the reference's debug structures per level
     (save_debug).  outputs (dict, optional) receives per level {'color': the RGB image
     before plt.imsave, 's', 'im', and with debug 'debug': debug_record(...)}.  Returns the
-    B' pyramid (numpy)."""
+    B' pyramid (numpy).
+
+    Multi-GPU (one process per GPU): comm='auto' shards the databases of the
+    large levels over the initialised torch.distributed group (every rank calls this with
+    the same files and config; rank / nranks default to the group's): one exchange per
+    sharded level (level_exchanges), released before returning.  comm may also be
+    exchanges the caller made (then pass rank and nranks).  Every rank ends with the same
+    B' (the exchange is deterministic); only rank 0 writes the output files and prints.
+    To spread independent runs over GPUs instead (the multi_script loop) use multi_main."""
     import matplotlib.pyplot as plt
+    r0, w0 = dist_world()
+    rank = r0 if rank is None else rank
+    nranks = (w0 if comm is not None else 1) if nranks is None else nranks
+    lead = rank == 0
+    say = print if lead else (lambda *a, **kw: None)
     begin_time = start_time = time.time()
-    if not os.path.exists(out_path):
+    if lead and not os.path.exists(out_path):
         os.makedirs(out_path)
     A_orig, B_orig = _read(A_fname), _read(B_fname)
     Ap_orig_list = [_read(f) for f in Ap_fname_list]
@@ -559,17 +664,30 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
              'c.AB_weight', 'c.k']
     vals = [A_fname, Ap_fname_list, B_fname, c.convert, c.remap_lum, c.init_rand, c.AB_weight,
             c.k]
-    save_metadata(out_path, names, vals)
+    if lead:
+        save_metadata(out_path, names, vals)
     torch.cuda.synchronize()
-    print('Environment Setup: %f' % (time.time() - start_time))
+    say('Environment Setup: %f' % (time.time() - start_time))
     weights = _ia.to_dev(c.weights)
+    own = None
+    if isinstance(comm, str):
+        if comm != 'auto':
+            raise ValueError("comm must be None, 'auto' or exchange objects")
+        own = comm = level_exchanges(Ap_pyr_list, c.max_levels, rank, nranks) if nranks > 1 else None
     # all levels on device, pipelined (ia_synth_levels); then each level's outputs
     start_time = time.time()
-    print('Computing levels 1 to %d' % (c.max_levels - 1))
-    res = synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c.max_levels, c.k, weights,
-                         lsh=algorithms.lsh_params(c), debug=debug)
-    torch.cuda.synchronize()
-    print('Synthesis time: %f' % (time.time() - start_time))
+    say('Computing levels 1 to %d' % (c.max_levels - 1))
+    try:
+        res = synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c.max_levels, c.k, weights,
+                             comm=comm, rank=rank, nranks=nranks if comm is not None else 1,
+                             lsh=algorithms.lsh_params(c), debug=debug)
+        torch.cuda.synchronize()
+    finally:
+        if own:
+            release_exchanges(own)
+    say('Synthesis time: %f' % (time.time() - start_time))
+    if not lead:
+        return [p.cpu().numpy() for p in Bp_pyr]
     for level in range(1, c.max_levels):
         s, im = res[level][0], res[level][1]
         color_im_out = color_output(level, Bp_pyr[level], s, im, color_pyr_list, c)
@@ -585,3 +703,24 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
         plt.imsave(out_path + out_path.split('/')[-2] + '.jpg', color_im_out)
     print('Total time: %f' % (time.time() - begin_time))
     return [p.cpu().numpy() for p in Bp_pyr]
+
+
+def multi_main(runs, c, debug=False, rank=None, world=None):
+    """The reference's batch scripts (multi_script.py:13-32, multi_script_2.py:31-40: a
+    serial loop of image_analogies_main calls, each with its own files and kappa) spread over
+    GPUs, one process per GPU: this rank runs runs[j] for j in rank_jobs(len(runs), rank,
+    world) (rank / world default to the initialised torch.distributed group's; (0, 1)
+    without one), each on its own GPU alone.  runs: (A_fname, Ap_fname_list, B_fname,
+    out_path[, overrides]) tuples; overrides is a dict of config fields set on `c` before
+    the run (multi_script.py:31 sets c.k so).  Returns {j: B' pyramid} of this rank's runs."""
+    r0, w0 = dist_world()
+    rank = r0 if rank is None else rank
+    world = w0 if world is None else world
+    out = {}
+    for j in rank_jobs(len(runs), rank, world):
+        A_fname, Ap_fname_list, B_fname, out_path = runs[j][:4]
+        for key, val in (runs[j][4] if len(runs[j]) > 4 else {}).items():
+            setattr(c, key, val)
+        out[j] = image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=debug,
+                                      rank=0, nranks=1)
+    return out

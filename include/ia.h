@@ -172,15 +172,19 @@ int ia_wdist_batch(const double *a, const double *q, const double *w, int n, dou
 /* ---- the rotated split-f16 database (R16; replaces the screen's 11 MFMAs
  * per 32x32 tile by 4 at P = 3).  Per level (shard): ia_db_cov -> the 55 x 55 covariance of ~64 k
  * sampled centred rows (fp64, cov[0 .. 56*56) row-major, stride 56; the rest of the buffer,
- * ia_db_cov_bytes() in all, is scratch); the caller takes its eigenvectors (host, any
- * orthonormal basis is exact: the bound adapts) and passes rot = V as fp32, rot[k * 56 + j]
+ * ia_db_cov_bytes() in all, is scratch); the caller takes its eigenvectors (host; any basis
+ * orthonormal to fp64 precision keeps the matcher exact: the bound adapts to the components'
+ * order) and passes rot = V rounded to fp32, rot[k * 56 + j]
  * = V[k][j] with the components j by decreasing variance, in a buffer of 13,312 B (zero
  * padded).  ia_db_build_rot then writes the rotated split rows (128 B per padded row at
  * P = 3), after them per 512-row segment A_skip,j (fp32, the max over the segment's rows of
  * the norm of components P..54) and a byte c_j with A_skip c_j / 255 >= A_skip,j (the exact
  * stage's per-segment bound), ia_db_rot_bytes in all; and amax[0] = A (as ia_db_build),
  * amax[1] = A_skip (max over all rows; zero it first).  ia_db_rot_applies: 1 where the synthesis
- * can use it (every level of the fused per-wave kernel, strip-order or not). */
+ * can use it (every level of the fused per-wave kernel, strip-order or not).
+ * Precondition, checked (IA_E_ARG otherwise; one 12 KB read-back of rot per call): with V_f
+ * the fp32 matrix passed, ||V_f^T V_f - I||_F <= 2 sqrt(55) 2^-24, the non-orthogonality the
+ * screen's bound budgets (an fp32 eigh result or a perturbed basis fails it). */
 int ia_db_rot_applies(const IaSrcLevel *src, long row0, long nrows);
 /* the build's R16 form: components carried as split pairs (P), K-slots per row (16 per MFMA) */
 int ia_db_rot_components(void);
@@ -276,6 +280,11 @@ typedef struct {
     const void *dbr;
     const float *rot;
 } IaSynthArgs;
+/* the resources of ia_screen_resources / ia_fused_resources per level, from its IaSynthArgs as ia_synth_level would run it (the fused
+ * kernel's form k_xstrip / k_xwave image / rows, or k_peer_finish without the fused kernel,
+ * and the screen: k_screen16r where the level has the rotated DB, else the 4-wave split-f16
+ * screen of its DB form): out = {waiting kernel LDS bytes, VGPRs, screen LDS bytes, VGPRs} */
+int ia_level_resources(const IaSynthArgs *a, int *out);
 #define IA_SYNTH_EAGER 1
 #define IA_SYNTH_PROF 2
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
@@ -284,7 +293,8 @@ int ia_synth_level3(const IaSynthArgs *a, void *stream);
 int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream);
 /* the rotated split screen for 3-channel rows (R16c): after ia_db3_build, the
  * caller takes the principal directions V of the level's centred rows (165 x 165, columns by
- * decreasing variance; any orthonormal V keeps the matcher exact) and passes them as fp32
+ * decreasing variance; any V orthonormal to fp64 precision keeps the matcher exact: checked,
+ * ||V_f^T V_f - I||_F <= 2 sqrt(165) 2^-24 or IA_E_ARG) and passes them rounded to fp32
  * rot[k * 168 + j] = V[k][j] (ia_db3_rot_floats floats); ia_db3_build_rot writes the rotated
  * split tiles (352 B per row: ia_db3_rot_components components as f16 pairs, the rest as f16)
  * and A_skip into dbr (ia_db3_rot_bytes).  IaSynthArgs.dbr / .rot then select the R16c screen

@@ -73,6 +73,10 @@ int ia_diag_set_screen_sched(int sched);
 /* strip-order image-form levels: the producer / consumer screen k_screen16p (1, default;
  * IA_SCREEN_PC) or k_screen16i (0); same minima; returns the previous value, -1 leaves it */
 int ia_diag_set_screen_pc(int on);
+/* the rotated screen's form for this process (IA_R16_FORM): 1 [default] the wave-owned
+ * k_screen16w (queries staged in LDS, DB tiles in each wave's registers), 0 the block form
+ * k_screen16r (DB staged through LDS); same minima; returns the previous value */
+int ia_diag_set_r16_form(int form);
 /* ia_db_build_image without rows: the fused one-pass build k_img_build (1, default;
  * IA_IMG_FUSED) or the range + bound + pad + norm-pass kernels (0); same bytes and amax */
 int ia_diag_set_img_fused(int on);

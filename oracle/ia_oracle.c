@@ -224,8 +224,12 @@ void ia_oracle_nn_batch(const double *db, long N, const double *Q, long M, long 
  * Pruning is by a lower bound that holds for every row: for orthonormal v_1..v_P,
  * |a - q|^2 >= sum_i ((a - q).v_i)^2 (Bessel).  Rows are sorted by their first
  * projection, so a query's candidates lie in one contiguous key window.  Rounding is
- * covered by margins: every projection is computed to within IX_DELTA (|values| <= 1e3,
- * 55 terms), the bound is shrunk by (1 - 1e-9) for the vectors' orthonormality error,
+ * covered by margins: a computed n-term projection differs from the exact one by at most
+ * gamma_n sum_k |a_k v_k| (gamma_n = n u / (1 - n u), u = 2^-53), so projection p uses the
+ * margin delta_p = max(IX_DELTA, gamma_n (S_p + s_p)) with S_p the largest such sum over the
+ * rows (taken at build time) and s_p the query's own (a fixed 1e-10 was argued
+ * for 55 terms of |values| <= 1e3 only; 165-dim rows need the dimension in it), the
+ * bound is shrunk by (1 - 1e-9) for the vectors' orthonormality error,
  * and a row is only skipped when its bound exceeds best * (1 + 1e-9) + 1e-300, while a
  * computed d differs from the exact |a - q|^2 by < 1e-13 relative.  So a row whose
  * computed d could equal or beat the best is never skipped (ties keep the lowest row).
@@ -239,6 +243,7 @@ typedef struct {
     int P;                      /* projections used (1..IX_PMAX)                      */
     int dim;                    /* row length: 55 or 165                              */
     double v[IX_PMAX][DMAX];    /* orthonormal projection vectors                     */
+    double smax[IX_PMAX];       /* max over rows of sum_k |a_k v_pk| (rounding margin) */
     long *orig;                 /* sorted position -> original row                    */
     double *proj;               /* N x P projections, sorted order                    */
     double *rows;               /* N x D rows, sorted order                           */
@@ -248,6 +253,16 @@ static double dotn(const double *a, const double *v, int n) {
     double s = 0.;
     for (int k = 0; k < n; k++) s += a[k] * v[k];
     return s;
+}
+static double absdotn(const double *a, const double *v, int n) {
+    double s = 0.;
+    for (int k = 0; k < n; k++) s += fabs(a[k] * v[k]);
+    return s;
+}
+/* gamma_n of an n-term sum (u = 2^-53), rounded up generously */
+static double ix_gamma(int n) {
+    const double nu = (double)(n + 1) * 0x1p-53;
+    return 1.01 * nu / (1.0 - nu);
 }
 
 static const double *g_sort_key;
@@ -289,6 +304,14 @@ IaOracleIndex *ia_oracle_index_build2(const double *db, long N, int Dn, const do
         memcpy(ix->rows + s * Dn, a, sizeof(double) * Dn);
         for (int p = 0; p < P; p++) ix->proj[s * P + p] = dotn(a, ix->v[p], Dn);
     }
+    for (int p = 0; p < P; p++) {
+        double m = 0.;
+        for (long i = 0; i < N; i++) {
+            const double t = absdotn(db + i * Dn, ix->v[p], Dn);
+            m = t > m ? t : m;
+        }
+        ix->smax[p] = m;
+    }
     free(key);
     return ix;
 }
@@ -302,10 +325,10 @@ void ia_oracle_index_free(IaOracleIndex *ix) {
 }
 
 /* lower bound of |a - q|^2 from the projections, rounding margins applied */
-static inline double ix_bound(const double *pa, const double *pq, int P) {
+static inline double ix_bound(const double *pa, const double *pq, const double *dl, int P) {
     double lb = 0.;
     for (int p = 0; p < P; p++) {
-        double g = fabs(pa[p] - pq[p]) - IX_DELTA;
+        double g = fabs(pa[p] - pq[p]) - dl[p];
         if (g > 0.) lb += g * g;
     }
     return lb * (1.0 - 1e-9);
@@ -313,12 +336,12 @@ static inline double ix_bound(const double *pa, const double *pq, int P) {
 
 /* (d, row) lexicographic minimum over sorted positions [lo, hi), starting from (*bd, *bi) */
 static void ix_scan(const IaOracleIndex *ix, long lo, long hi, const double *q, const double *pq,
-                    double *bd, long *bi) {
+                    const double *dl, double *bd, long *bi) {
     const int P = ix->P, Dn = ix->dim;
     double best = *bd;
     long bix = *bi;
     for (long s = lo; s < hi; s++) {
-        if (ix_bound(ix->proj + s * P, pq, P) > best * IX_SLACK + 1e-300) continue;
+        if (ix_bound(ix->proj + s * P, pq, dl, P) > best * IX_SLACK + 1e-300) continue;
         double d = distn(ix->rows + s * Dn, q, Dn);
         long r = ix->orig[s];
         if (d < best || (d == best && r < bix)) { best = d; bix = r; }
@@ -341,8 +364,13 @@ static long ix_lower(const IaOracleIndex *ix, double x) {
 long ia_oracle_index_nn(const IaOracleIndex *ix, const double *db, const double *q,
                         const long *seeds, int nseeds, double *dmin_out) {
     const int P = ix->P, Dn = ix->dim;
-    double pq[IX_PMAX];
-    for (int p = 0; p < P; p++) pq[p] = dotn(q, ix->v[p], Dn);
+    double pq[IX_PMAX], dl[IX_PMAX];
+    const double gam = ix_gamma(Dn);
+    for (int p = 0; p < P; p++) {
+        pq[p] = dotn(q, ix->v[p], Dn);
+        const double m = gam * (ix->smax[p] + absdotn(q, ix->v[p], Dn));
+        dl[p] = m > IX_DELTA ? m : IX_DELTA;
+    }
     double best = INFINITY;
     long bi = -1;
     for (int i = 0; i < nseeds; i++) {
@@ -352,15 +380,15 @@ long ia_oracle_index_nn(const IaOracleIndex *ix, const double *db, const double 
     /* seed from the key neighbourhood too */
     long c = ix_lower(ix, pq[0]);
     long s0 = c - 256 < 0 ? 0 : c - 256, s1 = c + 256 > ix->N ? ix->N : c + 256;
-    ix_scan(ix, s0, s1, q, pq, &best, &bi);
+    ix_scan(ix, s0, s1, q, pq, dl, &best, &bi);
     /* the key window that can hold a row with computed d <= best */
-    double r = sqrt(best * IX_SLACK / (1.0 - 1e-9)) + 2 * IX_DELTA;
+    double r = sqrt(best * IX_SLACK / (1.0 - 1e-9)) + 2 * dl[0];
     long lo = ix_lower(ix, pq[0] - r), hi = ix_lower(ix, pq[0] + r);
     while (hi < ix->N && ix->proj[hi * P] <= pq[0] + r) hi++;
     int T = ia_oracle_threads();
     if (T > 64) T = 64;
     if (T <= 1 || hi - lo < 8192) {
-        ix_scan(ix, lo, hi, q, pq, &best, &bi);
+        ix_scan(ix, lo, hi, q, pq, dl, &best, &bi);
     } else {
         double bd[64];
         long bix[64];
@@ -370,7 +398,7 @@ long ia_oracle_index_nn(const IaOracleIndex *ix, const double *db, const double 
         for (int t = 0; t < T; t++) {
             bd[t] = best;
             bix[t] = bi;
-            ix_scan(ix, lo + (hi - lo) * t / T, lo + (hi - lo) * (t + 1) / T, q, pq, &bd[t], &bix[t]);
+            ix_scan(ix, lo + (hi - lo) * t / T, lo + (hi - lo) * (t + 1) / T, q, pq, dl, &bd[t], &bix[t]);
         }
         for (int t = 0; t < T; t++)
             if (bd[t] < best || (bd[t] == best && bix[t] < bi)) { best = bd[t]; bi = bix[t]; }
@@ -425,6 +453,16 @@ static long nn_n(const double *db, long N, int n, const double *q) {
     for (int t = 0; t < T; t++)
         if (bix[t] >= 0 && bd[t] < best) { best = bd[t]; bi = bix[t]; }
     return bi;
+}
+
+/* exact 1-NN of M queries over rows of any length n (brute force; tests cross-check the
+ * projection index of 165-dim rows against it) */
+void ia_oracle_nn_n_batch(const double *db, long N, int n, const double *Q, long M, long *idx,
+                          double *dmin) {
+    for (long m = 0; m < M; m++) {
+        idx[m] = nn_n(db, N, n, Q + m * n);
+        dmin[m] = idx[m] >= 0 ? distn(db + idx[m] * n, Q + m * n, n) : INFINITY;
+    }
 }
 
 /* image_analogies.py:161-220 for one level (db may be NULL: rows built on the fly).

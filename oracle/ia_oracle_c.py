@@ -54,6 +54,8 @@ def lib():
         _lib.ia_oracle_index_free.argtypes = [ctypes.c_void_p]
         _lib.ia_oracle_index_nn_batch.argtypes = [ctypes.c_void_p, _dp, _dp, ctypes.c_long,
                                                   ctypes.POINTER(ctypes.c_long), _dp]
+        _lib.ia_oracle_nn_n_batch.argtypes = [_dp, ctypes.c_long, ctypes.c_int, _dp, ctypes.c_long,
+                                              ctypes.POINTER(ctypes.c_long), _dp]
         _lib.ia_oracle_synth_level_ix.restype = ctypes.c_long
         _lib.ia_oracle_synth_level_ix.argtypes = [ctypes.POINTER(IaOracleLevel), _dp,
                                                   ctypes.c_void_p]
@@ -189,6 +191,16 @@ class LevelDB:
         if self.D != 55:
             return self.index().nn(Q)
         return nn_batch(self.ptr, self.N, Q)
+
+    def scan(self, Q):
+        """Exact 1-NN by the brute-force scan, any row length (no index)."""
+        Q = np.ascontiguousarray(Q, dtype=np.float64)
+        M = Q.shape[0]
+        idx = np.empty(M, np.int64)
+        d = np.empty(M, np.float64)
+        lib().ia_oracle_nn_n_batch(self.ptr, self.N, self.D, _d(Q), M,
+                                   idx.ctypes.data_as(ctypes.POINTER(ctypes.c_long)), _d(d))
+        return idx, d
 
     def index(self, P=4):
         """An exact projection Index over these rows (same answers as nn, faster)."""

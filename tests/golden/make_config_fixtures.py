@@ -17,16 +17,20 @@ exact brute-force matcher, algorithms.py:73-75 restated):
   c4_full.npz     config c4 (job seed 0) with EVERY level in full, the finest included
                   (1,048,576 B' pixels against the 4,194,304-row database): s, im and the
                   SHA-256 of B' per level.  The 1-NN goes through the oracle's projection
-                  index (ia_oracle_c.Index: the brute-force scan's exact answer, checked
-                  against it in tests/test_oracle.py and against c4_queries.npz), which
-                  makes the run minutes instead of a day.
+                  index (ia_oracle_c.Index: the brute-force scan's exact answer; pinned to
+                  the scan on small DBs and, at this level's full 4,194,304 rows, to
+                  c4_queries.npz's brute-force answers by tests/test_oracle.py
+                  ::test_oracle_index_equals_scan_at_c4_scale), which makes the run minutes
+                  instead of a day.
 
   c1rgb_oracle.npz  3-channel matching (convert=False, the reference's default: num_ch = 3,
                   165-dim rows) at the c1 size (180 x 117 colour A = A' blur, B; kappa 0.5):
                   every level in full (colour_workload: the pyramids are the oracle's per
                   channel, skimage multichannel semantics).
-  c3rgb_oracle.npz  the same at the c3 size (362 x 638 colour, kappa 25, 5-level cap), every
-                  level below the finest.
+  c3rgb_oracle.npz  the same at the c3 size (362 x 638 colour, kappa 25, 5-level cap): the
+                  synthesized levels s1..s5, the finest included.  Both colour fixtures go
+                  through the projection index; c1rgb is re-derived by the brute-force scan
+                  in tests/test_oracle.py::test_colour_fixture_equals_brute_force_scan.
 
 Usage:  python tests/golden/make_config_fixtures.py c3|c4|c4levels|c4full|c5|c1rgb|c3rgb [threads]
 The inputs are rebuilt from bench.py's workload definitions, so the GPU tests regenerate

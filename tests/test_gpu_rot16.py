@@ -153,3 +153,47 @@ def test_r16_batch_equals_image_form(gpu, monkeypatch):
     for jr, ji in zip(r, i):
         for (b0, s0, m0), (b1, s1, m1) in zip(jr, ji):
             assert np.array_equal(s0, s1) and np.array_equal(m0, m1) and np.array_equal(b0, b1)
+
+
+def _segmin_r16(idx, Q, M, N):
+    import _ia
+    lib = _ia.lib()
+    qrows = lib.ia_diag_qp_rows(M)
+    q64 = torch.zeros((M, _ia.IA_DP), dtype=torch.float64, device='cuda')
+    q64[:, :55] = dev(Q[:M])
+    nseg = lib.ia_db_rows_padded(N) // min(lib.ia_db_chunk_rows(N), 512)
+    q16 = torch.zeros((qrows, Q16_HALVES), dtype=torch.float16, device='cuda')
+    nq = torch.zeros(qrows, dtype=torch.float64, device='cuda')
+    nsk = torch.zeros(qrows, dtype=torch.float64, device='cuda')
+    segmin = torch.full((qrows, nseg), float('nan'), dtype=torch.float32, device='cuda')
+    _ia.check(lib.ia_diag_screen16r(ctypes.byref(idx.src), idx.row0, N, _ia.ptr(idx.dbr), _ia.ptr(idx.rot),
+                                    _ia.ptr(idx.amax), _ia.ptr(idx.center), _ia.ptr(q64), M, _ia.ptr(q16),
+                                    _ia.ptr(nq), _ia.ptr(nsk), _ia.ptr(segmin), _ia.stream()),
+              'ia_diag_screen16r')
+    torch.cuda.synchronize()
+    return segmin[:M].cpu().numpy()
+
+
+@pytest.mark.parametrize('shape,cap', [((1024, 1024), 2), ((512, 256), 2), ((2048, 1024), 2)])
+def test_r16_wave_form_equals_block_form(gpu, shape, cap):
+    """The wave-owned screen (k_screen16w, the default) and the block form (k_screen16r) give
+    the same segment minima bit for bit at every block shape (G = 1..11, split launches),
+    on levels of 512-row (1 M and 2 M rows) and 256-row (131 k rows) segments."""
+    import _ia
+    lib = _ia.lib()
+    idx, As = _level(45, shape, cap)
+    rs = np.random.RandomState(8)
+    n = len(As)
+    Q = np.vstack([As[rs.randint(0, n, 64)], As[rs.randint(0, n, 300)] + rs.randn(300, 55) * 0.01,
+                   rs.rand(336, 55) * As.max()])
+    prev = lib.ia_diag_set_r16_form(1)
+    try:
+        for M in [1, 20, 64, 65, 128, 192, 256, 320, 342, 353, 700]:
+            lib.ia_diag_set_r16_form(1)
+            w = _segmin_r16(idx, Q, M, n)
+            lib.ia_diag_set_r16_form(0)
+            b = _segmin_r16(idx, Q, M, n)
+            assert np.isfinite(w).all(), M
+            assert np.array_equal(w.view(np.uint32), b.view(np.uint32)), M
+    finally:
+        lib.ia_diag_set_r16_form(prev)

@@ -561,3 +561,159 @@ def test_pass_check_classifies_a_cascade_as_an_exchange_failure(monkeypatch):
         bench.pass_check([object()])
     monkeypatch.setattr(_ia, 'lib', lambda: FakeLib(0, 0))
     bench.pass_check([object()])
+
+
+def test_residency_rule_takes_each_levels_own_kernels():
+    """the rule must take every sharded level's own fused kernel.  A non-strip
+    level runs k_xwave (2 workgroups per CU: ~52 KB of LDS, ~252 VGPRs), so a CU beside a
+    screen holds at most one waiting workgroup of it (j_max 1), not the strip kernel's two:
+    2 ranks sharing one GPU on a ~1000-px-wide sharded level (2 x 335 waiting workgroups)
+    are admitted with k_xstrip's resources and refused with k_xwave's; a strip level plus a
+    k_xwave level are pipelined only if the worst of both fits."""
+    import image_analogies as ia
+    xstrip, xwave, screen = (36864, 135), (52224, 252), (60416, 158)
+    lvl = [(1000, 1000)]
+    assert ia.residency_ok(2 * ia.wave_max_queries(1000, 1000), xstrip, screen)[0]
+    assert ia.sharded_schedule(lvl, True, 2, [xstrip], [screen]) is True
+    ok, j = ia.residency_ok(2 * ia.wave_max_queries(1000, 1000), xwave, screen)
+    assert not ok and j == 1
+    with pytest.raises(RuntimeError, match='forward progress'):
+        ia.sharded_schedule(lvl, True, 2, [xwave], [screen])
+    # one rank per GPU: c4's finest (strip) level beside a k_xwave level of 172 queries
+    two = [(1024, 1024), (512, 512)]
+    assert ia.sharded_schedule(two, True, 1, [xstrip, xstrip], [screen, screen]) is True
+    assert ia.sharded_schedule(two, True, 1, [xstrip, xwave], [screen, screen]) is False
+
+
+# ---- multi-GPU from the package API (gloo, 2 ranks; the device calls are faked) -------------
+
+def test_rank_jobs_partition_and_bench_seeds():
+    """image_analogies.rank_jobs splits n jobs over ranks as j = rank (mod world): disjoint,
+    complete, and bench.py's c5 job seeds (1000 + 3 (rank + world i)) are its indices."""
+    import image_analogies as ia
+    for n, world in ((32 * 8, 8), (7, 3), (2, 4), (0, 2)):
+        parts = [ia.rank_jobs(n, r, world) for r in range(world)]
+        flat = sorted(j for p in parts for j in p)
+        assert flat == list(range(n))
+        for r, p in enumerate(parts):
+            assert all(j % world == r for j in p)
+    assert [1000 + 3 * j for j in ia.rank_jobs(16, 1, 4)] == [1000 + 3 * (1 + 4 * i) for i in range(4)]
+    with pytest.raises(ValueError):
+        ia.rank_jobs(4, 2, 2)
+
+
+class _Shape:
+    def __init__(self, *shape):
+        self.shape = shape
+
+
+def _api_worker(rank, world, port, tmp, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import _ia
+    import image_analogies as ia
+    log = {'batch': [], 'single': [], 'dev': [], 'exch': 0, 'destroyed': 0, 'main': []}
+    # synthesize_jobs: the whole job list; this rank's entries are callables, the others None
+    jobs = [(lambda j=j: ('job', j, None, None)) if j % world == rank else None for j in range(7)]
+
+    def fake_batch(ins, L, ks, w, prof=False, debug=False, check=True):
+        log['batch'].append(([x[1] for x in ins], list(ks)))
+        return [{'job': x[1]} for x in ins]
+
+    def fake_dev(A_pyr, Ap, B_pyr, Bp, L, k, w, comm=None, rank=0, nranks=1, **kw):
+        if A_pyr == 'job':
+            log['single'].append((Ap, k))
+            return {'job': Ap}
+        log['dev'].append((None if comm is None else len(comm), rank, nranks))
+        return {l: (None, None) for l in range(1, L)}
+    ia.synthesize_batch_dev = fake_batch
+    ia.synthesize_dev = fake_dev
+    ks = [0.5 * j for j in range(7)]
+    res = ia.synthesize_jobs(jobs, 4, ks, None, rank, world, batch=2)
+    out['jobs%d' % rank] = (sorted(res), log['batch'], log['single'])
+    # image_analogies_main(comm='auto'): one exchange per sharded level, the device calls
+    # with this rank's place, files written by rank 0 only
+    import config as c
+
+    class FakeLib:
+        def ia_comm_destroy(self, h):
+            log['destroyed'] += 1
+            return 0
+    _ia.lib = lambda: FakeLib()
+    _ia.to_dev = lambda x: x
+    _ia.exchange_status = lambda cm: None
+
+    def fake_exchange(r, wsz, kind=None):
+        assert (r, wsz) == (rank, world)
+        log['exch'] += 1
+        return object()
+    _ia.exchange = fake_exchange
+    torch.cuda.synchronize = lambda *a: None
+    ia._read = lambda f: np.zeros((4, 4))
+    Ap_pyr = [_Shape(2, 2), _Shape(256, 256), _Shape(768, 768), _Shape(1024, 1024)]
+
+    class Lvl:
+        def __init__(self, n):
+            self.shape = (n, n)
+
+        def cpu(self):
+            return self
+
+        def numpy(self):
+            return np.zeros(self.shape)
+
+    def fake_setup(A, Aps, B, cc):
+        cc.max_levels = 4
+        cc.weights = np.ones(55)
+        return None, [Ap_pyr], None, [Lvl(2), Lvl(256), Lvl(512), Lvl(1024)], None
+    ia.setup_dev = fake_setup
+    ia.color_output = lambda *a: np.zeros((2, 2, 3))
+    import matplotlib
+    matplotlib.use('Agg')
+    import matplotlib.pyplot as plt
+    plt.imsave = lambda path, im: open(path, 'w').close()
+    path = os.path.join(tmp, 'run%d/' % 0)
+    ia.image_analogies_main('A.jpg', ['Ap.jpg'], 'B.jpg', path, c, comm='auto')
+    out['main%d' % rank] = (log['dev'], log['exch'], log['destroyed'])
+    # multi_main: the serial script loop spread over the ranks, overrides applied per run
+    runs = [('A%d' % j, ['Ap%d' % j], 'B%d' % j, os.path.join(tmp, 'm%d/' % j), {'k': j + 0.5})
+            for j in range(5)]
+
+    def fake_main(A, Aps, B, p, cc, debug=False, rank=None, nranks=None, **kw):
+        log['main'].append((A, cc.k, rank, nranks))
+        return A
+    ia.image_analogies_main = fake_main
+    got = ia.multi_main(runs, c)
+    out['multi%d' % rank] = (sorted(got), log['main'])
+    dist.destroy_process_group()
+
+
+def test_multi_gpu_package_entry_points_gloo(tmp_path):
+    """multi-GPU reachable from the drop-in API, driven over a gloo world of 2
+    (device calls faked, no GPU): synthesize_jobs runs rank r's jobs j = r (mod 2) in
+    batches with their own kappas; image_analogies_main(comm='auto') makes one exchange per
+    sharded level (c4-like shapes: the two levels of >= 2^19 rows), passes each rank's place
+    to the synthesis, releases the exchanges, and only rank 0 writes the outputs;
+    multi_main spreads the script's runs likewise with each run's config overrides."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 33500 + np.random.RandomState(17).randint(0, 1000)
+    mp.spawn(_api_worker, args=(world, port, str(tmp_path), out), nprocs=world, join=True)
+    ks = [0.5 * j for j in range(7)]
+    for r in range(world):
+        mine, batches, singles = out['jobs%d' % r]
+        assert mine == [j for j in range(7) if j % world == r]
+        flat = [j for b, _ in batches for j in b] + [j for j, _ in singles]
+        assert sorted(flat) == mine
+        assert all(len(b) <= 2 for b, _ in batches)
+        for b, kk in batches:
+            assert kk == [ks[j] for j in b]
+        dev, nexch, ndestroyed = out['main%d' % r]
+        assert dev == [(2, r, world)] and nexch == 2 and ndestroyed == 2
+        got, calls = out['multi%d' % r]
+        assert got == [j for j in range(5) if j % world == r]
+        assert [(a, k) for a, k, _, _ in calls] == [('A%d' % j, j + 0.5) for j in got]
+        assert all(rk == 0 and nr == 1 for _, _, rk, nr in calls)
+    assert os.path.exists(os.path.join(str(tmp_path), 'run0', 'metadata.txt'))

@@ -314,3 +314,76 @@ def test_level_features_3ch_match_extract_patches_2d(full):
                      for r in range(h) for c in range(w)])
     got = o.level_features(sm, lg, full)
     assert got.shape == ref.shape and np.array_equal(got, ref)
+
+
+# ---- the projection index the full-size fixtures were generated through ------------------
+
+def _fixture_module():
+    import os
+    import sys
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+    if here not in sys.path:
+        sys.path.insert(0, here)
+    import make_config_fixtures as mf
+    return mf
+
+
+def test_oracle_index_equals_scan_at_c4_scale():
+    """c4_full.npz was generated through the oracle's projection index.  On
+    c4's finest level (4,194,304 rows, bench.py's seed-0 inputs) the index must return the
+    brute-force scan's row and distance for every committed c4 query (512 captured from a
+    GPU synthesis + 64 near-ties; c4_queries.npz holds the scan's answers,
+    make_config_fixtures.make_c4), at P = 1 and P = 4 projections (~20 s on 8 threads)."""
+    mf = _fixture_module()
+    prev = oc.set_threads(8)
+    try:
+        A, Aps, B, k, cap, seed = mf.workload('c4')
+        A_pyr = o.compute_gaussian_pyramid(A, 3, cap)
+        Ap_pyr = o.compute_gaussian_pyramid(Aps[0], 3, cap)
+        db = oc.LevelDB(len(A_pyr) - 1, A_pyr, [Ap_pyr])
+        assert db.N == 4194304
+        f = golden('c4_queries.npz')
+        for P in (1, 4):
+            ix = db.index(P)
+            idx, d = ix.nn(f['q'])
+            del ix
+            assert np.array_equal(idx, f['idx']), P
+            assert np.array_equal(d, f['dist']), P
+    finally:
+        oc.set_threads(prev)
+
+
+def test_colour_index_equals_scan_165_dims():
+    """the index's rounding margin for 165-dim rows.  Random rows, exact
+    duplicates, 1e-12 near-ties and nudged rows of a 3-channel level: index == scan."""
+    rs = np.random.RandomState(11)
+    mf = _fixture_module()
+    A_pyr, Ap_list, B_pyr, Bp_pyr, L, k = mf.colour_workload('c1rgb')
+    db = oc.LevelDB(L - 1, A_pyr, Ap_list)
+    assert db.D == 165
+    N = db.N
+    Q = np.vstack([db.rows[rs.randint(0, N, 16)], db.rows[rs.randint(0, N, 16)] + 1e-12,
+                   db.rows[rs.randint(0, N, 16)] + rs.randn(16, 165) * 1e-3, rs.rand(8, 165)])
+    i0, d0 = db.scan(Q)
+    for P in (1, 4):
+        i1, d1 = db.index(P).nn(Q)
+        assert np.array_equal(i0, i1) and np.array_equal(d0, d1), P
+
+
+def test_colour_fixture_equals_brute_force_scan():
+    """c1rgb_oracle.npz (generated through the projection index) re-derived with the
+    brute-force scan at every level: s, im and the B' hash (~60 s on 8 threads)."""
+    mf = _fixture_module()
+    prev = oc.set_threads(8)
+    try:
+        A_pyr, Ap_list, B_pyr, Bp_pyr, L, k = mf.colour_workload('c1rgb')
+        w = o.compute_weights(3, 5, 12, 3)
+        out = oc.synthesize(A_pyr, Ap_list, B_pyr, Bp_pyr, L, k, w, indexed=False)
+    finally:
+        oc.set_threads(prev)
+    f = golden('c1rgb_oracle.npz')
+    assert sorted(out) == list(range(1, int(f['max_levels'])))
+    for l, (bp, s, im) in out.items():
+        assert np.array_equal(s.astype(np.int16), f['s%d' % l]), l
+        assert np.array_equal(im.astype(np.uint8), f['im%d' % l]), l
+        assert mf.bp_hash(bp) == str(f['bp_sha%d' % l]), l
