@@ -31,10 +31,10 @@ constexpr int MAX_G = 11;
 constexpr int SPC_MAX = 16;
 // stage buffers (r16_body) and blocks per CU the kernel is built for (A/B builds)
 #ifndef IA_R16_RING
-#define IA_R16_RING 3
+#define IA_R16_RING 2
 #endif
 #ifndef IA_R16_OCC
-#define IA_R16_OCC 2
+#define IA_R16_OCC 4
 #endif
 constexpr int R16_RING = IA_R16_RING;
 // (Round 5's lab builds that skipped loads, barriers, folds or operand reads to time the
@@ -49,7 +49,7 @@ constexpr int R16_RING = IA_R16_RING;
 #define IA_R16_PIN 1
 #endif
 #ifndef IA_R16_SPC
-#define IA_R16_SPC 8
+#define IA_R16_SPC 2
 #endif
 constexpr int SPC_STAGE = IA_R16_SPC;   // segments of minima staged in LDS at a time
 
@@ -338,7 +338,7 @@ __device__ __forceinline__ void stage_barrier() {
 
 template <int G, int W>
 __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *sbuf, int *smin,
-                                         const StageMap &sm, long chunk, int nstage, int tps,
+                                         const StageMap &sm, long chunk, int s0, int nstage, int tps,
                                          const half8 *__restrict__ q16, float *__restrict__ segmin,
                                          long seg0, long nseg, int q0, int M) {
     constexpr int NS = R16_S16 ? c16_ns<G, W>() : bal_ns(G, W);
@@ -367,7 +367,7 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
     }
     // one stage = 4 consecutive tiles: 4 R16_MFMA wave-instructions of 1 KiB, R16_MFMA per wave
     auto issue = [&](int s) {
-        const half8 *src = db16 + (stage_lrow(sm, chunk, s) >> 5) * R16_TILE_H8 + W * 64 + lane;
+        const half8 *src = db16 + (stage_lrow(sm, chunk, s0 + s) >> 5) * R16_TILE_H8 + W * 64 + lane;
         half8 *dst = sbuf + (s % R16_RING) * STAGE_H8 + W * 64;
 #pragma unroll
         for (int k = 0; k < R16_MFMA; ++k)
@@ -419,14 +419,16 @@ __device__ __forceinline__ void r16_body(const half8 *__restrict__ db16, half8 *
     }
 }
 
-// grid: (nchunks rounded up to 8) x groups, XCD-aware (all groups of a chunk share
-// blockIdx % 8); group g holds query tiles [g G, g G + G); grid y = job of a batch
+// grid: (nchunks x split rounded up to 8) x groups, XCD-aware (all groups of a part share
+// blockIdx % 8); part p = chunk p / split, its stages [(p % split) nstage / split, ...) (a
+// whole number of segments: the screen's grid, 4 blocks per CU, independent of the DB's
+// chunking); group g holds query tiles [g G, g G + G); grid y = job of a batch
 template <int G>
 __global__ __launch_bounds__(256, IA_R16_OCC) void k_screen16r(const half8 *__restrict__ db16, int nchunks, int ch,
                                                       int seg_rows, StageMap sm,
                                                       const half8 *__restrict__ q16, int M, int groups,
                                                       float *__restrict__ segmin, long nseg,
-                                                      const XJob *jobs, int parity) {
+                                                      const XJob *jobs, int parity, int split) {
     __shared__ half8 sbuf[R16_RING * STAGE_H8];
     __shared__ int smin[SPC_STAGE * G * 32];
     if (jobs) {
@@ -437,21 +439,24 @@ __global__ __launch_bounds__(256, IA_R16_OCC) void k_screen16r(const half8 *__re
     }
     const int b = blockIdx.x;
     const int slot = b >> 3;
-    const int chunk = (slot / groups) * 8 + (b & 7);
+    const int part = (slot / groups) * 8 + (b & 7);
     const int group = slot - (slot / groups) * groups;
-    if (chunk >= nchunks) return;   // uniform over the block, before any barrier
+    if (part >= nchunks * split) return;   // uniform over the block, before any barrier
+    const int lsp = __builtin_ctz((unsigned)split);
+    const int chunk = part >> lsp, half = part & (split - 1);
     const int spc = ch / seg_rows;
     for (int i = threadIdx.x; i < SPC_STAGE * G * 32; i += 256) smin[i] = 0x7fffffff;
-    const int nstage = ch / (STAGE_TILES * 32);
+    const int nstage = (ch / (STAGE_TILES * 32)) >> lsp;
     const int tps = seg_rows >> 5;
     const half8 *qg = q16 + (long)group * G * 32 * Q16_ROW;
-    const long seg0 = (long)chunk * spc;
+    const long seg0 = (long)chunk * spc + (long)half * (spc >> lsp);
     const int q0 = group * G * 32;
+    const int s0 = half * nstage;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wv == 0) r16_body<G, 0>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
-    else if (wv == 1) r16_body<G, 1>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
-    else if (wv == 2) r16_body<G, 2>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
-    else r16_body<G, 3>(db16, sbuf, smin, sm, chunk, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    if (wv == 0) r16_body<G, 0>(db16, sbuf, smin, sm, chunk, s0, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    else if (wv == 1) r16_body<G, 1>(db16, sbuf, smin, sm, chunk, s0, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    else if (wv == 2) r16_body<G, 2>(db16, sbuf, smin, sm, chunk, s0, nstage, tps, qg, segmin, seg0, nseg, q0, M);
+    else r16_body<G, 3>(db16, sbuf, smin, sm, chunk, s0, nstage, tps, qg, segmin, seg0, nseg, q0, M);
 }
 
 // ---- the wave-owned form (IA_R16_FORM = 1): DB tiles straight into each wave's registers ----
@@ -474,7 +479,10 @@ __global__ __launch_bounds__(256, IA_R16_OCC) void k_screen16r(const half8 *__re
 #endif
 constexpr int W_RING = IA_R16W_RING;   // tiles in flight per wave
 constexpr int W_WAVES = 8;             // waves per workgroup
-constexpr int W_SPB_MAX = 16;          // segments per workgroup (LDS minima)
+#ifndef IA_R16W_SPB
+#define IA_R16W_SPB 16
+#endif
+constexpr int W_SPB_MAX = IA_R16W_SPB;  // segments per workgroup (LDS minima)
 constexpr int W_LAG = 2;               // query blocks between an MFMA pair and its fold
 
 __device__ __forceinline__ void w_fold(const floatx4 &x, const floatx4 &y, float &mn) {
@@ -782,10 +790,12 @@ __global__ __launch_bounds__(64) void k_query_rows_r16(const double *__restrict_
 
 }  // namespace
 
-// the rotated screen's form (IA_R16_FORM / ia_diag_set_r16_form): 0 the block form k_screen16r
-// (DB staged through LDS), 1 the wave-owned form k_screen16w (queries in LDS, DB tiles in each
-// wave's registers); the same minima
-static std::atomic<int> g_r16_form{env_int("IA_R16_FORM", 1)};
+// the rotated screen's form (IA_R16_FORM / ia_diag_set_r16_form): 0 [default] the block form
+// k_screen16r (DB staged through LDS), 1 the wave-owned form k_screen16w (queries in LDS, DB
+// tiles in each wave's registers); the same minima.  Measured on c4 (same box, A/B/A/B): the
+// wave form's launches 155 vs 159 us but the step 781-789 vs 777-781 ms; the block form at 4
+// blocks per CU (ring 2) 758-763 ms, 148.5-148.9 us: the default
+static std::atomic<int> g_r16_form{env_int("IA_R16_FORM", 0)};
 static int r16_form() { return g_r16_form.load(std::memory_order_relaxed); }
 
 int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Float16 *q16, int M,
@@ -804,7 +814,18 @@ int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Flo
     const int T = (M + 31) / 32;
     const int groups = (T + MAX_G - 1) / MAX_G;
     const int G = (T + groups - 1) / groups;
-    const long nb = ((nchunks + 7) / 8) * 8 * groups;
+    // block-form parts per chunk: a power of two dividing the chunk's segments, doubled while
+    // the grid stays within one round of IA_R16_OCC blocks per CU (256 CUs)
+    static const long cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return (long)n;
+    }();
+    const int spc = ch / seg_rows;
+    int split = 1;
+    while (2 * split <= spc && nchunks * 2 * split * groups * njobs <= cus * IA_R16_OCC) split *= 2;
+    const long nb = ((nchunks * split + 7) / 8) * 8 * groups;
     IA_ARG(nb < (1L << 31), "screen grid too large");
     const dim3 grid((unsigned)nb, (unsigned)njobs);
     // the wave-owned form (k_screen16w): segments per workgroup spb, a power of two dividing
@@ -823,7 +844,7 @@ int launch_screen16r(const void *dbr, long nrows, const StageMap &sm, const _Flo
                                                    groups, segmin, nseg, jobs, parity);             \
         else                                                                                        \
             k_screen16r<GG><<<grid, 256, 0, st>>>(db16, (int)nchunks, ch, seg_rows, sm, q, M,       \
-                                                  groups, segmin, nseg, jobs, parity);              \
+                                                  groups, segmin, nseg, jobs, parity, split);       \
         break;
     switch (G) {
         IA_R16_CASE(1)
