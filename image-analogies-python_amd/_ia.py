@@ -72,6 +72,7 @@ _SIGS = {
     'ia_version': (ctypes.c_int, []),
     'ia_rgb_to_yiq': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_long, ctypes.c_double, _dp, _dp, _dp]),
     'ia_yiq_to_rgb': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp]),
+    'ia_color_output': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]),
     'ia_scale_to_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_long, ctypes.c_double, _dp, _dp]),
     'ia_axpb_f64': (ctypes.c_int, [_dp, ctypes.c_long, ctypes.c_int, ctypes.c_double,
                                    ctypes.c_double, ctypes.c_double, _dp, _dp]),
@@ -81,6 +82,7 @@ _SIGS = {
                                          ctypes.POINTER(ctypes.c_double), _dp, _dp]),
     'ia_mean_workspace_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_mean_f64': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp, _dp]),
+    'ia_var_f64': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp, _dp]),
     'ia_level_features_f64': (ctypes.c_int, [_dp, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, _dp, _dp]),
     'ia_db_rows_padded': (ctypes.c_long, [ctypes.c_long]),
@@ -92,7 +94,7 @@ _SIGS = {
     'ia_db_rot_components': (ctypes.c_int, []),
     'ia_screen_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'ia_fused_resources': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
-    'ia_level_resources': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    'ia_level_resources': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.POINTER(ctypes.c_int)]),
     'ia_db_rot_slots': (ctypes.c_int, []),
     'ia_db_rot_eps_a2': (ctypes.c_double, []),
     'ia_db_cov_bytes': (ctypes.c_size_t, []),
@@ -114,10 +116,13 @@ _SIGS = {
                                                    ctypes.c_int]),
     'ia_synth_level': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
     'ia_synth_level3': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), _dp]),
+    'ia_synth3_status': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_synth_levels3': (ctypes.c_int, [ctypes.POINTER(IaSynthArgs), ctypes.c_int, _dp]),
     'ia_db3_rot_bytes': (ctypes.c_size_t, [ctypes.c_long]),
     'ia_db3_rot_components': (ctypes.c_int, []),
     'ia_db3_rot_floats': (ctypes.c_int, []),
+    'ia_db3_cov_bytes': (ctypes.c_size_t, []),
+    'ia_db3_cov': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]),
     'ia_db3_build_rot': (ctypes.c_int, [_dp, ctypes.c_long, _dp, _dp, _dp]),
     'ia_synth3_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_long]),
     'ia_db3_bytes': (ctypes.c_size_t, [ctypes.c_long]),
@@ -400,6 +405,15 @@ def mean_dev(t):
     ws = workspace(lib().ia_mean_workspace_bytes(t.numel()))
     check(lib().ia_mean_f64(ptr(t), t.numel(), ptr(out), ptr(ws), stream()), 'ia_mean_f64')
     return float(out.item())
+
+
+def var_f64(t):
+    """Unbiased device variance of a fp64 tensor (ia_var_f64, two passes) -> python float."""
+    t = t.contiguous()
+    out = torch.empty(2, dtype=torch.float64, device=t.device)
+    ws = workspace(lib().ia_mean_workspace_bytes(t.numel()))
+    check(lib().ia_var_f64(ptr(t), t.numel(), ptr(out), ptr(ws), stream()), 'ia_var_f64')
+    return float(out[0].item())
 
 
 _EXCHANGE_FALLBACK = []   # reasons the device-side exchange was replaced by RCCL

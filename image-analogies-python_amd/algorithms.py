@@ -162,7 +162,7 @@ class LevelIndex:
         L, k = int(tables), int(hashes)
         if not (1 <= L and 1 <= k and L * k <= 64):
             raise ValueError('LSH needs 1 <= tables * hashes <= 64')
-        var = (34 * float(self.A_lg.var()) + 21 * float(self.Ap_lg.var())) / 55.0
+        var = (34 * _ia.var_f64(self.A_lg) + 21 * _ia.var_f64(self.Ap_lg)) / 55.0
         w = float(width) * max(np.sqrt(var), 1e-6)
         self.lsh_proj_host = lsh_projections(L, k, w, seed)
         self.lsh_proj = torch.as_tensor(self.lsh_proj_host).to(dev)
@@ -215,14 +215,13 @@ class LevelIndex:
 
 def rot3_build(db3, N):
     """The rotated split DB of the 3-channel screen (R16c) from an ia_db3_build
-    buffer: the covariance of ~64 k sampled rows around their mean (device GEMM), its
-    eigenvectors on the host (165 x 165; any orthonormal basis keeps the matcher exact, the
-    principal one keeps the bound tight), then ia_db3_build_rot.  Returns (rot, dbr)."""
+    buffer: the covariance of ~64 k sampled rows around their mean (ia_db3_cov, on device),
+    its eigenvectors on the host (165 x 165; any orthonormal basis keeps the matcher exact,
+    the principal one keeps the bound tight), then ia_db3_build_rot.  Returns (rot, dbr)."""
     lib, st = _ia.lib(), _ia.stream()
-    rows = db3[:N * 168].view(N, 168)[:, :165]
-    X = rows[::max(1, N // 65536)]
-    Xc = X - X.mean(0)
-    w, V = np.linalg.eigh((Xc.T @ Xc).cpu().numpy())
+    cov = torch.empty(lib.ia_db3_cov_bytes() // 8, dtype=torch.float64, device=db3.device)
+    _ia.check(lib.ia_db3_cov(_ia.ptr(db3), N, _ia.ptr(cov), st), 'ia_db3_cov')
+    w, V = np.linalg.eigh(cov[:165 * 168].view(165, 168)[:, :165].cpu().numpy())
     R = np.zeros(lib.ia_db3_rot_floats(), dtype=np.float32)
     R.reshape(165, 168)[:, :165] = V[:, ::-1]
     rot = torch.as_tensor(R).to(db3.device)

@@ -556,6 +556,70 @@ __global__ __launch_bounds__(256, 1) void k_db3_rot(const double *__restrict__ r
     }
 }
 
+// ---- the covariance of a 3-channel level's rows (ia_db3_cov, rot3_build's matrix) -------
+// ~64 k rows sampled every `step` (rot3_build's rows[::max(1, N // 65536)]), centred at their
+// mean, fp64: column sums per sample slice, the mean, then per (16 output rows a, slice) the
+// centred products with every column b, 32 sampled rows staged in LDS at a time; partials
+// reduced in slice order (deterministic).  Any orthonormal basis keeps the matcher exact; the
+// principal one of this matrix keeps its bound tight.
+constexpr int C3C_SPLIT = 16, C3C_AB = 16, C3C_NA = (D3 + C3C_AB - 1) / C3C_AB, C3C_TR = 32;
+__global__ __launch_bounds__(256) void k_db3_colsum(const double *__restrict__ rows, long step, long nsamp,
+                                                    double *__restrict__ part) {
+    const int t = threadIdx.x, sl = blockIdx.x;
+    const long i0 = nsamp * sl / C3C_SPLIT, i1 = nsamp * (sl + 1) / C3C_SPLIT;
+    if (t >= D3) return;
+    double acc = 0.0;
+    for (long i = i0; i < i1; ++i) acc += rows[i * step * D3P + t];
+    part[sl * D3P + t] = acc;
+}
+__global__ __launch_bounds__(256) void k_db3_mean(const double *__restrict__ part, long nsamp, double *__restrict__ mean) {
+    const int t = threadIdx.x;
+    if (t >= D3P) return;
+    double acc = 0.0;
+    for (int sl = 0; sl < C3C_SPLIT; ++sl) acc += part[sl * D3P + t];
+    mean[t] = t < D3 ? acc / (double)nsamp : 0.0;
+}
+__global__ __launch_bounds__(256) void k_db3_cov(const double *__restrict__ rows, long step, long nsamp,
+                                                 const double *__restrict__ mean, double *__restrict__ part) {
+    __shared__ double X[C3C_TR][D3P];
+    const int t = threadIdx.x, a0 = blockIdx.x * C3C_AB, sl = blockIdx.y;
+    const long i0 = nsamp * sl / C3C_SPLIT, i1 = nsamp * (sl + 1) / C3C_SPLIT;
+    double acc[C3C_AB];
+#pragma unroll
+    for (int j = 0; j < C3C_AB; ++j) acc[j] = 0.0;
+    const double mu = t < D3 ? mean[t] : 0.0;
+    for (long r0 = i0; r0 < i1; r0 += C3C_TR) {
+        __syncthreads();
+        for (int e = t; e < C3C_TR * D3P; e += 256) {
+            const int rr = e / D3P, k = e - rr * D3P;
+            const long i = r0 + rr;
+            X[rr][k] = i < i1 && k < D3 ? rows[i * step * D3P + k] - mean[k] : 0.0;
+        }
+        __syncthreads();
+        if (t < D3) {
+            for (int rr = 0; rr < C3C_TR; ++rr) {
+                const double xb = X[rr][t];
+#pragma unroll
+                for (int j = 0; j < C3C_AB; ++j) acc[j] += X[rr][a0 + j < D3 ? a0 + j : 0] * xb;
+            }
+        }
+    }
+    (void)mu;
+    if (t < D3) {
+#pragma unroll
+        for (int j = 0; j < C3C_AB; ++j)
+            if (a0 + j < D3) part[((long)sl * D3 + a0 + j) * D3P + t] = acc[j];
+    }
+}
+__global__ __launch_bounds__(256) void k_db3_cov_reduce(const double *__restrict__ part, double *__restrict__ cov) {
+    const int a = blockIdx.x, t = threadIdx.x;
+    if (t >= D3P) return;
+    double acc = 0.0;
+    if (t < D3)
+        for (int sl = 0; sl < C3C_SPLIT; ++sl) acc += part[((long)sl * D3 + a) * D3P + t];
+    cov[(long)a * D3P + t] = acc;
+}
+
 // the R16c query operand of query m from thread k's centred feature d (256 threads):
 // kappa_j = sum_k V[k][j] d_k (thread j, fp64 from the fp32 V in global memory), |q'|^2 ->
 // qn, |kappa_skip|^2 -> nsk, the slots into the query tile (m >= M: zero columns)
@@ -959,8 +1023,35 @@ __device__ __forceinline__ double acc8_sum(const Acc8 *acc, bool weighted) {
 // sums, so the winner's weighted distance needs no second read), with the 15 coherence rows
 // in the first tile's round trip; the lexicographic (distance, row) minimum carries its
 // weighted distance; coherence pick, kappa test and the B' update as k_finish3w.
-__global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
+// FUSE (the R16c path, IA_C3_FUSE): the same launch also writes the query rows of wave t + 1
+// (as k_query3r / r3_query; k_xwave's scheme): the workgroup of pixel (y, x)
+// builds the row of (y, x + 1).  Of its 165 features only the B' samples of two pixels can
+// come from wave t: this pixel (its new value, from LDS) and the upper neighbour (y - 1,
+// x + 3) (its three new channels from six tagged 8-byte decision granules, dbox[8 (y - 1)
+// ...]); the rest are loaded at the start.  Pixels take their index from a ticket counter, so a
+// workgroup waits only for a lower ticket (dispatched earlier); extra workgroups (index >= M)
+// build the first row of the rows that enter wave t + 1.  Query buffers alternate by wave parity.
+struct Nx3 {
+    Img3 Bsm, Blg, Bpsm, Bplg;
+    int M, y_lo_n, M_n, H;
+    const Col16Meta *meta;
+    const float *rot;
+    double *q3n, *qnn, *nskn;
+    half8 *q16n;
+    unsigned *tickets;            // [2]; tickets[t & 1] is this launch's
+    unsigned *err;                // a decision wait timed out
+    unsigned long long *dbox;     // 8 granules per row: channel c's bits at 2c (lo), 2c + 1 (hi)
+};
+constexpr unsigned long long C3_WAIT_TICKS = 1000000000ULL;   // 10 s of s_memrealtime
+__device__ __forceinline__ unsigned long long c3_gran(unsigned tag, unsigned bits) {
+    return ((unsigned long long)tag << 32) | bits;
+}
+
+template <bool FUSE>
+__global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc, Nx3 nx) {
     __shared__ double qs[D3P], wsh[D3P];
+    __shared__ double ownv[3], nbv[3], qred[4], qds[D3];
+    __shared__ int tks, anydep;
     __shared__ Acc8 acc[32 * 8];                // a tile's rows (32 x 8 parts)
     __shared__ Acc8 cacc[15 * 8];               // the coherence rows
     __shared__ double sump[15], sumw[15];
@@ -970,12 +1061,43 @@ __global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
     __shared__ long long ri[4];
     __shared__ float fmn[4];
     __shared__ int clist[C3_CAND], ccount;
-    const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int m = blockIdx.x;
+    if constexpr (FUSE) {
+        if (tid == 0) {
+            tks = (int)atomicAdd(&nx.tickets[f.t & 1], 1u);
+            anydep = 0;
+        }
+        __syncthreads();
+        m = tks;
+        if (m == 0 && tid == 0) __hip_atomic_store(&nx.tickets[(f.t + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const int ro = tid >> 3, j = tid & 7;
     const int y = f.y_lo + m, x = f.t - 3 * y;
     const int W = f.W, Ah = f.Ah, Aw = f.Aw;
     const long hw = (long)Ah * Aw;
     const bool first = y == 0 && x == 0;
+    const bool cur = !FUSE || m < nx.M;
+    const bool nxt = FUSE && y >= nx.y_lo_n && y < nx.y_lo_n + nx.M_n;
+    // FUSE: feature tid of the next query (y, x + 1): loaded now unless it is a wave-t sample
+    double nv = 0.0;
+    int dep = 0, dch = 0;
+    if (FUSE && nxt && tid < D3) {
+        const int X = x + 1;
+        if (tid < D3_FULL) {
+            nv = feat3(nx.Bsm, nx.Blg, y, X, tid);
+        } else if (tid < D3_FULL + 27) {
+            nv = feat3(nx.Bpsm, nx.Bplg, y, X, tid - D3_FULL);
+        } else {
+            const int t2 = (tid - D3_FULL - 27) / 3;
+            dch = (tid - D3_FULL - 27) - 3 * t2;
+            const int rr = symi2(y + t2 / 5 - 2, nx.H), cc = symi2(X + t2 % 5 - 2, W);
+            dep = (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
+            if (dep == 0) nv = nx.Bplg.p[((long)rr * W + cc) * 3 + dch];
+        }
+        if (dep == 2) anydep = 1;
+    }
+    if (cur) {
     // ---- one round trip: query, weights, coherence s / im, tile minima
     if (tid < D3P) {
         qs[tid] = f.q3[(long)m * D3P + tid];
@@ -1102,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
     }
     if (lane == 0) { rd[wv] = bd; ri[wv] = bi; rw[wv] = bw; }
     __syncthreads();
-    if (wv != 0) return;
+    if (wv == 0) {
     double wd = rd[0], ww = rw[0];
     long long wi = ri[0];
 #pragma unroll
@@ -1127,8 +1249,19 @@ __global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
     int pr = ar, pc = ac;
     if (valid && d_coh <= d_app * f.kappa_factor) { pr = wr; pc = wc; img = wim; }
     const long qpx = (long)y * W + x;
-    if (lane < 3)
-        f.Bp_lg[qpx * 3 + lane] = f.Ap_lg[((img * hw) + (long)pr * Aw + pc) * 3 + lane];
+    if (lane < 3) {
+        const double val = f.Ap_lg[((img * hw) + (long)pr * Aw + pc) * 3 + lane];
+        f.Bp_lg[qpx * 3 + lane] = val;
+        if constexpr (FUSE) {
+            // the decision for the lower neighbour's next query, and this pixel's own
+            ownv[lane] = val;
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(val);
+            unsigned long long *d = nx.dbox + 8 * (long)y + 2 * lane;
+            __hip_atomic_store(d, c3_gran(f.t + 1, (unsigned)bits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d + 1, c3_gran(f.t + 1, (unsigned)(bits >> 32)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (lane == 0) {
         f.s[2 * qpx] = pr;
         f.s[2 * qpx + 1] = pc;
@@ -1144,6 +1277,45 @@ __global__ __launch_bounds__(256) void k_exact3(Fin3 f, Scr3 sc) {
             o[6] = valid;
             f.dbg_dist[2 * qpx] = valid ? d_app : 0.0;
             f.dbg_dist[2 * qpx + 1] = valid ? d_coh : 0.0;
+        }
+    }
+    }   // wave 0
+    }   // cur
+    if constexpr (FUSE) {
+        __syncthreads();   // ownv, anydep
+        if (nxt) {
+            if (anydep && tid == 0) {   // the upper neighbour (ticket m - 1) decided (y - 1, x + 3)
+                const unsigned long long *d = nx.dbox + 8 * (long)(y - 1);
+                const unsigned tag = (unsigned)(f.t + 1);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    bool ok = true;
+                    unsigned long long g[6];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        g[c] = __hip_atomic_load(d + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = ok && (unsigned)(g[c] >> 32) == tag;
+                    }
+                    if (ok) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            nbv[c] = __longlong_as_double(
+                                (long long)(((g[2 * c + 1] & 0xffffffffULL) << 32) | (g[2 * c] & 0xffffffffULL)));
+                        break;
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > C3_WAIT_TICKS) {
+                        atomicOr(nx.err, 1u);
+                        nbv[0] = nbv[1] = nbv[2] = 0.0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            const double v = dep == 1 ? ownv[dch] : dep == 2 ? nbv[dch] : nv;
+            const int mq = y - nx.y_lo_n;
+            if (tid < D3P) nx.q3n[(long)mq * D3P + tid] = tid < D3 ? v : 0.0;
+            r3_query(mq, nx.M_n, tid, v, nx.meta, nx.rot, nx.qnn, nx.nskn, nx.q16n, qds, qred);
         }
     }
 }
@@ -1323,14 +1495,27 @@ static inline int match3_blocks(long nrows) { return (int)((nrows + M3_ROWS - 1)
 static std::atomic<int> g_color16{env_int("IA_COLOR16", 1)};
 static unsigned long long *g_c3_stats = nullptr;   // diagnostic counters (ia_diag_color16_stats)
 
-// the synthesis workspace: q3 | best | partials (fp64 search) | q16 | qn | tile minima
+// the synthesis workspace: q3 | best | partials (fp64 search) | q16 | qn | tile minima, and for
+// the fused R16c tail (k_exact3<true>) the odd waves' query set, the control words and the
+// decision granules
 struct Ws3 {
     double *q3;
     Best *best, *part;
     half8 *q16;              // the query tiles of either screen (C16_TILE >= R3_TILE)
     double *qn, *nsk;
     float *smin;
+    double *q3b, *qnb, *nskb;
+    half8 *q16b;
+    unsigned *ctl;           // tickets[2], error word
+    unsigned long long *dbox;
 };
+constexpr int C3_CTL_ERR = 2;
+// the fused colour tail (k_exact3<true>: the next wave's query rows from the exact stage's
+// launch; IA_C3_FUSE, default 1) on R16c levels
+static inline bool c3_fuse() {
+    static const int v = env_int("IA_C3_FUSE", 1);
+    return v != 0;
+}
 static_assert(C16_TILE >= R3_TILE, "query tiles");
 static inline size_t ws3_layout(int H, int W, long nrows, char *base, Ws3 *w) {
     const size_t M = (size_t)max_wave(H, W), Mp = (M + 31) / 32 * 32;
@@ -1343,7 +1528,19 @@ static inline size_t ws3_layout(int H, int W, long nrows, char *base, Ws3 *w) {
     char *qn = take(Mp * sizeof(double));
     char *nsk = take(Mp * sizeof(double));
     char *smin = take(M * (size_t)c3_stride((int)db3_tiles(nrows)) * sizeof(float));
+    char *q3b = take(Mp * D3P * sizeof(double));
+    char *q16b = take(Mp / 32 * C16_TILE * sizeof(half8));
+    char *qnb = take(Mp * sizeof(double));
+    char *nskb = take(Mp * sizeof(double));
+    char *ctl = take(256);
+    char *dbox = take((size_t)H * 8 * sizeof(unsigned long long));
     if (w) {
+        w->q3b = reinterpret_cast<double *>(q3b);
+        w->q16b = reinterpret_cast<half8 *>(q16b);
+        w->qnb = reinterpret_cast<double *>(qnb);
+        w->nskb = reinterpret_cast<double *>(nskb);
+        w->ctl = reinterpret_cast<unsigned *>(ctl);
+        w->dbox = reinterpret_cast<unsigned long long *>(dbox);
         w->q3 = reinterpret_cast<double *>(q3);
         w->best = reinterpret_cast<Best *>(best);
         w->part = reinterpret_cast<Best *>(part);
@@ -1366,8 +1563,9 @@ struct Level3 {
     Img3 Bsm{}, Blg{}, Bpsm{}, Bplg{};
     int H = 0, W = 0, nw = 0, nb = 0, ntiles = 0;
     bool split = true, rot = false;   // rot: the R16c screen (a->dbr, a->rot: ia_db3_build_rot)
+    bool fuse = false;                // rot with the fused tail (k_exact3<true>)
     const half8 *dbr = nullptr;
-    int init(const IaSynthArgs *a_) {
+    int init(const IaSynthArgs *a_, hipStream_t st) {
         a = a_;
         IA_ARG(a && a->db && a->B_sm && a->B_lg && a->Bp_sm && a->Bp_lg && a->weights && a->s && a->im &&
                    a->workspace && a->H > 0 && a->W > 0,
@@ -1393,6 +1591,9 @@ struct Level3 {
         sc = Scr3{w.smin, ntiles, a->nrows, w.qn, v.meta, g_c3_stats, rot ? w.nsk : nullptr,
                   rot ? db3r_meta(const_cast<void *>(a->dbr), a->nrows) : nullptr};
         nw = (W - 1) + 3 * (H - 1) + 1;
+        fuse = rot && c3_fuse();
+        IA_HIP(hipMemsetAsync(w.ctl, 0, 256, st));
+        if (fuse) IA_HIP(hipMemsetAsync(w.dbox, 0, (size_t)H * 8 * sizeof(unsigned long long), st));
         return IA_OK;
     }
     static void rows(int H, int W, int t, int &y_lo, int &M) {
@@ -1405,14 +1606,37 @@ struct Level3 {
         if (M <= 0) return IA_OK;
         f.t = t;
         f.y_lo = y_lo;
-        if (rot) {
+        if (fuse) {
+            // wave t's query set b (wave 0's built here, the later ones by the previous wave's
+            // k_exact3<true>), wave t + 1's into set b ^ 1
+            const int b = t & 1;
+            double *q3s[2] = {w.q3, w.q3b}, *qns[2] = {w.qn, w.qnb}, *nsks[2] = {w.nsk, w.nskb};
+            half8 *q16s[2] = {w.q16, w.q16b};
+            int tpw;
+            const dim3 grid = screen3r_grid(ntiles, M, tpw);
+            if (t == 0)
+                k_query3r<<<(M + 31) / 32 * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, a->rot, nullptr,
+                                                              q3s[0], qns[0], nsks[0], q16s[0]);
+            k_screen3r<<<grid, 256, 0, st>>>(dbr, ntiles, q16s[b], M, tpw, w.smin);
+            int y_lo_n = 0, M_n = 0;
+            if (t + 1 < nw) rows(H, W, t + 1, y_lo_n, M_n);
+            const Nx3 nx{Bsm, Blg, Bpsm, Bplg, M, y_lo_n, M_n, H, v.meta, a->rot, q3s[b ^ 1], qns[b ^ 1],
+                         nsks[b ^ 1], q16s[b ^ 1], w.ctl, w.ctl + C3_CTL_ERR, w.dbox};
+            Fin3 fb = f;
+            fb.q3 = q3s[b];
+            Scr3 sb = sc;
+            sb.qn = qns[b];
+            sb.nsk = nsks[b];
+            const int R = std::max(M, M_n > 0 ? y_lo_n + M_n - y_lo : 0);
+            k_exact3<true><<<R, 256, 0, st>>>(fb, sb, nx);
+        } else if (rot) {
             const int QT = (M + 31) / 32;
             int tpw;
             const dim3 grid = screen3r_grid(ntiles, M, tpw);
             k_query3r<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, a->rot, nullptr, w.q3,
                                                w.qn, w.nsk, w.q16);
             k_screen3r<<<grid, 256, 0, st>>>(dbr, ntiles, w.q16, M, tpw, w.smin);
-            k_exact3<<<M, 256, 0, st>>>(f, sc);
+            k_exact3<false><<<M, 256, 0, st>>>(f, sc, Nx3{});
         } else if (split) {
             const int QT = (M + 31) / 32;
             int tpw;
@@ -1420,7 +1644,7 @@ struct Level3 {
             k_query3s<<<QT * 32, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, M, v.meta, w.q3, w.qn,
                                                reinterpret_cast<_Float16 *>(w.q16));
             k_screen3<<<grid, 256, 0, st>>>(v.db16, ntiles, w.q16, M, tpw, w.smin);
-            k_exact3<<<M, 256, 0, st>>>(f, sc);
+            k_exact3<false><<<M, 256, 0, st>>>(f, sc, Nx3{});
         } else {
             k_query3<<<M, 256, 0, st>>>(Bsm, Blg, Bpsm, Bplg, t, y_lo, w.q3);
             k_match3<<<nb, 256, 0, st>>>(f.db3, a->nrows, 0, w.q3, M, w.part);
@@ -1580,6 +1804,24 @@ int ia_match3_batch(const double *db3, long nrows, const double *q165, int M, in
 size_t ia_synth3_workspace_bytes(int H, int W, long nrows) { return ws3_layout(H, W, nrows, nullptr, nullptr); }
 
 size_t ia_db3_rot_bytes(long nrows) { return nrows > 0 ? db3r_tiles_bytes(nrows) + sizeof(Rot3Meta) : 0; }
+
+size_t ia_db3_cov_bytes(void) {
+    return (size_t)(D3 * D3P + D3P + C3C_SPLIT * D3P + (size_t)C3C_SPLIT * D3 * D3P) * sizeof(double);
+}
+
+int ia_db3_cov(const double *db3, long nrows, double *cov, void *stream) {
+    IA_ARG(db3 && cov && nrows > 0, "ia_db3_cov: bad args");
+    hipStream_t st = S(stream);
+    const long step = nrows / 65536 > 1 ? nrows / 65536 : 1;
+    const long nsamp = (nrows + step - 1) / step;
+    double *mean = cov + D3 * D3P, *cpart = mean + D3P, *vpart = cpart + C3C_SPLIT * D3P;
+    k_db3_colsum<<<C3C_SPLIT, 256, 0, st>>>(db3, step, nsamp, cpart);
+    k_db3_mean<<<1, 256, 0, st>>>(cpart, nsamp, mean);
+    k_db3_cov<<<dim3(C3C_NA, C3C_SPLIT), 256, 0, st>>>(db3, step, nsamp, mean, vpart);
+    k_db3_cov_reduce<<<D3, 256, 0, st>>>(vpart, cov);
+    IA_LAUNCH_CHECK("ia_db3_cov");
+    return IA_OK;
+}
 int ia_db3_rot_components(void) { return R3_P; }
 int ia_db3_rot_floats(void) { return R3_ROT_FLOATS; }
 
@@ -1608,10 +1850,29 @@ int ia_diag_db3_askip(const void *dbr, long nrows, float *out) {
     return IA_OK;
 }
 
+int ia_synth3_status(const IaSynthArgs *levels, int n, void *stream) {
+    IA_ARG(levels && n >= 1, "ia_synth3_status: bad args");
+    IA_HIP(hipStreamSynchronize(S(stream)));
+    for (int j = 0; j < n; ++j) {
+        const IaSynthArgs &a = levels[j];
+        IA_ARG(a.workspace && a.H > 0 && a.W > 0 && a.nrows > 0, "ia_synth3_status: bad level");
+        Ws3 w{};
+        ws3_layout(a.H, a.W, a.nrows, reinterpret_cast<char *>(a.workspace), &w);
+        unsigned e = 0;
+        IA_HIP(hipMemcpy(&e, w.ctl + C3_CTL_ERR, sizeof(e), hipMemcpyDeviceToHost));
+        if (e) {
+            set_error("ia_synth3_status: a wait for a neighbouring pixel's decision timed out "
+                      "(device schedule fault)");
+            return IA_E_SCHED;
+        }
+    }
+    return IA_OK;
+}
+
 int ia_synth_level3(const IaSynthArgs *a, void *stream) {
     hipStream_t st = S(stream);
     Level3 run;
-    int rc = run.init(a);
+    int rc = run.init(a, st);
     if (rc) return rc;
     for (int t = 0; t < run.nw; ++t)
         if ((rc = run.wave(t, st))) return rc;
@@ -1638,18 +1899,19 @@ int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
     std::vector<Level3> run(n);
     std::vector<std::vector<hipEvent_t>> blk(n);   // blk[j][b]: level j done through block b
     for (int j = 0; j < n; ++j) {
-        int rc = run[j].init(&levels[j]);
+        IA_HIP(hipStreamWaitEvent(ss[j], start, 0));   // (init's memsets too: after the caller's work)
+        int rc = run[j].init(&levels[j], ss[j]);
         if (rc) return rc;
         blk[j].assign((run[j].nw + C3_PIPE_BLOCK - 1) / C3_PIPE_BLOCK, nullptr);
     }
     // every level whole, coarse to fine: a level's waits name events already recorded
     for (int j = 0; j < n; ++j) {
         hipStream_t sj = ss[j];
-        IA_HIP(hipStreamWaitEvent(sj, start, 0));
         int waited = -1;
         for (int t = 0; t < run[j].nw; ++t) {
             if (j > 0) {
-                const int w = c3_need(levels[j], t);
+                // (the fused tail's launch of wave t also builds wave t + 1's query rows)
+                const int w = c3_need(levels[j], run[j].fuse && t + 1 < run[j].nw ? t + 1 : t);
                 if (w > waited) {
                     const int b = w / C3_PIPE_BLOCK;
                     IA_HIP(hipStreamWaitEvent(sj, blk[j - 1][b], 0));

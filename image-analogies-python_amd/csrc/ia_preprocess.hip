@@ -53,6 +53,27 @@ __global__ void k_yiq_to_rgb(const double *in, long npix, double *out) {
     out[3 * i + 2] = (1. * x0 + 1.702 * x2) + -1.105 * x1;
 }
 
+// the colour image of a level (image_analogies.py:216-217, 255-258): convert, YIQ (B' as Y,
+// B's I / Q) to RGB clipped to [0, 1] (np.clip); otherwise each pixel's source colour in the
+// A' images (im, s), C channels (a luminance A' is repeated over RGB)
+__global__ void k_color_output(const double *bp, const double *yiq, const int32_t *s, const int32_t *im,
+                               const double *ap, long ah, long aw, int C, long npix, double *out) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    if (yiq) {
+        const double x0 = bp[i], x1 = yiq[3 * i + 1], x2 = yiq[3 * i + 2];
+        const double r = (1. * x0 + 0.621 * x2) + 0.956 * x1;
+        const double g = (1. * x0 + -0.647 * x2) + -0.272 * x1;
+        const double b = (1. * x0 + 1.702 * x2) + -1.105 * x1;
+        out[3 * i] = fmin(fmax(r, 0.0), 1.0);
+        out[3 * i + 1] = fmin(fmax(g, 0.0), 1.0);
+        out[3 * i + 2] = fmin(fmax(b, 0.0), 1.0);
+    } else {
+        const long p = ((long)im[i] * ah + s[2 * i]) * aw + s[2 * i + 1];
+        for (int c = 0; c < 3; ++c) out[3 * i + c] = ap[p * C + (C == 1 ? 0 : c)];
+    }
+}
+
 __global__ void k_scale(const void *src, int dt, long n, double div, double *out) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = load_any(src, dt, i) / div;
@@ -658,6 +679,24 @@ __global__ __launch_bounds__(256) void k_sum_final(const double *part, int nb, l
 
 constexpr int MEAN_BLOCKS = 1024;
 
+// sum of squared deviations from *mean (ia_var_f64's second pass), per block as k_sum_partial
+__global__ __launch_bounds__(256) void k_sqdev_partial(const double *x, long n, const double *mean, double *part) {
+    __shared__ double s[256];
+    const double m = *mean;
+    double acc = 0.0;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const double d = x[i] - m;
+        acc += d * d;
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
 }  // namespace ia
 
 using namespace ia;
@@ -683,6 +722,16 @@ int ia_yiq_to_rgb(const double *in, long npix, double *out, void *stream) {
     if (npix == 0) return IA_OK;
     k_yiq_to_rgb<<<nblk(npix, 256), 256, 0, S(stream)>>>(in, npix, out);
     IA_LAUNCH_CHECK("k_yiq_to_rgb");
+    return IA_OK;
+}
+
+int ia_color_output(const double *bp, const double *yiq, const int32_t *s, const int32_t *im, const double *ap,
+                    int ah, int aw, int C, long npix, double *out, void *stream) {
+    IA_ARG(out && npix >= 0 && ((bp && yiq) || (s && im && ap && ah > 0 && aw > 0 && (C == 1 || C == 3))),
+           "ia_color_output: bad args");
+    if (npix == 0) return IA_OK;
+    k_color_output<<<nblk(npix, 256), 256, 0, S(stream)>>>(yiq ? bp : nullptr, yiq, s, im, ap, ah, aw, C, npix, out);
+    IA_LAUNCH_CHECK("k_color_output");
     return IA_OK;
 }
 
@@ -797,6 +846,20 @@ int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w
 }
 
 size_t ia_mean_workspace_bytes(long n) { (void)n; return MEAN_BLOCKS * sizeof(double); }
+
+int ia_var_f64(const double *x, long n, double *out, void *workspace, void *stream) {
+    // two passes: the mean into out[1], then sum (x - mean)^2 / (n - 1) into out[0]
+    // (torch's unbiased var, up to rounding order)
+    IA_ARG(x && out && workspace && n > 1, "ia_var_f64: bad args");
+    double *part = reinterpret_cast<double *>(workspace);
+    int nb = (int)std::min<long>(MEAN_BLOCKS, (n + 255) / 256);
+    k_sum_partial<<<nb, 256, 0, S(stream)>>>(x, n, part);
+    k_sum_final<<<1, 256, 0, S(stream)>>>(part, nb, n, out + 1);
+    k_sqdev_partial<<<nb, 256, 0, S(stream)>>>(x, n, out + 1, part);
+    k_sum_final<<<1, 256, 0, S(stream)>>>(part, nb, n - 1, out);
+    IA_LAUNCH_CHECK("ia_var_f64");
+    return IA_OK;
+}
 
 int ia_mean_f64(const double *x, long n, double *out, void *workspace, void *stream) {
     IA_ARG(x && out && workspace && n > 0, "ia_mean_f64: bad args");

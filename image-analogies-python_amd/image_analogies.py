@@ -215,7 +215,7 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
     weights = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
     if pipeline is None:
         pipeline = pipeline_default()
-    out, args, keep = {}, [], []
+    out, args, keep, done = {}, [], [], []
     for level in range(1, max_levels):
         if levels is not None and level not in levels:
             continue
@@ -255,6 +255,7 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
             a.dbr, a.rot = _ia.ptr(dbr).value, _ia.ptr(rot).value
         if dbg is not None:
             a.dbg_px, a.dbg_dist = _ia.ptr(dbg[0]).value, _ia.ptr(dbg[1]).value
+        done.append((a, (A_sm, A_lg, Ap_sm, Ap_lg, B_sm, B_lg, db3, ws, rot, dbr)))
         if not pipeline:
             _ia.check(lib.ia_synth_level3(ctypes.byref(a), st), 'ia_synth_level3')
         else:
@@ -275,6 +276,10 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
         # the level streams are joined into st: buffers freed after this return are reused
         # only by work queued on st behind that join (the caching allocator's stream order)
         del keep
+    if done:
+        # a decision wait of the fused colour tail that timed out leaves wrong pixels: raise
+        arr = (_ia.IaSynthArgs * len(done))(*[x[0] for x in done])
+        _ia.check(lib.ia_synth3_status(arr, len(done), st), 'ia_synth3_status')
     return out
 
 
@@ -563,23 +568,25 @@ def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
 
 
 def color_output(level, Bp_lvl, s, im, color_pyr_list, c):
-    """Colour image of a level (image_analogies.py:216-217, 255-258): with convert, Y from
-    B' and I/Q from B's pyramid (the reference takes color_pyr_list[i] with the LAST
-    pixel's i; there is one colour pyramid then), clipped; otherwise the A' colour of each
-    pixel's source."""
+    """Colour image of a level (image_analogies.py:216-217, 255-258), on device
+    (ia_color_output): with convert, Y from B' and I/Q from B's pyramid (the reference takes
+    color_pyr_list[i] with the LAST pixel's i; there is one colour pyramid then), clipped;
+    otherwise the A' colour of each pixel's source.  Returns (H, W, 3) numpy."""
     H, W = Bp_lvl.shape[:2]
+    out = torch.empty((H, W, 3), dtype=torch.float64, device=Bp_lvl.device)
     if c.convert:
-        yiq = torch.stack([Bp_lvl, color_pyr_list[0][level][:, :, 1], color_pyr_list[0][level][:, :, 2]], -1)
-        out = torch.empty_like(yiq)
-        _ia.check(_ia.lib().ia_yiq_to_rgb(_ia.ptr(yiq.contiguous()), H * W, _ia.ptr(out),
-                                          _ia.stream()), 'ia_yiq_to_rgb')
-        return out.clamp(0, 1).cpu().numpy()
-    src = torch.stack([p[level] for p in color_pyr_list])           # (nAp, h, w[, 3])
-    vals = src[im.long(), s[:, 0].long(), s[:, 1].long()]
-    vals = vals.reshape(H, W, *src.shape[3:])
-    if vals.dim() == 2:
-        vals = vals[..., None].expand(H, W, 3)
-    return vals.cpu().numpy()
+        yiq = color_pyr_list[0][level].contiguous()
+        _ia.check(_ia.lib().ia_color_output(_ia.ptr(Bp_lvl.contiguous()), _ia.ptr(yiq), None, None, None,
+                                            0, 0, 0, H * W, _ia.ptr(out), _ia.stream()), 'ia_color_output')
+        return out.cpu().numpy()
+    base = color_pyr_list[0][level]                                   # (h, w[, 3])
+    ah, aw = base.shape[:2]
+    C = 3 if base.dim() == 3 else 1
+    src = (base if len(color_pyr_list) == 1 else
+           torch.stack([p[level] for p in color_pyr_list])).contiguous()  # (nAp, h, w[, 3])
+    _ia.check(_ia.lib().ia_color_output(None, None, _ia.ptr(s.contiguous()), _ia.ptr(im.contiguous()), _ia.ptr(src),
+                                        int(ah), int(aw), C, H * W, _ia.ptr(out), _ia.stream()), 'ia_color_output')
+    return out.cpu().numpy()
 
 
 def debug_record(s, im, dbg, shape):

@@ -55,6 +55,12 @@ int ia_rgb_to_yiq(const void *src, int src_dtype, long npix, double div, double 
                   double *y, void *stream);
 /* img_preprocess.py:16-22 convert_to_RGB: in npix x 3 -> out npix x 3. */
 int ia_yiq_to_rgb(const double *in, long npix, double *out, void *stream);
+/* the colour image of a level before plt.imsave (image_analogies.py:216-217, 255-258), npix
+ * pixels -> out (npix x 3 fp64): yiq non-NULL (convert): RGB of (bp, yiq[.., 1], yiq[.., 2])
+ * clipped to [0, 1]; else the source colour of every pixel, ap[((im * ah + s_r) * aw + s_c)
+ * * C + c] (nAp x ah x aw x C, C = 1 repeated over RGB, or 3) */
+int ia_color_output(const double *bp, const double *yiq, const int32_t *s, const int32_t *im, const double *ap,
+                    int ah, int aw, int C, long npix, double *out, void *stream);
 /* scale only (convert=False path, image_analogies.py:51-56): out = src / div. */
 int ia_scale_to_f64(const void *src, int src_dtype, long n, double div, double *out,
                     void *stream);
@@ -75,6 +81,9 @@ int ia_pyr_reduce_f64(const double *src, int H, int W, double *dst, int h, int w
 /* deterministic mean of n doubles (used for the screening centre). */
 size_t ia_mean_workspace_bytes(long n);
 int ia_mean_f64(const double *x, long n, double *out, void *workspace, void *stream);
+/* unbiased variance of x[0..n): out[0] = sum (x - mean)^2 / (n - 1), out[1] = mean (two
+ * passes; workspace of ia_mean_workspace_bytes(n)) */
+int ia_var_f64(const double *x, long n, double *out, void *workspace, void *stream);
 
 /* ---- a9: algorithms.py:11-47 compute_feature_array, one level, 1 channel.
  * out: (h*w) x (full ? 34 : 21) fp64. */
@@ -290,6 +299,9 @@ int ia_level_resources(const IaSynthArgs *a, int *out);
 size_t ia_synth_workspace_bytes(int H, int W, long nrows, int nranks);
 int ia_synth_level(const IaSynthArgs *a, void *stream);
 int ia_synth_level3(const IaSynthArgs *a, void *stream);
+/* after ia_synth_level3 / ia_synth_levels3 of these levels: synchronises the stream and returns
+ * IA_E_SCHED if a wait for a neighbouring pixel's decision timed out in the fused colour tail */
+int ia_synth3_status(const IaSynthArgs *levels, int n, void *stream);
 int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream);
 /* the rotated split screen for 3-channel rows (R16c): after ia_db3_build, the
  * caller takes the principal directions V of the level's centred rows (165 x 165, columns by
@@ -303,6 +315,11 @@ size_t ia_db3_rot_bytes(long nrows);
 int ia_db3_rot_components(void);
 int ia_db3_rot_floats(void);
 int ia_db3_build_rot(const double *db3, long nrows, const float *rot, void *dbr, void *stream);
+/* the matrix whose eigenvectors rot3_build takes: the 165 x 165 covariance (fp64, cov[a * 168
+ * + b]) of ~64 k rows of an ia_db3_build buffer sampled every max(1, nrows / 65536) rows,
+ * centred at their mean; cov holds ia_db3_cov_bytes() (the rest is scratch) */
+size_t ia_db3_cov_bytes(void);
+int ia_db3_cov(const double *db3, long nrows, double *cov, void *stream);
 /* n consecutive levels (coarse to fine: levels[j].Bp_sm == levels[j-1].Bp_lg) at once, with
  * the same results as n ia_synth_level calls in order: each level runs on its own stream
  * and wave t of level j waits only for the waves of level j-1 its 3x3 coarse windows read
