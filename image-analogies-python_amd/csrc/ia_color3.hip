@@ -562,15 +562,25 @@ __global__ __launch_bounds__(256, 1) void k_db3_rot(const double *__restrict__ r
 // centred products with every column b, 32 sampled rows staged in LDS at a time; partials
 // reduced in slice order (deterministic).  Any orthonormal basis keeps the matcher exact; the
 // principal one of this matrix keeps its bound tight.
-constexpr int C3C_SPLIT = 16, C3C_AB = 16, C3C_NA = (D3 + C3C_AB - 1) / C3C_AB, C3C_TR = 32;
+constexpr int C3C_SPLIT = 128, C3C_AB = 16, C3C_NA = (D3 + C3C_AB - 1) / C3C_AB, C3C_TR = 32;
 __global__ __launch_bounds__(256) void k_db3_colsum(const double *__restrict__ rows, long step, long nsamp,
                                                     double *__restrict__ part) {
+    __shared__ double X[C3C_TR][D3P];
     const int t = threadIdx.x, sl = blockIdx.x;
     const long i0 = nsamp * sl / C3C_SPLIT, i1 = nsamp * (sl + 1) / C3C_SPLIT;
-    if (t >= D3) return;
     double acc = 0.0;
-    for (long i = i0; i < i1; ++i) acc += rows[i * step * D3P + t];
-    part[sl * D3P + t] = acc;
+    for (long r0 = i0; r0 < i1; r0 += C3C_TR) {
+        __syncthreads();
+        for (int e = t; e < C3C_TR * D3P; e += 256) {
+            const int rr = e / D3P, k = e - rr * D3P;
+            const long i = r0 + rr;
+            X[rr][k] = i < i1 ? rows[i * step * D3P + k] : 0.0;
+        }
+        __syncthreads();
+        if (t < D3)
+            for (int rr = 0; rr < C3C_TR; ++rr) acc += X[rr][t];
+    }
+    if (t < D3P) part[sl * D3P + t] = t < D3 ? acc : 0.0;
 }
 __global__ __launch_bounds__(256) void k_db3_mean(const double *__restrict__ part, long nsamp, double *__restrict__ mean) {
     const int t = threadIdx.x;
@@ -709,8 +719,10 @@ __global__ __launch_bounds__(256) void k_query3r(Img3 Bsm, Img3 Blg, Img3 Bpsm, 
 // the R16c screen: as k_screen3 with 11 operand groups per tile and 11 MFMAs per (row tile,
 // query tile); up to 8 query tiles staged per workgroup (a c3 wave's 213 queries: one group,
 // each DB tile read once per wave)
-constexpr int S3R_QG = 8;                 // query tiles per group (LDS: 8 x 11 KiB)
-__global__ __launch_bounds__(256, 1) void k_screen3r(const half8 *__restrict__ db16, int ntiles,
+// 7 query tiles per group (a c3 wave's <= 213 queries: one group; LDS 77 KiB, two workgroups
+// per CU: the grid's ~450 workgroups in one round instead of two)
+constexpr int S3R_QG = 7;
+__global__ __launch_bounds__(256, 2) void k_screen3r(const half8 *__restrict__ db16, int ntiles,
                                                      const half8 *__restrict__ q16, int M, int tpw,
                                                      float *__restrict__ smin) {
     __shared__ half8 qsh[S3R_QG * R3_TILE];
@@ -732,17 +744,35 @@ __global__ __launch_bounds__(256, 1) void k_screen3r(const half8 *__restrict__ d
         if (more)
 #pragma unroll
             for (int c = 0; c < R3_MFMA; ++c) n[c] = db16[(long)tn * R3_TILE + c * 64 + lane];
-        for (int j = 0; j < nq; ++j) {
-            const half8 *qb = qsh + j * R3_TILE + lane;
-            floatx16 acc = zero;
+        // two query tiles per pass: both tiles' 22 operand reads issued first, the two
+        // accumulation chains interleaved (each MFMA's operand and the other chain's MFMA
+        // cover one another's latency; one wave per SIMD here), then both folds
+        for (int j = 0; j < nq; j += 2) {
+            const int j1 = j + 1 < nq ? j + 1 : j;
+            const half8 *qb0 = qsh + j * R3_TILE + lane, *qb1 = qsh + j1 * R3_TILE + lane;
+            half8 b0[R3_MFMA], b1[R3_MFMA];
 #pragma unroll
-            for (int c = 0; c < R3_MFMA; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[c], qb[c * 64], acc, 0, 0, 0);
-            float mn = acc[0];
+            for (int c = 0; c < R3_MFMA; ++c) {
+                b0[c] = qb0[c * 64];
+                b1[c] = qb1[c * 64];
+            }
+            floatx16 acc0 = zero, acc1 = zero;
 #pragma unroll
-            for (int i = 1; i < 16; ++i) mn = fminf(mn, acc[i]);
-            mn = fminf(mn, __shfl_xor(mn, 32));
-            const int q = (qt0 + j) * 32 + lane;
-            if (lane < 32 && q < M) smin[(long)q * c3_stride(ntiles) + t] = mn;
+            for (int c = 0; c < R3_MFMA; ++c) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[c], b0[c], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[c], b1[c], acc1, 0, 0, 0);
+            }
+            float mn0 = acc0[0], mn1 = acc1[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) {
+                mn0 = fminf(mn0, acc0[i]);
+                mn1 = fminf(mn1, acc1[i]);
+            }
+            mn0 = fminf(mn0, __shfl_xor(mn0, 32));
+            mn1 = fminf(mn1, __shfl_xor(mn1, 32));
+            const int q0 = (qt0 + j) * 32 + lane, q1 = (qt0 + j1) * 32 + lane;
+            if (lane < 32 && q0 < M) smin[(long)q0 * c3_stride(ntiles) + t] = mn0;
+            if (lane < 32 && j1 != j && q1 < M) smin[(long)q1 * c3_stride(ntiles) + t] = mn1;
         }
         if (!more) break;
 #pragma unroll
