@@ -306,7 +306,8 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
     constexpr size_t POOL = IMG ? (size_t)4 * WIN_SLOT : 0;
     constexpr size_t RESB = XW_STAGE_B + XW_RAW_B;
     __shared__ __attribute__((aligned(16))) char pool[POOL > RESB ? POOL : RESB];
-    __shared__ double cx[XW_NCOH][IA_DP], cw[XW_NCOH][IA_DP];
+    // (rows of IA_DP + 1 doubles: lane c's pairwise sum over cx[c] then hits distinct banks)
+    __shared__ double cx[XW_NCOH][IA_DP + 1], cw[XW_NCOH][IA_DP + 1];
     __shared__ double qs[IA_DP], wts[IA_DP];
     __shared__ float qf[IA_DP];
     __shared__ int slist[RESCORE_SEGCAP];
@@ -429,36 +430,61 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
         const int lseg = __builtin_ctz((unsigned)a.seg_rows);
         // wave 1: the coherence candidates (p_r = s(r) + q - r inside A'); an invalid one gets
         // position (0, 0, 0) so that its (unused) copies read valid memory
-        if (wv == 1) {
-            if (lane < XW_NCOH) {
-                const int sr = s_r + y - rr0, sc = s_c + x - rc0;
-                const bool ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
-                ccix[lane] = ok ? ((long)src.A.h * s_i + sr) * src.A.w + sc : -1;
-                cpos[lane][0] = ok ? sr : 0; cpos[lane][1] = ok ? sc : 0; cpos[lane][2] = ok ? s_i : 0;
-            }
-            wave_lds_sync();
-        }
+        // cm: the candidates whose features are copied and scored.  The row form skips the
+        // invalid ones and every repeat of an earlier candidate (same A' pixel: the same
+        // distance at a higher index, never the first minimum; c5's finest level: 5.5 distinct
+        // of 11.9 valid per pixel); the window form copies all 15 (its vmcnt count is fixed)
+        unsigned cm = (1u << XW_NCOH) - 1;
+        int c_r = 0, c_c = 0, c_i = 0;   // wave 1, lane c: candidate c's A' row, column, image
         // wave 1: the candidates' A' values and all their features requested at once by LDS
-        // DMA (candidate c's lo / hi words in cx / cw): EXACTLY XW_COH_DMA copies, none
-        // skipped, so that a window copied in before them is waited for with vmcnt
-        // (loads return in order)
+        // DMA (candidate c's lo / hi words in cx / cw); the window form: EXACTLY XW_COH_DMA
+        // copies, none skipped, so that a window copied in before them is waited for with
+        // vmcnt (loads return in order)
         auto coh_issue = [&]() {
             const long long cl = lane < XW_NCOH ? ccix[lane] : -1;
             dma_f64(src.Ap.lg + (cl >= 0 ? cl : 0), true, cvw[0], cvw[1]);
             unsigned *clo = reinterpret_cast<unsigned *>(&cx[0][0]);
             unsigned *chi = reinterpret_cast<unsigned *>(&cw[0][0]);
+            // (the positions broadcast from wave 1's registers: no LDS round trip per candidate)
 #pragma unroll 1
-            for (int c = 0; c < XW_NCOH; ++c) {
+            for (unsigned m = cm; m; m &= m - 1) {
+                const int c = __builtin_ctz(m);
+                const int pr = __builtin_amdgcn_readlane(c_r, c), pc = __builtin_amdgcn_readlane(c_c, c);
+                const int pi = __builtin_amdgcn_readlane(c_i, c);
                 ImgPair ap = src.Ap;
-                ap.sm += (long)cpos[c][2] * src.hws;
-                ap.lg += (long)cpos[c][2] * src.hw;
+                ap.sm += (long)pi * src.hws;
+                ap.lg += (long)pi * src.hw;
                 int rr, cc;
-                const double *fp = feat_addr(src.A, ap, cpos[c][0], cpos[c][1], lane < IA_D ? lane : 0, rr, cc);
+                const double *fp = feat_addr(src.A, ap, pr, pc, lane < IA_D ? lane : 0, rr, cc);
                 dma_f64(fp, true, clo + c * 64, chi + c * 64);
             }
             wstamp(13);
         };
 
+        if (wv == 1) {
+            long long mine = -1;
+            if (lane < XW_NCOH) {
+                const int sr = s_r + y - rr0, sc = s_c + x - rc0;
+                const bool ok = cpos_ok && sr >= 0 && sr < src.A.h && sc >= 0 && sc < src.A.w;
+                mine = ok ? ((long)src.A.h * s_i + sr) * src.A.w + sc : -1;
+                ccix[lane] = mine;
+                c_r = ok ? sr : 0; c_c = ok ? sc : 0; c_i = ok ? s_i : 0;
+                cpos[lane][0] = c_r; cpos[lane][1] = c_c; cpos[lane][2] = c_i;
+            }
+            if constexpr (!IMG) {
+                // (lane j's value by readlane: a scalar broadcast, not an LDS round trip)
+                bool keep = mine >= 0;
+                const int mlo = (int)mine, mhi = (int)(mine >> 32);
+#pragma unroll
+                for (int j = 0; j < XW_NCOH - 1; ++j) {
+                    const long long o = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(mhi, j) << 32) |
+                                                    (unsigned)__builtin_amdgcn_readlane(mlo, j));
+                    keep = keep && !(j < lane && o == mine);
+                }
+                cm = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)__ballot(keep && lane < XW_NCOH));
+            }
+            wave_lds_sync();
+        }
         // ---- 2. fp32 re-screen of the candidate segments' rows; rows within Trow to the
         // list (overflow rows rescored in place: never on the measured configs)
         unsigned int mine = 0;
@@ -586,13 +612,14 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
             // only cover the words of candidates >= c, already read)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_lds_sync();
-            const long long cix = lane < XW_NCOH ? ccix[lane] : -1;
+            const long long cix = lane < XW_NCOH && ((cm >> lane) & 1u) ? ccix[lane] : -1;
             const double cvl = cix >= 0 ? lds_f64(cvw[0], cvw[1], lane) : 0.0;
             const double ql = lane < IA_D ? qs[lane] : 0.0, wl = lane < IA_D ? wts[lane] : 0.0;
             const unsigned *clo = reinterpret_cast<const unsigned *>(&cx[0][0]);
             const unsigned *chi = reinterpret_cast<const unsigned *>(&cw[0][0]);
 #pragma unroll 1
             for (int c = XW_NCOH - 1; c >= 0; --c) {
+                if (!((cm >> c) & 1u)) continue;
                 const double g = lds_f64(clo + c * 64, chi + c * 64, lane);
                 wave_lds_sync();   // every lane has candidate c's words
                 if (lane < IA_D) {
