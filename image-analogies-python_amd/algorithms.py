@@ -138,7 +138,7 @@ class LevelIndex:
         _ia.check(lib.ia_db_cov(ctypes.byref(self.src), self.row0, self.nrows,
                                 _ia.ptr(self.center), _ia.ptr(cov), st), 'ia_db_cov')
         C = cov[:56 * 56].view(56, 56)[:55, :55].cpu().numpy()
-        w, V = np.linalg.eigh(C)
+        w, V = _eigh(C)
         V = V[:, ::-1]                       # components by decreasing variance
         R = np.zeros(_ia.R16_ROT_FLOATS, dtype=np.float32)
         R[:56 * 56].reshape(56, 56)[:55, :55] = V.astype(np.float32)
@@ -213,21 +213,45 @@ class LevelIndex:
         return torch.cat(rows, 0)
 
 
-def rot3_build(db3, N):
-    """The rotated split DB of the 3-channel screen (R16c) from an ia_db3_build
-    buffer: the covariance of ~64 k sampled rows around their mean (ia_db3_cov, on device),
-    its eigenvectors on the host (165 x 165; any orthonormal basis keeps the matcher exact,
-    the principal one keeps the bound tight), then ia_db3_build_rot.  Returns (rot, dbr)."""
+def _eigh(C):
+    """np.linalg.eigh of a small covariance (55 or 165 square) on ONE BLAS thread: the
+    threaded LAPACK is slower at this size (165: 3.8-4.6 vs 5.7-6.0 ms on 8 threads, more
+    with 16 busy ones)."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:   # (the pin is only a speed-up)
+        return np.linalg.eigh(C)
+    with threadpool_limits(1):
+        return np.linalg.eigh(C)
+
+
+def rot3_rotation(db3, N):
+    """The rotation of the 3-channel screen (R16c) from an ia_db3_build buffer:
+    the covariance of ~64 k sampled rows around their mean (ia_db3_cov, on device), its
+    eigenvectors on the host (165 x 165; one device sync).  Any orthonormal basis keeps the
+    matcher exact; the principal one keeps the bound tight."""
     lib, st = _ia.lib(), _ia.stream()
     cov = torch.empty(lib.ia_db3_cov_bytes() // 8, dtype=torch.float64, device=db3.device)
     _ia.check(lib.ia_db3_cov(_ia.ptr(db3), N, _ia.ptr(cov), st), 'ia_db3_cov')
-    w, V = np.linalg.eigh(cov[:165 * 168].view(165, 168)[:, :165].cpu().numpy())
+    w, V = _eigh(cov[:165 * 168].view(165, 168)[:, :165].cpu().numpy())
     R = np.zeros(lib.ia_db3_rot_floats(), dtype=np.float32)
     R.reshape(165, 168)[:, :165] = V[:, ::-1]
-    rot = torch.as_tensor(R).to(db3.device)
+    return torch.as_tensor(R).to(db3.device)
+
+
+def rot3_apply(db3, N, rot):
+    """The rotated split DB of one level under rotation rot (ia_db3_build_rot)."""
+    lib, st = _ia.lib(), _ia.stream()
     dbr = torch.empty(lib.ia_db3_rot_bytes(N), dtype=torch.uint8, device=db3.device)
     _ia.check(lib.ia_db3_build_rot(_ia.ptr(db3), N, _ia.ptr(rot), _ia.ptr(dbr), st), 'ia_db3_build_rot')
-    return rot, dbr
+    return dbr
+
+
+def rot3_build(db3, N):
+    """The rotated split DB of the 3-channel screen from one level's own principal directions.
+    Returns (rot, dbr)."""
+    rot = rot3_rotation(db3, N)
+    return rot, rot3_apply(db3, N, rot)
 
 
 class LevelIndex3:

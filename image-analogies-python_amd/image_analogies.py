@@ -216,19 +216,33 @@ def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, l
     if pipeline is None:
         pipeline = pipeline_default()
     out, args, keep, done = {}, [], [], []
-    for level in range(1, max_levels):
-        if levels is not None and level not in levels:
-            continue
+    todo = [l for l in range(1, max_levels) if levels is None or l in levels]
+    built = {}
+    for level in todo:
         A_sm, A_lg = A_pyr[level - 1].contiguous(), A_pyr[level].contiguous()
         Ap_sm = torch.stack([p[level - 1] for p in Ap_pyr_list]).contiguous()
         Ap_lg = torch.stack([p[level] for p in Ap_pyr_list]).contiguous()
         src = _src_level3(A_sm, A_lg, Ap_sm, Ap_lg)
         N = src.nAp * src.Ah * src.Aw
-        dev = A_lg.device
-        db3 = torch.empty(lib.ia_db3_bytes(N) // 8, dtype=torch.float64, device=dev)
+        db3 = torch.empty(lib.ia_db3_bytes(N) // 8, dtype=torch.float64, device=A_lg.device)
         _ia.check(lib.ia_db3_build(ctypes.byref(src), 0, N, _ia.ptr(db3), st), 'ia_db3_build')
+        built[level] = (A_sm, A_lg, Ap_sm, Ap_lg, src, N, db3)
+    # the rotated split screen (R16c), bit-identical results: one rotation for every level,
+    # the principal directions of the finest level's rows (IA_ROT3_SHARED, default 1: one
+    # device sync and one 165 x 165 eigh per call instead of one per level; the coarser
+    # levels' rows have nearly the same principal directions, and any orthonormal basis keeps
+    # the matcher exact); 0: each level its own
+    shared = None
+    if _ia.db_rot_enabled() and todo and os.environ.get('IA_ROT3_SHARED', '1') != '0':
+        _, _, _, _, _, Nf, db3f = built[todo[-1]]
+        shared = algorithms.rot3_rotation(db3f, Nf)
+    for level in todo:
+        A_sm, A_lg, Ap_sm, Ap_lg, src, N, db3 = built[level]
+        dev = A_lg.device
         rot = dbr = None
-        if _ia.db_rot_enabled():   # the rotated split screen (R16c), bit-identical results
+        if shared is not None:
+            rot, dbr = shared, algorithms.rot3_apply(db3, N, shared)
+        elif _ia.db_rot_enabled():
             rot, dbr = algorithms.rot3_build(db3, N)
         B_sm, B_lg = B_pyr[level - 1].contiguous(), B_pyr[level].contiguous()
         Bp_sm, Bp_lg = Bp_pyr[level - 1], Bp_pyr[level]
