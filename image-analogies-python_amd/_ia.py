@@ -335,6 +335,7 @@ def prof_end():
     return out
 
 
+IA_E_ARG = -1          # include/ia.h: a bad argument, shape or precondition
 IA_E_TIMEOUT = -5      # include/ia.h: a device-side exchange wait for another rank
 IA_E_SCHED = -6        # include/ia.h: a neighbour-decision wait inside the fused kernel
 

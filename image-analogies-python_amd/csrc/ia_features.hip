@@ -20,17 +20,47 @@ namespace ia {
 
 thread_local long g_db_chunk_target = DB_TARGET_CHUNKS;
 
+// column a of V^T V - I: part[a] = sum over b of (sum_k V[k][a] V[k][b] - [a == b])^2 in fp64
+// (one block per column a; threads over b: the row reads are coalesced)
+constexpr int ROT_CHECK_NMAX = 192;
+__global__ __launch_bounds__(256) void k_rot_gram(const float *__restrict__ rot, int n, int ld,
+                                                  double *__restrict__ part) {
+    __shared__ double col[ROT_CHECK_NMAX];
+    __shared__ double red[4];
+    const int a = blockIdx.x, tid = threadIdx.x;
+    for (int k = tid; k < n; k += 256) col[k] = (double)rot[(long)k * ld + a];
+    __syncthreads();
+    double s = 0.0;
+    for (int b = tid; b < n; b += 256) {
+        double e = a == b ? -1.0 : 0.0;
+        for (int k = 0; k < n; ++k) e += col[k] * (double)rot[(long)k * ld + b];
+        s += e * e;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) part[a] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// per host thread: the n column sums (device) and their host copy
+struct RotCheckBuf {
+    double *dev = nullptr;
+    ~RotCheckBuf() {}   // (freed with the process: the HIP runtime may be gone at thread exit)
+};
+static thread_local RotCheckBuf g_rot_check;
+
 int rot_check_orthonormal(const float *rot, int n, int ld, hipStream_t st, const char *who) {
-    std::vector<float> V((size_t)n * ld);
-    IA_HIP(hipMemcpyAsync(V.data(), rot, V.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+    IA_ARG(n > 0 && n <= ROT_CHECK_NMAX && ld >= n, "rot_check_orthonormal: bad shape");
+    if (!g_rot_check.dev) IA_HIP(hipMalloc(&g_rot_check.dev, ROT_CHECK_NMAX * sizeof(double)));
+    // V^T V on the device (a per-level host loop of n^3 fp64 products cost 1.8 ms at n = 165,
+    // the GPU idle meanwhile: 8 gaps per colour step, profiles/r06_colour_c3_trace.txt)
+    k_rot_gram<<<n, 256, 0, st>>>(rot, n, ld, g_rot_check.dev);
+    IA_LAUNCH_CHECK("k_rot_gram");
+    double part[ROT_CHECK_NMAX];
+    IA_HIP(hipMemcpyAsync(part, g_rot_check.dev, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st));
     IA_HIP(hipStreamSynchronize(st));
     double fro = 0.0;
-    for (int a = 0; a < n; ++a)
-        for (int b = 0; b < n; ++b) {
-            double e = a == b ? -1.0 : 0.0;
-            for (int k = 0; k < n; ++k) e += (double)V[(size_t)k * ld + a] * (double)V[(size_t)k * ld + b];
-            fro += e * e;
-        }
+    for (int a = 0; a < n; ++a) fro += part[a];
     const double budget = 2.0 * std::sqrt((double)n) * 0x1p-24;
     if (!(std::sqrt(fro) <= budget)) {
         char msg[256];

@@ -197,3 +197,36 @@ def test_r16_wave_form_equals_block_form(gpu, shape, cap):
             assert np.array_equal(w.view(np.uint32), b.view(np.uint32)), M
     finally:
         lib.ia_diag_set_r16_form(prev)
+
+
+def test_build_rot_refuses_a_non_orthonormal_rotation(gpu):
+    """The builders' precondition (include/ia.h): a rotation that is not orthonormal
+    to fp32 rounding (here the principal basis scaled by 1 + 1e-4, ||V^T V - I||_F ~ 1.5e-3
+    against the budget 2 sqrt(n) 2^-24) is refused with IA_E_ARG, for the luminance builder
+    (n = 55) and the 3-channel one (n = 165); the unscaled basis passes both."""
+    import _ia
+    import algorithms
+    lib = _ia.lib()
+    idx, _ = _level(73, (128, 128), 2)
+    ok = lib.ia_db_build_rot(ctypes.byref(idx.src), idx.row0, idx.nrows, _ia.ptr(idx.center),
+                             _ia.ptr(idx.rot), _ia.ptr(idx.amax), _ia.ptr(idx.dbr), _ia.stream())
+    assert ok == 0
+    bad = idx.rot.clone()
+    bad[:56 * 56].view(56, 56)[:55, :55] *= 1.0001
+    rc = lib.ia_db_build_rot(ctypes.byref(idx.src), idx.row0, idx.nrows, _ia.ptr(idx.center),
+                             _ia.ptr(bad), _ia.ptr(idx.amax), _ia.ptr(idx.dbr), _ia.stream())
+    assert rc == _ia.IA_E_ARG and b'not orthonormal' in lib.ia_last_error()
+    # 3 channels
+    A, Aps, _ = analogy_inputs(74, (40, 36), (8, 8), n_ap=1)
+    A3 = np.dstack([A, A ** 2, np.sqrt(A)])
+    Ap3 = np.dstack([Aps[0], Aps[0] ** 2, np.sqrt(Aps[0])])
+    A_pyr = [dev(p) for p in o.compute_gaussian_pyramid(A3, 3, cap=2)]
+    Ap_pyr = [dev(p) for p in o.compute_gaussian_pyramid(Ap3, 3, cap=2)]
+    ix3 = algorithms.LevelIndex3(A_pyr[0], A_pyr[1], torch.stack([Ap_pyr[0]]), torch.stack([Ap_pyr[1]]))
+    rot = algorithms.rot3_rotation(ix3.db3, ix3.N)
+    dbr = algorithms.rot3_apply(ix3.db3, ix3.N, rot)
+    assert dbr is not None
+    bad3 = rot.clone()
+    bad3[:165 * 168].view(165, 168)[:, :165] *= 1.0001
+    rc = lib.ia_db3_build_rot(_ia.ptr(ix3.db3), ix3.N, _ia.ptr(bad3), _ia.ptr(dbr), _ia.stream())
+    assert rc == _ia.IA_E_ARG and b'not orthonormal' in lib.ia_last_error()

@@ -5,6 +5,7 @@ syntheses (device pyramids, B' reset, every level), inputs resident in HBM.
 
 usage: python tools/colour_bench.py [H W] [steps]      (default 180 117 (c1 size), 3 steps)
        COLOUR_PIPE=0: the colour levels one at a time (default: pipelined, ia_synth_levels3)
+       COLOUR_ONLY=1: the 3-channel run alone (kernel traces of it)
 Also reports the colour exact stage's candidate tiles per query (ia_diag_color16_stats) and a
 B' checksum (equal with and without the pipeline).
 """
@@ -37,9 +38,10 @@ def main():
     import _ia
     pipe = os.environ.get('COLOUR_PIPE', '1') != '0'
     out = {'size': [H, W], 'pipeline': pipe}
-    for name, (a, ap, b, ww) in {
-            'rgb': (A, Ap, B, w),
-            'luminance': (A[..., 0], Ap[..., 0], B[..., 0], w1)}.items():
+    runs = {'rgb': (A, Ap, B, w), 'luminance': (A[..., 0], Ap[..., 0], B[..., 0], w1)}
+    if os.environ.get('COLOUR_ONLY', '0') != '0':
+        del runs['luminance']
+    for name, (a, ap, b, ww) in runs.items():
         a, ap, b = (torch.as_tensor(x).to(dev) for x in (a, ap, b))
         nB = ip.num_layers(H, W, cfg.n_sm, None)
         L = nB + 1
@@ -75,7 +77,8 @@ def main():
                      'bp_checksum': float(sum(float(x.sum()) for x in Bp[1:L]))}
         if name == 'rgb':
             out[name]['candidate_tiles_per_query'], out[name]['full_scans'] = cand
-    out['rgb_vs_luminance_slowdown'] = out['luminance']['px_per_s'] / out['rgb']['px_per_s']
+    if 'luminance' in out:
+        out['rgb_vs_luminance_slowdown'] = out['luminance']['px_per_s'] / out['rgb']['px_per_s']
     print(json.dumps(out))
 
 
