@@ -53,7 +53,7 @@ HBM_PEAK_GBS = 8000.0
 # MI355X_MICROARCH.md §HBM; counters cannot be read from inside the measured process).
 # The file records a hash of the screen's sources; a file from other sources is stale and
 # the bench then reports traffic null.
-SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r05_screen_traffic_bench_pmc.json')
+SCREEN_PMC_FILE = os.path.join(ROOT, 'profiles', 'r06_screen_traffic_bench_pmc.json')
 SCREEN_SRCS = ('ia_screen16.hip', 'ia_split16.h', 'ia_imgwin.h', 'ia_internal.h', 'ia_screen16r.hip',
                'ia_rot16.h')
 
@@ -75,7 +75,7 @@ def screen_pmc():
     return {'bytes': d['traffic_bytes'], 'kernel': d['kernel'], 'dispatches': d['dispatches'],
             'source': os.path.relpath(SCREEN_PMC_FILE, ROOT)}
 
-SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r05_screen_sq_pmc.json')
+SCREEN_SQ_FILE = os.path.join(ROOT, 'profiles', 'r06_screen_sq_pmc.json')
 
 
 def screen_sq():

@@ -34,8 +34,10 @@ def main(path, sub=None):
            'clock_ghz': cyc / (d['us'] * 1e3),
            'mfma_busy': d['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / cyc,
            'wait_inst_share': d['SQ_WAIT_INST_ANY'] / d['SQ_WAVE_CYCLES'],
-           'lds_bank_conflict_share': (d['SQ_LDS_BANK_CONFLICT'] / d['SQ_ACTIVE_INST_LDS']
-                                       if 'SQ_LDS_BANK_CONFLICT' in d else None),
+           # conflict cycles over LDS-active cycles (SQ_LDS_IDX_ACTIVE); round 5 divided by
+           # SQ_ACTIVE_INST_LDS, an instruction count, and overstated the share (0.357 vs 0.105)
+           'lds_bank_conflict_share': (d['SQ_LDS_BANK_CONFLICT'] / d['SQ_LDS_IDX_ACTIVE']
+                                       if 'SQ_LDS_BANK_CONFLICT' in d and 'SQ_LDS_IDX_ACTIVE' in d else None),
            'wait_any_share': d['SQ_WAIT_ANY'] / d['SQ_WAVE_CYCLES'] if 'SQ_WAIT_ANY' in d else None,
            'mfma_coexec': (d['SQ_VALU_MFMA_COEXEC_CYCLES'] / 1024 / cyc
                            if 'SQ_VALU_MFMA_COEXEC_CYCLES' in d else None),
