@@ -329,7 +329,10 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         # one exchange cannot serve two levels running at once (their records would share
         # the exchange's box cells): levels one at a time then
         pipeline = False
-    peer_rule = sharded and comm is not None and _ia.exchange_kind() == 'peer' and torch.cuda.is_available()
+    # (a 1-rank exchange never waits on another rank: each workgroup publishes its record
+    # before it collects its own, so the forward-progress rule only binds for nranks > 1)
+    peer_rule = (sharded and comm is not None and nranks > 1 and _ia.exchange_kind() == 'peer'
+                 and torch.cuda.is_available())
     out = {}
     t_start = time.time()
     calls = []
@@ -355,6 +358,9 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
         cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
         pipeline = sharded_schedule([tuple(B_pyr[l].shape[:2]) for l in sharded], pipeline, share,
                                     [r[0] for r in res], [r[1] for r in res], cus)
+        if os.environ.get('IA_VERBOSE'):
+            print('[ia] sharded levels %s: kernels %s, pipelined %s' % (sharded, res, pipeline),
+                  file=sys.stderr, flush=True)
     for level in todo:
         call = early.pop(level, None) or make_call(level)
         if pipeline:
