@@ -204,12 +204,15 @@ def _src_level3(A_sm, A_lg, Ap_sm, Ap_lg):
 def synthesize3_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights, levels=None,
                     debug=False, pipeline=None):
     """3-channel synthesis (num_ch = 3: convert=False on colour images, 165-dim rows): per
-    level the materialised fp64 database (ia_db3_build: the exact stage's rows and the
-    split-f16 operand of the MFMA screen k_screen3), then every wave's query rows, screen
-    and exact fp64 rescore of the candidate tiles (the oracle's first minimum, DESIGN.md
-    §4c), the coherence / kappa tail and the 3-channel B' update.  pipeline (default
-    pipeline_default()): the levels run concurrently (ia_synth_levels3), else one after the
-    other (ia_synth_level3); the same results.  Same return value as synthesize_dev."""
+    level the materialised fp64 database (ia_db3_build), and by default (IA_DB_ROT) its
+    rotated split-f16 form (R16c, DESIGN.md §4e: ia_db3_build_rot under ONE rotation for all
+    levels, the finest level's principal directions, IA_ROT3_SHARED); per wave the rotated
+    screen k_screen3r and the fused k_exact3<true> (exact fp64 rescore of the candidate
+    tiles in the oracle's order, the coherence / kappa tail, the 3-channel B' update and the
+    next wave's rotated query rows).  IA_DB_ROT=0: the split-f16 screen k_screen3 and the
+    unfused exact stage (§4c).  pipeline (default pipeline_default()): the levels run
+    concurrently (ia_synth_levels3), else one after the other (ia_synth_level3); the same
+    results.  Same return value as synthesize_dev."""
     lib = _ia.lib()
     st = _ia.stream()
     weights = weights if torch.is_tensor(weights) else _ia.to_dev(weights)
