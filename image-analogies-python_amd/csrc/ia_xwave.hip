@@ -63,6 +63,28 @@ __device__ __forceinline__ const double *feat_addr(const ImgPair &X, const ImgPa
     cc = symi2(c0, w);
     return base + (long)rr * w + cc;
 }
+// feat_addr for a pair whose two images share their dimensions (A and an A' image: the
+// exact stage's rows and the coherence candidates), from VALUES: the base pointers and the
+// fine / coarse dimensions arrive as uniform scalars, so the per-lane choice is a select of
+// registers.  (feat_addr's per-lane choice between two fields of the argument structs
+// compiled to per-lane loads from the kernel-argument memory and a vmcnt(0) wait, which also
+// waited for every copy the wave had in flight: ~1 us before wave 1's first coherence copy)
+__device__ __forceinline__ const double *feat_addr_v(const double *xs, const double *xl, const double *ys,
+                                                     const double *yl, int h, int w, int hs, int ws, int r,
+                                                     int c, int k, int &rr, int &cc) {
+    const bool yk = k >= 34;
+    const int kk = yk ? k - 34 : k;
+    const bool coarse = kk < 9;
+    const int t = coarse ? kk : kk - 9;
+    const int hh = coarse ? hs : h, ww = coarse ? ws : w;
+    const double *base = yk ? (coarse ? ys : yl) : (coarse ? xs : xl);
+    const int r0 = coarse ? (r >> 1) + t / 3 - 1 : r + t / 5 - 2;
+    const int c0 = coarse ? (c >> 1) + t % 3 - 1 : c + t % 5 - 2;
+    rr = symi2(r0, hh);
+    cc = symi2(c0, ww);
+    return base + (long)rr * ww + cc;
+}
+
 // image, row and column of global DB row g (< 2^31: the fused kernel's host check)
 __device__ __forceinline__ void row_pos(long g, long hw, int w, int &img, int &r, int &c) {
     const unsigned u = (unsigned)g, im = u / (unsigned)hw, rem = u - im * (unsigned)hw;
@@ -370,7 +392,9 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
     int pdep = 0;
     if (wv == 0 && nxt) {
         int rr = 0, cc = 0;
-        const double *p = feat_addr(a.B, a.Bp, y, x + 1, lane < IA_D ? lane : 0, rr, cc);
+        // (B and B' share their dimensions: feat_addr_v, no argument loads before the copies)
+        const double *p = feat_addr_v(a.B.sm, a.B.lg, a.Bp.sm, a.Bp.lg, a.B.h, a.B.w, a.B.hs, a.B.ws, y, x + 1,
+                                      lane < IA_D ? lane : 0, rr, cc);
         // 1: this pixel's new value, 2: the upper neighbour's
         pdep = lane < 43 || lane >= IA_D ? 0 : (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
         dma_f64(p, lane < IA_D && pdep == 0, nxw[0], nxw[1]);
@@ -445,17 +469,19 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
             dma_f64(src.Ap.lg + (cl >= 0 ? cl : 0), true, cvw[0], cvw[1]);
             unsigned *clo = reinterpret_cast<unsigned *>(&cx[0][0]);
             unsigned *chi = reinterpret_cast<unsigned *>(&cw[0][0]);
-            // (the positions broadcast from wave 1's registers: no LDS round trip per candidate)
+            // (the positions broadcast from wave 1's registers: no LDS round trip per candidate;
+            // the images' bases and dimensions as scalars: feat_addr_v)
+            const double *As = src.A.sm, *Al = src.A.lg, *Ps = src.Ap.sm, *Pl = src.Ap.lg;
+            const int fh = src.A.h, fw = src.A.w, chh = src.A.hs, cww = src.A.ws;
+            const long hws = src.hws, hw = src.hw;
 #pragma unroll 1
             for (unsigned m = cm; m; m &= m - 1) {
                 const int c = __builtin_ctz(m);
                 const int pr = __builtin_amdgcn_readlane(c_r, c), pc = __builtin_amdgcn_readlane(c_c, c);
                 const int pi = __builtin_amdgcn_readlane(c_i, c);
-                ImgPair ap = src.Ap;
-                ap.sm += (long)pi * src.hws;
-                ap.lg += (long)pi * src.hw;
                 int rr, cc;
-                const double *fp = feat_addr(src.A, ap, pr, pc, lane < IA_D ? lane : 0, rr, cc);
+                const double *fp = feat_addr_v(As, Al, Ps + (long)pi * hws, Pl + (long)pi * hw, fh, fw, chh, cww,
+                                               pr, pc, lane < IA_D ? lane : 0, rr, cc);
                 dma_f64(fp, true, clo + c * 64, chi + c * 64);
             }
             wstamp(13);
@@ -576,11 +602,10 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
                 for (int j = 0; j < XW_RPW && base + j < nl; ++j) {
                     const int ri = __shfl(li, j), rr = __shfl(lr_, j), rc = __shfl(lc, j);
                     const long rg = __shfl(lg, j);
-                    ImgPair ap = src.Ap;
-                    ap.sm += (long)ri * src.hws;
-                    ap.lg += (long)ri * src.hw;
                     int r2, c2;
-                    const double *fp = feat_addr(src.A, ap, rr, rc, lane < IA_D ? lane : 0, r2, c2);
+                    const double *fp = feat_addr_v(src.A.sm, src.A.lg, src.Ap.sm + (long)ri * src.hws,
+                                                   src.Ap.lg + (long)ri * src.hw, src.A.h, src.A.w, src.A.hs,
+                                                   src.A.ws, rr, rc, lane < IA_D ? lane : 0, r2, c2);
                     dma_f64(lane == IA_D ? src.Ap.lg + rg : fp, true, rw + j * 128, rw + j * 128 + 64);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1124,7 +1149,9 @@ __global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArg
     int pdep = 0;
     if (wv == 0 && nxt) {
         int rr = 0, cc = 0;
-        const double *p = feat_addr(a.B, a.Bp, y, x + 1, lane < IA_D ? lane : 0, rr, cc);
+        // (B and B' share their dimensions: feat_addr_v, no argument loads before the copies)
+        const double *p = feat_addr_v(a.B.sm, a.B.lg, a.Bp.sm, a.Bp.lg, a.B.h, a.B.w, a.B.hs, a.B.ws, y, x + 1,
+                                      lane < IA_D ? lane : 0, rr, cc);
         pdep = lane < 43 || lane >= IA_D ? 0 : (rr == y && cc == x) ? 1 : (rr == y - 1 && cc == x + 3) ? 2 : 0;
         dma_f64(p, lane < IA_D && pdep == 0, nxw[0], nxw[1]);
         dma_f64(a.center + (lane < IA_D ? lane : 0), lane < IA_D, nxw[2], nxw[3]);
