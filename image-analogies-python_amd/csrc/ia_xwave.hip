@@ -945,31 +945,34 @@ __device__ __forceinline__ double pw55_lanes(double v) {
 // t3 + 192 j of the query's minima in registers (XS_REG of them: c4's 8192 segments on one
 // GPU), the rest are streamed.  Same e* and candidate set as segmin_* over 256 threads.
 constexpr int XS_REG = 11;
-__device__ __forceinline__ void seg3_load(const float4 *sq4, long n4, int t3, float4 (&v)[XS_REG]) {
+template <int XR>
+__device__ __forceinline__ void seg3_load(const float4 *sq4, long n4, int t3, float4 (&v)[XR]) {
 #pragma unroll
-    for (int j = 0; j < XS_REG; ++j) {
+    for (int j = 0; j < XR; ++j) {
         const long i = t3 + (long)j * 192;
         const float4 x = sq4[i < n4 ? i : 0];   // unconditional (a valid index past the end)
         v[j] = i < n4 ? x : make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
     }
 }
-__device__ __forceinline__ float seg3_wave_min(const float4 *sq4, long n4, int t3, const float4 (&v)[XS_REG]) {
+template <int XR>
+__device__ __forceinline__ float seg3_wave_min(const float4 *sq4, long n4, int t3, const float4 (&v)[XR]) {
     float emin = FLT_MAX;
 #pragma unroll
-    for (int j = 0; j < XS_REG; ++j) emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
-    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+    for (int j = 0; j < XR; ++j) emin = fminf(emin, fminf(fminf(v[j].x, v[j].y), fminf(v[j].z, v[j].w)));
+    for (long i = t3 + (long)XR * 192; i < n4; i += 192) {
         const float4 x = sq4[i];
         emin = fminf(emin, fminf(fminf(x.x, x.y), fminf(x.z, x.w)));
     }
     for (int o = 32; o > 0; o >>= 1) emin = fminf(emin, __shfl_xor(emin, o));
     return emin;
 }
-__device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, const float4 (&v)[XS_REG],
+template <int XR>
+__device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, const float4 (&v)[XR],
                                             double Tseg, int *slist, int *scount) {
-    static_assert(XS_REG * 4 <= 64, "one 64-bit mask");
+    static_assert(XR * 4 <= 64, "one 64-bit mask");
     unsigned long long m = 0;
 #pragma unroll
-    for (int j = 0; j < XS_REG; ++j) {
+    for (int j = 0; j < XR; ++j) {
         m |= (unsigned long long)((double)v[j].x <= Tseg) << (4 * j);
         m |= (unsigned long long)((double)v[j].y <= Tseg) << (4 * j + 1);
         m |= (unsigned long long)((double)v[j].z <= Tseg) << (4 * j + 2);
@@ -984,7 +987,7 @@ __device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, 
             ++pos;
         }
     }
-    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+    for (long i = t3 + (long)XR * 192; i < n4; i += 192) {
         const float4 x = sq4[i];
         unsigned mt = ((double)x.x <= Tseg ? 1u : 0u) | ((double)x.y <= Tseg ? 2u : 0u) |
                       ((double)x.z <= Tseg ? 4u : 0u) | ((double)x.w <= Tseg ? 8u : 0u);
@@ -1002,9 +1005,10 @@ __device__ __forceinline__ void seg3_select(const float4 *sq4, long n4, int t3, 
 // R16 levels: the same phases with the per-segment skip bound (ia_rot16.h r16_kseg): cv[j] holds
 // the codes of the 4 segments of v[j] (one byte each, r16_askc); the reduction takes
 // min fl32(m + Kf c) and the selection m <= T0 + K c
-__device__ __forceinline__ void seg3_load_codes(const unsigned *ac4, long n4, int t3, unsigned (&cv)[XS_REG]) {
+template <int XR>
+__device__ __forceinline__ void seg3_load_codes(const unsigned *ac4, long n4, int t3, unsigned (&cv)[XR]) {
 #pragma unroll
-    for (int j = 0; j < XS_REG; ++j) {
+    for (int j = 0; j < XR; ++j) {
         const long i = t3 + (long)j * 192;
         cv[j] = ac4[i < n4 ? i : 0];
     }
@@ -1012,14 +1016,15 @@ __device__ __forceinline__ void seg3_load_codes(const unsigned *ac4, long n4, in
 __device__ __forceinline__ float seg_uval(float m, unsigned c, int b, float Kf) {
     return fmaf(Kf, (float)((c >> (8 * b)) & 255u), m);
 }
+template <int XR>
 __device__ __forceinline__ float seg3_wave_umin(const float4 *sq4, const unsigned *ac4, long n4, int t3,
-                                                const float4 (&v)[XS_REG], const unsigned (&cv)[XS_REG], float Kf) {
+                                                const float4 (&v)[XR], const unsigned (&cv)[XR], float Kf) {
     float u = FLT_MAX;
 #pragma unroll
-    for (int j = 0; j < XS_REG; ++j)
+    for (int j = 0; j < XR; ++j)
         u = fminf(u, fminf(fminf(seg_uval(v[j].x, cv[j], 0, Kf), seg_uval(v[j].y, cv[j], 1, Kf)),
                            fminf(seg_uval(v[j].z, cv[j], 2, Kf), seg_uval(v[j].w, cv[j], 3, Kf))));
-    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+    for (long i = t3 + (long)XR * 192; i < n4; i += 192) {
         const float4 x = sq4[i];
         const unsigned c = ac4[i];
         u = fminf(u, fminf(fminf(seg_uval(x.x, c, 0, Kf), seg_uval(x.y, c, 1, Kf)),
@@ -1034,12 +1039,13 @@ __device__ __forceinline__ unsigned seg_sel4(const float4 &x, unsigned c, double
            ((double)x.z <= fma(K, (double)((c >> 16) & 255u), T0) ? 4u : 0u) |
            ((double)x.w <= fma(K, (double)(c >> 24), T0) ? 8u : 0u);
 }
+template <int XR>
 __device__ __forceinline__ void seg3_select_codes(const float4 *sq4, const unsigned *ac4, long n4, int t3,
-                                                  const float4 (&v)[XS_REG], const unsigned (&cv)[XS_REG],
+                                                  const float4 (&v)[XR], const unsigned (&cv)[XR],
                                                   double T0, double K, int *slist, int *scount) {
     unsigned long long m = 0;
 #pragma unroll
-    for (int j = 0; j < XS_REG; ++j) m |= (unsigned long long)seg_sel4(v[j], cv[j], T0, K) << (4 * j);
+    for (int j = 0; j < XR; ++j) m |= (unsigned long long)seg_sel4(v[j], cv[j], T0, K) << (4 * j);
     if (m) {
         int pos = atomicAdd(scount, __builtin_popcountll(m));
         while (m) {
@@ -1049,7 +1055,7 @@ __device__ __forceinline__ void seg3_select_codes(const float4 *sq4, const unsig
             ++pos;
         }
     }
-    for (long i = t3 + (long)XS_REG * 192; i < n4; i += 192) {
+    for (long i = t3 + (long)XR * 192; i < n4; i += 192) {
         unsigned mt = seg_sel4(sq4[i], ac4[i], T0, K);
         if (mt) {
             int pos = atomicAdd(scount, __builtin_popcount(mt));
@@ -1076,7 +1082,10 @@ __device__ __forceinline__ void sync3(unsigned *cnt, unsigned g, int lane) {
 // rotated (the rotation copied into LDS by wave 0 at the start)
 // workgroups per CU the batch form (k_xstrip<true>) is built for (A/B builds)
 #ifndef IA_XSTRIP_BOCC
-#define IA_XSTRIP_BOCC 3
+#define IA_XSTRIP_BOCC 4
+#endif
+#ifndef IA_XSTRIP_BREG
+#define IA_XSTRIP_BREG 2   // float4s of segment minima per thread in registers, batch form
 #endif
 template <bool BATCH, bool ROT>
 __global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArgs a0) {
@@ -1173,8 +1182,11 @@ __global__ __launch_bounds__(256, BATCH ? IA_XSTRIP_BOCC : 3) void k_xstrip(XArg
         const float am = amx, ask = ROT ? a.amax[vidx(1)] : 0.f;
         const long n4 = a.nseg / 4;
         const float4 *sq4 = reinterpret_cast<const float4 *>(a.segmin + (long)i * a.nseg);
-        float4 v[XS_REG];
-        unsigned sgc[XS_REG];
+        // (the batch form holds fewer float4s of minima in registers: a c5 job's 512 segments
+        // fit in 2 per thread, and the freed VGPRs buy a fourth workgroup per CU)
+        constexpr int XR = BATCH ? IA_XSTRIP_BREG : XS_REG;
+        float4 v[XR];
+        unsigned sgc[XR];
         const unsigned *ac4 = ROT ? reinterpret_cast<const unsigned *>(a.askc.get()) : nullptr;
         if (wv != 1) {
             seg3_load(sq4, n4, t3, v);

@@ -439,6 +439,11 @@ def test_hot_kernels_do_not_spill():
                 name = m.group(1)
                 continue
             m = re.search(r'ScratchSize \[bytes/lane\]: (\d+)', line)
+            # (the batch form k_xstrip<true, ...> is built for 4 workgroups per CU and spills
+            # 17 VGPRs there: measured faster than unspilled at 3 per CU, c5 +2.3-3.6 % on one
+            # box, profiles/r06_c5_xstrip_occupancy_ab.txt; the single-job form is checked)
+            if m and name and 'k_xstripILb1E' in name:
+                continue
             if m and name and any(h in name for h in hot):
                 seen += 1
                 if int(m.group(1)) != 0:
