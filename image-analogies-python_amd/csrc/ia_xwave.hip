@@ -107,6 +107,26 @@ __device__ __forceinline__ double lds_f64(const unsigned *lo, const unsigned *hi
     return __longlong_as_double((long long)(((unsigned long long)hi[l] << 32) | lo[l]));
 }
 
+// lexicographic (d, i) minimum over the 16 lanes of each row by DPP row rotations (8, 4, 2, 1):
+// every lane of a row ends with its row's minimum (fin_best's order: the lowest i on ties)
+__device__ __forceinline__ void rowmin16_lex(double &bd, long long &bl) {
+    auto step = [&](auto ctrl) {
+        constexpr int C = decltype(ctrl)::value;
+        const long long db = __double_as_longlong(bd);
+        const int dlo = __builtin_amdgcn_update_dpp((int)db, (int)db, C, 0xf, 0xf, false);
+        const int dhi = __builtin_amdgcn_update_dpp((int)(db >> 32), (int)(db >> 32), C, 0xf, 0xf, false);
+        const int ilo = __builtin_amdgcn_update_dpp((int)bl, (int)bl, C, 0xf, 0xf, false);
+        const int ihi = __builtin_amdgcn_update_dpp((int)(bl >> 32), (int)(bl >> 32), C, 0xf, 0xf, false);
+        const double od = __longlong_as_double((long long)(((unsigned long long)(unsigned)dhi << 32) | (unsigned)dlo));
+        const long long ol = (long long)(((unsigned long long)(unsigned)ihi << 32) | (unsigned)ilo);
+        fin_best(bd, bl, od, ol);
+    };
+    step(std::integral_constant<int, 0x128>{});   // row_ror:8
+    step(std::integral_constant<int, 0x124>{});   // row_ror:4
+    step(std::integral_constant<int, 0x122>{});   // row_ror:2
+    step(std::integral_constant<int, 0x121>{});   // row_ror:1
+}
+
 // numpy pairwise_sum of v[0..54] (Pw55's order, ia_common.h) from LDS
 __device__ __forceinline__ double pw55_lds(const double *v) {
     double r[8];
@@ -642,16 +662,32 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
             const double ql = lane < IA_D ? qs[lane] : 0.0, wl = lane < IA_D ? wts[lane] : 0.0;
             const unsigned *clo = reinterpret_cast<const unsigned *>(&cx[0][0]);
             const unsigned *chi = reinterpret_cast<const unsigned *>(&cw[0][0]);
+            // (four candidates per LDS round trip, highest first: a chunk's squares only cover
+            // words of candidates it or an earlier chunk has read)
 #pragma unroll 1
-            for (int c = XW_NCOH - 1; c >= 0; --c) {
-                if (!((cm >> c) & 1u)) continue;
-                const double g = lds_f64(clo + c * 64, chi + c * 64, lane);
-                wave_lds_sync();   // every lane has candidate c's words
-                if (lane < IA_D) {
-                    const double xx = g - ql;
-                    const double xw = xx * wl;
-                    cx[c][lane] = xx * xx;
-                    cw[c][lane] = xw * xw;
+            for (unsigned rem = cm; rem;) {
+                int ci[4];
+                double gv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    ci[u] = -1;
+                    gv[u] = 0.0;
+                    if (rem) {
+                        const int c = 31 - __builtin_clz(rem);
+                        rem &= ~(1u << c);
+                        ci[u] = c;
+                        gv[u] = lds_f64(clo + c * 64, chi + c * 64, lane);
+                    }
+                }
+                wave_lds_sync();   // every lane has the chunk's words
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (ci[u] >= 0 && lane < IA_D) {
+                        const double xx = gv[u] - ql;
+                        const double xw = xx * wl;
+                        cx[ci[u]][lane] = xx * xx;
+                        cw[ci[u]][lane] = xw * xw;
+                    }
                 }
             }
             wave_lds_sync();
@@ -663,17 +699,22 @@ __global__ __launch_bounds__(256, IA_XWAVE_OCC) void k_xwave(XArgs a0) {
                 cwd = s * s;
                 cl = lane;
             }
+            // the first minimum over lanes 0..14 (row 0 of the wave): DPP rotations within the
+            // row (no LDS round trip per step); every lane of row 0 ends with it
             double bd = cd;
             long long bl = cl;
-            for (int o = 32; o > 0; o >>= 1) {
-                const double od = __shfl_xor(bd, o);
-                const long long ol = __shfl_xor(bl, o);
-                fin_best(bd, bl, od, ol);
-            }
+            rowmin16_lex(bd, bl);
+            bl = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bl >> 32), 0) << 32) |
+                             (unsigned)__builtin_amdgcn_readlane((int)bl, 0));
             const int win = bl == LLONG_MAX ? 0 : (int)bl;
             const long long wix = ccix[win];
             const int wr = cpos[win][0], wc = cpos[win][1], wim = cpos[win][2];
-            const double wd = __shfl(cwd, win), wval = __shfl(cvl, win);
+            auto lane_f64 = [&](double v) {   // v of lane win (uniform)
+                const long long b = __double_as_longlong(v);
+                return __longlong_as_double((long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), win) << 32) |
+                                                        (unsigned)__builtin_amdgcn_readlane((int)b, win)));
+            };
+            const double wd = lane_f64(cwd), wval = lane_f64(cvl);
             wstamp(15);
             if (lane == 0) {
                 cs = bl == LLONG_MAX ? CohSel{0, 0, 0, 0, 0, 0, 0, 0.0}
