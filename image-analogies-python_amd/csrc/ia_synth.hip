@@ -1133,10 +1133,13 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
         }
         return IA_OK;
     };
-    // enqueue order (IA_PIPE_ORDER): 1 [default] every level whole, coarse to fine (the
-    // coarse levels' commands are all in flight before the finest level's); 0 the finest
-    // level first, coarse waves just ahead of their need
-    static const int order = env_int("IA_PIPE_ORDER", 1);
+    // enqueue order (IA_PIPE_ORDER): 0 [default] the finest level first, coarse waves just
+    // ahead of their need; 1 every level whole, coarse to fine.  One host thread enqueues
+    // ~10 us of launches per wave, so with 1 the finest level's first wave was enqueued only
+    // after every coarse wave (c1: at +14 ms of a 27 ms traced step, tools/trace_queues.py).
+    // Same box, round 6: c1 18.51 -> 16.30, c3 76.0 -> 71.3, c4 783.7 -> 750.8, c5 794 -> 786
+    // ms/step (profiles/r06_pipe_order_ab.txt)
+    static const int order = env_int("IA_PIPE_ORDER", 0);
     for (int i = 0; i < n; ++i) {
         const int j = order ? i : n - 1 - i;
         int rc = advance(j, run[j].nw - 1);
