@@ -705,7 +705,14 @@ struct LevelRun {
 // step's critical path becomes ~ the finest level's waves instead of the sum of all
 // levels' waves.  Levels wait on events recorded every PIPE_BLOCK waves of the level below.
 constexpr int PIPE_BLOCK = 4;
-constexpr int PIPE_AHEAD = 64;   // waves a coarse level is enqueued ahead of its need
+// waves a coarse level is enqueued ahead of its need (IA_PIPE_AHEAD, default 16): every
+// coarse wave enqueued before the finest level's first costs ~10 us of host time; same box,
+// two passes: c1 16.22 / 16.30 (64), 15.99 / 15.95 (32), 15.24 / 15.12 (16), 15.55 / 15.72 (8)
+// ms/step, c3 1 % better at 16-32, c4 unchanged (profiles/r06_pipe_ahead_sweep.txt)
+static int pipe_ahead() {
+    static const int v = env_int("IA_PIPE_AHEAD", 16);
+    return v < 0 ? 0 : v;
+}
 
 static int coarse_need(const IaSynthArgs *a, int t) {
     int y_lo, M;
@@ -1115,7 +1122,7 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
                 w = need_max[j];
                 if (w > waited[j]) {
                     const int b = w / PIPE_BLOCK;
-                    int rc = advance(j - 1, b * PIPE_BLOCK + PIPE_BLOCK - 1 + PIPE_AHEAD);
+                    int rc = advance(j - 1, b * PIPE_BLOCK + PIPE_BLOCK - 1 + pipe_ahead());
                     if (rc) return rc;
                     IA_HIP(hipStreamWaitEvent(sj, blk[j - 1][b], 0));
                     waited[j] = b * PIPE_BLOCK + PIPE_BLOCK - 1;
