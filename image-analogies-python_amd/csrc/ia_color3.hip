@@ -1705,6 +1705,8 @@ struct Pipe3 {   // per host thread: the level streams and events of ia_synth_le
     hipStream_t plain = nullptr;   // level n-1 (the finest): plain priority
     std::vector<hipEvent_t> events;
     size_t next = 0;
+    hipEvent_t last = nullptr;     // the previous call's end (IA_PIPE_DRAIN, ia_synth.hip)
+    bool last_rec = false;
     // the streams of an n-level call: the pools grow as needed, and the finest level always
     // takes the plain stream whatever n the first call had
     hipError_t streams(int n, std::vector<hipStream_t> &out) {
@@ -1728,6 +1730,9 @@ struct Pipe3 {   // per host thread: the level streams and events of ia_synth_le
         if (plain && r == hipSuccess) r = hipStreamDestroy(plain);
         for (hipEvent_t e : events)
             if (r == hipSuccess) r = hipEventDestroy(e);
+        if (last && r == hipSuccess) r = hipEventDestroy(last);
+        last = nullptr;
+        last_rec = false;
         hi.clear();
         plain = nullptr;
         events.clear();
@@ -1920,6 +1925,10 @@ int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
                "ia_synth_levels3: levels must be consecutive (level j's coarse B' = level j-1's B')");
     hipStream_t st = S(stream);
     Pipe3 &P = g_pipe3;
+    // the previous call of this thread ends first (IA_PIPE_DRAIN, default 1: packets queued
+    // in the high-priority streams behind a running call slow its finest level, ia_synth.hip)
+    static const int drain = env_int("IA_PIPE_DRAIN", 1);
+    if (drain && P.last_rec) IA_HIP(hipEventSynchronize(P.last));
     std::vector<hipStream_t> ss;   // ss[j] runs level j: high priority but the finest
     IA_HIP(P.streams(n, ss));
     P.next = 0;
@@ -1964,6 +1973,9 @@ int ia_synth_levels3(const IaSynthArgs *levels, int n, void *stream) {
         IA_HIP(hipEventRecord(e, ss[j]));
         IA_HIP(hipStreamWaitEvent(st, e, 0));
     }
+    if (!P.last) IA_HIP(hipEventCreateWithFlags(&P.last, hipEventDisableTiming));
+    IA_HIP(hipEventRecord(P.last, st));
+    P.last_rec = true;
     return IA_OK;
 }
 

@@ -738,6 +738,8 @@ struct PipeRes {   // per host thread: the level streams and events of ia_synth_
     size_t pin_bytes = 0;
     hipEvent_t staged = nullptr;
     bool staged_rec = false;
+    hipEvent_t last = nullptr;          // the previous call's end (on its caller's stream)
+    bool last_rec = false;
     hipError_t staging(size_t bytes, void **p) {
         hipError_t r = hipSuccess;
         if (!staged && (r = hipEventCreateWithFlags(&staged, hipEventDisableTiming)) != hipSuccess) return r;
@@ -879,6 +881,9 @@ int ia_release_thread_resources(void) {
     g_pipe.pin_bytes = 0;
     g_pipe.staged = nullptr;
     g_pipe.staged_rec = false;
+    if (g_pipe.last) IA_HIP(hipEventDestroy(g_pipe.last));
+    g_pipe.last = nullptr;
+    g_pipe.last_rec = false;
     g_pipe.next_event = 0;
     if (g_graphs.cap) { IA_HIP(hipStreamDestroy(g_graphs.cap)); g_graphs.cap = nullptr; }
     if (g_graphs.done) { IA_HIP(hipEventDestroy(g_graphs.done)); g_graphs.done = nullptr; }
@@ -1043,6 +1048,15 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
     // level's plateau screens undisturbed: k_screen16<11> 400 vs 396 us); enqueued just
     // ahead of their need 1619-1621 ms but the plateau screens contended (414 us)
     static const int prio_on = env_int("IA_PIPE_PRIO", 1);
+    // a call waits on the host for this thread's previous call to end (IA_PIPE_DRAIN,
+    // default 1) before it enqueues anything.  Queued behind a running call, the coarse
+    // levels' first packets (their waits on `start`) sit in the high-priority queues for the
+    // whole of the previous call's finest level, and while they do the finest level's
+    // launches run ~4x slower (c1 with no host sync between steps: 61 vs 15 ms/step, screens
+    // 39 vs 9.4 us; IA_PIPE_PRIO=0 18 ms; profiles/r06_pipe_drain_ab.txt).  The host's other
+    // per-call work (the level indexes) still overlaps the previous call
+    static const int drain = env_int("IA_PIPE_DRAIN", 1);
+    if (drain && g_pipe.last_rec) IA_HIP(hipEventSynchronize(g_pipe.last));
     // the pools grow as needed; the finest level always takes the plain-priority stream,
     // whatever n the first call had (a pool sized by a smaller first call used to hand a
     // later call's coarse level a plain stream and its finest a high-priority one)
@@ -1162,6 +1176,9 @@ static int synth_levels(const IaSynthArgs *levels, int n, int K, void *stream) {
         IA_HIP(hipStreamWaitEvent(st, e, 0));
     }
     if (pinned) IA_HIP(hipEventRecord(g_pipe.staged, st));
+    if (!g_pipe.last) IA_HIP(hipEventCreateWithFlags(&g_pipe.last, hipEventDisableTiming));
+    IA_HIP(hipEventRecord(g_pipe.last, st));
+    g_pipe.last_rec = true;
     return IA_OK;
 }
 

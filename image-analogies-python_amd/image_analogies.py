@@ -312,8 +312,9 @@ def synthesize_dev(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, max_levels, k, weights,
     if a wait inside the device schedule timed out (ia_synth_status: the results would be
     wrong) -- a blocking call (one stream sync and one small copy per level, every level's
     workspace kept alive until then); check=False returns as soon as the work is queued,
-    and the caller checks later (_ia.sched_status(), as bench.py does once per timed pass).
-    Returns {level: (s, im[, debug])} device tensors."""
+    and the caller checks later (_ia.sched_status(), as bench.py does once per timed pass);
+    a later pipelined call of the same thread then waits for it to end before it enqueues
+    (IA_PIPE_DRAIN).  Returns {level: (s, im[, debug])} device tensors."""
     if B_pyr[-1].dim() == 3:     # 3-channel matching (num_ch = 3)
         if comm is not None or nranks > 1 or lsh is not None:
             raise NotImplementedError('3-channel matching runs on one GPU with the exact matcher')
