@@ -88,6 +88,7 @@ class _LevelCall:
         a.H, a.W = H, W
         a.Bp_sm, a.Bp_lg = _ia.ptr(Bp_sm).value, _ia.ptr(Bp_lg).value
         a.weights = _ia.ptr(weights).value
+        self.keep = (weights, B_sm, B_lg, Bp_sm, Bp_lg)   # read by every wave: alive with the call
         a.kappa_factor = kappa_factor(level, max_levels, k)
         a.s, a.im = _ia.ptr(self.s).value, _ia.ptr(self.im).value
         a.workspace = _ia.ptr(self.ws).value

@@ -331,6 +331,36 @@ def test_pipelined_levels_equal_sequential(gpu, seed):
             assert np.array_equal(o_[l][2], ref[l][0]), l
 
 
+def test_back_to_back_pipelined_calls_match_oracle(gpu):
+    """Two pipelined calls queued with no host sync between them (every level index built
+    first, so the second ia_synth_levels enters while the first runs): the second waits for
+    the first on the host (IA_PIPE_DRAIN) and reuses its streams and events; both equal the
+    oracle bit for bit."""
+    import algorithms
+    import image_analogies as ia
+    w = o.compute_weights(3, 5, 12, 1)
+    runs = []
+    for seed in (61, 62):
+        A, Aps, B = analogy_inputs(seed, (64, 77), (60, 84), n_ap=2, flat=(seed == 62))
+        A_pyr, Ap_list, B_pyr, Bp_pyr, L = o.setup_luminance(A, Aps, B, seed=seed)
+        ref = oc.synthesize(A_pyr, Ap_list, B_pyr, [b.copy() for b in Bp_pyr], L, 1.0, w)
+        Ad, Apd, Bd = [dev(p) for p in A_pyr], [[dev(p) for p in q] for q in Ap_list], [dev(p) for p in B_pyr]
+        Bp_dev = [dev(b) for b in Bp_pyr]
+        wd = dev(w)
+        calls = [ia._LevelCall(l, L, algorithms.level_index(Ad, Apd, l), Bd[l - 1], Bd[l],
+                               Bp_dev[l - 1], Bp_dev[l], wd, 1.0)
+                 for l in range(1, L)]
+        runs.append((ref, calls, Bp_dev, (Ad, Apd, Bd, wd)))
+    torch.cuda.synchronize()
+    outs = [ia.synthesize_levels_dev(calls) for _, calls, _, _ in runs]   # no sync between
+    torch.cuda.synchronize()
+    for (ref, calls, Bp_dev, _), out in zip(runs, outs):
+        for i, l in enumerate(range(1, len(calls) + 1)):
+            assert np.array_equal(out[i][0].cpu().numpy(), ref[l][1]), l
+            assert np.array_equal(out[i][1].cpu().numpy(), ref[l][2]), l
+            assert np.array_equal(Bp_dev[l].cpu().numpy(), ref[l][0]), l
+
+
 def test_sharded_level_index_rows(gpu):
     """Per-rank shards: each rank's exact local winner, combined with the lexicographic
     (distance, row) rule, equals the global exact winner (the rule k_finish applies to the
