@@ -704,7 +704,13 @@ struct LevelRun {
 // level l-1 has finished need(0) and run concurrently behind it on its own stream: the
 // step's critical path becomes ~ the finest level's waves instead of the sum of all
 // levels' waves.  Levels wait on events recorded every PIPE_BLOCK waves of the level below.
-constexpr int PIPE_BLOCK = 4;
+// waves per recorded event (build-time IA_PIPE_BLOCK).  8 against 4, same boxes, two
+// rounds: c1 14.73-15.07 vs 14.93-15.19, c3 69.2-70.7 vs 69.9-72.3, c4 734-743 vs 735-744
+// ms/step; 2 is slower (c1 16.1), 16 mixed (profiles/r06_pipe_block_ab.txt)
+#ifndef IA_PIPE_BLOCK
+#define IA_PIPE_BLOCK 8
+#endif
+constexpr int PIPE_BLOCK = IA_PIPE_BLOCK;
 // waves a coarse level is enqueued ahead of its need (IA_PIPE_AHEAD, default 16): every
 // coarse wave enqueued before the finest level's first costs ~10 us of host time; same box,
 // two passes: c1 16.22 / 16.30 (64), 15.99 / 15.95 (32), 15.24 / 15.12 (16), 15.55 / 15.72 (8)
