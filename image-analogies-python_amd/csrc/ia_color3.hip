@@ -1698,7 +1698,12 @@ static int c3_need(const IaSynthArgs &a, int t) {
     }
     return need;
 }
-constexpr int C3_PIPE_BLOCK = 4;   // waves per recorded event
+// 8 against 4 at the c3 size, same box, A/B/A/B: 112.6 / 111.0 vs 113.8 / 112.6 ms per
+// step, same checksum (profiles/r06_pipe_block_ab.txt)
+#ifndef IA_C3_PIPE_BLOCK
+#define IA_C3_PIPE_BLOCK 8
+#endif
+constexpr int C3_PIPE_BLOCK = IA_C3_PIPE_BLOCK;   // waves per recorded event (build-time)
 
 struct Pipe3 {   // per host thread: the level streams and events of ia_synth_levels3
     std::vector<hipStream_t> hi;   // levels 0 .. n-2 of a call (the coarser ones): high priority
